@@ -1,0 +1,164 @@
+/*
+ * oracle.h — CPU restatement of the matternet-rs (crate `surfface`) hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  Nothing under oracle/ is part of the product:
+ * only tests/, __graft_entry__.smoke() and bench.py's `cpu_baseline` leg may
+ * load liboracle.so, and only as the checker (or the timed CPU baseline),
+ * never as the thing measured or shipped.  The HIP library
+ * (matternet-rs_amd/csrc, include/matternet_hip.h) never links or calls it.
+ *
+ * Provenance / pinning.  The reference is Rust; no Rust toolchain exists in
+ * this image and the hot-path sources (src_legacy/) are not a compile target
+ * of the reference workspace, so the reference cannot be built here
+ * (SURVEY.md §8c).  The reference ships no golden vectors.  This restatement
+ * is therefore pinned by (1) every known-answer test the reference's own test
+ * suites hold for this path (tests/golden/reference_known_answers.json, each
+ * case citing its reference test file:line), and (2) an independent
+ * pure-Python restatement (tests/golden/make_golden.py) whose small-case
+ * outputs are committed as fixtures.  Bit patterns beyond those fixtures are
+ * pinned only by the arithmetic contracts transcribed from the reference
+ * (SURVEY.md Appendix A), cited per function below.
+ *
+ * Build: oracle/Makefile (gcc -O3 -fno-fast-math -ffp-contract=off -fopenmp).
+ * All functions return 0 on success, negative on error (-1 EINVAL,
+ * -3 non-finite distance: the reference panics in partial_cmp().unwrap()).
+ */
+#ifndef MATTERNET_ORACLE_H
+#define MATTERNET_ORACLE_H
+#include <stdint.h>
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- K1: brute-force kNN ------------------------------------------------ */
+
+/* A.1  L2^2 kNN over rows of X [n][d] f32 row-major.
+ *   surfface-core/src/distance.rs:206-213 (squared_euclidean_distance_slice:
+ *   sequential f32 fold of (a-b)^2, no FMA), surfface-core/src/mst.rs:330-360
+ *   (build_candidate_graph: j != i, stable sort_by(partial_cmp) => ties by
+ *   ascending j, truncate k = min(k, n-1)).
+ * Query rows [q_begin, q_end) are computed; outputs are indexed by
+ * (i - q_begin) * k.  Slots beyond min(k, n-1) get idx -1, dist +inf.
+ * mode 0 = faithful (full stable sort of all n-1 candidates, as the
+ * reference), mode 1 = restated-efficient (bounded max-heap on the same
+ * (dist, j) total order; identical output).  nthreads <= 0 => OpenMP default.
+ */
+int or_knn_l2sq_f32(const float *X, int64_t n, int32_t d, int32_t k,
+                    int64_t q_begin, int64_t q_end, int mode, int nthreads,
+                    int32_t *out_idx, float *out_dist);
+
+/* A.1c rectified-cosine kNN, f64 arithmetic on exactly-widened f32 inputs.
+ *   src_legacy/tests/test_helpers.rs:77-126 (build_adjacency_matrix):
+ *   norms sqrt(sum x*x) sequential f64; dot sequential f64;
+ *   cos = denom > 1e-12 ? clamp(dot/denom,-1,1) : 0; dist = 1 - max(cos,0);
+ *   keep dist <= eps and w = 1/(1+(dist/sigma)^p) > 1e-12;
+ *   sort by (dist asc, j asc); truncate topk.
+ * out_w may be NULL.  Unused slots: idx -1, dist +inf, w 0.
+ */
+int or_knn_cos_f64(const float *X, int64_t n, int32_t d, int32_t topk,
+                   double eps, double sigma, double p,
+                   int64_t q_begin, int64_t q_end, int nthreads,
+                   int32_t *out_idx, double *out_dist, double *out_w);
+
+/* ---- K2: Laplacian assembly --------------------------------------------- */
+
+/* A.2 UNION / unnormalised (legacy).
+ *   src_legacy/laplacian.rs:297-348 (_symmetrise_adjancency: every directed
+ *   edge inserted as (i,j,w) and (j,i,w), self loops dropped, rows sorted by
+ *   j) and :351-419 (_build_sparse_laplacian: L_ii = sum_j w_ij sequential
+ *   f64 in ascending j starting from -0.0 (Rust >= 1.83 float Sum), stored
+ *   for every i; L_ij = -w_ij; CSR sorted by (row, col)).
+ * Input: directed neighbour rows nbr_idx/nbr_w [n][k] (idx < 0 = empty slot).
+ * When both (i,j) and (j,i) exist with different weights the reference's
+ * DashMap keeps whichever write lands last (nondeterministic); this contract
+ * keeps the larger weight (identical for symmetric metrics).
+ * Output CSR: indptr [n+1] int64, indices/values capacity `cap`.
+ */
+int or_laplacian_union(int64_t n, int32_t k, const int32_t *nbr_idx,
+                       const double *nbr_w, int64_t cap, int64_t *indptr,
+                       int32_t *indices, double *values, int64_t *nnz_out);
+
+/* A.2 MAX / Stage C (f32).
+ *   surfface-core/src/laplacian.rs:320-394 (build_laplacian_flat: undirected
+ *   key (min,max) with max weight; drop i==j or w <= thr; degrees f32;
+ *   normalize: L_ii = 1 iff d_i > thr, L_ij = -w/sqrt(d_i d_j) iff both
+ *   > thr; else L_ii = d_i iff d_i > thr, L_ij = -w) and :209-219 (dense ->
+ *   CSR keeps |v| > 1e-9).
+ * Degree summation order in the reference is DashMap iteration order (not
+ * reproducible); here: undirected edges in ascending (min,max) key order.
+ * nnz_ref_out receives the reference's `nnz` counter (pre-filter count).
+ */
+int or_laplacian_max(int64_t n, int64_t n_edges, const int32_t *src,
+                     const int32_t *dst, const float *w, float thr,
+                     int normalize, int64_t cap, int64_t *indptr,
+                     int32_t *indices, float *values, int64_t *nnz_out,
+                     float *degrees, int64_t *nnz_ref_out);
+
+/* ---- K3: energy row reductions ------------------------------------------ */
+
+enum { OR_TAU_FIXED = 0, OR_TAU_MEDIAN = 1, OR_TAU_MEAN = 2, OR_TAU_PERCENTILE = 3 };
+enum { OR_G_TAUMODE = 0, OR_G_ENERGYMAPS = 1 };
+
+/* src_legacy/taumode.rs:29-70 (select_tau; TAU_FLOOR = 1e-10 at :25). */
+double or_select_tau(const double *x, int64_t n, int mode, double param);
+
+/* Per row x (f32 storage widened to f64) of X [n_rows][f] against CSR L
+ * (f x f, f64 values):
+ *  g_mode OR_G_TAUMODE: src_legacy/taumode.rs:261-408
+ *    zero test all |x_t| <= 1e-10 => lambda 0 (:268-274, approx::relative_eq);
+ *    E = rayleigh (:326-361) num = sum_i sum_{j in row i} (x_i*L_ij)*x_j,
+ *        den = sum x^2, E = den > 1e-12 ? max(num/den, 0) : 0
+ *        (reference sums with rayon par_bridge: order nondeterministic; here
+ *        rows ascending, entries ascending);
+ *    G over ordered pairs i != j with w = max(-L_ij,0) > 0 (:366-408);
+ *    tau = select_tau(x); lambda = tau*E/(E+tau) + (1-tau)*clamp(G,0,1).
+ *  g_mode OR_G_ENERGYMAPS: src_legacy/energymaps.rs:923-1045
+ *    E = max(x.(Lx)/x.x, 0) with (Lx)_i = sum_j L_ij x_j (graph.rs:464-501);
+ *    G over j > i only; lambda = E (tau unused, G reported separately).
+ * E, G, lambda: [n_rows] (any may be NULL).
+ */
+int or_energy_rows(const float *X, int64_t n_rows, int32_t f,
+                   const int64_t *indptr, const int32_t *indices,
+                   const double *values, int g_mode, int tau_mode,
+                   double tau_param, int nthreads, double *E, double *G,
+                   double *lambda);
+
+/* src_legacy/core.rs:1341-1354 normalise_lambdas: min = fold(+inf,min),
+ * max = fold(0.0,max), range = max(max-min,1e-9), x' = (x-min)/range. */
+int or_normalise_lambdas(double *lam, int64_t n, double *min_out,
+                         double *max_out, double *range_out);
+
+/* surfface-core/src/spectral/mod.rs:69-181 (compute_lambdas_gpu, f32):
+ * R = clamp(num/(den+1e-9), -1e6, 1e6); W = max(0,-L); deg = W.1;
+ * row = sum_f max(0, deg_f x_f^2 - 2 x_f (Wx)_f + (Wx^2)_f);
+ * D = clamp(row / (sum rows + 1e-12), 0, 1); lambda = R + D.
+ * (Burn matmul summation order is backend-defined: tolerance only.) */
+int or_spectral_lambdas_f32(const float *X, int64_t n, int32_t f,
+                            const int64_t *indptr, const int32_t *indices,
+                            const float *values, float *out);
+
+/* ---- K4: sorted lambda index -------------------------------------------- */
+
+/* src_legacy/sorted_index.rs:22-54: ascending OrderedFloat(lambda) (all NaN
+ * equal and greatest, -0.0 == +0.0), ties by decimal-string id compared as
+ * bytes ("10" < "2").  order_out[r] = idx at rank r; key_out[r] = the
+ * bucket key (first-inserted lambda of the equal class).  std_out (may be
+ * NULL) = laplacian.rs:421-448 std_deviation (f32 arithmetic). */
+int or_sorted_index(const double *lam, int64_t n, int64_t *order_out,
+                    double *key_out, double *std_out);
+
+/* ---- K5: SF-GRASS ------------------------------------------------------- */
+
+/* src_legacy/sparsification.rs:32-113: avg = sum len / n; avg < 10 => copy;
+ * score = w * sqrt((deg_i*deg_j) as f64), sort desc (ties: ascending
+ * position in the input row — the reference's sort_unstable leaves ties
+ * unspecified), keep min(max(ceil(len*ratio),1),len), kept edges returned in
+ * score order. */
+int or_sfgrass(int64_t n, const int64_t *indptr, const int32_t *indices,
+               const double *w, double ratio, int64_t *out_indptr,
+               int32_t *out_indices, double *out_w);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,191 @@
+"""ctypes binding of liboracle.so — TEST INFRASTRUCTURE ONLY.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may
+import this module, and only as the checker / the timed CPU baseline.  The
+product (matternet-rs_amd/, include/matternet_hip.h) never touches it.
+See oracle.h for the reference citations of every function.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB = None
+
+TAU_FIXED, TAU_MEDIAN, TAU_MEAN, TAU_PERCENTILE = 0, 1, 2, 3
+G_TAUMODE, G_ENERGYMAPS = 0, 1
+
+
+def build() -> str:
+    """Compile liboracle.so in place (gcc); returns its path."""
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+    return os.path.join(_HERE, "liboracle.so")
+
+
+def lib() -> C.CDLL:
+    global _LIB
+    if _LIB is None:
+        path = os.path.join(_HERE, "liboracle.so")
+        src = os.path.join(_HERE, "oracle.c")
+        if not os.path.exists(path) or os.path.getmtime(path) < os.path.getmtime(src):
+            build()
+        _LIB = C.CDLL(path)
+        _declare(_LIB)
+    return _LIB
+
+
+P = C.c_void_p
+I64 = C.c_int64
+I32 = C.c_int32
+D = C.c_double
+F = C.c_float
+
+
+def _declare(L):
+    L.or_knn_l2sq_f32.argtypes = [P, I64, I32, I32, I64, I64, C.c_int, C.c_int, P, P]
+    L.or_knn_cos_f64.argtypes = [P, I64, I32, I32, D, D, D, I64, I64, C.c_int, P, P, P]
+    L.or_laplacian_union.argtypes = [I64, I32, P, P, I64, P, P, P, P]
+    L.or_laplacian_max.argtypes = [I64, I64, P, P, P, F, C.c_int, I64, P, P, P, P, P, P]
+    L.or_select_tau.argtypes = [P, I64, C.c_int, D]
+    L.or_select_tau.restype = D
+    L.or_energy_rows.argtypes = [P, I64, I32, P, P, P, C.c_int, C.c_int, D, C.c_int, P, P, P]
+    L.or_normalise_lambdas.argtypes = [P, I64, P, P, P]
+    L.or_spectral_lambdas_f32.argtypes = [P, I64, I32, P, P, P, P]
+    L.or_sorted_index.argtypes = [P, I64, P, P, P]
+    L.or_sfgrass.argtypes = [I64, P, P, P, D, P, P, P]
+
+
+def _p(a):
+    return a.ctypes.data_as(P) if a is not None else None
+
+
+def _check(rc, name):
+    if rc != 0:
+        raise RuntimeError(f"oracle {name} failed with code {rc}")
+
+
+def knn_l2sq(X, k, q_begin=0, q_end=None, mode=1, nthreads=0):
+    X = np.ascontiguousarray(X, dtype=np.float32)
+    n, d = X.shape
+    q_end = n if q_end is None else q_end
+    m = q_end - q_begin
+    idx = np.empty((m, k), np.int32)
+    dist = np.empty((m, k), np.float32)
+    _check(lib().or_knn_l2sq_f32(_p(X), n, d, k, q_begin, q_end, mode, nthreads, _p(idx), _p(dist)),
+           "knn_l2sq")
+    return idx, dist
+
+
+def knn_cos(X, topk, eps=1.0, sigma=1.0, p=2.0, q_begin=0, q_end=None, nthreads=0):
+    X = np.ascontiguousarray(X, dtype=np.float32)
+    n, d = X.shape
+    q_end = n if q_end is None else q_end
+    m = q_end - q_begin
+    idx = np.empty((m, topk), np.int32)
+    dist = np.empty((m, topk), np.float64)
+    w = np.empty((m, topk), np.float64)
+    _check(lib().or_knn_cos_f64(_p(X), n, d, topk, eps, sigma, p, q_begin, q_end, nthreads,
+                                _p(idx), _p(dist), _p(w)), "knn_cos")
+    return idx, dist, w
+
+
+def laplacian_union(nbr_idx, nbr_w):
+    nbr_idx = np.ascontiguousarray(nbr_idx, dtype=np.int32)
+    nbr_w = np.ascontiguousarray(nbr_w, dtype=np.float64)
+    n, k = nbr_idx.shape
+    cap = 2 * n * k + n
+    indptr = np.empty(n + 1, np.int64)
+    indices = np.empty(cap, np.int32)
+    values = np.empty(cap, np.float64)
+    nnz = np.zeros(1, np.int64)
+    _check(lib().or_laplacian_union(n, k, _p(nbr_idx), _p(nbr_w), cap, _p(indptr), _p(indices),
+                                    _p(values), _p(nnz)), "laplacian_union")
+    nz = int(nnz[0])
+    return indptr, indices[:nz].copy(), values[:nz].copy()
+
+
+def laplacian_max(n, src, dst, w, thr=1e-9, normalize=True):
+    src = np.ascontiguousarray(src, dtype=np.int32)
+    dst = np.ascontiguousarray(dst, dtype=np.int32)
+    w = np.ascontiguousarray(w, dtype=np.float32)
+    m = len(src)
+    cap = 2 * m + n
+    indptr = np.empty(n + 1, np.int64)
+    indices = np.empty(cap, np.int32)
+    values = np.empty(cap, np.float32)
+    nnz = np.zeros(1, np.int64)
+    deg = np.empty(n, np.float32)
+    nnz_ref = np.zeros(1, np.int64)
+    _check(lib().or_laplacian_max(n, m, _p(src), _p(dst), _p(w), thr, int(normalize), cap,
+                                  _p(indptr), _p(indices), _p(values), _p(nnz), _p(deg),
+                                  _p(nnz_ref)), "laplacian_max")
+    nz = int(nnz[0])
+    return indptr, indices[:nz].copy(), values[:nz].copy(), deg, int(nnz_ref[0])
+
+
+def select_tau(x, mode, param=0.0):
+    x = np.ascontiguousarray(x, dtype=np.float64)
+    return float(lib().or_select_tau(_p(x), len(x), mode, param))
+
+
+def energy_rows(X, indptr, indices, values, g_mode=G_TAUMODE, tau_mode=TAU_MEDIAN,
+                tau_param=0.0, nthreads=0):
+    X = np.ascontiguousarray(X, dtype=np.float32)
+    n, f = X.shape
+    indptr = np.ascontiguousarray(indptr, dtype=np.int64)
+    indices = np.ascontiguousarray(indices, dtype=np.int32)
+    values = np.ascontiguousarray(values, dtype=np.float64)
+    E = np.empty(n, np.float64)
+    G = np.empty(n, np.float64)
+    lam = np.empty(n, np.float64)
+    _check(lib().or_energy_rows(_p(X), n, f, _p(indptr), _p(indices), _p(values), g_mode,
+                                tau_mode, tau_param, nthreads, _p(E), _p(G), _p(lam)),
+           "energy_rows")
+    return E, G, lam
+
+
+def normalise_lambdas(lam):
+    lam = np.array(lam, dtype=np.float64, copy=True)
+    mn, mx, rg = np.zeros(1), np.zeros(1), np.zeros(1)
+    _check(lib().or_normalise_lambdas(_p(lam), len(lam), _p(mn), _p(mx), _p(rg)), "normalise")
+    return lam, float(mn[0]), float(mx[0]), float(rg[0])
+
+
+def spectral_lambdas(X, indptr, indices, values):
+    X = np.ascontiguousarray(X, dtype=np.float32)
+    n, f = X.shape
+    out = np.empty(n, np.float32)
+    _check(lib().or_spectral_lambdas_f32(
+        _p(X), n, f, _p(np.ascontiguousarray(indptr, np.int64)),
+        _p(np.ascontiguousarray(indices, np.int32)), _p(np.ascontiguousarray(values, np.float32)),
+        _p(out)), "spectral")
+    return out
+
+
+def sorted_index(lam):
+    lam = np.ascontiguousarray(lam, dtype=np.float64)
+    n = len(lam)
+    order = np.empty(n, np.int64)
+    keys = np.empty(n, np.float64)
+    std = np.zeros(1)
+    _check(lib().or_sorted_index(_p(lam), n, _p(order), _p(keys), _p(std)), "sorted_index")
+    return order, keys, float(std[0])
+
+
+def sfgrass(indptr, indices, w, ratio=0.5):
+    indptr = np.ascontiguousarray(indptr, dtype=np.int64)
+    indices = np.ascontiguousarray(indices, dtype=np.int32)
+    w = np.ascontiguousarray(w, dtype=np.float64)
+    n = len(indptr) - 1
+    cap = max(int(indptr[-1]), 1)
+    oi = np.empty(n + 1, np.int64)
+    oj = np.empty(cap, np.int32)
+    ow = np.empty(cap, np.float64)
+    _check(lib().or_sfgrass(n, _p(indptr), _p(indices), _p(w), ratio, _p(oi), _p(oj), _p(ow)),
+           "sfgrass")
+    nz = int(oi[-1])
+    return oi, oj[:nz].copy(), ow[:nz].copy()

@@ -1,0 +1,230 @@
+"""Pin the CPU oracle (oracle/liboracle.so) before trusting it.
+
+* against every known-answer case the reference's own tests assert
+  (tests/golden/reference_known_answers.json, each citing its test file:line);
+* against the independent pure-Python restatement's fixtures
+  (tests/golden/golden_small.npz, made by tests/golden/make_golden.py).
+Bit-exact for integer/index outputs and for the sequential-fold distances;
+1e-12 relative for the f64 energy scalars (same summation order).
+"""
+import json
+import math
+import os
+
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+KA = json.load(open(os.path.join(HERE, "golden", "reference_known_answers.json")))
+GS = np.load(os.path.join(HERE, "golden", "golden_small.npz"))
+
+
+def _num(v):
+    if isinstance(v, str):
+        return {"nan": math.nan, "inf": math.inf, "-inf": -math.inf}[v]
+    return float(v)
+
+
+MODES = {"fixed": O.TAU_FIXED, "median": O.TAU_MEDIAN, "mean": O.TAU_MEAN,
+         "percentile": O.TAU_PERCENTILE}
+
+
+@pytest.mark.parametrize("case", KA["select_tau"], ids=lambda c: c["cite"])
+def test_select_tau_known_answers(case):
+    x = np.array([_num(v) for v in case["x"]], np.float64)
+    got = O.select_tau(x, MODES[case["mode"]], _num(case.get("param", 0.0)))
+    tol = case.get("tol", 0.0)
+    assert abs(got - case["expect"]) <= tol, (got, case)
+
+
+def test_l2sq_known_answers():
+    c = KA["l2sq_distance"]
+    X = np.array([c[0]["a"], c[0]["b"]], np.float32)
+    _, dist = O.knn_l2sq(X, 1)
+    assert abs(dist[0, 0] - c[0]["expect"]) <= c[0]["tol"]
+    X = np.array([c[1]["a"], c[1]["b"]], np.float32)
+    _, dist = O.knn_l2sq(X, 1)
+    assert abs(math.sqrt(dist[0, 0]) - c[1]["expect_sqrt"]) <= c[1]["tol"]
+
+
+def test_cosine_known_answers():
+    for c in KA["cosine"]:
+        X = np.array([c["a"], c["b"]], np.float32)
+        _, dist, _ = O.knn_cos(X, 1, eps=1.0, sigma=1.0, p=2.0)
+        if "expect_cos" in c:
+            assert abs((1.0 - dist[0, 0]) - c["expect_cos"]) <= c["tol"]
+        else:
+            assert abs(dist[0, 0] - c["expect_dist"]) <= c["tol"]
+
+
+def test_knn_line_tie_rule():
+    c = KA["knn_line"]
+    idx, dist = O.knn_l2sq(np.array(c["X"], np.float32), c["k"])
+    assert idx.tolist() == c["expect_idx"]
+    assert dist.tolist() == c["expect_dist"]
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+@pytest.mark.parametrize("name,k", [("l2_uniform", 5), ("l2_clustered", 7), ("l2_grid", 6)])
+def test_knn_l2sq_vs_python_restatement(name, k, mode):
+    idx, dist = O.knn_l2sq(GS[name + "_X"], k, mode=mode)
+    np.testing.assert_array_equal(idx, GS[name + "_idx"])
+    np.testing.assert_array_equal(dist.view(np.uint32), GS[name + "_dist"].view(np.uint32))
+
+
+def test_knn_l2sq_query_range_and_small_n():
+    X = GS["l2_uniform_X"]
+    i_all, d_all = O.knn_l2sq(X, 5)
+    i_sub, d_sub = O.knn_l2sq(X, 5, q_begin=7, q_end=19)
+    np.testing.assert_array_equal(i_sub, i_all[7:19])
+    # k > n-1: reference truncates to min(k, n-1)
+    idx, dist = O.knn_l2sq(X[:3], 5)
+    assert (idx[:, 2:] == -1).all() and np.isinf(dist[:, 2:]).all()
+
+
+def test_knn_l2sq_nonfinite_is_error():
+    X = np.array([[0, 0], [np.nan, 1], [1, 1]], np.float32)
+    with pytest.raises(RuntimeError):
+        O.knn_l2sq(X, 1)
+
+
+def test_knn_cos_vs_python_restatement():
+    idx, dist, w = O.knn_cos(GS["cos_X"], 4, eps=1.0, sigma=1.0, p=2.0)
+    np.testing.assert_array_equal(idx, GS["cos_idx"])
+    np.testing.assert_array_equal(dist, GS["cos_dist"])
+    np.testing.assert_array_equal(w, GS["cos_w"])
+
+
+def test_laplacian_union_vs_python_restatement():
+    ip, ix, iv = O.laplacian_union(GS["cos_idx"], GS["cos_w"])
+    np.testing.assert_array_equal(ip, GS["lapu_indptr"])
+    np.testing.assert_array_equal(ix, GS["lapu_indices"])
+    np.testing.assert_array_equal(iv, GS["lapu_values"])
+
+
+def test_laplacian_d_minus_a_known_answer():
+    c = KA["laplacian_d_minus_a"]
+    X = np.array(c["items"], np.float32)
+    p = c["params"]
+    idx, dist, w = O.knn_cos(X, p["topk"], eps=p["eps"], sigma=p["sigma"], p=p["p"])
+    ip, ix, iv = O.laplacian_union(idx, w)
+    n = X.shape[0]
+    L = np.zeros((n, n))
+    for i in range(n):
+        L[i, ix[ip[i]:ip[i + 1]]] = iv[ip[i]:ip[i + 1]]
+    A = -L.copy()
+    np.fill_diagonal(A, 0.0)
+    assert np.all(np.diag(A) == 0)
+    for i in range(n):
+        assert abs(L[i, i] - A[i].sum()) < 1e-10
+    assert np.allclose(L, L.T, atol=1e-10)
+
+
+def test_energy_taumode_vs_python_restatement():
+    E, G, lam = O.energy_rows(GS["energy_X"], GS["lapu_indptr"], GS["lapu_indices"],
+                              GS["lapu_values"], O.G_TAUMODE, O.TAU_MEDIAN)
+    np.testing.assert_allclose(E, GS["energy_E"], rtol=1e-12, atol=1e-15)
+    np.testing.assert_allclose(G, GS["energy_G"], rtol=1e-12, atol=1e-15)
+    np.testing.assert_allclose(lam, GS["energy_lambda"], rtol=1e-12, atol=1e-15)
+    assert lam[3] == 0.0  # zero-vector path (taumode.rs:268-274)
+
+
+def _csr(Ld):
+    Ld = np.array(Ld, np.float64)
+    ip, ix, iv = [0], [], []
+    for i in range(Ld.shape[0]):
+        for j in range(Ld.shape[1]):
+            if Ld[i, j] != 0:
+                ix.append(j)
+                iv.append(Ld[i, j])
+        ip.append(len(ix))
+    return np.array(ip, np.int64), np.array(ix, np.int32), np.array(iv)
+
+
+@pytest.mark.parametrize("case", KA["rayleigh"], ids=lambda c: c["cite"])
+def test_rayleigh_known_answers(case):
+    ip, ix, iv = _csr(case["L_dense"])
+    X = np.array(case["x"], np.float32)
+    E, G, lam = O.energy_rows(X, ip, ix, iv, O.G_TAUMODE, O.TAU_MEDIAN)
+    assert np.all(np.abs(E - np.array(case["expect_E"])) < case["tol"])
+    spec = O.spectral_lambdas(X, ip, ix, iv.astype(np.float32))
+    if case.get("expect_lambda0_zero"):
+        assert abs(spec[0]) < case["tol"]
+    if case.get("expect_lambda1_gt_lambda0"):
+        assert spec[1] > spec[0]
+
+
+def test_dispersion_constant_rows_known_answer():
+    c = KA["dispersion_constant_rows"]
+    ip, ix, iv = _csr(c["L_dense"])
+    X = np.array(c["x"], np.float32)
+    E, G, _ = O.energy_rows(X, ip, ix, iv, O.G_TAUMODE, O.TAU_MEDIAN)
+    assert np.all(np.abs(G) < c["tol"])
+    # spectral lambda = R + D; the reference asserts the Dirichlet part D == 0
+    spec = O.spectral_lambdas(X, ip, ix, iv.astype(np.float32))
+    assert np.all(np.abs(spec - E) < c["tol"])
+
+
+def test_energymaps_dispersion_is_twice_taumode_shares_relation():
+    # upper-triangle G uses half the pairs; on a symmetric L the
+    # ordered-pair total S is 2x the upper total, each share halves => G_tau = G_em / 2.
+    X = GS["energy_X"]
+    args = (GS["lapu_indptr"], GS["lapu_indices"], GS["lapu_values"])
+    _, Gt, _ = O.energy_rows(X, *args, O.G_TAUMODE, O.TAU_MEDIAN)
+    _, Ge, _ = O.energy_rows(X, *args, O.G_ENERGYMAPS, O.TAU_MEDIAN)
+    nz = Gt > 0
+    np.testing.assert_allclose(Ge[nz], 2.0 * Gt[nz], rtol=1e-9)
+
+
+def test_sorted_index_known_answer_and_restatement():
+    c = KA["sorted_index_ascending"]
+    order, keys, std = O.sorted_index(np.array(c["lambda"]))
+    assert order.tolist() == c["expect_order"]
+    order, keys, _ = O.sorted_index(GS["sort_lambda"])
+    np.testing.assert_array_equal(order, GS["sort_order"])
+
+
+def test_normalise_known_answer():
+    c = KA["normalise_lambdas"]
+    lam, mn, mx, rg = O.normalise_lambdas(c["lambda"])
+    np.testing.assert_allclose(lam, c["expect"], rtol=0, atol=1e-15)
+    assert mx == 0.0 and mn == -3.0
+
+
+def test_sfgrass_known_answers_and_restatement():
+    c = KA["sfgrass_basic"]
+    rows = c["rows"]
+    ip = np.cumsum([0] + [len(r) for r in rows])
+    ix = np.array([j for r in rows for j, _ in r])
+    w = np.array([x for r in rows for _, x in r])
+    oi, oj, ow = O.sfgrass(ip, ix, w)
+    assert len(oi) - 1 == 3 and all(oi[i + 1] > oi[i] for i in range(3))
+    oi, oj, ow = O.sfgrass(GS["sf_in_indptr"], GS["sf_in_indices"], GS["sf_in_w"])
+    np.testing.assert_array_equal(oi, GS["sf_out_indptr"])
+    np.testing.assert_array_equal(oj, GS["sf_out_indices"])
+    np.testing.assert_array_equal(ow, GS["sf_out_w"])
+    assert oi[-1] < GS["sf_in_indptr"][-1]
+
+
+def test_laplacian_max_properties():
+    X = GS["l2_uniform_X"]
+    idx, dist = O.knn_l2sq(X, 5)
+    n, k = idx.shape
+    w = (1.0 / (1.0 + dist)).astype(np.float32)
+    src = np.repeat(np.arange(n), k)
+    ip, ix, iv, deg, nnz_ref = O.laplacian_max(n, src, idx.ravel(), w.ravel(), normalize=True)
+    L = np.zeros((n, n))
+    for i in range(n):
+        L[i, ix[ip[i]:ip[i + 1]]] = iv[ip[i]:ip[i + 1]]
+    assert np.allclose(L, L.T)
+    assert np.allclose(np.diag(L), 1.0)
+    assert (L - np.diag(np.diag(L)) <= 0).all()
+    # null space: L D^{1/2} 1 = 0 (surfface-core tests/test_laplacian.rs invariants)
+    assert np.abs(L @ np.sqrt(deg.astype(np.float64))).max() < 1e-5
+    ip, ix, iv, deg, _ = O.laplacian_max(n, src, idx.ravel(), w.ravel(), normalize=False)
+    L = np.zeros((n, n))
+    for i in range(n):
+        L[i, ix[ip[i]:ip[i + 1]]] = iv[ip[i]:ip[i + 1]]
+    assert np.abs(L.sum(axis=1)).max() < 1e-4
