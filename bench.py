@@ -1,0 +1,205 @@
+"""Headline benchmark: k-NN graph build vector-pairs/sec (BASELINE.json configs[1] /
+configs[3]) on MI355X through the HIP C ABI.
+
+  python bench.py [--gpus N --steps K --warmup W]
+  N>1: python -m torch.distributed.run --nnodes=1 --nproc-per-node N \
+           --master-addr 127.0.0.1 --master-port P bench.py --gpus N ...
+
+One step = one exact kNN graph build (k=32, squared L2, self excluded) over all
+rows: at N=1 the C2 workload (1M x 768 f32), at N GPUs N x 1M rows row-sharded
+(C4 at N=8): every rank keeps its 1M-row corpus shard resident, receives all
+query rows (all-gather over RCCL/xGMI), computes the exact per-shard top-k of
+every query, and the per-shard lists are exchanged (all-to-all) and merged on
+each query's owner rank.  Inputs are generated on device before timing.
+value = N_total^2 vector pairs / max-over-ranks step time.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+for p in (ROOT, os.path.join(ROOT, "matternet-rs_amd"), os.path.join(ROOT, "tests")):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md chip-level table (dense f32 MFMA)
+HBM_PEAK_GBS = 8000.0
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=1)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--rows-per-gpu", type=int, default=1_000_000)
+    ap.add_argument("--dim", type=int, default=768)
+    ap.add_argument("--k", type=int, default=32)
+    ap.add_argument("--seed", type=int, default=42)
+    ap.add_argument("--cpu-seconds", type=float, default=15.0,
+                    help="target CPU time of the sampled cpu_baseline leg (0 = skip)")
+    ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_gram_latest.json"),
+                    help="PMC-derived HBM bytes per launch of the Gram kernel (optional)")
+    return ap.parse_args()
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != a.gpus:
+        if world == 1 and a.gpus > 1:
+            raise SystemExit("--gpus N>1 must be launched with torch.distributed.run")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=dev)
+
+    import surfface_hip as S
+    from surfface_hip import _lib
+    L = _lib.lib()
+
+    n_loc, d, k = a.rows_per_gpu, a.dim, a.k
+    n_tot = n_loc * world
+    X = torch.empty((n_loc, d), dtype=torch.float32, device=dev)
+    stream = torch.cuda.current_stream(dev)
+    _lib.check(L.mn_fill_uniform_f32(X.data_ptr(), n_loc, d, a.seed, rank * n_loc,
+                                     stream.cuda_stream))
+    if world > 1:
+        Xall = torch.empty((n_tot, d), dtype=torch.float32, device=dev)
+        dist.all_gather_into_tensor(Xall, X)
+        recv_i = torch.empty((world, n_loc, k), dtype=torch.int32, device=dev)
+        recv_d = torch.empty((world, n_loc, k), dtype=torch.float32, device=dev)
+    torch.cuda.synchronize()
+
+    gram_ms = []
+
+    def step():
+        if world == 1:
+            r = S.knn_l2sq(X, k, timing=True)
+            gram_ms.append(r.stats["ms_gram"])
+            return r.idx, r.dist, r.stats
+        # per-shard exact top-k of ALL queries against this rank's corpus shard
+        r = S.knn_l2sq_qc(Xall, X, k, q_offset=0, c_offset=rank * n_loc, timing=True)
+        gram_ms.append(r.stats["ms_gram"])
+        # owner of query rows [j*n_loc, (j+1)*n_loc) is rank j: all-to-all the lists
+        dist.all_to_all_single(recv_i.view(world, -1), r.idx.view(world, -1))
+        dist.all_to_all_single(recv_d.view(world, -1), r.dist.view(world, -1))
+        idx, dd = S.merge_parts(recv_i, recv_d)
+        return idx, dd, r.stats
+
+    for _ in range(a.warmup):
+        step()
+    gram_ms.clear()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    out = None
+    for _ in range(a.steps):
+        out = step()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    if dist:
+        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    ms_step = el * 1e3 / a.steps
+    pairs = float(n_tot) * float(n_tot)
+    value = pairs * a.steps / el
+
+    # roofline of the dominant kernel (k_gram_topk): algorithmic flops per launch
+    # = 2 * nq * nc_shard * d (full Gram); duration from HIP
+    # events recorded on the launch stream inside the library.
+    nq = n_tot
+    flops_launch = 2.0 * nq * n_loc * d
+    gms = float(np.mean(gram_ms)) if gram_ms else float("nan")
+    achieved = flops_launch / (gms * 1e-3) / 1e12
+    traffic = None
+    if os.path.exists(a.pmc_json):
+        try:
+            pm = json.load(open(a.pmc_json))
+            if pm.get("rows_per_gpu") == n_loc and pm.get("dim") == d and world == 1:
+                traffic = pm.get("hbm_bytes_per_launch")
+        except (OSError, ValueError):
+            traffic = None
+    roof = {"bound": "mfma", "kernel": "k_gram_topk", "achieved": round(achieved, 3),
+            "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+            "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": traffic,
+            "ms_per_launch": round(gms, 3), "flop_per_launch": flops_launch}
+
+    cpu = None
+    parity = None
+    if rank == 0 and world == 1 and a.cpu_seconds > 0:
+        cpu, parity = cpu_baseline(X, out[0], out[1], k, a.cpu_seconds)
+
+    if rank == 0:
+        st = out[2]
+        line = {
+            "metric": "vector-pairs/sec for k-NN graph build (N=1M, d=768) + Laplacian energy rows/sec",
+            "value": value, "unit": "pairs/s", "n_gpus": world, "steps": a.steps,
+            "warmup": a.warmup, "ms_per_step": round(ms_step, 3), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic U[-1,1) f32 (splitmix64 counter stream, seed 42), generated on device",
+            "config": {"workload": ("C2: 1M x 768 f32 exact kNN k=32" if world == 1 else
+                                    f"C4-style: {n_tot} x {d} f32 exact kNN k={k}, row-sharded"),
+                       "n_rows": n_tot, "dim": d, "k": k, "rows_per_gpu": n_loc,
+                       "metric_space": "squared L2 (reference sequential f32 fold)",
+                       "parallelism": f"corpus row-shard x{world} + RCCL all-gather/all-to-all"},
+            "roofline": roof,
+            "cpu_baseline": cpu,
+            "parity_sample": parity,
+            "knn_stats": {"uncertified_rows": st["n_uncertified"], "slices": st["slices"],
+                          "list_len": st["list_len"], "ms_norms": st["ms_norms"],
+                          "ms_gram": st["ms_gram"], "ms_rerank": st["ms_rerank"],
+                          "ms_fallback": st["ms_fallback"]},
+        }
+        print(json.dumps(line), flush=True)
+    if dist:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def cpu_baseline(X, idx, dd, k, target_s):
+    """Oracle (C restatement, OpenMP) timed on the host on a bounded sample of
+    query rows against the full corpus; also a free bit-exact parity check of
+    those rows against the GPU result."""
+    from oracle import oracle as O
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+    Xh = X.cpu().numpy()
+    n = Xh.shape[0]
+    rng = np.random.default_rng(1)
+    cal = np.sort(rng.choice(n, threads, replace=False))
+    t0 = time.perf_counter()
+    i0, d0 = O.knn_l2sq_rows(Xh, k, cal, nthreads=threads)
+    tc = time.perf_counter() - t0
+    m = int(max(threads, min(4096, threads * round(target_s / max(tc, 1e-3)))))
+    rows = np.sort(rng.choice(n, m, replace=False))
+    t0 = time.perf_counter()
+    ri, rd = O.knn_l2sq_rows(Xh, k, rows, nthreads=threads)
+    el = time.perf_counter() - t0
+    gi = idx.cpu().numpy()[rows]
+    gd = dd.cpu().numpy()[rows]
+    ok = int(np.sum(np.all(gi == ri, axis=1) & np.all(gd.view(np.uint32) == rd.view(np.uint32),
+                                                       axis=1)))
+    cpu = {"value": m * (n - 1) / el, "unit": "pairs/s", "cores": threads, "kind": "port",
+           "sample": f"{m} random query rows x {n} corpus rows, d={Xh.shape[1]}, k={k} "
+                     f"(oracle/or_knn_l2sq_rows_f32, OpenMP), {el:.1f}s"}
+    parity = {"rows_checked": m, "rows_bit_exact": ok, "plus_calibration_rows": threads,
+              "calibration_bit_exact": bool(np.array_equal(i0, idx.cpu().numpy()[cal]))}
+    return cpu, parity
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,116 @@
+/*
+ * matternet_hip.h — C ABI of the MI355X-native (gfx950) surfface hot path.
+ *
+ * The reference (tuned-org-uk/matternet-rs, crate `surfface`) has no FFI of its
+ * own (surfface-py/src/main.rs:1-3 is a hello-world; no extern "C" anywhere).
+ * Its de-facto operator API for this path is the set of Rust functions listed
+ * in SURVEY.md §8(b); each entry point below names the reference function it
+ * replaces (file:line).  INTEGRATION.md shows the `extern "C"` block a Rust
+ * `matternet-hip-sys` crate would declare to bind exactly these symbols.
+ *
+ * Conventions
+ *  - Plain C: pointers + sizes, no torch / HIP types in signatures
+ *    (`stream` is an opaque hipStream_t, NULL = the legacy default stream).
+ *  - Array arguments are DEVICE pointers (HBM) unless a comment says "host".
+ *    mn_device_alloc/mn_memcpy_* are provided for callers without a HIP
+ *    runtime of their own.
+ *  - Every call is synchronous with respect to its stream on return (so the
+ *    error code is final) and reentrant across threads; per-thread error text
+ *    via mn_last_error().
+ *  - Return value: MN_OK (0) or a negative MN_E* code.  The reference panics
+ *    (assert!/partial_cmp().unwrap()) where these return errors.
+ *  - Indices are int32 (graphs up to 2^31-1 nodes), CSR row pointers int64.
+ */
+#ifndef MATTERNET_HIP_H
+#define MATTERNET_HIP_H
+#include <stddef.h>
+#include <stdint.h>
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MN_OK 0
+#define MN_EINVAL (-1)     /* bad argument (reference: assert!/panic)          */
+#define MN_ENOMEM (-2)     /* device allocation failed                          */
+#define MN_ENONFINITE (-3) /* NaN/inf input (reference: partial_cmp().unwrap()) */
+#define MN_ECAP (-4)       /* output capacity too small (nnz_out holds need)   */
+#define MN_EHIP (-5)       /* HIP runtime error                                 */
+#define MN_ENOTSUP (-6)    /* unsupported parameter combination                 */
+
+/* ---------------------------------------------------------------------- */
+/* Library / memory plumbing                                              */
+/* ---------------------------------------------------------------------- */
+int mn_version(void);                 /* 100*major + minor                  */
+const char *mn_last_error(void);      /* thread-local, valid until next call */
+int mn_device_alloc(size_t bytes, void **out);
+int mn_device_free(void *p);
+int mn_memcpy_h2d(void *dst_dev, const void *src_host, size_t bytes, void *stream);
+int mn_memcpy_d2h(void *dst_host, const void *src_dev, size_t bytes, void *stream);
+int mn_stream_synchronize(void *stream);
+
+/* Synthetic input generator, identical to tests/datagen.py:
+ * X[r][c] = 2*((splitmix64(seed ^ ((row0+r)*d + c)) >> 40) * 2^-24) - 1. */
+int mn_fill_uniform_f32(float *X, int64_t n, int32_t d, uint64_t seed,
+                        int64_t row0, void *stream);
+
+/* ---------------------------------------------------------------------- */
+/* K1 — brute-force kNN (Gram on MFMA + LDS top-k + exact re-rank)        */
+/* ---------------------------------------------------------------------- */
+enum mn_metric {
+    MN_L2SQ = 0,     /* surfface-core/src/distance.rs:206-213 (f32 fold)     */
+    MN_COS_RECT = 1  /* src_legacy/tests/test_helpers.rs:77-126 (f64)        */
+};
+
+typedef struct mn_knn_opts {
+    int32_t k;            /* neighbours per row; rows get min(k, n-1) (mst.rs:317) */
+    int32_t metric;       /* enum mn_metric                                        */
+    int32_t exclude_self; /* 1 = the reference behaviour (mst.rs:336 j != i)       */
+    int32_t margin;       /* candidate margin m (list length L = k + m); 0 => 16   */
+    int32_t timing;       /* 1 = record per-kernel HIP-event times in mn_knn_stats */
+    int32_t reserved0;
+    void *stream;         /* hipStream_t or NULL                                   */
+} mn_knn_opts;
+
+typedef struct mn_knn_stats {
+    int64_t n_queries;
+    int64_t n_uncertified;  /* rows resolved by the exact fallback scan         */
+    int32_t slices;         /* corpus split factor used                         */
+    int32_t list_len;       /* L = k + margin                                   */
+    float ms_norms, ms_gram, ms_rerank, ms_fallback, ms_total; /* timing == 1   */
+} mn_knn_stats;
+
+/* Self kNN over the rows of X [n][d] f32 (device, row-major): replaces
+ * MSTStage::build_candidate_graph's kNN (surfface-core/src/mst.rs:312-363,
+ * DistanceMetric::SquaredEuclidean) and the brute-force kNN inside
+ * build_laplacian_matrix / topk_by_l2 (src_legacy/laplacian.rs:205-294,
+ * energymaps.rs:875-892).  Output row i: out_idx[i*k + r], out_dist[i*k + r]
+ * in (dist asc, idx asc) order — bit-identical to the reference's sequential
+ * f32 fold and stable sort.  Slots beyond min(k, n-1): idx -1, dist +inf.
+ * metric must be MN_L2SQ (cosine: mn_knn_cos_f32 / mn_knn_cos_bf16). */
+int mn_knn_f32(const float *X, int64_t n, int32_t d, const mn_knn_opts *opts,
+               int32_t *out_idx, float *out_dist);
+
+/* Queries Q [nq][d] against a corpus C [nc][d] (both device).  Global ids:
+ * query i is q_offset+i, corpus row j is c_offset+j; out_idx holds global
+ * corpus ids; exclude_self drops pairs with equal global id.  This is the
+ * per-shard primitive of the row-sharded multi-GPU build:
+ * the result is the EXACT per-shard top-k, so merging shards with
+ * mn_knn_merge is exact. */
+int mn_knn_f32_qc(const float *Q, int64_t nq, const float *C, int64_t nc,
+                  int32_t d, int64_t q_offset, int64_t c_offset,
+                  const mn_knn_opts *opts, int32_t *out_idx, float *out_dist);
+
+/* Merge `parts` exact per-shard lists per query (each [nq][k], device,
+ * parts-major: part p row i at (p*nq + i)*k) into the global top-k by
+ * (dist asc, idx asc).  idx < 0 entries are empty. */
+int mn_knn_merge_f32(const int32_t *part_idx, const float *part_dist,
+                     int32_t parts, int64_t nq, int32_t k, int32_t *out_idx,
+                     float *out_dist, void *stream);
+
+/* Statistics of the calling thread's last mn_knn_* call. */
+int mn_knn_last_stats(mn_knn_stats *out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MATTERNET_HIP_H */

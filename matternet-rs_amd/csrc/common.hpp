@@ -1,0 +1,133 @@
+// common.hpp — shared plumbing for the matternet HIP library (gfx950 only).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdarg>
+#include <cstdint>
+#include <cstdio>
+
+#include "matternet_hip.h"
+
+namespace mn {
+
+// Thread-local error text behind mn_last_error().
+void set_error(const char *fmt, ...);
+void clear_error();
+
+// Grow-only device scratch, one set of slots per (thread, device).  Growing
+// frees the old block (hipFree synchronises), so never call it while kernels
+// that use that slot are in flight on another stream of this thread.
+void *scratch(int slot, size_t bytes);
+
+enum ScratchSlot {
+    kSlotNorms = 0,
+    kSlotNorms2,
+    kSlotFlags,
+    kSlotLists,
+    kSlotListMeta,
+    kSlotFallback,
+    kSlotGeneric0,
+    kSlotGeneric1,
+    kSlotGeneric2,
+    kSlotGeneric3,
+    kNumSlots
+};
+
+// Per-call HIP-event timer (active only when requested).
+struct Timer {
+    bool on = false;
+    hipStream_t s = nullptr;
+    hipEvent_t ev[8] = {};
+    int n = 0;
+    void start(bool enable, hipStream_t stream);
+    void mark();               // records the next event
+    float ms(int a, int b);    // elapsed between marks a and b (after sync)
+    ~Timer();
+};
+
+}  // namespace mn
+
+#define MN_HIP_TRY(expr)                                                        \
+    do {                                                                        \
+        hipError_t _e = (expr);                                                 \
+        if (_e != hipSuccess) {                                                 \
+            mn::set_error("%s failed: %s (%s:%d)", #expr, hipGetErrorString(_e),\
+                          __FILE__, __LINE__);                                  \
+            return MN_EHIP;                                                     \
+        }                                                                       \
+    } while (0)
+
+#define MN_REQUIRE(cond, code, ...)                                             \
+    do {                                                                        \
+        if (!(cond)) {                                                          \
+            mn::set_error(__VA_ARGS__);                                         \
+            return (code);                                                      \
+        }                                                                       \
+    } while (0)
+
+// ---- device helpers ------------------------------------------------------
+
+namespace mn {
+
+// (dist, idx) lexicographic total order used by every selection in the path:
+// the reference's stable sort by distance over ascending j (mst.rs:344).
+__device__ __forceinline__ bool key_less(float da, int ia, float db, int ib) {
+    return da < db || (da == db && ia < ib);
+}
+__device__ __forceinline__ bool key_less(double da, int ia, double db, int ib) {
+    return da < db || (da == db && ia < ib);
+}
+
+// Bitonic sort of 64*NR (key, idx) pairs held one per lane per register:
+// element e = lane + 64*r.  Ascending by (key, idx).  Whole wave must call.
+template <int NR, typename T>
+__device__ __forceinline__ void wave_bitonic_sort(T (&d)[NR], int (&ix)[NR]) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int k = 2; k <= 64 * NR; k <<= 1) {
+#pragma unroll
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            if (j >= 64) {
+#pragma unroll
+                for (int r = 0; r < NR; ++r) {
+                    const int pr = r ^ (j >> 6);
+                    if (pr > r) {
+                        const int e = lane + 64 * r;
+                        const bool asc = (e & k) == 0;
+                        const bool sw = asc ? key_less(d[pr], ix[pr], d[r], ix[r])
+                                            : key_less(d[r], ix[r], d[pr], ix[pr]);
+                        if (sw) {
+                            T td = d[r]; d[r] = d[pr]; d[pr] = td;
+                            int ti = ix[r]; ix[r] = ix[pr]; ix[pr] = ti;
+                        }
+                    }
+                }
+            } else {
+#pragma unroll
+                for (int r = 0; r < NR; ++r) {
+                    const int e = lane + 64 * r;
+                    const T pd = __shfl_xor(d[r], j);
+                    const int pi = __shfl_xor(ix[r], j);
+                    const bool asc = (e & k) == 0;
+                    const bool lower = (e & j) == 0;
+                    const bool keep_min = (asc == lower);
+                    const bool take = keep_min ? key_less(pd, pi, d[r], ix[r])
+                                               : key_less(d[r], ix[r], pd, pi);
+                    if (take) { d[r] = pd; ix[r] = pi; }
+                }
+            }
+        }
+    }
+}
+
+// Read element `pos` of a register-distributed array (wave-uniform pos).
+template <int NR, typename T>
+__device__ __forceinline__ T wave_elem(const T (&d)[NR], int pos) {
+    const int r = pos >> 6, l = pos & 63;
+    T v = d[0];
+#pragma unroll
+    for (int q = 1; q < NR; ++q) if (q == r) v = d[q];
+    return __shfl(v, l);
+}
+
+}  // namespace mn

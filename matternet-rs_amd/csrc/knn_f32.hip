@@ -1,0 +1,708 @@
+// knn_f32.hip — K1: brute-force L2^2 kNN on gfx950, bit-exact vs the reference.
+//
+// Reference semantics (what the output must equal, bit for bit):
+//   surfface-core/src/distance.rs:206-213  d(a,b) = sequential f32 fold of
+//       (a_t - b_t)^2, no FMA;
+//   surfface-core/src/mst.rs:330-360       for every row i, all j != i, stable
+//       sort by d (=> ties by ascending j), keep min(k, n-1).
+//
+// MI355X design:
+//   1. k_row_norms      one wave per row: ||x||^2 (f32), max corpus norm,
+//                       non-finite input flag (reference panics on NaN).
+//   2. k_gram_topk      candidate generation.  A 128-query x 256-corpus tile of
+//                       the Gram matrix on MFMA v_mfma_f32_16x16x4_f32 (exact
+//                       f32 products, f32 accumulate), operands staged through
+//                       LDS (register staging, double buffer, padded rows =>
+//                       conflict-free ds_read_b128).  The epilogue forms
+//                       d~ = |q|^2 + |c|^2 - 2 q.c and filters it against a
+//                       per-query threshold tau (the current L-th best);
+//                       survivors go to an LDS queue per query; a full queue is
+//                       merged into the query's sorted top-L list (global
+//                       memory, wave-wide bitonic sort).  The N x N matrix is
+//                       never materialised.
+//   3. k_rerank         one wave per query: the L (x slices) candidates are
+//                       re-ranked with the REFERENCE arithmetic (sequential f32
+//                       fold, contraction off: the library is compiled with
+//                       -ffp-contract=off), sorted by (dist, idx) and
+//                       certified: every non-candidate has d~ >= tau_L, and
+//                       |d~ - d| <= delta = 2(4d+16)u(|q|^2 + max|c|^2), so
+//                       tau_L - delta > D_k proves the top-k is exact.
+//   4. k_fallback       uncertified rows (massive exact ties, overflow) are
+//                       recomputed by an exact brute-force scan.
+#include <algorithm>
+#include <climits>
+
+#include "common.hpp"
+
+namespace mn {
+namespace knn {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int BM = 128;             // query rows per block (8 waves x 16 rows)
+constexpr int BN = 256;             // corpus rows per tile (16 column tiles of 16)
+constexpr int BK = 16;              // feature depth per LDS stage
+constexpr int LDK = BK + 8;         // padded row stride (floats, 96 B): conflict-free b128 reads
+constexpr int NWAVES = 8;
+constexpr int NT = 64 * NWAVES;
+constexpr int NCT = BN / 16;        // column tiles per corpus tile
+constexpr int QCAP = 48;            // LDS candidate queue per query
+constexpr int QPRE = QCAP - 16;     // merge before a column tile if cnt > QPRE
+constexpr int LMAX = 128 - QCAP;    // L + QCAP <= 128 (two elements per lane)
+constexpr int KMAX = 64;            // k limit (fallback keeps k per thread in LDS)
+constexpr int FB_THREADS = 128;
+
+struct alignas(16) GramSmem {
+    float A[2][BM][LDK];
+    float B[2][BN][LDK];
+    float qd[BM][QCAP];
+    int qi[BM][QCAP];
+    float cn[2][BN];
+    float qn[BM];
+    float tau[BM];
+    int cnt[BM];
+    int lsz[BM];
+};
+
+// ---------------------------------------------------------------------------
+// 1. row norms + input validation
+// ---------------------------------------------------------------------------
+template <bool VEC4>
+__global__ __launch_bounds__(256) void k_row_norms(const float *__restrict__ X, int64_t n,
+                                                   int d, float *__restrict__ nrm,
+                                                   unsigned *__restrict__ maxbits,
+                                                   int *__restrict__ nonfinite) {
+    const int lane = threadIdx.x & 63;
+    const int64_t wave0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+    for (int64_t row = wave0; row < n; row += nwaves) {
+        const float *p = X + row * (int64_t)d;
+        float s = 0.f;
+        bool bad = false;
+        if (VEC4) {
+            for (int t = lane * 4; t < d; t += 256) {
+                const float4 v = *reinterpret_cast<const float4 *>(p + t);
+                s = __builtin_fmaf(v.x, v.x, s);
+                s = __builtin_fmaf(v.y, v.y, s);
+                s = __builtin_fmaf(v.z, v.z, s);
+                s = __builtin_fmaf(v.w, v.w, s);
+                bad |= !(__builtin_isfinite(v.x) && __builtin_isfinite(v.y) &&
+                         __builtin_isfinite(v.z) && __builtin_isfinite(v.w));
+            }
+        } else {
+            for (int t = lane; t < d; t += 64) {
+                const float v = p[t];
+                s = __builtin_fmaf(v, v, s);
+                bad |= !__builtin_isfinite(v);
+            }
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+        const bool anybad = __any(bad);
+        if (lane == 0) {
+            nrm[row] = s;
+            if (anybad) atomicOr(nonfinite, 1);
+            atomicMax(maxbits, __builtin_isfinite(s) ? __float_as_uint(s) : 0x7f800000u);
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// 2. Gram (MFMA) + threshold filter + per-query top-L lists
+// ---------------------------------------------------------------------------
+template <bool VEC4>
+__device__ __forceinline__ float4 load4(const float *__restrict__ X, int64_t row, int64_t nrows,
+                                        int d, int k) {
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (row >= nrows) return v;
+    const float *p = X + row * (int64_t)d + k;
+    if (VEC4) {
+        if (k < d) v = *reinterpret_cast<const float4 *>(p);
+    } else {
+        if (k + 0 < d) v.x = p[0];
+        if (k + 1 < d) v.y = p[1];
+        if (k + 2 < d) v.z = p[2];
+        if (k + 3 < d) v.w = p[3];
+    }
+    return v;
+}
+
+// Merge the LDS queue of `row` into its sorted top-L list (global).  Wave-wide.
+__device__ __forceinline__ void merge_row(GramSmem &sm, int row, int L, float *__restrict__ ld,
+                                          int *__restrict__ li) {
+    const int lane = threadIdx.x & 63;
+    const int s = sm.lsz[row];
+    const int c = sm.cnt[row];
+    float d[2];
+    int ix[2];
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+        const int e = lane + 64 * r;
+        if (e < s) {
+            d[r] = ld[e];
+            ix[r] = li[e];
+        } else if (e < s + c) {
+            d[r] = sm.qd[row][e - s];
+            ix[r] = sm.qi[row][e - s];
+        } else {
+            d[r] = __builtin_inff();
+            ix[r] = INT_MAX;
+        }
+    }
+    wave_bitonic_sort<2>(d, ix);
+    const int ns = min(L, s + c);
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+        const int e = lane + 64 * r;
+        if (e < ns) {
+            ld[e] = d[r];
+            li[e] = ix[r];
+        }
+    }
+    const float tl = wave_elem<2>(d, L - 1);
+    __builtin_amdgcn_wave_barrier();
+    if (lane == 0) {
+        sm.lsz[row] = ns;
+        sm.cnt[row] = 0;
+        sm.tau[row] = (ns == L) ? tl : __builtin_inff();
+    }
+    __builtin_amdgcn_wave_barrier();
+}
+
+template <bool VEC4>
+__global__ __launch_bounds__(NT) void k_gram_topk(
+    const float *__restrict__ Q, int64_t nq, const float *__restrict__ C, int64_t nc, int d,
+    int64_t q_off, int64_t c_off, int excl, const float *__restrict__ qnrm,
+    const float *__restrict__ cnrm, int L, int S, int64_t chunk, float *__restrict__ list_d,
+    int *__restrict__ list_i, int *__restrict__ out_lsz, float *__restrict__ out_tau) {
+    __shared__ GramSmem sm;
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int w = tid >> 6;
+    const int g = lane >> 4;   // MFMA row group (C/D: row = 4g + reg)
+    const int cl = lane & 15;  // MFMA column within a 16-wide tile
+    const int64_t q0 = (int64_t)blockIdx.x * BM;
+    const int sl = blockIdx.y;
+    const int64_t cbeg = (int64_t)sl * chunk;
+    const int64_t cend = min(nc, cbeg + chunk);
+
+    for (int r = tid; r < BM; r += NT) {
+        sm.qn[r] = (q0 + r < nq) ? qnrm[q0 + r] : 0.f;
+        sm.tau[r] = __builtin_inff();
+        sm.cnt[r] = 0;
+        sm.lsz[r] = 0;
+    }
+    __syncthreads();
+
+    const int nk = (d + BK - 1) / BK;
+    // staging map: A = 128 rows x 4 float4 (1 per thread), B = 256 x 4 (2 per thread)
+    const int a_row = tid >> 2, a_c4 = tid & 3;
+    int tile_par = 0;
+
+    for (int64_t c0 = cbeg; c0 < cend; c0 += BN, tile_par ^= 1) {
+        if (tid < BN) sm.cn[tile_par][tid] = (c0 + tid < cend) ? cnrm[c0 + tid] : 0.f;
+
+        f32x4 acc[NCT];
+#pragma unroll
+        for (int t = 0; t < NCT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+        float4 ra, rb0, rb1;
+        ra = load4<VEC4>(Q, q0 + a_row, nq, d, 4 * a_c4);
+        rb0 = load4<VEC4>(C, c0 + a_row, cend, d, 4 * a_c4);
+        rb1 = load4<VEC4>(C, c0 + 128 + a_row, cend, d, 4 * a_c4);
+        *reinterpret_cast<float4 *>(&sm.A[0][a_row][4 * a_c4]) = ra;
+        *reinterpret_cast<float4 *>(&sm.B[0][a_row][4 * a_c4]) = rb0;
+        *reinterpret_cast<float4 *>(&sm.B[0][128 + a_row][4 * a_c4]) = rb1;
+        __syncthreads();
+
+        for (int kt = 0; kt < nk; ++kt) {
+            const int cur = kt & 1;
+            const bool more = kt + 1 < nk;
+            if (more) {
+                const int k = (kt + 1) * BK + 4 * a_c4;
+                ra = load4<VEC4>(Q, q0 + a_row, nq, d, k);
+                rb0 = load4<VEC4>(C, c0 + a_row, cend, d, k);
+                rb1 = load4<VEC4>(C, c0 + 128 + a_row, cend, d, k);
+            }
+            const float4 a = *reinterpret_cast<const float4 *>(&sm.A[cur][16 * w + cl][4 * g]);
+#pragma unroll
+            for (int t = 0; t < NCT; ++t) {
+                const float4 b = *reinterpret_cast<const float4 *>(&sm.B[cur][16 * t + cl][4 * g]);
+                acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, b.x, acc[t], 0, 0, 0);
+                acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, b.y, acc[t], 0, 0, 0);
+                acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.z, b.z, acc[t], 0, 0, 0);
+                acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.w, b.w, acc[t], 0, 0, 0);
+            }
+            if (more) {
+                *reinterpret_cast<float4 *>(&sm.A[cur ^ 1][a_row][4 * a_c4]) = ra;
+                *reinterpret_cast<float4 *>(&sm.B[cur ^ 1][a_row][4 * a_c4]) = rb0;
+                *reinterpret_cast<float4 *>(&sm.B[cur ^ 1][128 + a_row][4 * a_c4]) = rb1;
+            }
+            __syncthreads();
+        }
+
+        // ---- epilogue: filter + queue + merge (this wave's 16 rows only) ----
+#pragma unroll 1
+        for (int t = 0; t < NCT; ++t) {
+            {   // pre-merge rows that could overflow while taking 16 more candidates
+                const int myrow = 16 * w + cl;
+                const int c = sm.cnt[myrow];
+                uint64_t need = __ballot(lane < 16 && c > QPRE);
+                while (need) {
+                    const int rr = __builtin_ctzll(need);
+                    need &= need - 1;
+                    const int row = 16 * w + rr;
+                    const int64_t base = ((q0 + row) * S + sl) * (int64_t)L;
+                    merge_row(sm, row, L, list_d + base, list_i + base);
+                }
+            }
+            f32x4 curv;
+            switch (t) {
+#define MN_CASE(T) case T: curv = acc[T]; break;
+                MN_CASE(0) MN_CASE(1) MN_CASE(2) MN_CASE(3) MN_CASE(4) MN_CASE(5) MN_CASE(6)
+                MN_CASE(7) MN_CASE(8) MN_CASE(9) MN_CASE(10) MN_CASE(11) MN_CASE(12)
+                MN_CASE(13) MN_CASE(14) MN_CASE(15)
+#undef MN_CASE
+                default: curv = acc[0];
+            }
+            const int64_t col = c0 + 16 * t + cl;
+            const bool colok = col < cend;
+            const float cv = sm.cn[tile_par][16 * t + cl];
+            const int64_t gcol = c_off + col;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int lrow = 16 * w + 4 * g + i;
+                const int64_t q = q0 + lrow;
+                const float tv = sm.tau[lrow];
+                const float dd = __builtin_fmaf(-2.f, curv[i], sm.qn[lrow] + cv);
+                const bool valid = colok && (q < nq) && !(excl && (q_off + q) == gcol);
+                const bool pass = valid && (dd < tv);
+                const uint64_t m = __ballot(pass);
+                if (m) {
+#pragma unroll
+                    for (int gg = 0; gg < 4; ++gg) {
+                        const uint32_t mg = (uint32_t)(m >> (16 * gg)) & 0xFFFFu;
+                        if (!mg) continue;
+                        const int row = 16 * w + 4 * gg + i;
+                        const int c = sm.cnt[row];
+                        if (g == gg && pass) {
+                            const int pos = c + __popc(mg & ((1u << cl) - 1u));
+                            sm.qd[row][pos] = dd;
+                            sm.qi[row][pos] = (int)gcol;
+                        }
+                        __builtin_amdgcn_wave_barrier();
+                        if (lane == 0) sm.cnt[row] = c + __popc(mg);
+                        __builtin_amdgcn_wave_barrier();
+                    }
+                }
+            }
+        }
+    }
+
+    // ---- flush the queues, publish list sizes and thresholds ----
+    for (int rr = 0; rr < 16; ++rr) {
+        const int row = 16 * w + rr;
+        if (sm.cnt[row] > 0) {
+            const int64_t base = ((q0 + row) * S + sl) * (int64_t)L;
+            merge_row(sm, row, L, list_d + base, list_i + base);
+        }
+    }
+    if (lane < 16) {
+        const int row = 16 * w + lane;
+        const int64_t q = q0 + row;
+        if (q < nq) {
+            out_lsz[q * S + sl] = sm.lsz[row];
+            out_tau[q * S + sl] = sm.tau[row];
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// 3. exact re-rank + certification
+// ---------------------------------------------------------------------------
+
+// The reference fold (distance.rs:206-213): acc starts at -0.0 and adds each
+// (a-b)^2 in feature order; -ffp-contract=off keeps mul and add separate.
+template <bool VEC4>
+__device__ __forceinline__ float exact_l2sq(const float *__restrict__ a,
+                                            const float *__restrict__ b, int d) {
+    float acc = -0.0f;
+    if (VEC4) {
+        const float4 *a4 = reinterpret_cast<const float4 *>(a);
+        const float4 *b4 = reinterpret_cast<const float4 *>(b);
+        for (int t = 0; t < (d >> 2); ++t) {
+            const float4 x = a4[t], y = b4[t];
+            float df = x.x - y.x; acc = acc + df * df;
+            df = x.y - y.y; acc = acc + df * df;
+            df = x.z - y.z; acc = acc + df * df;
+            df = x.w - y.w; acc = acc + df * df;
+        }
+    } else {
+        for (int t = 0; t < d; ++t) {
+            const float df = a[t] - b[t];
+            acc = acc + df * df;
+        }
+    }
+    return acc;
+}
+
+template <int NR, bool VEC4>
+__global__ __launch_bounds__(256) void k_rerank(
+    const float *__restrict__ Q, int64_t nq, const float *__restrict__ C, int64_t nc, int d,
+    int64_t c_off, const float *__restrict__ qnrm, const unsigned *__restrict__ cmax_bits,
+    int S, int L, const float *__restrict__ list_d, const int *__restrict__ list_i,
+    const int *__restrict__ lsz, const float *__restrict__ ltau, int k, float cert_c,
+    int32_t *__restrict__ out_idx, float *__restrict__ out_dist, int *__restrict__ fb_count,
+    int *__restrict__ fb_list) {
+    (void)list_d;
+    (void)nc;
+    const int lane = threadIdx.x & 63;
+    const int64_t q = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (q >= nq) return;
+    float dd[NR];
+    int ix[NR];
+    int M = 0;
+    float G = __builtin_inff();
+    for (int s = 0; s < S; ++s) {
+        const int sz = lsz[q * S + s];
+        if (sz >= L) G = fminf(G, ltau[q * S + s]);
+#pragma unroll
+        for (int r = 0; r < NR; ++r) {
+            const int e = lane + 64 * r;
+            if (s == 0) ix[r] = -1;
+            if (e >= M && e < M + sz) ix[r] = list_i[(q * S + s) * (int64_t)L + (e - M)];
+        }
+        M += sz;
+    }
+    const float *qrow = Q + q * (int64_t)d;
+#pragma unroll
+    for (int r = 0; r < NR; ++r) {
+        if (ix[r] >= 0) {
+            dd[r] = exact_l2sq<VEC4>(qrow, C + ((int64_t)ix[r] - c_off) * d, d);
+        } else {
+            dd[r] = __builtin_inff();
+            ix[r] = INT_MAX;
+        }
+    }
+    wave_bitonic_sort<NR>(dd, ix);
+    const int keff = min(k, M);
+    if (G < __builtin_inff()) {  // some slice rejected candidates: certify
+        const float Dk = keff > 0 ? wave_elem<NR>(dd, keff - 1) : -__builtin_inff();
+        const float cmax = __uint_as_float(*cmax_bits);
+        const float delta = cert_c * (qnrm[q] + cmax) + 1e-38f;
+        const bool cert = (G - delta) > Dk;  // NaN/inf-safe: false => fallback
+        if (!cert && lane == 0) {
+            const int pos = atomicAdd(fb_count, 1);
+            fb_list[pos] = (int)q;
+        }
+    }
+    if (lane < k) {
+        const bool ok = lane < keff;
+        out_idx[q * k + lane] = ok ? ix[0] : -1;
+        out_dist[q * k + lane] = ok ? dd[0] : __builtin_inff();
+    }
+}
+
+// ---------------------------------------------------------------------------
+// 4. exact fallback scan for uncertified rows
+// ---------------------------------------------------------------------------
+struct alignas(16) FallbackSmem {
+    float ld[FB_THREADS][KMAX];
+    int li[FB_THREADS][KMAX];
+    float rd[2];
+    int ri[2];
+    int rt[2];
+};
+
+template <bool VEC4>
+__global__ __launch_bounds__(FB_THREADS) void k_fallback(
+    const float *__restrict__ Q, const float *__restrict__ C, int64_t nc, int d, int64_t q_off,
+    int64_t c_off, int excl, int k, const int *__restrict__ fb_count,
+    const int *__restrict__ fb_list, int32_t *__restrict__ out_idx,
+    float *__restrict__ out_dist) {
+    __shared__ FallbackSmem sm;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int nfb = *fb_count;
+    for (int f = blockIdx.x; f < nfb; f += gridDim.x) {
+        const int64_t q = fb_list[f];
+        const int64_t gq = q_off + q;
+        const bool self_in = excl && gq >= c_off && gq < c_off + nc;
+        const int64_t valid = nc - (self_in ? 1 : 0);
+        const int keff = (int)min((int64_t)k, valid);
+        const float *qrow = Q + q * (int64_t)d;
+        int cnt = 0;
+        for (int64_t j = tid; keff > 0 && j < nc; j += FB_THREADS) {
+            const int64_t gj = c_off + j;
+            if (excl && gj == gq) continue;
+            const float dist = exact_l2sq<VEC4>(qrow, C + j * (int64_t)d, d);
+            const int gi = (int)gj;
+            if (cnt == keff && !key_less(dist, gi, sm.ld[tid][keff - 1], sm.li[tid][keff - 1]))
+                continue;
+            int p = cnt < keff ? cnt : keff - 1;
+            while (p > 0 && key_less(dist, gi, sm.ld[tid][p - 1], sm.li[tid][p - 1])) {
+                sm.ld[tid][p] = sm.ld[tid][p - 1];
+                sm.li[tid][p] = sm.li[tid][p - 1];
+                --p;
+            }
+            sm.ld[tid][p] = dist;
+            sm.li[tid][p] = gi;
+            if (cnt < keff) ++cnt;
+        }
+        __syncthreads();
+        int head = 0;
+        for (int r = 0; r < keff; ++r) {
+            float bd = head < cnt ? sm.ld[tid][head] : __builtin_inff();
+            int bi = head < cnt ? sm.li[tid][head] : INT_MAX;
+            int bt = tid;
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) {
+                const float od = __shfl_xor(bd, o);
+                const int oi = __shfl_xor(bi, o);
+                const int ot = __shfl_xor(bt, o);
+                if (key_less(od, oi, bd, bi)) { bd = od; bi = oi; bt = ot; }
+            }
+            if (lane == 0) { sm.rd[w] = bd; sm.ri[w] = bi; sm.rt[w] = bt; }
+            __syncthreads();
+            const bool first = key_less(sm.rd[0], sm.ri[0], sm.rd[1], sm.ri[1]) ||
+                               !key_less(sm.rd[1], sm.ri[1], sm.rd[0], sm.ri[0]);
+            const int win = first ? 0 : 1;
+            if (tid == sm.rt[win]) {
+                out_idx[q * k + r] = sm.ri[win];
+                out_dist[q * k + r] = sm.rd[win];
+                ++head;
+            }
+            __syncthreads();
+        }
+        for (int r = keff + tid; r < k; r += FB_THREADS) {
+            out_idx[q * k + r] = -1;
+            out_dist[q * k + r] = __builtin_inff();
+        }
+        __syncthreads();
+    }
+}
+
+// ---------------------------------------------------------------------------
+// 5. merge of exact per-shard lists (row-sharded multi-GPU build)
+// ---------------------------------------------------------------------------
+constexpr int MAX_PARTS = 16;
+
+__global__ __launch_bounds__(256) void k_merge_parts(const int32_t *__restrict__ pidx,
+                                                     const float *__restrict__ pdist, int P,
+                                                     int64_t nq, int k,
+                                                     int32_t *__restrict__ out_idx,
+                                                     float *__restrict__ out_dist) {
+    const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= nq) return;
+    int head[MAX_PARTS];
+#pragma unroll
+    for (int p = 0; p < MAX_PARTS; ++p) head[p] = 0;
+    for (int r = 0; r < k; ++r) {
+        int bp = -1;
+        float bd = __builtin_inff();
+        int bi = INT_MAX;
+#pragma unroll
+        for (int p = 0; p < MAX_PARTS; ++p) {
+            if (p >= P) break;
+            const int h = head[p];
+            if (h >= k) continue;
+            const int64_t off = ((int64_t)p * nq + q) * k + h;
+            const int ci = pidx[off];
+            if (ci < 0) continue;
+            const float cd = pdist[off];
+            if (bp < 0 || key_less(cd, ci, bd, bi)) { bp = p; bd = cd; bi = ci; }
+        }
+#pragma unroll
+        for (int p = 0; p < MAX_PARTS; ++p)
+            if (p == bp) head[p]++;
+        out_idx[q * k + r] = bp < 0 ? -1 : bi;
+        out_dist[q * k + r] = bp < 0 ? __builtin_inff() : bd;
+    }
+}
+
+}  // namespace knn
+
+namespace {
+thread_local mn_knn_stats t_stats{};
+}
+
+// Host driver shared by mn_knn_f32 and mn_knn_f32_qc.
+static int knn_f32_impl(const float *Q, int64_t nq, const float *C, int64_t nc, int32_t d,
+                        int64_t q_off, int64_t c_off, const mn_knn_opts *opts,
+                        int32_t *out_idx, float *out_dist) {
+    using namespace knn;
+    clear_error();
+    t_stats = mn_knn_stats{};
+    MN_REQUIRE(opts, MN_EINVAL, "mn_knn: opts is NULL");
+    MN_REQUIRE(Q && C && out_idx && out_dist, MN_EINVAL, "mn_knn: NULL pointer argument");
+    MN_REQUIRE(nq >= 0 && nc >= 0 && d >= 1, MN_EINVAL, "mn_knn: bad shape nq=%lld nc=%lld d=%d",
+               (long long)nq, (long long)nc, d);
+    MN_REQUIRE(opts->metric == MN_L2SQ, MN_ENOTSUP, "mn_knn_f32: metric %d not supported here",
+               opts->metric);
+    const int k = opts->k;
+    MN_REQUIRE(k >= 1 && k <= KMAX, MN_ENOTSUP, "mn_knn: k=%d outside [1,%d]", k, KMAX);
+    const int margin = opts->margin > 0 ? opts->margin : 16;
+    const int L = k + margin;
+    MN_REQUIRE(L <= LMAX, MN_ENOTSUP, "mn_knn: k+margin=%d exceeds %d", L, LMAX);
+    MN_REQUIRE(q_off >= 0 && c_off >= 0 && q_off + nq <= INT_MAX && c_off + nc <= INT_MAX,
+               MN_EINVAL, "mn_knn: global ids must fit int32");
+    const int excl = opts->exclude_self ? 1 : 0;
+    hipStream_t s = (hipStream_t)opts->stream;
+    t_stats.n_queries = nq;
+    if (nq == 0) return MN_OK;
+
+    const bool vec4 = (d % 4 == 0) && (((uintptr_t)Q | (uintptr_t)C) % 16 == 0);
+    const bool same = (Q == C) && (nq == nc) && (q_off == c_off);
+
+    // corpus split: enough blocks to fill 256 CUs, bounded by the re-rank width
+    const int64_t blocks_q = (nq + BM - 1) / BM;
+    int64_t S = 1;
+    if (blocks_q < 512) S = (512 + blocks_q - 1) / blocks_q;
+    S = std::min<int64_t>(S, 256 / L);
+    S = std::min<int64_t>(S, std::max<int64_t>(1, (nc + BN - 1) / BN));
+    S = std::max<int64_t>(S, 1);
+    int64_t chunk = (nc + S - 1) / S;
+    chunk = ((chunk + BN - 1) / BN) * BN;
+    if (chunk == 0) chunk = BN;
+    S = std::max<int64_t>(1, (nc + chunk - 1) / chunk);
+    const int SL = (int)(S * L);
+    const int NR = SL <= 64 ? 1 : (SL <= 128 ? 2 : 4);
+    t_stats.slices = (int)S;
+    t_stats.list_len = L;
+
+    float *qn = (float *)scratch(kSlotNorms, sizeof(float) * (size_t)nq);
+    float *cn = same ? qn : (float *)scratch(kSlotNorms2, sizeof(float) * (size_t)std::max<int64_t>(nc, 1));
+    int *flags = (int *)scratch(kSlotFlags, 64);
+    const size_t nlist = (size_t)nq * S * L;
+    char *lists = (char *)scratch(kSlotLists, nlist * 8);
+    char *meta = (char *)scratch(kSlotListMeta, (size_t)nq * S * 8);
+    int *fb_list = (int *)scratch(kSlotFallback, sizeof(int) * (size_t)nq);
+    MN_REQUIRE(qn && cn && flags && lists && meta && fb_list, MN_ENOMEM,
+               "mn_knn: device scratch allocation failed");
+    float *list_d = (float *)lists;
+    int *list_i = (int *)(lists + nlist * 4);
+    int *lsz = (int *)meta;
+    float *ltau = (float *)(meta + (size_t)nq * S * 4);
+    unsigned *maxbits = (unsigned *)flags;
+    int *nonfinite = flags + 1;
+    int *fb_count = flags + 2;
+
+    Timer tm;
+    tm.start(opts->timing != 0, s);
+    MN_HIP_TRY(hipMemsetAsync(flags, 0, 64, s));
+    auto norms = [&](const float *X, int64_t n, float *out) {
+        if (n == 0) return;
+        int64_t blocks = std::min<int64_t>((n + 3) / 4, 8192);
+        if (vec4)
+            hipLaunchKernelGGL(k_row_norms<true>, dim3((unsigned)blocks), dim3(256), 0, s, X, n, d,
+                               out, maxbits, nonfinite);
+        else
+            hipLaunchKernelGGL(k_row_norms<false>, dim3((unsigned)blocks), dim3(256), 0, s, X, n, d,
+                               out, maxbits, nonfinite);
+    };
+    if (!same) {
+        norms(Q, nq, qn);
+        // query norms must not feed the corpus max: recompute flags after
+    }
+    MN_HIP_TRY(hipMemsetAsync(maxbits, 0, 4, s));
+    norms(C, nc, cn);
+    MN_HIP_TRY(hipGetLastError());
+    int hflags[4] = {0, 0, 0, 0};
+    MN_HIP_TRY(hipMemcpyAsync(hflags, flags, 16, hipMemcpyDeviceToHost, s));
+    MN_HIP_TRY(hipStreamSynchronize(s));
+    MN_REQUIRE(hflags[1] == 0, MN_ENONFINITE,
+               "mn_knn: input contains NaN/inf (the reference panics in partial_cmp().unwrap())");
+    tm.mark();
+
+    if (nc > 0) {
+        dim3 grid((unsigned)blocks_q, (unsigned)S);
+        if (vec4)
+            hipLaunchKernelGGL(k_gram_topk<true>, grid, dim3(NT), 0, s, Q, nq, C, nc, d, q_off,
+                               c_off, excl, qn, cn, L, (int)S, chunk, list_d, list_i, lsz, ltau);
+        else
+            hipLaunchKernelGGL(k_gram_topk<false>, grid, dim3(NT), 0, s, Q, nq, C, nc, d, q_off,
+                               c_off, excl, qn, cn, L, (int)S, chunk, list_d, list_i, lsz, ltau);
+        MN_HIP_TRY(hipGetLastError());
+    } else {
+        MN_HIP_TRY(hipMemsetAsync(lsz, 0, sizeof(int) * (size_t)nq * S, s));
+    }
+    tm.mark();
+
+    const float cert_c = 2.0f * (4.0f * (float)d + 16.0f) * 0x1p-24f;
+    const dim3 rgrid((unsigned)((nq + 3) / 4));
+#define MN_RERANK(NRV, V)                                                                       \
+    hipLaunchKernelGGL((k_rerank<NRV, V>), rgrid, dim3(256), 0, s, Q, nq, C, nc, d, c_off, qn,   \
+                       maxbits, (int)S, L, list_d, list_i, lsz, ltau, k, cert_c, out_idx,        \
+                       out_dist, fb_count, fb_list)
+    if (vec4) {
+        if (NR == 1) MN_RERANK(1, true);
+        else if (NR == 2) MN_RERANK(2, true);
+        else MN_RERANK(4, true);
+    } else {
+        if (NR == 1) MN_RERANK(1, false);
+        else if (NR == 2) MN_RERANK(2, false);
+        else MN_RERANK(4, false);
+    }
+#undef MN_RERANK
+    MN_HIP_TRY(hipGetLastError());
+    tm.mark();
+
+    const unsigned fgrid = (unsigned)std::min<int64_t>(nq, 1024);
+    if (vec4)
+        hipLaunchKernelGGL(k_fallback<true>, dim3(fgrid), dim3(FB_THREADS), 0, s, Q, C, nc, d,
+                           q_off, c_off, excl, k, fb_count, fb_list, out_idx, out_dist);
+    else
+        hipLaunchKernelGGL(k_fallback<false>, dim3(fgrid), dim3(FB_THREADS), 0, s, Q, C, nc, d,
+                           q_off, c_off, excl, k, fb_count, fb_list, out_idx, out_dist);
+    MN_HIP_TRY(hipGetLastError());
+    tm.mark();
+    MN_HIP_TRY(hipMemcpyAsync(hflags, flags, 16, hipMemcpyDeviceToHost, s));
+    MN_HIP_TRY(hipStreamSynchronize(s));
+    t_stats.n_uncertified = hflags[2];
+    if (tm.on) {
+        t_stats.ms_norms = tm.ms(0, 1);
+        t_stats.ms_gram = tm.ms(1, 2);
+        t_stats.ms_rerank = tm.ms(2, 3);
+        t_stats.ms_fallback = tm.ms(3, 4);
+        t_stats.ms_total = tm.ms(0, 4);
+    }
+    return MN_OK;
+}
+
+}  // namespace mn
+
+extern "C" {
+
+int mn_knn_f32(const float *X, int64_t n, int32_t d, const mn_knn_opts *opts, int32_t *out_idx,
+               float *out_dist) {
+    return mn::knn_f32_impl(X, n, X, n, d, 0, 0, opts, out_idx, out_dist);
+}
+
+int mn_knn_f32_qc(const float *Q, int64_t nq, const float *C, int64_t nc, int32_t d,
+                  int64_t q_offset, int64_t c_offset, const mn_knn_opts *opts, int32_t *out_idx,
+                  float *out_dist) {
+    return mn::knn_f32_impl(Q, nq, C, nc, d, q_offset, c_offset, opts, out_idx, out_dist);
+}
+
+int mn_knn_merge_f32(const int32_t *part_idx, const float *part_dist, int32_t parts, int64_t nq,
+                     int32_t k, int32_t *out_idx, float *out_dist, void *stream) {
+    mn::clear_error();
+    MN_REQUIRE(part_idx && part_dist && out_idx && out_dist, MN_EINVAL,
+               "mn_knn_merge_f32: NULL pointer");
+    MN_REQUIRE(parts >= 1 && parts <= mn::knn::MAX_PARTS && nq >= 0 && k >= 1, MN_EINVAL,
+               "mn_knn_merge_f32: bad args parts=%d k=%d", parts, k);
+    if (nq == 0) return MN_OK;
+    hipStream_t s = (hipStream_t)stream;
+    hipLaunchKernelGGL(mn::knn::k_merge_parts, dim3((unsigned)((nq + 255) / 256)), dim3(256), 0,
+                       s, part_idx, part_dist, parts, nq, k, out_idx, out_dist);
+    MN_HIP_TRY(hipGetLastError());
+    MN_HIP_TRY(hipStreamSynchronize(s));
+    return MN_OK;
+}
+
+int mn_knn_last_stats(mn_knn_stats *out) {
+    if (!out) return MN_EINVAL;
+    *out = mn::t_stats;
+    return MN_OK;
+}
+
+}  // extern "C"

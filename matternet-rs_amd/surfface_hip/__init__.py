@@ -1,0 +1,12 @@
+"""surfface_hip — host-side mirror of the surfface (matternet-rs) hot-path API
+over the MI355X HIP C ABI (include/matternet_hip.h, libmatternet_hip.so).
+
+Every op runs on the GPU through the C ABI; there is no CPU fallback.
+"""
+from . import _lib
+from ._lib import MnError, lib
+from .knn import (DistanceMetric, KnnResult, build_candidate_graph, knn_l2sq, knn_l2sq_qc,
+                  last_stats, merge_parts)
+
+__all__ = ["MnError", "lib", "DistanceMetric", "KnnResult", "build_candidate_graph", "knn_l2sq",
+           "knn_l2sq_qc", "last_stats", "merge_parts"]

@@ -1,0 +1,85 @@
+"""Loader for libmatternet_hip.so (the C ABI in include/matternet_hip.h).
+
+The product path has no CPU fallback: if the HIP library is missing or fails
+to load, every op raises.  Build it with `make -C matternet-rs_amd/csrc` (or
+`python -c "import __graft_entry__ as g; g.build()"`).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(os.path.dirname(PKG_DIR), "libmatternet_hip.so")
+
+MN_OK, MN_EINVAL, MN_ENOMEM, MN_ENONFINITE, MN_ECAP, MN_EHIP, MN_ENOTSUP = 0, -1, -2, -3, -4, -5, -6
+_NAMES = {-1: "MN_EINVAL", -2: "MN_ENOMEM", -3: "MN_ENONFINITE", -4: "MN_ECAP", -5: "MN_EHIP",
+          -6: "MN_ENOTSUP"}
+
+MN_L2SQ, MN_COS_RECT = 0, 1
+
+
+class MnError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"{_NAMES.get(code, code)}: {msg}")
+        self.code = code
+
+
+class KnnOpts(C.Structure):
+    _fields_ = [("k", C.c_int32), ("metric", C.c_int32), ("exclude_self", C.c_int32),
+                ("margin", C.c_int32), ("timing", C.c_int32), ("reserved0", C.c_int32),
+                ("stream", C.c_void_p)]
+
+
+class KnnStats(C.Structure):
+    _fields_ = [("n_queries", C.c_int64), ("n_uncertified", C.c_int64), ("slices", C.c_int32),
+                ("list_len", C.c_int32), ("ms_norms", C.c_float), ("ms_gram", C.c_float),
+                ("ms_rerank", C.c_float), ("ms_fallback", C.c_float), ("ms_total", C.c_float)]
+
+    def as_dict(self):
+        return {f: getattr(self, f) for f, _ in self._fields_}
+
+
+P = C.c_void_p
+I64 = C.c_int64
+I32 = C.c_int32
+
+# name -> (restype, argtypes); every symbol declared in include/matternet_hip.h
+SIGNATURES = {
+    "mn_version": (C.c_int, []),
+    "mn_last_error": (C.c_char_p, []),
+    "mn_device_alloc": (C.c_int, [C.c_size_t, C.POINTER(C.c_void_p)]),
+    "mn_device_free": (C.c_int, [P]),
+    "mn_memcpy_h2d": (C.c_int, [P, P, C.c_size_t, P]),
+    "mn_memcpy_d2h": (C.c_int, [P, P, C.c_size_t, P]),
+    "mn_stream_synchronize": (C.c_int, [P]),
+    "mn_fill_uniform_f32": (C.c_int, [P, I64, I32, C.c_uint64, I64, P]),
+    "mn_knn_f32": (C.c_int, [P, I64, I32, C.POINTER(KnnOpts), P, P]),
+    "mn_knn_f32_qc": (C.c_int, [P, I64, P, I64, I32, I64, I64, C.POINTER(KnnOpts), P, P]),
+    "mn_knn_merge_f32": (C.c_int, [P, P, I32, I64, I32, P, P, P]),
+    "mn_knn_last_stats": (C.c_int, [C.POINTER(KnnStats)]),
+}
+
+_LIB = None
+
+
+def lib() -> C.CDLL:
+    """Load the HIP library (raises loudly if it is missing: no fallback path)."""
+    global _LIB
+    if _LIB is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(f"libmatternet_hip.so not built at {LIB_PATH}; "
+                              "run `make -C matternet-rs_amd/csrc`")
+        L = C.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _LIB = L
+    return _LIB
+
+
+def check(rc: int) -> None:
+    if rc != MN_OK:
+        msg = lib().mn_last_error()
+        raise MnError(rc, msg.decode() if msg else "")

@@ -1,0 +1,107 @@
+"""K1 — brute-force kNN through the HIP C ABI (mn_knn_f32 / _qc / merge).
+
+Host-side mirror of the reference's kNN entry points:
+  * surfface-core/src/mst.rs:312-363  MSTStage::build_candidate_graph
+    (DistanceMetric::SquaredEuclidean / Euclidean)  -> build_candidate_graph()
+  * surfface-core/src/distance.rs:195-213 squared/euclidean distance
+Results are bit-identical to the reference's sequential f32 fold + stable sort.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+from enum import IntEnum
+
+import torch
+
+from . import _lib
+from ._torch import ptr, require_cuda, stream_handle, to_device
+
+
+class DistanceMetric(IntEnum):
+    """surfface-core/src/mst.rs:45-54 (Bhattacharyya is not on this path)."""
+    SquaredEuclidean = 0
+    Euclidean = 100  # same ordering as SquaredEuclidean; distances are sqrt'd
+
+
+@dataclass
+class KnnResult:
+    idx: torch.Tensor    # [n, k] int32 (global ids; -1 = empty slot)
+    dist: torch.Tensor   # [n, k] float32 (+inf = empty slot)
+    stats: dict
+
+
+def _opts(k, margin, timing, stream, exclude_self=True, metric=_lib.MN_L2SQ):
+    return _lib.KnnOpts(k=k, metric=metric, exclude_self=1 if exclude_self else 0,
+                        margin=margin, timing=1 if timing else 0, reserved0=0,
+                        stream=stream_handle(stream))
+
+
+def last_stats() -> dict:
+    st = _lib.KnnStats()
+    _lib.check(_lib.lib().mn_knn_last_stats(C.byref(st)))
+    return st.as_dict()
+
+
+def knn_l2sq(X: torch.Tensor, k: int, margin: int = 16, timing: bool = False,
+             stream=None, out_idx=None, out_dist=None) -> KnnResult:
+    """Exact kNN of every row of X [n, d] (f32, on device) by squared L2."""
+    X = require_cuda(X, torch.float32, "X", 2)
+    n, d = X.shape
+    idx = out_idx if out_idx is not None else torch.empty((n, k), dtype=torch.int32, device=X.device)
+    dist = out_dist if out_dist is not None else torch.empty((n, k), dtype=torch.float32, device=X.device)
+    o = _opts(k, margin, timing, stream)
+    _lib.check(_lib.lib().mn_knn_f32(ptr(X), n, d, C.byref(o), ptr(idx), ptr(dist)))
+    return KnnResult(idx, dist, last_stats())
+
+
+def knn_l2sq_qc(Qm: torch.Tensor, Cm: torch.Tensor, k: int, q_offset: int = 0, c_offset: int = 0,
+                exclude_self: bool = True, margin: int = 16, timing: bool = False,
+                stream=None) -> KnnResult:
+    """Exact per-shard top-k of queries Q against corpus C (global-id offsets)."""
+    Qm = require_cuda(Qm, torch.float32, "Q", 2)
+    Cm = require_cuda(Cm, torch.float32, "C", 2)
+    nq, d = Qm.shape
+    nc, d2 = Cm.shape
+    if d != d2:
+        raise ValueError("Q and C must have the same feature dimension")
+    idx = torch.empty((nq, k), dtype=torch.int32, device=Qm.device)
+    dist = torch.empty((nq, k), dtype=torch.float32, device=Qm.device)
+    o = _opts(k, margin, timing, stream, exclude_self)
+    _lib.check(_lib.lib().mn_knn_f32_qc(ptr(Qm), nq, ptr(Cm), nc, d, q_offset, c_offset,
+                                        C.byref(o), ptr(idx), ptr(dist)))
+    return KnnResult(idx, dist, last_stats())
+
+
+def merge_parts(part_idx: torch.Tensor, part_dist: torch.Tensor, stream=None):
+    """Merge P exact per-shard lists [P, nq, k] into the global top-k."""
+    part_idx = require_cuda(part_idx, torch.int32, "part_idx", 3)
+    part_dist = require_cuda(part_dist, torch.float32, "part_dist", 3)
+    P, nq, k = part_idx.shape
+    idx = torch.empty((nq, k), dtype=torch.int32, device=part_idx.device)
+    dist = torch.empty((nq, k), dtype=torch.float32, device=part_idx.device)
+    _lib.check(_lib.lib().mn_knn_merge_f32(ptr(part_idx), ptr(part_dist), P, nq, k, ptr(idx),
+                                           ptr(dist), stream_handle(stream)))
+    return idx, dist
+
+
+def build_candidate_graph(means, k_neighbors: int,
+                          metric: DistanceMetric = DistanceMetric.SquaredEuclidean):
+    """Mirror of MSTStage::build_candidate_graph (mst.rs:312-363), kNN part.
+
+    Returns directed edges (u, v, distance) as device tensors, k = min(k, C-1)
+    per node, in the reference's order (u ascending, then distance, then v).
+    """
+    X = to_device(means).float()
+    c = X.shape[0]
+    k = min(k_neighbors, c - 1)
+    if k < 1:
+        e = torch.empty(0, dtype=torch.int64, device=X.device)
+        return e, e.clone(), torch.empty(0, dtype=torch.float32, device=X.device)
+    r = knn_l2sq(X, k)
+    u = torch.arange(c, device=X.device, dtype=torch.int64).repeat_interleave(k)
+    v = r.idx.reshape(-1).to(torch.int64)
+    dist = r.dist.reshape(-1)
+    if metric == DistanceMetric.Euclidean:
+        dist = torch.sqrt(dist)
+    return u, v, dist

@@ -73,12 +73,31 @@ static void heap_sift_up(cand_f32 *h, int32_t i) {
     }
 }
 
+static int knn_l2sq_core(const float *X, int64_t n, int32_t d, int32_t k,
+                         int64_t q_begin, int64_t q_end, const int64_t *rows, int mode,
+                         int nthreads, int32_t *out_idx, float *out_dist);
+
 int or_knn_l2sq_f32(const float *X, int64_t n, int32_t d, int32_t k,
                     int64_t q_begin, int64_t q_end, int mode, int nthreads,
                     int32_t *out_idx, float *out_dist) {
     if (!X || !out_idx || !out_dist || n < 1 || d < 1 || k < 1 || q_begin < 0 ||
         q_end > n || q_begin > q_end)
         return OR_EINVAL;
+    return knn_l2sq_core(X, n, d, k, q_begin, q_end, NULL, mode, nthreads, out_idx, out_dist);
+}
+
+int or_knn_l2sq_rows_f32(const float *X, int64_t n, int32_t d, int32_t k,
+                         const int64_t *rows, int64_t nrows, int nthreads,
+                         int32_t *out_idx, float *out_dist) {
+    if (!X || !rows || !out_idx || !out_dist || n < 1 || d < 1 || k < 1 || nrows < 0)
+        return OR_EINVAL;
+    for (int64_t t = 0; t < nrows; ++t) if (rows[t] < 0 || rows[t] >= n) return OR_EINVAL;
+    return knn_l2sq_core(X, n, d, k, 0, nrows, rows, 1, nthreads, out_idx, out_dist);
+}
+
+static int knn_l2sq_core(const float *X, int64_t n, int32_t d, int32_t k,
+                         int64_t q_begin, int64_t q_end, const int64_t *rows, int mode,
+                         int nthreads, int32_t *out_idx, float *out_dist) {
     const int64_t keff64 = (n - 1) < (int64_t)k ? (n - 1) : (int64_t)k;
     const int32_t keff = (int32_t)keff64;
     int err = 0;
@@ -93,11 +112,12 @@ int or_knn_l2sq_f32(const float *X, int64_t n, int32_t d, int32_t k,
             err = OR_ENOMEM;
         }
 #pragma omp for schedule(dynamic, 16)
-        for (int64_t i = q_begin; i < q_end; ++i) {
+        for (int64_t qq = q_begin; qq < q_end; ++qq) {
             if (!buf) continue;
+            const int64_t i = rows ? rows[qq] : qq;
             const float *xi = X + i * (int64_t)d;
-            int32_t *oi = out_idx + (i - q_begin) * (int64_t)k;
-            float *od = out_dist + (i - q_begin) * (int64_t)k;
+            int32_t *oi = out_idx + (qq - q_begin) * (int64_t)k;
+            float *od = out_dist + (qq - q_begin) * (int64_t)k;
             int bad = 0;
             int32_t cnt = 0;
             for (int64_t j = 0; j < n; ++j) {

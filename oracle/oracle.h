@@ -47,6 +47,13 @@ int or_knn_l2sq_f32(const float *X, int64_t n, int32_t d, int32_t k,
                     int64_t q_begin, int64_t q_end, int mode, int nthreads,
                     int32_t *out_idx, float *out_dist);
 
+/* A.1 on an explicit list of query rows (rows[t] in [0,n)): output row t is
+ * the kNN of X[rows[t]] over all of X (self excluded).  Used for sampled
+ * parity checks and the sampled CPU baseline. */
+int or_knn_l2sq_rows_f32(const float *X, int64_t n, int32_t d, int32_t k,
+                         const int64_t *rows, int64_t nrows, int nthreads,
+                         int32_t *out_idx, float *out_dist);
+
 /* A.1c rectified-cosine kNN, f64 arithmetic on exactly-widened f32 inputs.
  *   src_legacy/tests/test_helpers.rs:77-126 (build_adjacency_matrix):
  *   norms sqrt(sum x*x) sequential f64; dot sequential f64;

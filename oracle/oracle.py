@@ -47,6 +47,7 @@ F = C.c_float
 
 def _declare(L):
     L.or_knn_l2sq_f32.argtypes = [P, I64, I32, I32, I64, I64, C.c_int, C.c_int, P, P]
+    L.or_knn_l2sq_rows_f32.argtypes = [P, I64, I32, I32, P, I64, C.c_int, P, P]
     L.or_knn_cos_f64.argtypes = [P, I64, I32, I32, D, D, D, I64, I64, C.c_int, P, P, P]
     L.or_laplacian_union.argtypes = [I64, I32, P, P, I64, P, P, P, P]
     L.or_laplacian_max.argtypes = [I64, I64, P, P, P, F, C.c_int, I64, P, P, P, P, P, P]
@@ -77,6 +78,17 @@ def knn_l2sq(X, k, q_begin=0, q_end=None, mode=1, nthreads=0):
     dist = np.empty((m, k), np.float32)
     _check(lib().or_knn_l2sq_f32(_p(X), n, d, k, q_begin, q_end, mode, nthreads, _p(idx), _p(dist)),
            "knn_l2sq")
+    return idx, dist
+
+
+def knn_l2sq_rows(X, k, rows, nthreads=0):
+    X = np.ascontiguousarray(X, dtype=np.float32)
+    n, d = X.shape
+    rows = np.ascontiguousarray(rows, dtype=np.int64)
+    idx = np.empty((len(rows), k), np.int32)
+    dist = np.empty((len(rows), k), np.float32)
+    _check(lib().or_knn_l2sq_rows_f32(_p(X), n, d, k, _p(rows), len(rows), nthreads, _p(idx),
+                                      _p(dist)), "knn_l2sq_rows")
     return idx, dist
 
 

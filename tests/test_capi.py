@@ -1,0 +1,61 @@
+"""CPU checks of the drop-in boundary: libmatternet_hip.so loads and exports
+every symbol include/*.h declares; argument validation fails loudly without
+touching the GPU (no compute calls here)."""
+import ctypes as C
+import glob
+import os
+import re
+
+import pytest
+
+import surfface_hip
+from surfface_hip import _lib
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _declared_symbols():
+    syms = set()
+    for h in glob.glob(os.path.join(ROOT, "include", "*.h")):
+        text = open(h).read()
+        text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+        for m in re.finditer(r"\b(mn_[a-z0-9_]+)\s*\(", text):
+            syms.add(m.group(1))
+    return syms
+
+
+def test_library_exports_every_declared_symbol():
+    L = _lib.lib()
+    declared = _declared_symbols()
+    assert declared, "no mn_* declarations found in include/"
+    missing = [s for s in sorted(declared) if not hasattr(L, s)]
+    assert not missing, missing
+    # and the Python binding declares a signature for each
+    assert declared <= set(_lib.SIGNATURES), declared - set(_lib.SIGNATURES)
+
+
+def test_version_and_error_paths_without_gpu():
+    L = _lib.lib()
+    assert L.mn_version() >= 100
+    # NULL opts / pointers are rejected before any HIP call
+    assert L.mn_knn_f32(None, 10, 4, None, None, None) == _lib.MN_EINVAL
+    assert b"opts" in L.mn_last_error()
+    o = _lib.KnnOpts(k=0, metric=0, exclude_self=1, margin=0, timing=0, reserved0=0, stream=None)
+    assert L.mn_knn_f32(C.c_void_p(16), 10, 4, C.byref(o), C.c_void_p(16), C.c_void_p(16)) \
+        == _lib.MN_ENOTSUP
+    o.k, o.metric = 5, 7
+    assert L.mn_knn_f32(C.c_void_p(16), 10, 4, C.byref(o), C.c_void_p(16), C.c_void_p(16)) \
+        == _lib.MN_ENOTSUP
+    with pytest.raises(surfface_hip.MnError):
+        _lib.check(_lib.MN_EINVAL)
+
+
+def test_no_cpu_fallback_in_product_path():
+    """The product package must not import the oracle (test infrastructure)."""
+    pkg = os.path.join(ROOT, "matternet-rs_amd")
+    for path in glob.glob(os.path.join(pkg, "**", "*.py"), recursive=True) + \
+            glob.glob(os.path.join(pkg, "csrc", "*")):
+        if os.path.isdir(path):
+            continue
+        text = open(path, errors="ignore").read()
+        assert not re.search(r"import\s+oracle|from\s+oracle|liboracle|\bor_[a-z0-9_]+\(", text), path

@@ -1,0 +1,111 @@
+"""K1 parity on the GPU: HIP kNN (through the C ABI) vs the CPU oracle.
+
+Contract: neighbour indices bit-exact and distances bit-exact
+(the re-rank IS the reference's sequential f32 fold), ties by ascending index.
+"""
+import numpy as np
+import pytest
+import torch
+
+import datagen
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+GS = np.load(__import__("os").path.join(__import__("os").path.dirname(__file__), "golden",
+                                        "golden_small.npz"))
+
+
+def hip_knn(X, k, **kw):
+    import surfface_hip as S
+    r = S.knn_l2sq(torch.from_numpy(np.ascontiguousarray(X)).cuda(), k, **kw)
+    torch.cuda.synchronize()
+    return r.idx.cpu().numpy(), r.dist.cpu().numpy(), r.stats
+
+
+def assert_exact(idx, dist, ridx, rdist):
+    np.testing.assert_array_equal(idx, ridx)
+    np.testing.assert_array_equal(dist.view(np.uint32), rdist.view(np.uint32))
+
+
+@pytest.mark.parametrize("name,k", [("l2_uniform", 5), ("l2_clustered", 7), ("l2_grid", 6)])
+def test_golden_fixtures(name, k):
+    idx, dist, _ = hip_knn(GS[name + "_X"], k)
+    assert_exact(idx, dist, GS[name + "_idx"], GS[name + "_dist"])
+
+
+def test_config1_shape_10k_x_64_k10():
+    X = datagen.uniform(10_000, 64, seed=42)
+    idx, dist, st = hip_knn(X, 10)
+    ridx, rdist = O.knn_l2sq(X, 10)
+    assert_exact(idx, dist, ridx, rdist)
+
+
+@pytest.mark.parametrize("n,d,k", [(3000, 96, 32), (2500, 17, 10), (1000, 5, 3), (700, 768, 32)])
+def test_clustered_duplicates_and_zero_rows(n, d, k):
+    X = datagen.clustered(n, d, seed=7, blobs=8, dup_frac=0.03, zero_frac=0.01)
+    idx, dist, st = hip_knn(X, k)
+    ridx, rdist = O.knn_l2sq(X, k)
+    assert_exact(idx, dist, ridx, rdist)
+    assert st["n_uncertified"] >= 1  # zero rows tie massively -> exact fallback exercised
+
+
+def test_small_n_and_k_clamp():
+    X = datagen.uniform(5, 8, seed=3)
+    idx, dist, _ = hip_knn(X, 10)
+    ridx, rdist = O.knn_l2sq(X, 10)
+    assert_exact(idx, dist, ridx, rdist)
+    assert (idx[:, 4:] == -1).all()
+
+
+def test_all_identical_rows_tie_by_index():
+    X = np.ones((300, 12), np.float32)
+    idx, dist, st = hip_knn(X, 8)
+    ridx, rdist = O.knn_l2sq(X, 8)
+    assert_exact(idx, dist, ridx, rdist)
+
+
+def test_huge_values_overflow_to_inf():
+    X = datagen.uniform(400, 8, seed=9)
+    X[17] *= 3e19  # its distances overflow to +inf in the f32 fold
+    idx, dist, st = hip_knn(X, 6)
+    ridx, rdist = O.knn_l2sq(X, 6)
+    assert_exact(idx, dist, ridx, rdist)
+
+
+def test_nonfinite_input_is_an_error():
+    import surfface_hip as S
+    X = datagen.uniform(100, 8, seed=1)
+    X[5, 3] = np.nan
+    with pytest.raises(S.MnError):
+        hip_knn(X, 4)
+
+
+def test_query_corpus_offsets_and_shard_merge():
+    import surfface_hip as S
+    X = datagen.uniform(6000, 64, seed=5)
+    Xd = torch.from_numpy(X).cuda()
+    k = 16
+    parts_i, parts_d = [], []
+    bounds = [0, 1500, 3100, 6000]
+    for a, b in zip(bounds[:-1], bounds[1:]):
+        r = S.knn_l2sq_qc(Xd, Xd[a:b], k, q_offset=0, c_offset=a)
+        parts_i.append(r.idx)
+        parts_d.append(r.dist)
+    idx, dist = S.merge_parts(torch.stack(parts_i), torch.stack(parts_d))
+    ridx, rdist = O.knn_l2sq(X, k)
+    assert_exact(idx.cpu().numpy(), dist.cpu().numpy(), ridx, rdist)
+
+
+def test_large_n_sampled_rows_d768():
+    """200k x 768, k=32: full GPU run, oracle on a sample of 192 query rows."""
+    n, d, k = 200_000, 768, 32
+    X = datagen.uniform(n, d, seed=42)
+    idx, dist, st = hip_knn(X, k)
+    rows = np.random.default_rng(0).choice(n, 192, replace=False)
+    ridx, rdist = O.knn_l2sq_rows(X, k, rows)
+    assert_exact(idx[rows], dist[rows], ridx, rdist)
+    # size-independent properties on every row
+    assert (np.diff(dist, axis=1) >= 0).all()
+    assert (idx != np.arange(n)[:, None]).all()
+    assert st["n_uncertified"] == 0

@@ -228,3 +228,12 @@ def test_laplacian_max_properties():
     for i in range(n):
         L[i, ix[ip[i]:ip[i + 1]]] = iv[ip[i]:ip[i + 1]]
     assert np.abs(L.sum(axis=1)).max() < 1e-4
+
+
+def test_knn_rows_variant_matches_full():
+    X = GS["l2_clustered_X"]
+    i_all, d_all = O.knn_l2sq(X, 7)
+    rows = np.array([5, 0, 35, 17, 17])
+    i_r, d_r = O.knn_l2sq_rows(X, 7, rows)
+    np.testing.assert_array_equal(i_r, i_all[rows])
+    np.testing.assert_array_equal(d_r, d_all[rows])
