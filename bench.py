@@ -180,15 +180,23 @@ def cpu_baseline(X, idx, dd, k, target_s):
     Xh = X.cpu().numpy()
     n = Xh.shape[0]
     rng = np.random.default_rng(1)
-    cal = np.sort(rng.choice(n, threads, replace=False))
-    t0 = time.perf_counter()
+    cal = np.sort(rng.choice(n, threads, replace=False))  # warms pages + threads
     i0, d0 = O.knn_l2sq_rows(Xh, k, cal, nthreads=threads)
-    tc = time.perf_counter() - t0
-    m = int(max(threads, min(4096, threads * round(target_s / max(tc, 1e-3)))))
-    rows = np.sort(rng.choice(n, m, replace=False))
-    t0 = time.perf_counter()
-    ri, rd = O.knn_l2sq_rows(Xh, k, rows, nthreads=threads)
-    el = time.perf_counter() - t0
+    perm = rng.permutation(n)
+    batch = threads * 4
+    done, el = 0, 0.0
+    ri_l, rd_l = [], []
+    while el < target_s and done + batch <= min(n, 65536):
+        rows_b = np.sort(perm[done:done + batch])
+        t0 = time.perf_counter()
+        a_i, a_d = O.knn_l2sq_rows(Xh, k, rows_b, nthreads=threads)
+        el += time.perf_counter() - t0
+        ri_l.append((rows_b, a_i, a_d))
+        done += batch
+    rows = np.concatenate([r for r, _, _ in ri_l])
+    ri = np.concatenate([x for _, x, _ in ri_l])
+    rd = np.concatenate([x for _, _, x in ri_l])
+    m = len(rows)
     gi = idx.cpu().numpy()[rows]
     gd = dd.cpu().numpy()[rows]
     ok = int(np.sum(np.all(gi == ri, axis=1) & np.all(gd.view(np.uint32) == rd.view(np.uint32),

@@ -62,6 +62,7 @@ struct alignas(16) GramSmem {
     float tau[BM];
     int cnt[BM];
     int lsz[BM];
+    int ovf[BM];  // a valid pair had a non-finite d~ (overflow): force the exact path
 };
 
 // ---------------------------------------------------------------------------
@@ -191,6 +192,7 @@ __global__ __launch_bounds__(NT) void k_gram_topk(
         sm.tau[r] = __builtin_inff();
         sm.cnt[r] = 0;
         sm.lsz[r] = 0;
+        sm.ovf[r] = 0;
     }
     __syncthreads();
 
@@ -277,6 +279,12 @@ __global__ __launch_bounds__(NT) void k_gram_topk(
                 const float dd = __builtin_fmaf(-2.f, curv[i], sm.qn[lrow] + cv);
                 const bool valid = colok && (q < nq) && !(excl && (q_off + q) == gcol);
                 const bool pass = valid && (dd < tv);
+                if (__ballot(valid && !(dd < __builtin_inff()))) {
+                    // d~ overflowed (or NaN): the threshold argument no longer
+                    // covers this pair, so the row is resolved exactly later.
+                    if (valid && !(dd < __builtin_inff())) sm.ovf[lrow] = 1;
+                    __builtin_amdgcn_wave_barrier();
+                }
                 const uint64_t m = __ballot(pass);
                 if (m) {
 #pragma unroll
@@ -312,7 +320,7 @@ __global__ __launch_bounds__(NT) void k_gram_topk(
         const int64_t q = q0 + row;
         if (q < nq) {
             out_lsz[q * S + sl] = sm.lsz[row];
-            out_tau[q * S + sl] = sm.tau[row];
+            out_tau[q * S + sl] = sm.ovf[row] ? -__builtin_inff() : sm.tau[row];
         }
     }
 }
@@ -363,9 +371,12 @@ __global__ __launch_bounds__(256) void k_rerank(
     int ix[NR];
     int M = 0;
     float G = __builtin_inff();
+    bool forced = false;
     for (int s = 0; s < S; ++s) {
         const int sz = lsz[q * S + s];
-        if (sz >= L) G = fminf(G, ltau[q * S + s]);
+        const float ts = ltau[q * S + s];
+        forced |= (ts == -__builtin_inff());
+        if (sz >= L) G = fminf(G, ts);
 #pragma unroll
         for (int r = 0; r < NR; ++r) {
             const int e = lane + 64 * r;
@@ -386,7 +397,12 @@ __global__ __launch_bounds__(256) void k_rerank(
     }
     wave_bitonic_sort<NR>(dd, ix);
     const int keff = min(k, M);
-    if (G < __builtin_inff()) {  // some slice rejected candidates: certify
+    if (forced) {
+        if (lane == 0) {
+            const int pos = atomicAdd(fb_count, 1);
+            fb_list[pos] = (int)q;
+        }
+    } else if (G < __builtin_inff()) {  // some slice rejected candidates: certify
         const float Dk = keff > 0 ? wave_elem<NR>(dd, keff - 1) : -__builtin_inff();
         const float cmax = __uint_as_float(*cmax_bits);
         const float delta = cert_c * (qnrm[q] + cmax) + 1e-38f;

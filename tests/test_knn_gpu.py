@@ -47,7 +47,6 @@ def test_clustered_duplicates_and_zero_rows(n, d, k):
     idx, dist, st = hip_knn(X, k)
     ridx, rdist = O.knn_l2sq(X, k)
     assert_exact(idx, dist, ridx, rdist)
-    assert st["n_uncertified"] >= 1  # zero rows tie massively -> exact fallback exercised
 
 
 def test_small_n_and_k_clamp():
@@ -63,6 +62,16 @@ def test_all_identical_rows_tie_by_index():
     idx, dist, st = hip_knn(X, 8)
     ridx, rdist = O.knn_l2sq(X, 8)
     assert_exact(idx, dist, ridx, rdist)
+    assert st["n_uncertified"] == 300  # every row ties beyond L -> exact fallback path
+
+
+def test_zero_rows_tie_beyond_candidate_list():
+    X = datagen.uniform(2000, 32, seed=4)
+    X[::7] = 0.0  # 286 identical zero rows: ties far beyond k + margin
+    idx, dist, st = hip_knn(X, 16)
+    ridx, rdist = O.knn_l2sq(X, 16)
+    assert_exact(idx, dist, ridx, rdist)
+    assert st["n_uncertified"] >= 286
 
 
 def test_huge_values_overflow_to_inf():
