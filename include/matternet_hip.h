@@ -46,6 +46,7 @@ int mn_device_alloc(size_t bytes, void **out);
 int mn_device_free(void *p);
 int mn_memcpy_h2d(void *dst_dev, const void *src_host, size_t bytes, void *stream);
 int mn_memcpy_d2h(void *dst_host, const void *src_dev, size_t bytes, void *stream);
+int mn_memcpy_d2d(void *dst_dev, const void *src_dev, size_t bytes, void *stream);
 int mn_stream_synchronize(void *stream);
 
 /* Synthetic input generator, identical to tests/datagen.py:
@@ -109,6 +110,68 @@ int mn_knn_merge_f32(const int32_t *part_idx, const float *part_dist,
 
 /* Statistics of the calling thread's last mn_knn_* call. */
 int mn_knn_last_stats(mn_knn_stats *out);
+
+
+/* ---------------------------------------------------------------------- */
+/* K2 — Laplacian assembly from kNN rows (CSR)                            */
+/* ---------------------------------------------------------------------- */
+enum mn_value_type { MN_F32 = 0, MN_F64 = 1 };
+enum mn_weight_kernel {
+    MN_W_GIVEN = 0,    /* nbr_val already holds edge weights                    */
+    MN_W_RATIONAL = 1  /* w = 1/(1+(dist/sigma)^p), dist <= eps, w > 1e-12
+                          (src_legacy/laplacian.rs:245-260)                      */
+};
+enum mn_symmetrise {
+    MN_SYM_UNION = 0,  /* legacy: union of directed edges, L = D - W, f64 values
+                          (src_legacy/laplacian.rs:297-419)                      */
+    MN_SYM_MAX = 1     /* Stage C: undirected max weight, optional L_sym, f32
+                          (surfface-core/src/laplacian.rs:312-394, 209-219)      */
+};
+
+typedef struct mn_lap_opts {
+    int32_t weight_kernel;   /* enum mn_weight_kernel                            */
+    int32_t symmetrise;      /* enum mn_symmetrise                               */
+    int32_t normalize;       /* MAX only: 1 = I - D^-1/2 W D^-1/2, 0 = D - W     */
+    int32_t reserved0;
+    double eps;              /* MN_W_RATIONAL: keep dist <= eps                  */
+    double sigma;            /* MN_W_RATIONAL: kernel scale (> 0)                */
+    double p;                /* MN_W_RATIONAL: kernel exponent                   */
+    double weight_threshold; /* MAX: drop w <= thr (LaplacianConfig 1e-9)        */
+    void *stream;
+} mn_lap_opts;
+
+/* CSR matrix; library-allocated device buffers, release with mn_csr_free. */
+typedef struct mn_csr {
+    int64_t n_rows, n_cols, nnz;
+    int64_t *indptr;   /* [n_rows + 1] */
+    int32_t *indices;  /* [nnz], ascending within a row */
+    void *values;      /* [nnz] of value_type */
+    int32_t value_type;
+    int32_t reserved0;
+} mn_csr;
+
+typedef struct mn_lap_stats {
+    int64_t nnz;
+    int64_t big_rows;  /* rows sorted by the block kernel (> 256 entries)      */
+    int64_t hub_rows;  /* rows resolved by the dense column map (> 8192)       */
+    float ms_total;
+    float reserved0;
+} mn_lap_stats;
+
+/* Directed kNN rows (nbr_idx [n][k], -1 = empty; nbr_val [n][k] distances for
+ * MN_W_RATIONAL or weights for MN_W_GIVEN, f64 if val_is_f64 else f32) ->
+ * symmetric Laplacian CSR.  Replaces _symmetrise_adjancency +
+ * _build_sparse_laplacian (src_legacy/laplacian.rs:297-419; UNION: values
+ * and structure bit-identical) and LaplacianStage::build_laplacian_flat + the
+ * dense->CSR pass (surfface-core/src/laplacian.rs:312-394, 209-219; MAX:
+ * structure identical, values within f32 tolerance because the reference
+ * sums degrees in DashMap order).  degrees_out (device, may be NULL): [n]
+ * f64 (UNION) or f32 (MAX). */
+int mn_laplacian_from_knn(const int32_t *nbr_idx, const void *nbr_val, int32_t val_is_f64,
+                          int64_t n, int32_t k, const mn_lap_opts *opts, mn_csr *out,
+                          void *degrees_out);
+int mn_csr_free(mn_csr *m);
+int mn_lap_last_stats(mn_lap_stats *out);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,595 @@
+// laplacian.hip — K2: kNN rows -> symmetric weighted graph -> Laplacian (CSR).
+//
+// Reference semantics:
+//   UNION / unnormalised (legacy, f64) — src_legacy/laplacian.rs:245-294
+//     (weight 1/(1+(dist/sigma)^p) for dist <= eps, kept if > 1e-12),
+//     :297-348 (_symmetrise_adjancency: every directed edge also inserted
+//     reversed, self loops dropped, rows sorted by column), :351-419
+//     (_build_sparse_laplacian: L_ii = sum_j w_ij summed sequentially in
+//     ascending j from -0.0 and stored for EVERY row, L_ij = -w_ij).
+//   MAX / Stage C (f32) — surfface-core/src/laplacian.rs:312-394 (undirected
+//     key with the max weight, w <= thr dropped, degrees in f32, optional
+//     L_sym = I - D^-1/2 W D^-1/2) and :209-219 (dense -> CSR keeps |v|>1e-9).
+//
+// GPU design: an O(E) counting-sort CSR build, no global sort —
+//   1. k_lap_weights     per row: weight kernel + validity, in-degree atomics
+//   2. scan              row capacity = out + in  -> segment offsets
+//   3. k_lap_scatter     forward entries in slot order, reverse entries by
+//                        atomic fill (order fixed by step 4)
+//   4. row sort+dedupe   (col asc, w desc) then unique col (keeps the max):
+//                        one wave per row (<=256 entries, bitonic in
+//                        registers), one 1024-thread block per row (<=8192,
+//                        bitonic in LDS), dense column map for hub rows
+//   5. degrees/values    one thread per row, sequential ascending-column sums
+//                        (exactly the reference order for the legacy path)
+//   6. scan + write      CSR with the diagonal at its sorted position.
+#include <algorithm>
+#include <climits>
+#include <vector>
+
+#include "common.hpp"
+#include "scan.hpp"
+
+namespace mn {
+namespace lap {
+
+struct Params {
+    int kernel;     // MN_W_GIVEN / MN_W_RATIONAL
+    int sym;        // MN_SYM_UNION / MN_SYM_MAX
+    int normalize;  // MAX only
+    double eps, sigma, p, thr;
+};
+
+constexpr int WAVE_CAP = 256;
+constexpr int BLOCK_CAP = 8192;
+
+__device__ __forceinline__ double pw(double x, double p) {
+    if (p == 2.0) return x * x;
+    if (p == 1.0) return x;
+    return pow(x, p);
+}
+
+__global__ __launch_bounds__(256) void k_lap_weights(const int32_t *__restrict__ nbr,
+                                                     const void *__restrict__ val, int val_f64,
+                                                     int64_t n, int k, Params P,
+                                                     int32_t *__restrict__ vidx,
+                                                     double *__restrict__ vw,
+                                                     int32_t *__restrict__ outcnt,
+                                                     int32_t *__restrict__ indeg,
+                                                     int *__restrict__ bad) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    int cnt = 0;
+    for (int r = 0; r < k; ++r) {
+        const int64_t s = i * k + r;
+        const int32_t j = nbr[s];
+        const double x = val_f64 ? ((const double *)val)[s] : (double)((const float *)val)[s];
+        bool valid = j >= 0 && (int64_t)j != i;
+        if (j >= (int64_t)n) { atomicOr(bad, 1); valid = false; }
+        double w = x;
+        if (valid && P.kernel == MN_W_RATIONAL) {
+            valid = x <= P.eps;  // laplacian.rs:252 (NaN fails)
+            w = 1.0 / (1.0 + pw(x / P.sigma, P.p));
+            valid = valid && (w > 1e-12);
+        }
+        if (valid && P.sym == MN_SYM_MAX) valid = w > P.thr;  // laplacian.rs:324
+        vidx[s] = valid ? j : -1;
+        vw[s] = w;
+        if (valid) {
+            ++cnt;
+            atomicAdd(&indeg[j], 1);
+        }
+    }
+    outcnt[i] = cnt;
+}
+
+__global__ void k_add_i32(const int32_t *__restrict__ a, const int32_t *__restrict__ b, int64_t n,
+                          int32_t *__restrict__ out) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) out[i] = a[i] + b[i];
+}
+
+__global__ __launch_bounds__(256) void k_lap_scatter(const int32_t *__restrict__ vidx,
+                                                     const double *__restrict__ vw, int64_t n,
+                                                     int k, const int64_t *__restrict__ offs,
+                                                     const int32_t *__restrict__ outcnt,
+                                                     int32_t *__restrict__ fill,
+                                                     int32_t *__restrict__ col,
+                                                     double *__restrict__ wt) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    int64_t pos = offs[i];
+    for (int r = 0; r < k; ++r) {
+        const int32_t j = vidx[i * k + r];
+        if (j < 0) continue;
+        const double w = vw[i * k + r];
+        col[pos] = j;
+        wt[pos] = w;
+        ++pos;
+        const int64_t q = offs[j] + outcnt[j] + atomicAdd(&fill[j], 1);
+        col[q] = (int32_t)i;
+        wt[q] = w;
+    }
+}
+
+// (col asc, w desc): the first entry of each column run carries the max weight
+__device__ __forceinline__ bool cw_less(int ca, double wa, int cb, double wb) {
+    return ca < cb || (ca == cb && wa > wb);
+}
+
+// one wave per row with m <= WAVE_CAP entries
+__global__ __launch_bounds__(256) void k_row_sort_wave(const int64_t *__restrict__ offs,
+                                                       int64_t n, int32_t *__restrict__ col,
+                                                       double *__restrict__ wt,
+                                                       int32_t *__restrict__ uniq,
+                                                       int32_t *__restrict__ big_list,
+                                                       int *__restrict__ big_count) {
+    constexpr int NR = WAVE_CAP / 64;
+    const int lane = threadIdx.x & 63;
+    const int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    if (i >= n) return;
+    const int64_t o = offs[i];
+    const int m = (int)(offs[i + 1] - o);
+    if (m > WAVE_CAP) {
+        if (lane == 0) big_list[atomicAdd(big_count, 1)] = (int32_t)i;
+        return;
+    }
+    int c[NR];
+    double w[NR];
+#pragma unroll
+    for (int r = 0; r < NR; ++r) {
+        const int e = lane + 64 * r;
+        c[r] = e < m ? col[o + e] : INT_MAX;
+        w[r] = e < m ? wt[o + e] : 0.0;
+    }
+#pragma unroll
+    for (int kk = 2; kk <= 64 * NR; kk <<= 1) {
+#pragma unroll
+        for (int j = kk >> 1; j > 0; j >>= 1) {
+            if (j >= 64) {
+#pragma unroll
+                for (int r = 0; r < NR; ++r) {
+                    const int pr = r ^ (j >> 6);
+                    if (pr > r) {
+                        const int e = lane + 64 * r;
+                        const bool asc = (e & kk) == 0;
+                        const bool sw = asc ? cw_less(c[pr], w[pr], c[r], w[r])
+                                            : cw_less(c[r], w[r], c[pr], w[pr]);
+                        if (sw) {
+                            int tc = c[r]; c[r] = c[pr]; c[pr] = tc;
+                            double tw = w[r]; w[r] = w[pr]; w[pr] = tw;
+                        }
+                    }
+                }
+            } else {
+#pragma unroll
+                for (int r = 0; r < NR; ++r) {
+                    const int e = lane + 64 * r;
+                    const int pc = __shfl_xor(c[r], j);
+                    const double pwv = __shfl_xor(w[r], j);
+                    const bool asc = (e & kk) == 0;
+                    const bool lower = (e & j) == 0;
+                    const bool take = (asc == lower) ? cw_less(pc, pwv, c[r], w[r])
+                                                     : cw_less(c[r], w[r], pc, pwv);
+                    if (take) { c[r] = pc; w[r] = pwv; }
+                }
+            }
+        }
+    }
+    // dedupe: keep e if e < m and (e == 0 or col[e] != col[e-1])
+    int base = 0;
+#pragma unroll
+    for (int r = 0; r < NR; ++r) {
+        const int e = lane + 64 * r;
+        int prev = __shfl_up(c[r], 1);
+        const int last_prev = (r > 0) ? __shfl(c[r > 0 ? r - 1 : 0], 63) : INT_MIN;
+        if (lane == 0) prev = (r == 0) ? INT_MIN : last_prev;
+        const bool keep = e < m && c[r] != prev;
+        const uint64_t mk = __ballot(keep);
+        if (keep) {
+            const int pos = base + (int)__popcll(mk & ((1ull << lane) - 1ull));
+            col[o + pos] = c[r];
+            wt[o + pos] = w[r];
+        }
+        base += (int)__popcll(mk);
+    }
+    if (lane == 0) uniq[i] = base;
+}
+
+// one 1024-thread block per row with WAVE_CAP < m <= BLOCK_CAP (bitonic in LDS)
+struct alignas(16) BigSmem {
+    double w[BLOCK_CAP];
+    int c[BLOCK_CAP];
+    int flag[BLOCK_CAP];
+    int wsum[16];
+};
+
+__global__ __launch_bounds__(1024) void k_row_sort_block(const int64_t *__restrict__ offs,
+                                                         const int32_t *__restrict__ big_list,
+                                                         const int *__restrict__ big_count,
+                                                         int32_t *__restrict__ col,
+                                                         double *__restrict__ wt,
+                                                         int32_t *__restrict__ uniq,
+                                                         int32_t *__restrict__ huge_list,
+                                                         int *__restrict__ huge_count) {
+    __shared__ BigSmem sm;
+    const int nb = *big_count;
+    for (int b = blockIdx.x; b < nb; b += gridDim.x) {
+        const int64_t i = big_list[b];
+        const int64_t o = offs[i];
+        const int m = (int)(offs[i + 1] - o);
+        if (m > BLOCK_CAP) {
+            if (threadIdx.x == 0) huge_list[atomicAdd(huge_count, 1)] = (int32_t)i;
+            continue;
+        }
+        int P = 1;
+        while (P < m) P <<= 1;
+        for (int e = threadIdx.x; e < P; e += blockDim.x) {
+            sm.c[e] = e < m ? col[o + e] : INT_MAX;
+            sm.w[e] = e < m ? wt[o + e] : 0.0;
+        }
+        __syncthreads();
+        for (int kk = 2; kk <= P; kk <<= 1) {
+            for (int j = kk >> 1; j > 0; j >>= 1) {
+                for (int e = threadIdx.x; e < P; e += blockDim.x) {
+                    const int pe = e ^ j;
+                    if (pe > e) {
+                        const bool asc = (e & kk) == 0;
+                        const bool sw = asc ? cw_less(sm.c[pe], sm.w[pe], sm.c[e], sm.w[e])
+                                            : cw_less(sm.c[e], sm.w[e], sm.c[pe], sm.w[pe]);
+                        if (sw) {
+                            int tc = sm.c[e]; sm.c[e] = sm.c[pe]; sm.c[pe] = tc;
+                            double tw = sm.w[e]; sm.w[e] = sm.w[pe]; sm.w[pe] = tw;
+                        }
+                    }
+                }
+                __syncthreads();
+            }
+        }
+        // dedupe with a block scan over keep flags (chunks of 1024)
+        int base = 0;
+        for (int c0 = 0; c0 < m; c0 += 1024) {
+            const int e = c0 + threadIdx.x;
+            const bool keep = e < m && (e == 0 || sm.c[e] != sm.c[e - 1]);
+            const uint64_t mk = __ballot(keep);
+            const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+            if (lane == 0) sm.wsum[wv] = (int)__popcll(mk);
+            __syncthreads();
+            int before = 0, tot = 0;
+            for (int q = 0; q < 16; ++q) {
+                if (q < wv) before += sm.wsum[q];
+                tot += sm.wsum[q];
+            }
+            if (keep) {
+                const int pos = base + before + (int)__popcll(mk & ((1ull << lane) - 1ull));
+                sm.flag[pos] = e;  // gather index (pos <= e: in-place safe via flag array)
+            }
+            base += tot;
+            __syncthreads();
+        }
+        for (int q = threadIdx.x; q < base; q += blockDim.x) {
+            col[o + q] = sm.c[sm.flag[q]];
+            wt[o + q] = sm.w[sm.flag[q]];
+        }
+        if (threadIdx.x == 0) uniq[i] = base;
+        __syncthreads();
+    }
+}
+
+// hub rows (m > BLOCK_CAP): dense column map, one row at a time
+__global__ void k_dense_fill(double *__restrict__ dense, int64_t n) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) dense[i] = -__builtin_inf();
+}
+__global__ void k_dense_scatter(const int32_t *__restrict__ col, const double *__restrict__ wt,
+                                int64_t o, int m, double *__restrict__ dense) {
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= m) return;
+    const int c = col[o + e];
+    const double w = wt[o + e];
+    unsigned long long *p = (unsigned long long *)&dense[c];
+    unsigned long long old = *p, assumed;
+    do {  // atomic max on doubles (any sign)
+        assumed = old;
+        if (!(w > __longlong_as_double((long long)assumed))) break;
+        old = atomicCAS(p, assumed, (unsigned long long)__double_as_longlong(w));
+    } while (old != assumed);
+}
+__global__ __launch_bounds__(256) void k_dense_flag(const double *__restrict__ dense, int64_t n,
+                                                    int32_t *__restrict__ flag) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) flag[i] = dense[i] != -__builtin_inf() ? 1 : 0;
+}
+__global__ void k_dense_compact(const double *__restrict__ dense, const int32_t *__restrict__ flag,
+                                const int64_t *__restrict__ pos, int64_t n, int64_t o,
+                                int32_t *__restrict__ col, double *__restrict__ wt) {
+    const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= n || !flag[c]) return;
+    col[o + pos[c]] = (int32_t)c;
+    wt[o + pos[c]] = dense[c];
+}
+__global__ void k_set_uniq(int32_t *uniq, int64_t i, const int64_t *total) {
+    uniq[i] = (int32_t)*total;
+}
+
+// ---- per-row degrees, kept counts, CSR write ----------------------------
+
+__global__ __launch_bounds__(256) void k_degrees(const int64_t *__restrict__ offs,
+                                                 const int32_t *__restrict__ uniq, int64_t n,
+                                                 const double *__restrict__ wt, int sym,
+                                                 double *__restrict__ deg64,
+                                                 float *__restrict__ deg32) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int64_t o = offs[i];
+    const int u = uniq[i];
+    if (sym == MN_SYM_UNION) {
+        double s = -0.0;  // laplacian.rs:367: s.iter().map(w).sum() in ascending j
+        for (int e = 0; e < u; ++e) s = s + wt[o + e];
+        deg64[i] = s;
+    } else {
+        float s = 0.0f;  // laplacian.rs:331-340 (order: ascending column here)
+        for (int e = 0; e < u; ++e) s = s + (float)wt[o + e];
+        deg32[i] = s;
+    }
+}
+
+__device__ __forceinline__ float max_offdiag(float w, float di, float dj, int normalize) {
+    return normalize ? -w / sqrtf(di * dj) : -w;
+}
+
+__global__ __launch_bounds__(256) void k_kept(const int64_t *__restrict__ offs,
+                                              const int32_t *__restrict__ col,
+                                              const double *__restrict__ wt,
+                                              const int32_t *__restrict__ uniq, int64_t n,
+                                              Params P, const float *__restrict__ deg32,
+                                              int32_t *__restrict__ kept) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int u = uniq[i];
+    if (P.sym == MN_SYM_UNION) {
+        kept[i] = u + 1;
+        return;
+    }
+    const float thr = (float)P.thr, di = deg32[i];
+    int c = 0;
+    if (di > thr) {
+        const float v = P.normalize ? 1.0f : di;
+        if (fabsf(v) > 1e-9f) ++c;
+    }
+    const int64_t o = offs[i];
+    for (int e = 0; e < u; ++e) {
+        const int j = col[o + e];
+        const float dj = deg32[j];
+        if (P.normalize && (di <= thr || dj <= thr)) continue;
+        const float v = max_offdiag((float)wt[o + e], di, dj, P.normalize);
+        if (fabsf(v) > 1e-9f) ++c;
+    }
+    kept[i] = c;
+}
+
+__global__ __launch_bounds__(256) void k_write_csr(const int64_t *__restrict__ offs,
+                                                   const int32_t *__restrict__ col,
+                                                   const double *__restrict__ wt,
+                                                   const int32_t *__restrict__ uniq, int64_t n,
+                                                   Params P, const double *__restrict__ deg64,
+                                                   const float *__restrict__ deg32,
+                                                   const int64_t *__restrict__ indptr,
+                                                   int32_t *__restrict__ out_col,
+                                                   double *__restrict__ out_v64,
+                                                   float *__restrict__ out_v32) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int64_t o = offs[i];
+    const int u = uniq[i];
+    int64_t q = indptr[i];
+    if (P.sym == MN_SYM_UNION) {
+        bool diag = false;
+        for (int e = 0; e < u; ++e) {
+            const int j = col[o + e];
+            if (!diag && j > i) {
+                out_col[q] = (int32_t)i; out_v64[q] = deg64[i]; ++q; diag = true;
+            }
+            out_col[q] = j;
+            out_v64[q] = -wt[o + e];
+            ++q;
+        }
+        if (!diag) { out_col[q] = (int32_t)i; out_v64[q] = deg64[i]; }
+        return;
+    }
+    const float thr = (float)P.thr, di = deg32[i];
+    const bool has_diag = di > thr && fabsf(P.normalize ? 1.0f : di) > 1e-9f;
+    bool diag = !has_diag;
+    for (int e = 0; e < u; ++e) {
+        const int j = col[o + e];
+        if (!diag && j > i) {
+            out_col[q] = (int32_t)i; out_v32[q] = P.normalize ? 1.0f : di; ++q; diag = true;
+        }
+        const float dj = deg32[j];
+        if (P.normalize && (di <= thr || dj <= thr)) continue;
+        const float v = max_offdiag((float)wt[o + e], di, dj, P.normalize);
+        if (!(fabsf(v) > 1e-9f)) continue;
+        out_col[q] = j;
+        out_v32[q] = v;
+        ++q;
+    }
+    if (!diag) { out_col[q] = (int32_t)i; out_v32[q] = P.normalize ? 1.0f : di; }
+}
+
+inline unsigned grid_for(int64_t n, int t = 256) { return (unsigned)std::max<int64_t>(1, (n + t - 1) / t); }
+
+}  // namespace lap
+
+static thread_local mn_lap_stats t_lap_stats{};
+
+static int laplacian_impl(const int32_t *nbr, const void *val, int32_t val_f64, int64_t n,
+                          int32_t k, const mn_lap_opts *opts, mn_csr *out, void *degrees_out) {
+    using namespace lap;
+    clear_error();
+    t_lap_stats = mn_lap_stats{};
+    MN_REQUIRE(opts && out, MN_EINVAL, "mn_laplacian_from_knn: NULL opts/out");
+    *out = mn_csr{};
+    MN_REQUIRE(n >= 1 && k >= 0 && (k == 0 || (nbr && val)), MN_EINVAL,
+               "mn_laplacian_from_knn: bad shape n=%lld k=%d", (long long)n, k);
+    MN_REQUIRE(n <= INT_MAX, MN_EINVAL, "mn_laplacian_from_knn: n must fit int32");
+    MN_REQUIRE(opts->weight_kernel == MN_W_GIVEN || opts->weight_kernel == MN_W_RATIONAL,
+               MN_EINVAL, "mn_laplacian_from_knn: unknown weight_kernel");
+    MN_REQUIRE(opts->symmetrise == MN_SYM_UNION || opts->symmetrise == MN_SYM_MAX, MN_EINVAL,
+               "mn_laplacian_from_knn: unknown symmetrise mode");
+    MN_REQUIRE(!(opts->symmetrise == MN_SYM_UNION && opts->normalize), MN_ENOTSUP,
+               "mn_laplacian_from_knn: the legacy UNION Laplacian is unnormalised (D - W)");
+    if (opts->weight_kernel == MN_W_RATIONAL)
+        MN_REQUIRE(opts->sigma > 0.0, MN_EINVAL, "mn_laplacian_from_knn: sigma must be > 0");
+    Params P{opts->weight_kernel, opts->symmetrise, opts->normalize ? 1 : 0, opts->eps,
+             opts->sigma, opts->p, opts->weight_threshold};
+    hipStream_t s = (hipStream_t)opts->stream;
+    const int64_t nk = n * (int64_t)k;
+
+    // scratch layout
+    char *g0 = (char *)scratch(kSlotGeneric0, (size_t)nk * 12 + 64);                 // vidx, vw
+    char *g1 = (char *)scratch(kSlotGeneric1, (size_t)n * 4 * 6 + (size_t)(n + 1) * 8 * 2 + 64 +
+                                               ((size_t)n / scan::SB + 2) * 8);
+    char *g2 = (char *)scratch(kSlotGeneric2, (size_t)(2 * nk + 1) * 12);             // col, w
+    MN_REQUIRE(g0 && g1 && g2, MN_ENOMEM, "mn_laplacian_from_knn: scratch allocation failed");
+    int32_t *vidx = (int32_t *)g0;
+    double *vw = (double *)(g0 + (((size_t)nk * 4 + 15) & ~(size_t)15));
+    int32_t *outcnt = (int32_t *)g1;
+    int32_t *indeg = outcnt + n;
+    int32_t *capv = indeg + n;
+    int32_t *fill = capv + n;
+    int32_t *uniq = fill + n;
+    int32_t *kept = uniq + n;
+    int64_t *offs = (int64_t *)(((uintptr_t)(kept + n) + 15) & ~(uintptr_t)15);
+    int64_t *part = offs + (n + 1);
+    int *flags = (int *)(part + (n / scan::SB + 2));
+    const int64_t E2 = 2 * nk;
+    int32_t *col = (int32_t *)g2;
+    double *wt = (double *)(g2 + (((size_t)E2 * 4 + 15) & ~(size_t)15));
+    int32_t *lists = (int32_t *)scratch(kSlotGeneric3, (size_t)n * 8 + 64);
+    MN_REQUIRE(lists, MN_ENOMEM, "mn_laplacian_from_knn: scratch allocation failed");
+    int32_t *big_list = lists, *huge_list = lists + n;
+
+    Timer tm;
+    tm.start(true, s);
+    MN_HIP_TRY(hipMemsetAsync(outcnt, 0, (size_t)n * 4 * 6, s));
+    MN_HIP_TRY(hipMemsetAsync(flags, 0, 16, s));
+    if (k > 0)
+        hipLaunchKernelGGL(k_lap_weights, dim3(grid_for(n)), dim3(256), 0, s, nbr, val, val_f64,
+                           n, k, P, vidx, vw, outcnt, indeg, flags);
+    hipLaunchKernelGGL(k_add_i32, dim3(grid_for(n)), dim3(256), 0, s, outcnt, indeg, n, capv);
+    MN_HIP_TRY(scan::exclusive_scan(capv, n, offs, part, s));
+    if (k > 0)
+        hipLaunchKernelGGL(k_lap_scatter, dim3(grid_for(n)), dim3(256), 0, s, vidx, vw, n, k, offs,
+                           outcnt, fill, col, wt);
+    hipLaunchKernelGGL(k_row_sort_wave, dim3(grid_for(n * 64)), dim3(256), 0, s, offs, n, col, wt,
+                       uniq, big_list, flags + 1);
+    hipLaunchKernelGGL(k_row_sort_block, dim3(256), dim3(1024), 0, s, offs, big_list, flags + 1,
+                       col, wt, uniq, huge_list, flags + 2);
+    MN_HIP_TRY(hipGetLastError());
+    int hf[4] = {0, 0, 0, 0};
+    MN_HIP_TRY(hipMemcpyAsync(hf, flags, 16, hipMemcpyDeviceToHost, s));
+    MN_HIP_TRY(hipStreamSynchronize(s));
+    MN_REQUIRE(hf[0] == 0, MN_EINVAL, "mn_laplacian_from_knn: neighbour index >= n");
+    t_lap_stats.big_rows = hf[1];
+    t_lap_stats.hub_rows = hf[2];
+    if (hf[2] > 0) {  // hub rows: dense column map, one at a time (rare)
+        std::vector<int32_t> hubs(hf[2]);
+        MN_HIP_TRY(hipMemcpyAsync(hubs.data(), huge_list, sizeof(int32_t) * hf[2],
+                                  hipMemcpyDeviceToHost, s));
+        std::vector<int64_t> hoffs(n + 1);
+        MN_HIP_TRY(hipMemcpyAsync(hoffs.data(), offs, sizeof(int64_t) * (n + 1),
+                                  hipMemcpyDeviceToHost, s));
+        MN_HIP_TRY(hipStreamSynchronize(s));
+        double *dense = nullptr;
+        int32_t *dflag = nullptr;
+        int64_t *dpos = nullptr, *dpart = nullptr;
+        MN_HIP_TRY(hipMalloc(&dense, sizeof(double) * n));
+        MN_HIP_TRY(hipMalloc(&dflag, sizeof(int32_t) * n));
+        MN_HIP_TRY(hipMalloc(&dpos, sizeof(int64_t) * (n + 1)));
+        MN_HIP_TRY(hipMalloc(&dpart, sizeof(int64_t) * (n / scan::SB + 2)));
+        for (int h = 0; h < hf[2]; ++h) {
+            const int64_t i = hubs[h], o = hoffs[i];
+            const int m = (int)(hoffs[i + 1] - o);
+            hipLaunchKernelGGL(k_dense_fill, dim3(grid_for(n)), dim3(256), 0, s, dense, n);
+            hipLaunchKernelGGL(k_dense_scatter, dim3(grid_for(m)), dim3(256), 0, s, col, wt, o, m,
+                               dense);
+            hipLaunchKernelGGL(k_dense_flag, dim3(grid_for(n)), dim3(256), 0, s, dense, n, dflag);
+            MN_HIP_TRY(scan::exclusive_scan(dflag, n, dpos, dpart, s));
+            hipLaunchKernelGGL(k_dense_compact, dim3(grid_for(n)), dim3(256), 0, s, dense, dflag,
+                               dpos, n, o, col, wt);
+            hipLaunchKernelGGL(k_set_uniq, dim3(1), dim3(1), 0, s, uniq, i, dpos + n);
+        }
+        MN_HIP_TRY(hipStreamSynchronize(s));
+        (void)hipFree(dense); (void)hipFree(dflag); (void)hipFree(dpos); (void)hipFree(dpart);
+    }
+    // degrees (into degrees_out when given, else scratch)
+    double *deg64 = nullptr;
+    float *deg32 = nullptr;
+    void *degbuf = degrees_out;
+    if (!degbuf) {
+        degbuf = scratch(kSlotNorms2, (size_t)n * 8);
+        MN_REQUIRE(degbuf, MN_ENOMEM, "mn_laplacian_from_knn: scratch allocation failed");
+    }
+    if (P.sym == MN_SYM_UNION) deg64 = (double *)degbuf; else deg32 = (float *)degbuf;
+    hipLaunchKernelGGL(k_degrees, dim3(grid_for(n)), dim3(256), 0, s, offs, uniq, n, wt, P.sym,
+                       deg64, deg32);
+    hipLaunchKernelGGL(k_kept, dim3(grid_for(n)), dim3(256), 0, s, offs, col, wt, uniq, n, P,
+                       deg32, kept);
+    int64_t *indptr = nullptr;
+    MN_HIP_TRY(hipMalloc(&indptr, sizeof(int64_t) * (n + 1)));
+    MN_HIP_TRY(scan::exclusive_scan(kept, n, indptr, part, s));
+    int64_t nnz = 0;
+    MN_HIP_TRY(hipMemcpyAsync(&nnz, indptr + n, 8, hipMemcpyDeviceToHost, s));
+    MN_HIP_TRY(hipStreamSynchronize(s));
+    int32_t *ocol = nullptr;
+    void *oval = nullptr;
+    const size_t vsz = P.sym == MN_SYM_UNION ? 8 : 4;
+    if (hipMalloc(&ocol, sizeof(int32_t) * std::max<int64_t>(nnz, 1)) != hipSuccess ||
+        hipMalloc(&oval, vsz * std::max<int64_t>(nnz, 1)) != hipSuccess) {
+        (void)hipFree(indptr); (void)hipFree(ocol);
+        set_error("mn_laplacian_from_knn: output allocation (nnz=%lld) failed", (long long)nnz);
+        return MN_ENOMEM;
+    }
+    hipLaunchKernelGGL(k_write_csr, dim3(grid_for(n)), dim3(256), 0, s, offs, col, wt, uniq, n, P,
+                       deg64, deg32, indptr, ocol, (double *)oval, (float *)oval);
+    MN_HIP_TRY(hipGetLastError());
+    tm.mark();
+    MN_HIP_TRY(hipStreamSynchronize(s));
+    t_lap_stats.ms_total = tm.ms(0, 1);
+    t_lap_stats.nnz = nnz;
+    out->n_rows = n;
+    out->n_cols = n;
+    out->nnz = nnz;
+    out->indptr = indptr;
+    out->indices = ocol;
+    out->values = oval;
+    out->value_type = P.sym == MN_SYM_UNION ? MN_F64 : MN_F32;
+    return MN_OK;
+}
+
+}  // namespace mn
+
+extern "C" {
+
+int mn_laplacian_from_knn(const int32_t *nbr_idx, const void *nbr_val, int32_t val_is_f64,
+                          int64_t n, int32_t k, const mn_lap_opts *opts, mn_csr *out,
+                          void *degrees_out) {
+    return mn::laplacian_impl(nbr_idx, nbr_val, val_is_f64, n, k, opts, out, degrees_out);
+}
+
+int mn_csr_free(mn_csr *m) {
+    if (!m) return MN_OK;
+    if (m->indptr) (void)hipFree(m->indptr);
+    if (m->indices) (void)hipFree(m->indices);
+    if (m->values) (void)hipFree(m->values);
+    *m = mn_csr{};
+    return MN_OK;
+}
+
+int mn_lap_last_stats(mn_lap_stats *out) {
+    if (!out) return MN_EINVAL;
+    *out = mn::t_lap_stats;
+    return MN_OK;
+}
+
+}  // extern "C"

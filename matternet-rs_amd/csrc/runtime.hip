@@ -129,6 +129,13 @@ int mn_memcpy_d2h(void *dst, const void *src, size_t bytes, void *stream) {
     return MN_OK;
 }
 
+int mn_memcpy_d2d(void *dst, const void *src, size_t bytes, void *stream) {
+    hipStream_t s = (hipStream_t)stream;
+    MN_HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, s));
+    MN_HIP_TRY(hipStreamSynchronize(s));
+    return MN_OK;
+}
+
 int mn_stream_synchronize(void *stream) {
     MN_HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
     return MN_OK;

@@ -5,8 +5,13 @@ Every op runs on the GPU through the C ABI; there is no CPU fallback.
 """
 from . import _lib
 from ._lib import MnError, lib
+from . import laplacian
+from .laplacian import (CsrMatrix, GraphParams, LaplacianConfig, LaplacianOutput,
+                        build_laplacian_from_knn, laplacian_stage_from_edges)
 from .knn import (DistanceMetric, KnnResult, build_candidate_graph, knn_l2sq, knn_l2sq_qc,
                   last_stats, merge_parts)
 
 __all__ = ["MnError", "lib", "DistanceMetric", "KnnResult", "build_candidate_graph", "knn_l2sq",
-           "knn_l2sq_qc", "last_stats", "merge_parts"]
+           "knn_l2sq_qc", "last_stats", "merge_parts", "CsrMatrix", "GraphParams",
+           "LaplacianConfig", "LaplacianOutput", "build_laplacian_from_knn",
+           "laplacian_stage_from_edges", "laplacian"]

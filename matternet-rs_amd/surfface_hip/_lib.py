@@ -40,6 +40,31 @@ class KnnStats(C.Structure):
         return {f: getattr(self, f) for f, _ in self._fields_}
 
 
+MN_F32, MN_F64 = 0, 1
+MN_W_GIVEN, MN_W_RATIONAL = 0, 1
+MN_SYM_UNION, MN_SYM_MAX = 0, 1
+
+
+class LapOpts(C.Structure):
+    _fields_ = [("weight_kernel", C.c_int32), ("symmetrise", C.c_int32), ("normalize", C.c_int32),
+                ("reserved0", C.c_int32), ("eps", C.c_double), ("sigma", C.c_double),
+                ("p", C.c_double), ("weight_threshold", C.c_double), ("stream", C.c_void_p)]
+
+
+class Csr(C.Structure):
+    _fields_ = [("n_rows", C.c_int64), ("n_cols", C.c_int64), ("nnz", C.c_int64),
+                ("indptr", C.c_void_p), ("indices", C.c_void_p), ("values", C.c_void_p),
+                ("value_type", C.c_int32), ("reserved0", C.c_int32)]
+
+
+class LapStats(C.Structure):
+    _fields_ = [("nnz", C.c_int64), ("big_rows", C.c_int64), ("hub_rows", C.c_int64),
+                ("ms_total", C.c_float), ("reserved0", C.c_float)]
+
+    def as_dict(self):
+        return {f: getattr(self, f) for f, _ in self._fields_ if f != "reserved0"}
+
+
 P = C.c_void_p
 I64 = C.c_int64
 I32 = C.c_int32
@@ -52,12 +77,16 @@ SIGNATURES = {
     "mn_device_free": (C.c_int, [P]),
     "mn_memcpy_h2d": (C.c_int, [P, P, C.c_size_t, P]),
     "mn_memcpy_d2h": (C.c_int, [P, P, C.c_size_t, P]),
+    "mn_memcpy_d2d": (C.c_int, [P, P, C.c_size_t, P]),
     "mn_stream_synchronize": (C.c_int, [P]),
     "mn_fill_uniform_f32": (C.c_int, [P, I64, I32, C.c_uint64, I64, P]),
     "mn_knn_f32": (C.c_int, [P, I64, I32, C.POINTER(KnnOpts), P, P]),
     "mn_knn_f32_qc": (C.c_int, [P, I64, P, I64, I32, I64, I64, C.POINTER(KnnOpts), P, P]),
     "mn_knn_merge_f32": (C.c_int, [P, P, I32, I64, I32, P, P, P]),
     "mn_knn_last_stats": (C.c_int, [C.POINTER(KnnStats)]),
+    "mn_laplacian_from_knn": (C.c_int, [P, P, I32, I64, I32, C.POINTER(LapOpts), C.POINTER(Csr), P]),
+    "mn_csr_free": (C.c_int, [C.POINTER(Csr)]),
+    "mn_lap_last_stats": (C.c_int, [C.POINTER(LapStats)]),
 }
 
 _LIB = None

@@ -1,0 +1,137 @@
+"""K2 — Laplacian assembly through the HIP C ABI (mn_laplacian_from_knn).
+
+Host-side mirror of the reference types/entry points:
+  * GraphParams            src_legacy/graph.rs:94-102
+  * build_laplacian_from_knn  == _build_adjacency's weight step +
+    _symmetrise_adjancency + _build_sparse_laplacian (src_legacy/laplacian.rs:
+    245-419): UNION symmetrisation, L = D - W, f64 values (bit-identical)
+  * LaplacianConfig / LaplacianOutput / laplacian_stage_from_edges
+    surfface-core/src/laplacian.rs:49-99, 312-394: MAX symmetrisation,
+    optional L_sym = I - D^-1/2 W D^-1/2, f32 values
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+from typing import Optional
+
+import numpy as np
+import torch
+
+from . import _lib
+from ._torch import ptr, require_cuda, stream_handle
+
+
+@dataclass
+class GraphParams:
+    """src_legacy/graph.rs:94-102 (builder defaults builder.rs:104-111)."""
+    eps: float = 1e-3
+    k: int = 6
+    topk: int = 3
+    p: float = 2.0
+    sigma: Optional[float] = None
+    normalise: bool = False
+    sparsity_check: bool = False
+
+
+@dataclass
+class LaplacianConfig:
+    """surfface-core/src/laplacian.rs:49-77."""
+    k_neighbors: int = 15
+    variance_regularizer: float = 1e-6
+    normalize: bool = True
+    weight_threshold: float = 1e-9
+
+
+@dataclass
+class CsrMatrix:
+    """Device CSR (torch tensors): indptr int64 [n+1], indices int32, values."""
+    indptr: torch.Tensor
+    indices: torch.Tensor
+    values: torch.Tensor
+    shape: tuple
+
+    @property
+    def nnz(self) -> int:
+        return int(self.indices.numel())
+
+    def to_numpy(self):
+        return (self.indptr.cpu().numpy(), self.indices.cpu().numpy(), self.values.cpu().numpy())
+
+    def to_dense(self) -> np.ndarray:
+        ip, ix, iv = self.to_numpy()
+        out = np.zeros(self.shape, dtype=iv.dtype)
+        for i in range(self.shape[0]):
+            out[i, ix[ip[i]:ip[i + 1]]] = iv[ip[i]:ip[i + 1]]
+        return out
+
+
+@dataclass
+class LaplacianOutput:
+    """surfface-core/src/laplacian.rs:84-99."""
+    matrix: CsrMatrix
+    n_features: int
+    nnz: int
+    degrees: torch.Tensor
+    sparsity: float
+
+
+def last_stats() -> dict:
+    st = _lib.LapStats()
+    _lib.check(_lib.lib().mn_lap_last_stats(C.byref(st)))
+    return st.as_dict()
+
+
+def _adopt(csr: _lib.Csr, device) -> CsrMatrix:
+    """Copy the library-owned CSR into torch tensors and free it."""
+    L = _lib.lib()
+    n, nnz = csr.n_rows, csr.nnz
+    vdt = torch.float64 if csr.value_type == _lib.MN_F64 else torch.float32
+    indptr = torch.empty(n + 1, dtype=torch.int64, device=device)
+    indices = torch.empty(nnz, dtype=torch.int32, device=device)
+    values = torch.empty(nnz, dtype=vdt, device=device)
+    try:
+        s = stream_handle()
+        _lib.check(L.mn_memcpy_d2d(ptr(indptr), csr.indptr, 8 * (n + 1), s))
+        if nnz:
+            _lib.check(L.mn_memcpy_d2d(ptr(indices), csr.indices, 4 * nnz, s))
+            _lib.check(L.mn_memcpy_d2d(ptr(values), csr.values, values.element_size() * nnz, s))
+    finally:
+        L.mn_csr_free(C.byref(csr))
+    return CsrMatrix(indptr, indices, values, (n, n))
+
+
+def build_laplacian_from_knn(nbr_idx: torch.Tensor, nbr_val: torch.Tensor, *,
+                             weight_kernel: str = "rational", symmetrise: str = "union",
+                             normalize: bool = False, eps: float = 1.0, sigma: float = 1.0,
+                             p: float = 2.0, weight_threshold: float = 1e-9, stream=None):
+    """kNN rows -> (Laplacian CSR on device, degrees on device)."""
+    nbr_idx = require_cuda(nbr_idx, torch.int32, "nbr_idx", 2)
+    if nbr_val.dtype not in (torch.float32, torch.float64):
+        raise TypeError("nbr_val must be float32 or float64")
+    nbr_val = require_cuda(nbr_val, nbr_val.dtype, "nbr_val", 2)
+    n, k = nbr_idx.shape
+    wk = {"given": _lib.MN_W_GIVEN, "rational": _lib.MN_W_RATIONAL}[weight_kernel]
+    sy = {"union": _lib.MN_SYM_UNION, "max": _lib.MN_SYM_MAX}[symmetrise]
+    o = _lib.LapOpts(weight_kernel=wk, symmetrise=sy, normalize=1 if normalize else 0,
+                     reserved0=0, eps=eps, sigma=sigma, p=p, weight_threshold=weight_threshold,
+                     stream=stream_handle(stream))
+    deg = torch.empty(n, dtype=torch.float64 if sy == _lib.MN_SYM_UNION else torch.float32,
+                      device=nbr_idx.device)
+    csr = _lib.Csr()
+    _lib.check(_lib.lib().mn_laplacian_from_knn(
+        ptr(nbr_idx), ptr(nbr_val), 1 if nbr_val.dtype == torch.float64 else 0, n, k,
+        C.byref(o), C.byref(csr), ptr(deg)))
+    return _adopt(csr, nbr_idx.device), deg
+
+
+def laplacian_stage_from_edges(nbr_idx: torch.Tensor, weights: torch.Tensor,
+                               config: LaplacianConfig = LaplacianConfig()) -> LaplacianOutput:
+    """LaplacianStage::execute steps 2-3 (surfface-core/src/laplacian.rs:179-227)
+    given the top-k affinity rows (the Bhattacharyya scoring itself is §8(f))."""
+    m, deg = build_laplacian_from_knn(nbr_idx, weights.float(), weight_kernel="given",
+                                      symmetrise="max", normalize=config.normalize,
+                                      weight_threshold=config.weight_threshold)
+    f = nbr_idx.shape[0]
+    return LaplacianOutput(matrix=m, n_features=f, nnz=m.nnz, degrees=deg,
+                           sparsity=1.0 - m.nnz / float(f * f))

@@ -1,0 +1,114 @@
+"""K2 parity on the GPU: HIP Laplacian assembly (C ABI) vs the CPU oracle.
+
+UNION / legacy (f64): CSR structure AND values bit-exact (the reference's
+degree is a sequential ascending-column sum, reproduced exactly).
+MAX / Stage C (f32): structure exact; values and degrees within 1e-5
+relative (the reference sums degrees in DashMap iteration order).
+"""
+import numpy as np
+import pytest
+import torch
+
+import datagen
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+GS = np.load(__import__("os").path.join(__import__("os").path.dirname(__file__), "golden",
+                                        "golden_small.npz"))
+
+
+def lap(idx, val, **kw):
+    import surfface_hip as S
+    m, deg = S.build_laplacian_from_knn(torch.from_numpy(np.ascontiguousarray(idx)).cuda(),
+                                        torch.from_numpy(np.ascontiguousarray(val)).cuda(), **kw)
+    return m.to_numpy() + (deg.cpu().numpy(),)
+
+
+def rational_weights(dist, eps, sigma, p):
+    d = dist.astype(np.float64)
+    w = 1.0 / (1.0 + (d / sigma) ** 2) if p == 2.0 else 1.0 / (1.0 + np.power(d / sigma, p))
+    valid = (d <= eps) & (w > 1e-12)
+    return np.where(valid, w, 0.0), valid
+
+
+def test_union_golden_cosine_graph():
+    ip, ix, iv, deg = lap(GS["cos_idx"], GS["cos_w"], weight_kernel="given")
+    np.testing.assert_array_equal(ip, GS["lapu_indptr"])
+    np.testing.assert_array_equal(ix, GS["lapu_indices"])
+    np.testing.assert_array_equal(iv.view(np.uint64), GS["lapu_values"].view(np.uint64))
+
+
+@pytest.mark.parametrize("n,d,k", [(5000, 32, 10), (20000, 64, 32)])
+def test_union_from_l2_knn_rational_kernel(n, d, k):
+    X = datagen.uniform(n, d, seed=3)
+    idx, dist = O.knn_l2sq(X, k)
+    eps, sigma = 1e30, 4.0
+    ip, ix, iv, deg = lap(idx, dist, weight_kernel="rational", eps=eps, sigma=sigma, p=2.0)
+    w, valid = rational_weights(dist, eps, sigma, 2.0)
+    ridx = np.where(valid, idx, -1).astype(np.int32)
+    rip, rix, riv = O.laplacian_union(ridx, w)
+    np.testing.assert_array_equal(ip, rip)
+    np.testing.assert_array_equal(ix, rix)
+    np.testing.assert_array_equal(iv.view(np.uint64), riv.view(np.uint64))
+    # degrees == diagonal, rows sum to zero (reference invariant)
+    diag = np.array([iv[ip[i]:ip[i + 1]][ix[ip[i]:ip[i + 1]] == i][0] for i in range(0, n, 97)])
+    np.testing.assert_array_equal(diag, deg[::97])
+
+
+def test_union_eps_filter_and_hub_rows():
+    import surfface_hip as S
+    n, k = 12000, 4
+    rng = np.random.default_rng(0)
+    idx = rng.integers(0, n, size=(n, k)).astype(np.int32)
+    idx[:, 0] = 0        # node 0 is everybody's neighbour: in-degree ~ n (> 8192: dense path)
+    idx[:700, 1] = 1     # node 1: in-degree ~ 500 valid (block path)
+    idx[5, 2] = 5        # self loop dropped
+    idx[7, 3] = -1       # empty slot
+    dist = rng.uniform(0, 2.0, size=(n, k)).astype(np.float64)
+    ip, ix, iv, deg = lap(idx, dist, weight_kernel="rational", eps=1.5, sigma=0.7, p=3.0)
+    st = S.laplacian.last_stats()
+    assert st["hub_rows"] >= 1 and st["big_rows"] >= 2
+    d = dist
+    w = 1.0 / (1.0 + np.power(d / 0.7, 3.0))
+    valid = (d <= 1.5) & (w > 1e-12) & (idx >= 0)
+    rip, rix, riv = O.laplacian_union(np.where(valid, idx, -1).astype(np.int32), w)
+    np.testing.assert_array_equal(ip, rip)
+    np.testing.assert_array_equal(ix, rix)
+    # pow(x, 3) on the device vs glibc may differ in the last ulp: values within 4 ulp
+    np.testing.assert_allclose(iv, riv, rtol=1e-15, atol=0)
+
+
+@pytest.mark.parametrize("normalize", [True, False])
+def test_max_variant_vs_oracle(normalize):
+    X = datagen.clustered(3000, 24, seed=7, blobs=6)
+    idx, dist = O.knn_l2sq(X, 15)
+    w = (1.0 / (1.0 + dist.astype(np.float64))).astype(np.float32)
+    w[::17, 3] = 1e-10   # below the weight threshold: dropped
+    ip, ix, iv, deg = lap(idx, w, weight_kernel="given", symmetrise="max", normalize=normalize,
+                          weight_threshold=1e-9)
+    n, k = idx.shape
+    src = np.repeat(np.arange(n), k)
+    rip, rix, riv, rdeg, _ = O.laplacian_max(n, src, idx.ravel(), w.ravel(), thr=1e-9,
+                                             normalize=normalize)
+    np.testing.assert_array_equal(ip, rip)
+    np.testing.assert_array_equal(ix, rix)
+    np.testing.assert_allclose(iv, riv, rtol=1e-5, atol=1e-7)
+    np.testing.assert_allclose(deg, rdeg, rtol=1e-5)
+
+
+def test_laplacian_stage_output_properties():
+    import surfface_hip as S
+    X = datagen.uniform(800, 16, seed=2)
+    idx, dist = O.knn_l2sq(X, 15)
+    w = torch.from_numpy((1.0 / (1.0 + dist)).astype(np.float32)).cuda()
+    out = S.laplacian_stage_from_edges(torch.from_numpy(idx).cuda(), w,
+                                       S.LaplacianConfig(k_neighbors=15))
+    L = out.matrix.to_dense().astype(np.float64)
+    assert np.allclose(L, L.T, atol=1e-6)
+    assert np.allclose(np.diag(L), 1.0)
+    off = L - np.diag(np.diag(L))
+    assert (off <= 0).all()
+    assert out.nnz <= 800 * (2 * 15 + 1)
+    # null space L D^{1/2} 1 = 0 (surfface-core tests/test_laplacian.rs invariant)
+    assert np.abs(L @ np.sqrt(out.degrees.cpu().numpy().astype(np.float64))).max() < 1e-4
