@@ -173,6 +173,50 @@ int mn_laplacian_from_knn(const int32_t *nbr_idx, const void *nbr_val, int32_t v
 int mn_csr_free(mn_csr *m);
 int mn_lap_last_stats(mn_lap_stats *out);
 
+
+/* ---------------------------------------------------------------------- */
+/* K3 — energy row reductions (Rayleigh E, dispersion G, taumode lambda)  */
+/* ---------------------------------------------------------------------- */
+enum mn_g_mode {
+    MN_G_TAUMODE = 0,    /* ordered pairs, lambda = tau*E/(E+tau)+(1-tau)G
+                            (src_legacy/taumode.rs:261-408)                      */
+    MN_G_ENERGYMAPS = 1  /* j > i pairs, lambda = E (energymaps.rs:923-1045)     */
+};
+enum mn_tau_mode { MN_TAU_FIXED = 0, MN_TAU_MEDIAN = 1, MN_TAU_MEAN = 2, MN_TAU_PERCENTILE = 3 };
+
+typedef struct mn_energy_opts {
+    int32_t g_mode;     /* enum mn_g_mode                                        */
+    int32_t tau_mode;   /* enum mn_tau_mode (TauMode, taumode.rs:17-23; default Median) */
+    double tau_param;   /* Fixed(t) / Percentile(p) parameter                    */
+    int32_t timing;
+    int32_t reserved0;
+    void *stream;
+} mn_energy_opts;
+
+typedef struct mn_energy_stats {
+    int64_t entries;    /* Laplacian entries streamed per row                   */
+    int32_t symmetric;  /* 1: upper-triangle list with multiplicity 2           */
+    int32_t reserved0;
+    float ms_rows, ms_total;
+} mn_energy_stats;
+
+/* Items X [n][f] (f32, device) against the f x f feature Laplacian L (CSR,
+ * f64 values, device; e.g. from mn_laplacian_from_knn UNION): writes E, G,
+ * lambda [n] (f64, device, any may be NULL).  Replaces
+ * TauMode::compute_taumode_lambdas_parallel's per-item work
+ * (src_legacy/taumode.rs:117-250, 261-408) and node_energy_and_dispersion
+ * (src_legacy/energymaps.rs:923-1045).  Tolerance 1e-9 relative (the
+ * reference sums in rayon order).  f <= 4096. */
+int mn_energy_rows(const mn_csr *L, const float *X, int64_t n, int32_t f,
+                   const mn_energy_opts *opts, double *E, double *G, double *lambda);
+
+/* In place: src_legacy/core.rs:1341-1354 normalise_lambdas (min fold +inf,
+ * max fold 0.0, range floor 1e-9).  out_min_max_range_host (host, 3 doubles,
+ * may be NULL). */
+int mn_normalise_lambdas(double *lambda, int64_t n, double *out_min_max_range_host,
+                         void *stream);
+int mn_energy_last_stats(mn_energy_stats *out);
+
 #ifdef __cplusplus
 }
 #endif

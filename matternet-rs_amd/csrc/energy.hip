@@ -1,0 +1,457 @@
+// energy.hip — K3: per-row Rayleigh energy / Dirichlet dispersion / taumode
+// lambda against a sparse F x F feature Laplacian, and lambda normalisation.
+//
+// Reference semantics (per item row x, f32 storage widened to f64):
+//   src_legacy/taumode.rs:261-318 compute_synthetic_lambda
+//     zero vector (all |x_t| <= 1e-10) -> lambda 0;  tau = select_tau(x)
+//     (:29-70: Fixed / Mean / Median / Percentile over the row's values,
+//     floor 1e-10); lambda = tau*E/(E+tau) + (1-tau)*clamp(G,0,1)
+//   :326-361 E = max(0, sum_i sum_j x_i L_ij x_j / sum x^2)  (den > 1e-12)
+//   :366-408 G = sum over ordered pairs i != j of (e_ij/S)^2,
+//            e_ij = max(0,-L_ij)(x_i-x_j)^2, S = sum e_ij (S <= 1e-12 -> 0)
+//   src_legacy/energymaps.rs:923-1045 node_energy_and_dispersion: same E,
+//     G over j > i only (lambda := E)
+//   src_legacy/core.rs:1341-1354 normalise_lambdas (min fold +inf, max fold 0)
+//
+// Tolerance contract: rel 1e-9 — the reference itself sums E
+// in rayon par_bridge order.  Here: G = Q/S^2 with Q = sum e^2 (one pass,
+// algebraically identical to sum (e/S)^2, within ~nnz*u relative).
+//
+// GPU design: one wave per item row; the row is staged in LDS (f32) for the
+// x_j gathers and held in registers for the order statistics.  The Laplacian
+// is flattened once per call into an entry list (i, j, v, multiplicity): for
+// an exactly symmetric L only the upper triangle is kept with multiplicity 2
+// (half the gathers and f64 flops); the list lives in LDS, shared by the
+// block's waves.  tau = median via an exact wave-level radix select on the
+// sortable f32 keys (no sort).  f64 accumulation throughout.
+#include <algorithm>
+#include <climits>
+#include <cmath>
+#include <vector>
+
+#include "common.hpp"
+
+namespace mn {
+namespace energy {
+
+constexpr int WAVES = 4;
+constexpr int FMAX = 4096;            // row length limit (registers: FMAX/64 per lane)
+constexpr int EDGE_LDS_CAP = 4096;    // entries kept in LDS (12 B each => 48 KB)
+
+// ---- build the entry list from CSR --------------------------------------
+__global__ void k_check_sym(const int64_t *__restrict__ ip, const int32_t *__restrict__ ix,
+                            const double *__restrict__ v, int f, int *__restrict__ asym) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= f) return;
+    for (int64_t p = ip[i]; p < ip[i + 1]; ++p) {
+        const int j = ix[p];
+        if (j < 0 || j >= f) { atomicOr(asym, 2); return; }
+        if (j == i) continue;
+        // binary search (j, i) in row j
+        int64_t lo = ip[j], hi = ip[j + 1] - 1, hit = -1;
+        while (lo <= hi) {
+            const int64_t mid = (lo + hi) >> 1;
+            const int c = ix[mid];
+            if (c == i) { hit = mid; break; }
+            if (c < i) lo = mid + 1; else hi = mid - 1;
+        }
+        if (hit < 0 || v[hit] != v[p]) { atomicOr(asym, 1); return; }
+    }
+}
+
+__global__ void k_count_entries(const int64_t *__restrict__ ip, const int32_t *__restrict__ ix,
+                                int f, int sym, int32_t *__restrict__ cnt) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= f) return;
+    int c = 0;
+    for (int64_t p = ip[i]; p < ip[i + 1]; ++p)
+        if (!sym || ix[p] >= i) ++c;
+    cnt[i] = c;
+}
+
+// entry list: packed (i | j << 16) + value; multiplicity is implied:
+// 2 for off-diagonal entries of the symmetric (upper-triangle) list, else 1
+__global__ void k_fill_entries(const int64_t *__restrict__ ip, const int32_t *__restrict__ ix,
+                               const double *__restrict__ v, int f, int sym,
+                               const int64_t *__restrict__ off, uint32_t *__restrict__ eij,
+                               double *__restrict__ ev) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= f) return;
+    int64_t q = off[i];
+    for (int64_t p = ip[i]; p < ip[i + 1]; ++p) {
+        const int j = ix[p];
+        if (sym && j < i) continue;
+        eij[q] = (uint32_t)i | ((uint32_t)j << 16);
+        ev[q] = v[p];
+        ++q;
+    }
+}
+
+// ---- wave-level exact order statistic on f32 keys -------------------------
+__device__ __forceinline__ uint32_t f2key(float x) {
+    const uint32_t u = __float_as_uint(x);
+    return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ __forceinline__ float key2f(uint32_t k) {
+    const uint32_t u = (k & 0x80000000u) ? (k & 0x7FFFFFFFu) : ~k;
+    return __uint_as_float(u);
+}
+
+// rank-th smallest key (0-based) among keys[0..nr) per lane (all lanes' keys)
+template <int NR>
+__device__ uint32_t wave_select(const uint32_t (&keys)[NR], int nr, int rank, int *hist) {
+    const int lane = threadIdx.x & 63;
+    uint32_t prefix = 0, mask = 0;
+    int target = rank;
+#pragma unroll
+    for (int pass = 0; pass < 4; ++pass) {
+        const int shift = 24 - 8 * pass;
+        hist[lane * 4 + 0] = 0; hist[lane * 4 + 1] = 0;
+        hist[lane * 4 + 2] = 0; hist[lane * 4 + 3] = 0;
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int r = 0; r < NR; ++r)
+            if (r < nr && (keys[r] & mask) == prefix) atomicAdd(&hist[(keys[r] >> shift) & 255], 1);
+        __builtin_amdgcn_wave_barrier();
+        const int c0 = hist[lane * 4], c1 = hist[lane * 4 + 1], c2 = hist[lane * 4 + 2],
+                  c3 = hist[lane * 4 + 3];
+        const int tot = c0 + c1 + c2 + c3;
+        int incl = tot;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int y = __shfl_up(incl, o);
+            if (lane >= o) incl += y;
+        }
+        const int excl = incl - tot;
+        const bool mine = target >= excl && target < incl;
+        int bin = 0, before = excl;
+        if (mine) {
+            if (target < excl + c0) { bin = 0; }
+            else if (target < excl + c0 + c1) { bin = 1; before += c0; }
+            else if (target < excl + c0 + c1 + c2) { bin = 2; before += c0 + c1; }
+            else { bin = 3; before += c0 + c1 + c2; }
+        }
+        const uint64_t who = __ballot(mine);
+        const int src = (int)__builtin_ctzll(who);
+        const int b = __shfl(lane * 4 + bin, src);
+        const int bf = __shfl(before, src);
+        target -= bf;
+        prefix |= (uint32_t)b << shift;
+        mask |= 255u << shift;
+        __builtin_amdgcn_wave_barrier();
+    }
+    return prefix;
+}
+
+__device__ __forceinline__ double wave_sum(double x) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o);
+    return x;
+}
+
+template <int NR>
+struct alignas(16) EnergySmem {
+    double ev[EDGE_LDS_CAP];
+    uint32_t eij[EDGE_LDS_CAP];
+    float xs[WAVES][NR * 64];
+    int hist[WAVES][256];
+};
+
+template <int NR>
+__global__ __launch_bounds__(64 * WAVES) void k_energy_rows(
+    const float *__restrict__ X, int64_t n, int f, int64_t ne, int sym,
+    const uint32_t *__restrict__ geij, const double *__restrict__ gev, int g_mode, int tau_mode,
+    double tau_param, int pct_rank, double *__restrict__ Eo, double *__restrict__ Go,
+    double *__restrict__ Lo) {
+    __shared__ EnergySmem<NR> sm;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const bool in_lds = ne <= EDGE_LDS_CAP;
+    if (in_lds) {
+        for (int64_t p = threadIdx.x; p < ne; p += blockDim.x) {
+            sm.eij[p] = geij[p];
+            sm.ev[p] = gev[p];
+        }
+    }
+    __syncthreads();
+    const uint32_t *EIJ = in_lds ? sm.eij : geij;
+    const double *EV = in_lds ? sm.ev : gev;
+    float *xs = sm.xs[w];
+    const int64_t nw = (int64_t)gridDim.x * WAVES;
+    for (int64_t row = (int64_t)blockIdx.x * WAVES + w; row < n; row += nw) {
+        const float *xr = X + row * (int64_t)f;
+        float xv[NR];
+        uint32_t keys[NR];
+        double den = 0.0, msum = 0.0;
+        bool nonzero = false;
+#pragma unroll
+        for (int r = 0; r < NR; ++r) {
+            const int t = lane + 64 * r;
+            const float x = t < f ? xr[t] : 0.f;
+            xv[r] = x;
+            if (t < f) {
+                xs[t] = x;
+                const double xd = (double)x;
+                den += xd * xd;
+                msum += xd;
+                nonzero |= !(fabs(xd) <= 1e-10);
+            }
+            keys[r] = t < f ? f2key(x) : 0xFFFFFFFFu;
+        }
+        __builtin_amdgcn_wave_barrier();
+        den = wave_sum(den);
+        const bool any_nonzero = __any(nonzero);
+        double e_raw = 0.0, g_raw = 0.0, lam = 0.0;
+        if (g_mode == MN_G_TAUMODE && !any_nonzero) {
+            // zero vector (taumode.rs:268-274): lambda = 0
+        } else {
+            double num = 0.0, S = 0.0, Q = 0.0;
+            for (int64_t p = lane; p < ne; p += 64) {
+                const uint32_t ij = EIJ[p];
+                const int i = (int)(ij & 0xFFFFu), j = (int)(ij >> 16);
+                const double v = EV[p];
+                const double m = (sym && i != j) ? 2.0 : 1.0;
+                const double xi = (double)xs[i], xj = (double)xs[j];
+                num += m * ((xi * v) * xj);
+                const bool counts = (g_mode == MN_G_TAUMODE) ? (i != j) : (j > i);
+                const double wgt = -v;
+                if (counts && wgt > 0.0) {
+                    const double dd = xi - xj;
+                    const double e = wgt * dd * dd;
+                    const double sm_ = (g_mode == MN_G_TAUMODE) ? m : 1.0;
+                    S += sm_ * e;
+                    Q += sm_ * (e * e);
+                }
+            }
+            num = wave_sum(num);
+            S = wave_sum(S);
+            Q = wave_sum(Q);
+            e_raw = den > 1e-12 ? fmax(num / den, 0.0) : 0.0;
+            if (S > 1e-12) {
+                const double g = Q / (S * S);
+                g_raw = g < 0.0 ? 0.0 : (g > 1.0 ? 1.0 : g);
+            }
+            if (g_mode == MN_G_TAUMODE) {
+                double tau = 1e-10;
+                if (tau_mode == MN_TAU_FIXED) {
+                    tau = (isfinite(tau_param) && tau_param > 0.0) ? tau_param : 1e-10;
+                } else if (tau_mode == MN_TAU_MEAN) {
+                    const double mean = wave_sum(msum) / (double)f;
+                    tau = fmax(mean, 1e-10);
+                } else {
+                    int rank;
+                    if (tau_mode == MN_TAU_PERCENTILE) rank = pct_rank;
+                    else rank = (f % 2 == 1) ? f / 2 : f / 2 - 1;
+                    const uint32_t ka = wave_select<NR>(keys, NR, rank, sm.hist[w]);
+                    double med = (double)key2f(ka);
+                    if (tau_mode == MN_TAU_MEDIAN && f % 2 == 0) {
+                        // element rank+1: equal to a if >= rank+2 keys are <= ka, else min{key > ka}
+                        int le = 0;
+                        uint32_t nxt = 0xFFFFFFFFu;
+#pragma unroll
+                        for (int r = 0; r < NR; ++r) {
+                            const int t = lane + 64 * r;
+                            if (t < f) {
+                                le += keys[r] <= ka ? 1 : 0;
+                                if (keys[r] > ka && keys[r] < nxt) nxt = keys[r];
+                            }
+                        }
+#pragma unroll
+                        for (int o = 32; o > 0; o >>= 1) {
+                            le += __shfl_xor(le, o);
+                            const uint32_t on = __shfl_xor(nxt, o);
+                            nxt = on < nxt ? on : nxt;
+                        }
+                        const double b = (le >= rank + 2) ? med : (double)key2f(nxt);
+                        med = 0.5 * (med + b);
+                    }
+                    tau = fmax(med, 1e-10);
+                }
+                const double eb = e_raw / (e_raw + tau);
+                lam = tau * eb + (1.0 - tau) * g_raw;
+            } else {
+                lam = e_raw;
+            }
+        }
+        if (lane == 0) {
+            if (Eo) Eo[row] = e_raw;
+            if (Go) Go[row] = g_raw;
+            if (Lo) Lo[row] = lam;
+        }
+        __builtin_amdgcn_wave_barrier();
+    }
+}
+
+// ---- normalise_lambdas -------------------------------------------------
+__device__ __forceinline__ unsigned long long d2key(double x) {
+    const unsigned long long u = (unsigned long long)__double_as_longlong(x);
+    return (u >> 63) ? ~u : (u | 0x8000000000000000ull);
+}
+__device__ __forceinline__ double key2d(unsigned long long k) {
+    const unsigned long long u = (k >> 63) ? (k & 0x7FFFFFFFFFFFFFFFull) : ~k;
+    return __longlong_as_double((long long)u);
+}
+
+__global__ __launch_bounds__(256) void k_minmax(const double *__restrict__ lam, int64_t n,
+                                                unsigned long long *__restrict__ mm) {
+    unsigned long long mn = ~0ull, mx = 0ull;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const double v = lam[i];
+        if (v != v) continue;  // f64::min / f64::max ignore NaN
+        const unsigned long long k = d2key(v);
+        mn = k < mn ? k : mn;
+        mx = k > mx ? k : mx;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const unsigned long long a = __shfl_xor(mn, o), b = __shfl_xor(mx, o);
+        mn = a < mn ? a : mn;
+        mx = b > mx ? b : mx;
+    }
+    if ((threadIdx.x & 63) == 0) {
+        atomicMin(&mm[0], mn);
+        atomicMax(&mm[1], mx);
+    }
+}
+
+__global__ __launch_bounds__(256) void k_normalise(double *__restrict__ lam, int64_t n,
+                                                   const unsigned long long *__restrict__ mm,
+                                                   double *__restrict__ out3) {
+    const double mnv = mm[0] == ~0ull ? __builtin_inf() : key2d(mm[0]);
+    double mxv = mm[1] == 0ull ? 0.0 : key2d(mm[1]);
+    mxv = fmax(mxv, 0.0);  // core.rs:1343 max fold starts at 0.0
+    const double range = fmax(mxv - mnv, 1e-9);
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) lam[i] = (lam[i] - mnv) / range;
+    if (i == 0 && out3) { out3[0] = mnv; out3[1] = mxv; out3[2] = range; }
+}
+
+}  // namespace energy
+
+static thread_local mn_energy_stats t_energy_stats{};
+
+static int energy_impl(const mn_csr *L, const float *X, int64_t n, int32_t f,
+                       const mn_energy_opts *opts, double *E, double *G, double *lam) {
+    using namespace energy;
+    clear_error();
+    t_energy_stats = mn_energy_stats{};
+    MN_REQUIRE(L && opts && X, MN_EINVAL, "mn_energy_rows: NULL argument");
+    MN_REQUIRE(f >= 1 && f <= FMAX && n >= 0, MN_EINVAL,
+               "mn_energy_rows: f=%d outside [1,%d]", f, FMAX);
+    MN_REQUIRE(L->n_rows == f && L->n_cols == f, MN_EINVAL,
+               "mn_energy_rows: Laplacian must be f x f (feature space), got %lld x %lld",
+               (long long)L->n_rows, (long long)L->n_cols);
+    MN_REQUIRE(L->value_type == MN_F64, MN_ENOTSUP,
+               "mn_energy_rows: Laplacian values must be f64 (legacy GraphLaplacian)");
+    MN_REQUIRE(opts->g_mode == MN_G_TAUMODE || opts->g_mode == MN_G_ENERGYMAPS, MN_EINVAL,
+               "mn_energy_rows: unknown g_mode");
+    MN_REQUIRE(opts->tau_mode >= MN_TAU_FIXED && opts->tau_mode <= MN_TAU_PERCENTILE, MN_EINVAL,
+               "mn_energy_rows: unknown tau_mode");
+    hipStream_t s = (hipStream_t)opts->stream;
+    if (n == 0) return MN_OK;
+    const int64_t nnz = L->nnz;
+    char *g = (char *)scratch(kSlotGeneric0, (size_t)nnz * 12 + (size_t)(f + 1) * 12 + 256);
+    MN_REQUIRE(g, MN_ENOMEM, "mn_energy_rows: scratch allocation failed");
+    uint32_t *eij = (uint32_t *)g;
+    int32_t *cnt = (int32_t *)(eij + nnz);
+    double *ev = (double *)(((uintptr_t)(cnt + f) + 15) & ~(uintptr_t)15);
+    int64_t *off = (int64_t *)(ev + nnz);
+    int *flag = (int *)(off + (f + 1));
+
+    Timer tm;
+    tm.start(opts->timing != 0, s);
+    MN_HIP_TRY(hipMemsetAsync(flag, 0, 8, s));
+    const unsigned fb = (unsigned)((f + 255) / 256);
+    hipLaunchKernelGGL(k_check_sym, dim3(fb), dim3(256), 0, s, L->indptr, L->indices,
+                       (const double *)L->values, f, flag);
+    int hflag = 0;
+    MN_HIP_TRY(hipMemcpyAsync(&hflag, flag, 4, hipMemcpyDeviceToHost, s));
+    MN_HIP_TRY(hipStreamSynchronize(s));
+    MN_REQUIRE(!(hflag & 2), MN_EINVAL, "mn_energy_rows: Laplacian column index out of range");
+    const int sym = (hflag & 1) ? 0 : 1;
+    hipLaunchKernelGGL(k_count_entries, dim3(fb), dim3(256), 0, s, L->indptr, L->indices, f, sym,
+                       cnt);
+    // tiny scan on the host side of the stream (f <= 4096)
+    std::vector<int32_t> hc(f);
+    std::vector<int64_t> ho(f + 1);
+    MN_HIP_TRY(hipMemcpyAsync(hc.data(), cnt, 4 * (size_t)f, hipMemcpyDeviceToHost, s));
+    MN_HIP_TRY(hipStreamSynchronize(s));
+    ho[0] = 0;
+    for (int i = 0; i < f; ++i) ho[i + 1] = ho[i] + hc[i];
+    const int64_t ne = ho[f];
+    MN_HIP_TRY(hipMemcpyAsync(off, ho.data(), 8 * (size_t)(f + 1), hipMemcpyHostToDevice, s));
+    hipLaunchKernelGGL(k_fill_entries, dim3(fb), dim3(256), 0, s, L->indptr, L->indices,
+                       (const double *)L->values, f, sym, off, eij, ev);
+    // finite check of X (the reference's order statistics filter non-finite
+    // values; a NaN/inf item is rejected here instead)
+    int pct_rank = 0;
+    if (opts->tau_mode == MN_TAU_PERCENTILE) {
+        double pp = opts->tau_param;
+        pp = pp != pp ? pp : (pp < 0.0 ? 0.0 : (pp > 1.0 ? 1.0 : pp));
+        const double fi = std::round((double)(f - 1) * pp);  // f64::round
+        pct_rank = (fi != fi || fi < 0) ? 0 : (int)std::min<double>(fi, f - 1);
+    }
+    tm.mark();
+    const int64_t blocks = std::min<int64_t>((n + WAVES - 1) / WAVES, 2048);
+    const int nr = (f + 63) / 64;
+#define MN_ER(NRV)                                                                              \
+    hipLaunchKernelGGL(k_energy_rows<NRV>, dim3((unsigned)blocks), dim3(64 * WAVES), 0, s, X,   \
+                       n, f, ne, sym, eij, ev, opts->g_mode, opts->tau_mode, opts->tau_param,   \
+                       pct_rank, E, G, lam)
+    if (nr <= 4) MN_ER(4);
+    else if (nr <= 8) MN_ER(8);
+    else if (nr <= 12) MN_ER(12);
+    else if (nr <= 16) MN_ER(16);
+    else if (nr <= 32) MN_ER(32);
+    else MN_ER(64);  // f <= 4096
+#undef MN_ER
+    MN_HIP_TRY(hipGetLastError());
+    tm.mark();
+    MN_HIP_TRY(hipStreamSynchronize(s));
+    t_energy_stats.entries = ne;
+    t_energy_stats.symmetric = sym;
+    t_energy_stats.ms_rows = tm.ms(1, 2);
+    t_energy_stats.ms_total = tm.ms(0, 2);
+    return MN_OK;
+}
+
+}  // namespace mn
+
+extern "C" {
+
+int mn_energy_rows(const mn_csr *L, const float *X, int64_t n, int32_t f,
+                   const mn_energy_opts *opts, double *E, double *G, double *lambda) {
+    return mn::energy_impl(L, X, n, f, opts, E, G, lambda);
+}
+
+int mn_normalise_lambdas(double *lambda, int64_t n, double *out_min_max_range_host,
+                         void *stream) {
+    mn::clear_error();
+    MN_REQUIRE(lambda || n == 0, MN_EINVAL, "mn_normalise_lambdas: NULL lambda");
+    hipStream_t s = (hipStream_t)stream;
+    unsigned long long *mm = (unsigned long long *)mn::scratch(mn::kSlotFlags, 64);
+    MN_REQUIRE(mm, MN_ENOMEM, "mn_normalise_lambdas: scratch allocation failed");
+    double *o3 = (double *)(mm + 2);
+    unsigned long long init[2] = {~0ull, 0ull};
+    MN_HIP_TRY(hipMemcpyAsync(mm, init, 16, hipMemcpyHostToDevice, s));
+    if (n > 0) {
+        const int64_t blocks = std::min<int64_t>((n + 255) / 256, 1024);
+        hipLaunchKernelGGL(mn::energy::k_minmax, dim3((unsigned)blocks), dim3(256), 0, s, lambda, n,
+                           mm);
+    }
+    hipLaunchKernelGGL(mn::energy::k_normalise, dim3((unsigned)std::max<int64_t>(1, (n + 255) / 256)),
+                       dim3(256), 0, s, lambda, n, mm, o3);
+    MN_HIP_TRY(hipGetLastError());
+    if (out_min_max_range_host)
+        MN_HIP_TRY(hipMemcpyAsync(out_min_max_range_host, o3, 24, hipMemcpyDeviceToHost, s));
+    MN_HIP_TRY(hipStreamSynchronize(s));
+    return MN_OK;
+}
+
+int mn_energy_last_stats(mn_energy_stats *out) {
+    if (!out) return MN_EINVAL;
+    *out = mn::t_energy_stats;
+    return MN_OK;
+}
+
+}  // extern "C"

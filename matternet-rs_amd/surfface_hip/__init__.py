@@ -5,7 +5,9 @@ Every op runs on the GPU through the C ABI; there is no CPU fallback.
 """
 from . import _lib
 from ._lib import MnError, lib
-from . import laplacian
+from . import energy, laplacian
+from .energy import (TauMode, compute_taumode_lambdas, energy_rows, node_energy_and_dispersion,
+                     normalise_lambdas)
 from .laplacian import (CsrMatrix, GraphParams, LaplacianConfig, LaplacianOutput,
                         build_laplacian_from_knn, laplacian_stage_from_edges)
 from .knn import (DistanceMetric, KnnResult, build_candidate_graph, knn_l2sq, knn_l2sq_qc,
@@ -14,4 +16,6 @@ from .knn import (DistanceMetric, KnnResult, build_candidate_graph, knn_l2sq, kn
 __all__ = ["MnError", "lib", "DistanceMetric", "KnnResult", "build_candidate_graph", "knn_l2sq",
            "knn_l2sq_qc", "last_stats", "merge_parts", "CsrMatrix", "GraphParams",
            "LaplacianConfig", "LaplacianOutput", "build_laplacian_from_knn",
-           "laplacian_stage_from_edges", "laplacian"]
+           "laplacian_stage_from_edges", "laplacian", "energy", "TauMode",
+           "compute_taumode_lambdas", "energy_rows", "node_energy_and_dispersion",
+           "normalise_lambdas"]

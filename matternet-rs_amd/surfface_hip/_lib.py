@@ -65,6 +65,23 @@ class LapStats(C.Structure):
         return {f: getattr(self, f) for f, _ in self._fields_ if f != "reserved0"}
 
 
+MN_G_TAUMODE, MN_G_ENERGYMAPS = 0, 1
+MN_TAU_FIXED, MN_TAU_MEDIAN, MN_TAU_MEAN, MN_TAU_PERCENTILE = 0, 1, 2, 3
+
+
+class EnergyOpts(C.Structure):
+    _fields_ = [("g_mode", C.c_int32), ("tau_mode", C.c_int32), ("tau_param", C.c_double),
+                ("timing", C.c_int32), ("reserved0", C.c_int32), ("stream", C.c_void_p)]
+
+
+class EnergyStats(C.Structure):
+    _fields_ = [("entries", C.c_int64), ("symmetric", C.c_int32), ("reserved0", C.c_int32),
+                ("ms_rows", C.c_float), ("ms_total", C.c_float)]
+
+    def as_dict(self):
+        return {f: getattr(self, f) for f, _ in self._fields_ if f != "reserved0"}
+
+
 P = C.c_void_p
 I64 = C.c_int64
 I32 = C.c_int32
@@ -87,6 +104,9 @@ SIGNATURES = {
     "mn_laplacian_from_knn": (C.c_int, [P, P, I32, I64, I32, C.POINTER(LapOpts), C.POINTER(Csr), P]),
     "mn_csr_free": (C.c_int, [C.POINTER(Csr)]),
     "mn_lap_last_stats": (C.c_int, [C.POINTER(LapStats)]),
+    "mn_energy_rows": (C.c_int, [C.POINTER(Csr), P, I64, I32, C.POINTER(EnergyOpts), P, P, P]),
+    "mn_normalise_lambdas": (C.c_int, [P, I64, P, P]),
+    "mn_energy_last_stats": (C.c_int, [C.POINTER(EnergyStats)]),
 }
 
 _LIB = None

@@ -1,0 +1,118 @@
+"""K3 parity on the GPU: HIP energy rows (C ABI) vs the CPU oracle.
+
+Contract: E, G, lambda within 1e-9 relative (abs 1e-12 near
+0) — the reference sums in rayon par_bridge order; normalise_lambdas uses the
+same min/max so its outputs inherit that tolerance.
+"""
+import numpy as np
+import pytest
+import torch
+
+import datagen
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+GS = np.load(__import__("os").path.join(__import__("os").path.dirname(__file__), "golden",
+                                        "golden_small.npz"))
+RTOL, ATOL = 1e-9, 1e-12
+
+
+def csr_dev(ip, ix, iv):
+    import surfface_hip as S
+    n = len(ip) - 1
+    return S.CsrMatrix(torch.from_numpy(ip.astype(np.int64)).cuda(),
+                       torch.from_numpy(ix.astype(np.int32)).cuda(),
+                       torch.from_numpy(iv.astype(np.float64)).cuda(), (n, n))
+
+
+def feature_laplacian(f=768, profile=1500, topk=4, seed=9):
+    """F x F union Laplacian from the rectified-cosine kNN of the feature
+    columns (graph.rs:214 builds the Laplacian on the transposed centroids)."""
+    P = datagen.uniform(profile, f, seed=seed)
+    idx, dist, w = O.knn_cos(np.ascontiguousarray(P.T), topk, eps=1.0, sigma=1.0, p=2.0)
+    return O.laplacian_union(idx, w)
+
+
+def run(X, ip, ix, iv, g_mode, tau):
+    import surfface_hip as S
+    E, G, lam = S.energy_rows(torch.from_numpy(X).cuda(), csr_dev(ip, ix, iv), g_mode, tau)
+    return E.cpu().numpy(), G.cpu().numpy(), lam.cpu().numpy()
+
+
+def test_golden_taumode_rows():
+    import surfface_hip as S
+    E, G, lam = run(GS["energy_X"], GS["lapu_indptr"], GS["lapu_indices"], GS["lapu_values"],
+                    0, S.TauMode.Median)
+    np.testing.assert_allclose(E, GS["energy_E"], rtol=RTOL, atol=ATOL)
+    np.testing.assert_allclose(G, GS["energy_G"], rtol=RTOL, atol=ATOL)
+    np.testing.assert_allclose(lam, GS["energy_lambda"], rtol=RTOL, atol=ATOL)
+    assert lam[3] == 0.0
+
+
+@pytest.mark.parametrize("tau", ["median", "mean", "pct", "fixed"])
+def test_taumode_768_features(tau):
+    import surfface_hip as S
+    ip, ix, iv = feature_laplacian()
+    X = datagen.uniform(20000, 768, seed=21)
+    X[5] = 0.0
+    X[6] = 3.0  # constant row: G = 0
+    X[7, ::2] = 0.25  # many ties for the order statistics
+    tm = {"median": (S.TauMode.Median, O.TAU_MEDIAN, 0.0),
+          "mean": (S.TauMode.Mean, O.TAU_MEAN, 0.0),
+          "pct": (S.TauMode.Percentile(0.3), O.TAU_PERCENTILE, 0.3),
+          "fixed": (S.TauMode.Fixed(0.2), O.TAU_FIXED, 0.2)}[tau]
+    E, G, lam = run(X, ip, ix, iv, 0, tm[0])
+    rE, rG, rl = O.energy_rows(X, ip, ix, iv, O.G_TAUMODE, tm[1], tm[2])
+    np.testing.assert_allclose(E, rE, rtol=RTOL, atol=ATOL)
+    np.testing.assert_allclose(G, rG, rtol=RTOL, atol=ATOL)
+    np.testing.assert_allclose(lam, rl, rtol=RTOL, atol=ATOL)
+    assert lam[5] == 0.0 and G[6] == 0.0
+
+
+def test_odd_feature_count_and_energymaps_mode():
+    import surfface_hip as S
+    ip, ix, iv = feature_laplacian(f=301, profile=800, topk=5, seed=4)
+    X = datagen.clustered(5000, 301, seed=3, blobs=4)
+    for gm, og in ((0, O.G_TAUMODE), (1, O.G_ENERGYMAPS)):
+        E, G, lam = run(X, ip, ix, iv, gm, S.TauMode.Median)
+        rE, rG, rl = O.energy_rows(X, ip, ix, iv, og, O.TAU_MEDIAN)
+        np.testing.assert_allclose(E, rE, rtol=RTOL, atol=ATOL)
+        np.testing.assert_allclose(G, rG, rtol=RTOL, atol=ATOL)
+        np.testing.assert_allclose(lam, rl, rtol=RTOL, atol=ATOL)
+
+
+def test_nonsymmetric_laplacian_path():
+    import surfface_hip as S
+    ip, ix, iv = feature_laplacian(f=200, profile=600, topk=3, seed=2)
+    iv = iv.copy()
+    iv[5] *= 1.5  # break exact symmetry: the kernel must stream all entries
+    X = datagen.uniform(3000, 200, seed=8)
+    E, G, lam = run(X, ip, ix, iv, 0, S.TauMode.Median)
+    assert S.energy.last_stats()["symmetric"] == 0
+    rE, rG, rl = O.energy_rows(X, ip, ix, iv, O.G_TAUMODE, O.TAU_MEDIAN)
+    np.testing.assert_allclose(lam, rl, rtol=RTOL, atol=ATOL)
+
+
+def test_known_answer_chain_and_constant_rows():
+    import surfface_hip as S
+    # surfface-core tests/test_spectral.rs:187-251 chain graph 0-1-2
+    ip = np.array([0, 2, 5, 7]); ix = np.array([0, 1, 0, 1, 2, 1, 2])
+    iv = np.array([1.0, -1.0, -1.0, 2.0, -1.0, -1.0, 1.0])
+    X = np.array([[1, 1, 1], [1, 0, -1]], np.float32)
+    E, G, lam = run(X, ip, ix, iv, 0, S.TauMode.Median)
+    assert abs(E[0]) < 1e-12 and G[0] == 0.0 and lam[1] > lam[0]
+
+
+def test_normalise_lambdas_vs_oracle():
+    import surfface_hip as S
+    lam = np.random.default_rng(0).normal(size=100_001)
+    t = torch.from_numpy(lam.copy()).cuda()
+    _, mn, mx, rg = S.normalise_lambdas(t)
+    r, rmn, rmx, rrg = O.normalise_lambdas(lam)
+    assert (mn, mx, rg) == (rmn, rmx, rrg)
+    np.testing.assert_array_equal(t.cpu().numpy(), r)
+    # all-negative input: max fold starts at 0.0 (core.rs:1343)
+    t = torch.tensor([-1.0, -3.0, -2.0], dtype=torch.float64).cuda()
+    S.normalise_lambdas(t)
+    np.testing.assert_allclose(t.cpu().numpy(), [2 / 3, 0.0, 1 / 3], atol=1e-15)
