@@ -217,6 +217,21 @@ int mn_normalise_lambdas(double *lambda, int64_t n, double *out_min_max_range_ho
                          void *stream);
 int mn_energy_last_stats(mn_energy_stats *out);
 
+
+/* ---------------------------------------------------------------------- */
+/* K4 — lambda-sorted index                                               */
+/* ---------------------------------------------------------------------- */
+/* SortedLambdas::build_from + to_vec (src_legacy/sorted_index.rs:22-54):
+ * order_out[r] (device, int64) = item index at rank r, ascending
+ * OrderedFloat(lambda) (NaN greatest, -0.0 == +0.0) with ties ordered by the
+ * DECIMAL STRING of the index ("10" < "2"); key_out[r] (device, may be NULL)
+ * = the bucket key (lambda of the smallest index in the equal class);
+ * std_out_host (host, may be NULL) = std_deviation (laplacian.rs:421-448),
+ * bit-exact (sequential fold on one device thread).  Order bit-exact given
+ * identical lambdas. */
+int mn_sorted_index(const double *lambda, int64_t n, int64_t *order_out, double *key_out,
+                    double *std_out_host, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -120,6 +120,12 @@ __device__ __forceinline__ void wave_bitonic_sort(T (&d)[NR], int (&ix)[NR]) {
     }
 }
 
+// Correctly rounded f32 square root.  On gfx950 / ROCm 7.2 both sqrtf() and
+// __fsqrt_rn() are NOT correctly rounded (measured: 1-ulp misses, e.g.
+// sqrt(0x3da6a80c)); the f64 square root rounded to f32 is (53 >= 2*24+2, so
+// the double rounding is innocuous) and matches Rust's IEEE f32::sqrt.
+__device__ __forceinline__ float sqrt_rn_f32(float x) { return (float)__builtin_sqrt((double)x); }
+
 // Read element `pos` of a register-distributed array (wave-uniform pos).
 template <int NR, typename T>
 __device__ __forceinline__ T wave_elem(const T (&d)[NR], int pos) {

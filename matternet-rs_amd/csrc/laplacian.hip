@@ -335,7 +335,7 @@ __global__ __launch_bounds__(256) void k_degrees(const int64_t *__restrict__ off
 }
 
 __device__ __forceinline__ float max_offdiag(float w, float di, float dj, int normalize) {
-    return normalize ? -w / sqrtf(di * dj) : -w;
+    return normalize ? -w / sqrt_rn_f32(di * dj) : -w;
 }
 
 __global__ __launch_bounds__(256) void k_kept(const int64_t *__restrict__ offs,

@@ -5,6 +5,7 @@
 
 namespace mn {
 namespace scan {
+namespace {  // internal linkage: this header is included by several TUs
 
 constexpr int SB = 1024;  // elements per block (256 threads x 4)
 
@@ -99,5 +100,6 @@ inline hipError_t exclusive_scan(const T *in, int64_t n, int64_t *out, int64_t *
     return hipGetLastError();
 }
 
+}  // namespace
 }  // namespace scan
 }  // namespace mn

@@ -1,0 +1,261 @@
+// sorted_index.hip — K4: the lambda-sorted index (SortedLambdas).
+//
+// Reference semantics (src_legacy/sorted_index.rs:22-54, core.rs:938-940):
+//   build_from(lambdas): for i ascending, zadd(lambda_i, i, i.to_string());
+//   BTreeMap<OrderedFloat<f64>, bucket> => ascending OrderedFloat order (all
+//   NaN equal and greatest, -0.0 == +0.0); inside a bucket the entries are
+//   re-sorted by the decimal-string id after every insert => ties ordered by
+//   the string ("10" < "2").  to_vec() yields (bucket key, idx), where the key
+//   is the first-inserted (smallest idx) lambda of the bucket.
+//   std_dev: laplacian.rs:421-448 std_deviation (f64 sum -> f32 mean, f32
+//   squared deviations).
+//
+// GPU design: every element gets a unique composite key
+//   (sortable 64-bit OrderedFloat key of lambda, lexrank(idx)) where
+//   lexrank(i) is the rank of i's decimal string among "0".."N-1", computed in
+//   closed form per element (digit DP, no strings) — so the BTreeMap +
+//   per-insert bucket re-sort (quadratic under ties, Appendix B.10) becomes ONE
+//   bitonic sort: LDS-fused stages for j < 2048, global stages above.
+//   Bit-exact order given identical lambdas.
+#include <algorithm>
+#include <climits>
+
+#include "common.hpp"
+#include "scan.hpp"
+
+namespace mn {
+namespace sidx {
+
+struct alignas(16) Key {
+    unsigned long long k1;  // OrderedFloat key
+    uint32_t k2;            // lexrank(idx)
+    uint32_t idx;
+};
+
+__device__ __forceinline__ bool key_lt(const Key &a, const Key &b) {
+    return a.k1 < b.k1 || (a.k1 == b.k1 && a.k2 < b.k2);
+}
+
+// OrderedFloat<f64> total order: -0 == +0, every NaN equal and greatest
+__device__ __forceinline__ unsigned long long of_key(double x) {
+    if (x != x) return ~0ull;
+    if (x == 0.0) x = 0.0;  // canonicalise -0.0
+    const unsigned long long u = (unsigned long long)__double_as_longlong(x);
+    return (u >> 63) ? ~u : (u | 0x8000000000000000ull);
+}
+
+// numbers in [0, N) whose decimal string starts with the digits of v (v > 0)
+__device__ __forceinline__ int64_t count_with_prefix(int64_t v, int64_t N) {
+    int64_t c = 0, lo = v, hi = v;
+    while (lo < N) {
+        c += min(hi, N - 1) - lo + 1;
+        if (lo > (INT64_MAX - 9) / 10) break;
+        lo *= 10;
+        hi = hi * 10 + 9;
+    }
+    return c;
+}
+
+// rank of str(i) among {str(0), ..., str(N-1)} in byte-lexicographic order
+__device__ int64_t lexrank(int64_t i, int64_t N) {
+    if (i == 0) return 0;
+    int dig[20];
+    int L = 0;
+    for (int64_t t = i; t > 0; t /= 10) dig[L++] = (int)(t % 10);
+    // digits most-significant first: dig[L-1] ... dig[0]
+    int64_t r = (L - 1) + 1;  // proper prefixes + "0"
+    int64_t pre = 0;
+    for (int p = 0; p < L; ++p) {
+        const int sp = dig[L - 1 - p];
+        for (int c = (p == 0 ? 1 : 0); c < sp; ++c) r += count_with_prefix(pre * 10 + c, N);
+        pre = pre * 10 + sp;
+    }
+    return r;
+}
+
+__global__ __launch_bounds__(256) void k_make_keys(const double *__restrict__ lam, int64_t n,
+                                                   int64_t P, Key *__restrict__ keys) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= P) return;
+    Key k;
+    if (i < n) {
+        k.k1 = of_key(lam[i]);
+        k.k2 = (uint32_t)lexrank(i, n);
+        k.idx = (uint32_t)i;
+    } else {  // padding sorts last
+        k.k1 = ~0ull;
+        k.k2 = 0xFFFFFFFFu;
+        k.idx = 0xFFFFFFFFu;
+    }
+    keys[i] = k;
+}
+
+constexpr int TILE = 2048;  // LDS-fused bitonic tile (32 KB of keys)
+
+// all stages with j < TILE for a given kk (and the full local sort when kk <= TILE)
+__global__ __launch_bounds__(1024) void k_bitonic_local(Key *__restrict__ keys, int64_t P,
+                                                        int64_t kk_from, int64_t kk_to) {
+    __shared__ Key sm[TILE];
+    const int64_t base = (int64_t)blockIdx.x * TILE;
+    for (int e = threadIdx.x; e < TILE; e += blockDim.x) sm[e] = keys[base + e];
+    __syncthreads();
+    for (int64_t kk = kk_from; kk <= kk_to; kk <<= 1) {
+        const int jstart = (int)((kk >> 1) < (int64_t)(TILE >> 1) ? (kk >> 1) : (TILE >> 1));
+        for (int j = jstart; j > 0; j >>= 1) {
+            for (int e = threadIdx.x; e < TILE; e += blockDim.x) {
+                const int pe = e ^ j;
+                if (pe > e) {
+                    const int64_t ge = base + e;
+                    const bool asc = (ge & kk) == 0;
+                    const bool sw = asc ? key_lt(sm[pe], sm[e]) : key_lt(sm[e], sm[pe]);
+                    if (sw) { Key t = sm[e]; sm[e] = sm[pe]; sm[pe] = t; }
+                }
+            }
+            __syncthreads();
+        }
+    }
+    for (int e = threadIdx.x; e < TILE; e += blockDim.x) keys[base + e] = sm[e];
+}
+
+__global__ __launch_bounds__(256) void k_bitonic_global(Key *__restrict__ keys, int64_t P,
+                                                        int64_t kk, int64_t j) {
+    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= P) return;
+    const int64_t pe = e ^ j;
+    if (pe <= e) return;
+    const bool asc = (e & kk) == 0;
+    const Key a = keys[e], b = keys[pe];
+    const bool sw = asc ? key_lt(b, a) : key_lt(a, b);
+    if (sw) { keys[e] = b; keys[pe] = a; }
+}
+
+// run starts (bucket boundaries) + per-run min index for the bucket key
+__global__ __launch_bounds__(256) void k_run_flags(const Key *__restrict__ keys, int64_t n,
+                                                   int32_t *__restrict__ start) {
+    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= n) return;
+    start[r] = (r == 0 || keys[r].k1 != keys[r - 1].k1) ? 1 : 0;
+}
+__global__ __launch_bounds__(256) void k_run_min(const Key *__restrict__ keys, int64_t n,
+                                                 const int32_t *__restrict__ start,
+                                                 const int64_t *__restrict__ pos,
+                                                 unsigned *__restrict__ run_min) {
+    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= n) return;
+    const int64_t run = pos[r] + start[r] - 1;  // inclusive scan - 1
+    atomicMin(&run_min[run], keys[r].idx);
+}
+__global__ __launch_bounds__(256) void k_emit(const Key *__restrict__ keys, int64_t n,
+                                              const int32_t *__restrict__ start,
+                                              const int64_t *__restrict__ pos,
+                                              const unsigned *__restrict__ run_min,
+                                              const double *__restrict__ lam,
+                                              int64_t *__restrict__ order,
+                                              double *__restrict__ key_out) {
+    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= n) return;
+    order[r] = keys[r].idx;
+    if (key_out) {
+        const int64_t run = pos[r] + start[r] - 1;
+        key_out[r] = lam[run_min[run]];
+    }
+}
+
+// laplacian.rs:421-448 std_deviation, reproduced bit-for-bit: the reference
+// folds sequentially (f64 sum -> f32 mean, then an f32 sum of squared
+// deviations), and no parallel order reproduces that rounding, so one thread
+// walks the array (loads unrolled ahead of the dependent adds).
+__global__ __launch_bounds__(64) void k_std_exact(const double *__restrict__ lam, int64_t n,
+                                                  float *__restrict__ out) {
+    if (threadIdx.x != 0) return;
+    double s = -0.0;
+    int64_t i = 0;
+    for (; i + 8 <= n; i += 8) {
+        double v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = lam[i + u];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) s = s + v[u];
+    }
+    for (; i < n; ++i) s = s + lam[i];
+    const float mean = __fdiv_rn((float)s, (float)n);
+    float var = -0.0f;
+    for (i = 0; i + 8 <= n; i += 8) {
+        double v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = lam[i + u];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const float d = mean - (float)v[u];
+            var = var + d * d;
+        }
+    }
+    for (; i < n; ++i) {
+        const float d = mean - (float)lam[i];
+        var = var + d * d;
+    }
+    *out = sqrt_rn_f32(__fdiv_rn(var, (float)n));
+}
+
+inline unsigned grid(int64_t n, int t = 256) {
+    return (unsigned)std::max<int64_t>(1, (n + t - 1) / t);
+}
+
+}  // namespace sidx
+
+static int sorted_index_impl(const double *lam, int64_t n, int64_t *order, double *key_out,
+                             double *std_host, void *stream) {
+    using namespace sidx;
+    clear_error();
+    MN_REQUIRE(n >= 0 && (n == 0 || (lam && order)), MN_EINVAL, "mn_sorted_index: bad args");
+    MN_REQUIRE(n <= 0xFFFFFFFELL, MN_EINVAL, "mn_sorted_index: n too large");
+    hipStream_t s = (hipStream_t)stream;
+    if (n == 0) return MN_OK;
+    int64_t P = TILE;
+    while (P < n) P <<= 1;
+    Key *keys = (Key *)scratch(kSlotGeneric1, sizeof(Key) * (size_t)P);
+    char *aux = (char *)scratch(kSlotGeneric2, (size_t)n * 16 + ((size_t)n / scan::SB + 2) * 8 + 64);
+    MN_REQUIRE(keys && aux, MN_ENOMEM, "mn_sorted_index: scratch allocation failed");
+    int32_t *start = (int32_t *)aux;
+    unsigned *run_min = (unsigned *)(start + n);
+    int64_t *pos = (int64_t *)(((uintptr_t)(run_min + n) + 15) & ~(uintptr_t)15);
+    int64_t *part = pos + (n + 1);
+    double *sums = (double *)scratch(kSlotFlags, 64);
+    MN_REQUIRE(sums, MN_ENOMEM, "mn_sorted_index: scratch allocation failed");
+
+    hipLaunchKernelGGL(k_make_keys, dim3(grid(P)), dim3(256), 0, s, lam, n, P, keys);
+    // local sort of every TILE, then merge levels: global stages j >= TILE, local j < TILE
+    hipLaunchKernelGGL(k_bitonic_local, dim3((unsigned)(P / TILE)), dim3(1024), 0, s, keys, P,
+                       (int64_t)2, (int64_t)TILE);
+    for (int64_t kk = 2 * TILE; kk <= P; kk <<= 1) {
+        for (int64_t j = kk >> 1; j >= TILE; j >>= 1)
+            hipLaunchKernelGGL(k_bitonic_global, dim3(grid(P)), dim3(256), 0, s, keys, P, kk, j);
+        hipLaunchKernelGGL(k_bitonic_local, dim3((unsigned)(P / TILE)), dim3(1024), 0, s, keys, P,
+                           kk, kk);
+    }
+    MN_HIP_TRY(hipGetLastError());
+    hipLaunchKernelGGL(k_run_flags, dim3(grid(n)), dim3(256), 0, s, keys, n, start);
+    // inclusive run id = exclusive scan + flag
+    MN_HIP_TRY(scan::exclusive_scan(start, n, pos, part, s));
+    MN_HIP_TRY(hipMemsetAsync(run_min, 0xFF, sizeof(unsigned) * (size_t)n, s));
+    hipLaunchKernelGGL(k_run_min, dim3(grid(n)), dim3(256), 0, s, keys, n, start, pos, run_min);
+    hipLaunchKernelGGL(k_emit, dim3(grid(n)), dim3(256), 0, s, keys, n, start, pos, run_min, lam,
+                       order, key_out);
+    if (std_host) {
+        hipLaunchKernelGGL(k_std_exact, dim3(1), dim3(64), 0, s, lam, n, (float *)sums);
+        float sd = 0.f;
+        MN_HIP_TRY(hipMemcpyAsync(&sd, sums, 4, hipMemcpyDeviceToHost, s));
+        MN_HIP_TRY(hipStreamSynchronize(s));
+        *std_host = (double)sd;
+    }
+    MN_HIP_TRY(hipGetLastError());
+    MN_HIP_TRY(hipStreamSynchronize(s));
+    return MN_OK;
+}
+
+}  // namespace mn
+
+extern "C" int mn_sorted_index(const double *lambda, int64_t n, int64_t *order_out,
+                               double *key_out, double *std_out_host, void *stream) {
+    return mn::sorted_index_impl(lambda, n, order_out, key_out, std_out_host, stream);
+}

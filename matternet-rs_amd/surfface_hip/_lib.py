@@ -107,6 +107,7 @@ SIGNATURES = {
     "mn_energy_rows": (C.c_int, [C.POINTER(Csr), P, I64, I32, C.POINTER(EnergyOpts), P, P, P]),
     "mn_normalise_lambdas": (C.c_int, [P, I64, P, P]),
     "mn_energy_last_stats": (C.c_int, [C.POINTER(EnergyStats)]),
+    "mn_sorted_index": (C.c_int, [P, I64, P, P, P, P]),
 }
 
 _LIB = None

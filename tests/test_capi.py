@@ -59,3 +59,28 @@ def test_no_cpu_fallback_in_product_path():
             continue
         text = open(path, errors="ignore").read()
         assert not re.search(r"import\s+oracle|from\s+oracle|liboracle|\bor_[a-z0-9_]+\(", text), path
+
+
+def test_lexicographic_rank_formula_matches_string_sort():
+    """The closed-form rank used by k_make_keys (sorted_index.hip), restated."""
+    def cwp(v, N):
+        c, lo, hi = 0, v, v
+        while lo < N:
+            c += min(hi, N - 1) - lo + 1
+            lo, hi = lo * 10, hi * 10 + 9
+        return c
+
+    def lexrank(i, N):
+        if i == 0:
+            return 0
+        s = str(i)
+        r, pre = len(s), 0
+        for p, ch in enumerate(s):
+            for c in range(1 if p == 0 else 0, int(ch)):
+                r += cwp(pre * 10 + c, N)
+            pre = pre * 10 + int(ch)
+        return r
+
+    for N in (1, 2, 9, 10, 11, 100, 101, 999, 1000, 4321):
+        ranks = {v: k for k, v in enumerate(sorted(range(N), key=str))}
+        assert all(lexrank(i, N) == ranks[i] for i in range(N))
