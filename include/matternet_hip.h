@@ -232,6 +232,26 @@ int mn_energy_last_stats(mn_energy_stats *out);
 int mn_sorted_index(const double *lambda, int64_t n, int64_t *order_out, double *key_out,
                     double *std_out_host, void *stream);
 
+
+/* ---------------------------------------------------------------------- */
+/* K5 — sparsification of directed neighbour rows                         */
+/* ---------------------------------------------------------------------- */
+enum mn_sparsify_mode {
+    MN_SPARSIFY_SFGRASS = 0, /* SfGrassSparsifier::sparsify_graph
+                                (src_legacy/sparsification.rs:32-113)            */
+    MN_SPARSIFY_INLINE = 1   /* _build_adjacency inline pruning
+                                (src_legacy/laplacian.rs:216-282)                */
+};
+/* Rows nbr_idx/nbr_w [n][k] (device; idx -1 = empty, k <= 64) -> out rows
+ * [n][k]: kept entries first in descending score w*sqrt(deg_i*deg_j) (ties by
+ * input position), the rest -1 / 0.0.  When the average degree does not
+ * enable pruning the rows are copied (compacted, slot order).  ratio: SF-GRASS
+ * target ratio (SfGrassSparsifier::new() = 0.5; with_target_ratio clamps to
+ * [0.1, 1]).  applied_host (host, may be NULL) = 1 if pruning ran.  Bit-exact. */
+int mn_sparsify_rows(const int32_t *nbr_idx, const double *nbr_w, int64_t n, int32_t k,
+                     double ratio, int32_t mode, int32_t *out_idx, double *out_w,
+                     int32_t *applied_host, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -5,7 +5,8 @@ Every op runs on the GPU through the C ABI; there is no CPU fallback.
 """
 from . import _lib
 from ._lib import MnError, lib
-from . import energy, laplacian, sorted_index
+from . import energy, laplacian, sorted_index, sparsification
+from .sparsification import SfGrassSparsifier, sparsify_rows
 from .sorted_index import SortedLambdas
 from .energy import (TauMode, compute_taumode_lambdas, energy_rows, node_energy_and_dispersion,
                      normalise_lambdas)
@@ -19,4 +20,5 @@ __all__ = ["MnError", "lib", "DistanceMetric", "KnnResult", "build_candidate_gra
            "LaplacianConfig", "LaplacianOutput", "build_laplacian_from_knn",
            "laplacian_stage_from_edges", "laplacian", "energy", "TauMode",
            "compute_taumode_lambdas", "energy_rows", "node_energy_and_dispersion",
-           "normalise_lambdas", "sorted_index", "SortedLambdas"]
+           "normalise_lambdas", "sorted_index", "SortedLambdas", "sparsification",
+           "SfGrassSparsifier", "sparsify_rows"]

@@ -108,7 +108,9 @@ SIGNATURES = {
     "mn_normalise_lambdas": (C.c_int, [P, I64, P, P]),
     "mn_energy_last_stats": (C.c_int, [C.POINTER(EnergyStats)]),
     "mn_sorted_index": (C.c_int, [P, I64, P, P, P, P]),
+    "mn_sparsify_rows": (C.c_int, [P, P, I64, I32, C.c_double, I32, P, P, P, P]),
 }
+MN_SPARSIFY_SFGRASS, MN_SPARSIFY_INLINE = 0, 1
 
 _LIB = None
 
