@@ -252,6 +252,33 @@ int mn_sparsify_rows(const int32_t *nbr_idx, const double *nbr_w, int64_t n, int
                      double ratio, int32_t mode, int32_t *out_idx, double *out_w,
                      int32_t *applied_host, void *stream);
 
+
+/* ---------------------------------------------------------------------- */
+/* K1 (cosine) — rectified-cosine kNN                                     */
+/* ---------------------------------------------------------------------- */
+typedef struct mn_cos_opts {
+    int32_t topk;       /* neighbours kept per node (GraphParams.topk)            */
+    int32_t margin;     /* candidate margin (0 => 16)                              */
+    double eps;         /* keep dist <= eps                                        */
+    double sigma;       /* weight 1/(1+(dist/sigma)^p)                              */
+    double p;
+    int32_t timing;
+    int32_t reserved0;
+    void *stream;
+} mn_cos_opts;
+
+/* Feature graph: nodes are the f COLUMNS of X [n_rows][f] (f32, device), each
+ * with an n_rows-long profile — GraphFactory::build_laplacian_matrix_from_k_cluster
+ * builds its Laplacian on the transposed data (src_legacy/graph.rs:214-228).
+ * Distances/weights/order are the brute-force spec of the legacy adjacency
+ * (src_legacy/tests/test_helpers.rs:77-126): f64 sequential norms and dots,
+ * rectified cosine distance, eps/weight filter, (dist, j) order, topk.
+ * Outputs [f][topk] (device): idx (-1 empty), dist (f64), w (f64, may be
+ * NULL).  Bit-exact.  2 <= f <= 4096, topk <= 64. */
+int mn_knn_cos_columns_f32(const float *X, int64_t n_rows, int32_t f, const mn_cos_opts *opts,
+                           int32_t *out_idx, double *out_dist, double *out_w);
+int mn_cos_last_stats(mn_knn_stats *out);
+
 #ifdef __cplusplus
 }
 #endif

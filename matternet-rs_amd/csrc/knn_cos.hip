@@ -1,0 +1,461 @@
+// knn_cos.hip — K1 (cosine): rectified-cosine kNN of the FEATURE columns of
+// X [n][f] (the feature graph of graph.rs:214, built on the transposed data),
+// bit-exact vs the reference's f64 arithmetic.
+//
+// Reference semantics (src_legacy/tests/test_helpers.rs:77-126, the
+// brute-force spec of build_adjacency; production _build_adjacency
+// laplacian.rs:245-290 uses the same distance and weight):
+//   norm_i = sqrt(sum_t x_ti^2)          sequential f64 over the profile
+//   dot_ij = sum_t x_ti x_tj             sequential f64 (products exact)
+//   cos = norm_i*norm_j > 1e-12 ? clamp(dot/(norm_i norm_j), -1, 1) : 0
+//   dist = 1 - max(cos, 0); keep dist <= eps and w = 1/(1+(dist/sigma)^p) >
+//   1e-12; sort by (dist, j); truncate topk.
+//
+// MI355X design (profiles are long: n ~ 1e6, f ~ 768):
+//   1. k_transpose        X -> XT [f][n] (LDS-tiled) so every profile streams.
+//   2. k_col_norms        exact sequential f64 norms (one lane per column).
+//   3. k_gram_f64         G = X^T X on MFMA v_mfma_f64_16x16x4_f64 (f32 inputs
+//                         widened: products exact), upper 64x64 block tiles,
+//                         split-K over rows, f64 atomics into G.
+//   4. k_cos_select       per node (one wave): approximate distances from G,
+//                         wave bitonic sort, top-L candidates + the (L+1)-th.
+//   5. k_cos_exact        per (node, candidate) thread: the reference's
+//                         sequential f64 dot over the full profile.
+//   6. k_cos_finish       per node: sort exact (dist, j), certify
+//                         (|d~ - d| <= 2(n+16)2^-53), filter, write; nodes
+//                         that fail go to the exact all-pairs fallback.
+#include <algorithm>
+#include <climits>
+#include <vector>
+
+#include "common.hpp"
+
+namespace mn {
+namespace kcos {
+
+typedef double f64x4 __attribute__((ext_vector_type(4)));
+
+constexpr int FMAXC = 4096;  // features (nodes) limit
+constexpr int LMAXC = 64;    // candidate list length limit
+
+// ---- 1. transpose -------------------------------------------------------
+__global__ __launch_bounds__(256) void k_transpose(const float *__restrict__ X, int64_t n, int f,
+                                                   float *__restrict__ XT) {
+    __shared__ float tile[64][65];
+    const int64_t r0 = (int64_t)blockIdx.x * 64;
+    const int c0 = blockIdx.y * 64;
+    const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+    for (int r = ty; r < 64; r += 4) {
+        const int64_t row = r0 + r;
+        const int col = c0 + tx;
+        tile[r][tx] = (row < n && col < f) ? X[row * f + col] : 0.f;
+    }
+    __syncthreads();
+    for (int c = ty; c < 64; c += 4) {
+        const int col = c0 + c;
+        const int64_t row = r0 + tx;
+        if (col < f && row < n) XT[(int64_t)col * n + row] = tile[tx][c];
+    }
+}
+
+// ---- 2. exact sequential norms --------------------------------------------
+__global__ __launch_bounds__(64) void k_col_norms(const float *__restrict__ XT, int64_t n, int f,
+                                                  double *__restrict__ nrm) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= f) return;
+    const float *p = XT + (int64_t)i * n;
+    double acc = -0.0;
+    int64_t t = 0;
+    for (; t + 8 <= n; t += 8) {
+        float v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = p[t + u];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const double x = (double)v[u];
+            acc = acc + x * x;
+        }
+    }
+    for (; t < n; ++t) {
+        const double x = (double)p[t];
+        acc = acc + x * x;
+    }
+    nrm[i] = __builtin_sqrt(acc);
+}
+
+// ---- 3. Gram on f64 MFMA --------------------------------------------------
+constexpr int GT = 64;  // output tile
+constexpr int GK = 16;  // rows per LDS stage
+
+__global__ __launch_bounds__(256) void k_gram_f64(const float *__restrict__ X, int64_t n, int f,
+                                                  int ntile, int64_t kchunk, int nchunk,
+                                                  double *__restrict__ G) {
+    __shared__ float As[GK][GT + 4];
+    __shared__ float Bs[GK][GT + 4];
+    // blockIdx.x = chunk-major over upper-triangle tiles (concurrent blocks share rows)
+    const int ntri = ntile * (ntile + 1) / 2;
+    const int chunk = blockIdx.x / ntri;
+    int t = blockIdx.x % ntri, bi = 0;
+    while (t >= ntile - bi) { t -= ntile - bi; ++bi; }
+    const int bj = bi + t;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int wr = w >> 1, wc = w & 1;
+    const int64_t k0 = (int64_t)chunk * kchunk;
+    const int64_t k1 = min(n, k0 + kchunk);
+    f64x4 acc[2][2];
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b) acc[a][b] = f64x4{0.0, 0.0, 0.0, 0.0};
+    const int lr = threadIdx.x >> 4, lc4 = (threadIdx.x & 15) * 4;  // 16 rows x 16 float4
+    for (int64_t kb = k0; kb < k1; kb += GK) {
+        const int64_t row = kb + lr;
+        float4 va = make_float4(0.f, 0.f, 0.f, 0.f), vb = va;
+        if (row < k1) {
+            const float *pr = X + row * f;
+            const int ca = bi * GT + lc4, cb = bj * GT + lc4;
+            if (ca + 3 < f && (f & 3) == 0) va = *reinterpret_cast<const float4 *>(pr + ca);
+            else {
+                va.x = ca < f ? pr[ca] : 0.f; va.y = ca + 1 < f ? pr[ca + 1] : 0.f;
+                va.z = ca + 2 < f ? pr[ca + 2] : 0.f; va.w = ca + 3 < f ? pr[ca + 3] : 0.f;
+            }
+            if (cb + 3 < f && (f & 3) == 0) vb = *reinterpret_cast<const float4 *>(pr + cb);
+            else {
+                vb.x = cb < f ? pr[cb] : 0.f; vb.y = cb + 1 < f ? pr[cb + 1] : 0.f;
+                vb.z = cb + 2 < f ? pr[cb + 2] : 0.f; vb.w = cb + 3 < f ? pr[cb + 3] : 0.f;
+            }
+        }
+        __syncthreads();
+        *reinterpret_cast<float4 *>(&As[lr][lc4]) = va;
+        *reinterpret_cast<float4 *>(&Bs[lr][lc4]) = vb;
+        __syncthreads();
+#pragma unroll
+        for (int s = 0; s < GK / 4; ++s) {
+            const int kr = s * 4 + (lane >> 4);
+            double a[2], b[2];
+#pragma unroll
+            for (int m = 0; m < 2; ++m) a[m] = (double)As[kr][wr * 32 + m * 16 + (lane & 15)];
+#pragma unroll
+            for (int m = 0; m < 2; ++m) b[m] = (double)Bs[kr][wc * 32 + m * 16 + (lane & 15)];
+#pragma unroll
+            for (int ma = 0; ma < 2; ++ma)
+#pragma unroll
+                for (int mb = 0; mb < 2; ++mb)
+                    acc[ma][mb] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[ma], b[mb], acc[ma][mb],
+                                                                       0, 0, 0);
+        }
+    }
+    // C/D (f64 16x16x4): col = lane & 15, row = (lane >> 4) + 4 * reg
+#pragma unroll
+    for (int ma = 0; ma < 2; ++ma)
+#pragma unroll
+        for (int mb = 0; mb < 2; ++mb)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int gi = bi * GT + wr * 32 + ma * 16 + (lane >> 4) + 4 * r;
+                const int gj = bj * GT + wc * 32 + mb * 16 + (lane & 15);
+                if (gi < f && gj < f) atomicAdd(&G[(int64_t)gi * f + gj], acc[ma][mb][r]);
+            }
+}
+
+__device__ __forceinline__ double gram_at(const double *G, int f, int i, int j) {
+    return ((i / GT) <= (j / GT)) ? G[(int64_t)i * f + j] : G[(int64_t)j * f + i];
+}
+
+// the reference's distance from (dot, norms)
+__device__ __forceinline__ double cos_dist(double dot, double ni, double nj) {
+    const double denom = ni * nj;
+    double cs = 0.0;
+    if (denom > 1e-12) {
+        cs = dot / denom;
+        cs = cs < -1.0 ? -1.0 : (cs > 1.0 ? 1.0 : cs);  // NaN stays NaN
+    }
+    return 1.0 - (cs > 0.0 ? cs : 0.0);
+}
+
+// ---- 4. per node candidate selection ---------------------------------------
+template <int NR>
+__global__ __launch_bounds__(256) void k_cos_select(const double *__restrict__ G,
+                                                    const double *__restrict__ nrm, int f, int L,
+                                                    int32_t *__restrict__ cand,
+                                                    double *__restrict__ gnext) {
+    const int lane = threadIdx.x & 63;
+    const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (i >= f) return;
+    double d[NR];
+    int ix[NR];
+    const double ni = nrm[i];
+    bool nan = false;
+#pragma unroll
+    for (int r = 0; r < NR; ++r) {
+        const int j = lane + 64 * r;
+        if (j < f && j != i) {
+            d[r] = cos_dist(gram_at(G, f, i, j), ni, nrm[j]);
+            if (d[r] != d[r]) { d[r] = 2.0; nan = true; }  // non-finite data
+            ix[r] = j;
+        } else {
+            d[r] = __builtin_inf();
+            ix[r] = INT_MAX;
+        }
+    }
+    const bool any_nan = __any(nan);
+    wave_bitonic_sort<NR>(d, ix);
+    if (lane < L) cand[(int64_t)i * L + lane] = ix[0];
+    double gn = (L < f - 1) ? wave_elem<NR>(d, L) : __builtin_inf();
+    if (any_nan) gn = -__builtin_inf();  // the bound argument fails: exact path
+    if (lane == 0) gnext[i] = gn;
+}
+
+// ---- 5. exact sequential dot for (node, candidate) ---------------------------
+__global__ __launch_bounds__(256) void k_cos_exact(const float *__restrict__ XT, int64_t n,
+                                                   const int32_t *__restrict__ pi,
+                                                   const int32_t *__restrict__ pj, int64_t npairs,
+                                                   const double *__restrict__ nrm,
+                                                   double *__restrict__ dist) {
+    const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= npairs) return;
+    const int i = pi[q], j = pj[q];
+    if (i < 0 || j < 0) { dist[q] = __builtin_inf(); return; }
+    const double denom = nrm[i] * nrm[j];
+    if (!(denom > 1e-12)) { dist[q] = 1.0; return; }  // cos = 0 without a dot
+    const float *a = XT + (int64_t)i * n;
+    const float *b = XT + (int64_t)j * n;
+    double acc = -0.0;
+    int64_t t = 0;
+    for (; t + 8 <= n; t += 8) {
+        float va[8], vb[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) { va[u] = a[t + u]; vb[u] = b[t + u]; }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) acc = acc + (double)va[u] * (double)vb[u];
+    }
+    for (; t < n; ++t) acc = acc + (double)a[t] * (double)b[t];
+    dist[q] = cos_dist(acc, nrm[i], nrm[j]);
+}
+
+__global__ void k_cand_pairs(const int32_t *__restrict__ cand, int f, int L,
+                             int32_t *__restrict__ pi, int32_t *__restrict__ pj) {
+    const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= (int64_t)f * L) return;
+    pi[q] = (int32_t)(q / L);
+    const int c = cand[q];
+    pj[q] = c == INT_MAX ? -1 : c;
+}
+
+__device__ __forceinline__ double weight_of(double d, double sigma, double p) {
+    const double x = d / sigma;
+    const double pw = p == 2.0 ? x * x : (p == 1.0 ? x : pow(x, p));
+    return 1.0 / (1.0 + pw);
+}
+
+// ---- 6. exact sort + certification + filter ----------------------------------
+__global__ __launch_bounds__(256) void k_cos_finish(const int32_t *__restrict__ cand,
+                                                    const double *__restrict__ cdist,
+                                                    const double *__restrict__ gnext, int f, int L,
+                                                    int topk, double eps, double sigma, double p,
+                                                    double delta, int32_t *__restrict__ out_idx,
+                                                    double *__restrict__ out_dist,
+                                                    double *__restrict__ out_w,
+                                                    int *__restrict__ fb_count,
+                                                    int32_t *__restrict__ fb_list) {
+    const int lane = threadIdx.x & 63;
+    const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (i >= f) return;
+    double d[1];
+    int ix[1];
+    const bool ok = lane < L && cand[(int64_t)i * L + lane] != INT_MAX;
+    d[0] = ok ? cdist[(int64_t)i * L + lane] : __builtin_inf();
+    ix[0] = ok ? cand[(int64_t)i * L + lane] : INT_MAX;
+    wave_bitonic_sort<1>(d, ix);
+    const int M = min(L, f - 1);
+    const int keff = min(topk, M);
+    const double gn = gnext[i];
+    bool cert = true;
+    if (gn < __builtin_inf() && keff > 0) {
+        const double Dk = wave_elem<1>(d, keff - 1);
+        cert = (gn - delta) > Dk;
+    }
+    if (!cert) {
+        if (lane == 0) fb_list[atomicAdd(fb_count, 1)] = i;
+        return;
+    }
+    // filter (dist <= eps, w > 1e-12) is monotone in dist: a prefix survives
+    const double wv = weight_of(d[0], sigma, p);
+    const bool keep = lane < keff && d[0] <= eps && wv > 1e-12;
+    const uint64_t km = __ballot(keep);
+    const int nkeep = __popcll(~km) == 0 ? 64 : (int)__builtin_ctzll(~km);  // prefix length
+    if (lane < topk) {
+        const bool k2 = lane < nkeep;
+        out_idx[(int64_t)i * topk + lane] = k2 ? ix[0] : -1;
+        out_dist[(int64_t)i * topk + lane] = k2 ? d[0] : __builtin_inf();
+        if (out_w) out_w[(int64_t)i * topk + lane] = k2 ? wv : 0.0;
+    }
+}
+
+// ---- fallback: exact all-pairs for uncertified nodes -----------------------------
+__global__ void k_fb_pairs(const int32_t *__restrict__ fb_list, const int *__restrict__ fb_count,
+                           int f, int32_t *__restrict__ pi, int32_t *__restrict__ pj) {
+    const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t total = (int64_t)(*fb_count) * f;
+    if (q >= total) return;
+    const int node = fb_list[q / f];
+    const int j = (int)(q % f);
+    pi[q] = node;
+    pj[q] = j == node ? -1 : j;
+}
+
+template <int NR>
+__global__ __launch_bounds__(256) void k_fb_finish(const int32_t *__restrict__ fb_list,
+                                                   const int *__restrict__ fb_count,
+                                                   const double *__restrict__ fdist, int f,
+                                                   int topk, double eps, double sigma, double p,
+                                                   int32_t *__restrict__ out_idx,
+                                                   double *__restrict__ out_dist,
+                                                   double *__restrict__ out_w) {
+    const int lane = threadIdx.x & 63;
+    const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (b >= *fb_count) return;
+    const int i = fb_list[b];
+    double d[NR];
+    int ix[NR];
+#pragma unroll
+    for (int r = 0; r < NR; ++r) {
+        const int j = lane + 64 * r;
+        const bool ok = j < f && j != i;
+        d[r] = ok ? fdist[(int64_t)b * f + j] : __builtin_inf();
+        ix[r] = ok ? j : INT_MAX;
+    }
+    wave_bitonic_sort<NR>(d, ix);
+    const int keff = min(topk, f - 1);
+    const double wv = weight_of(d[0], sigma, p);
+    const bool keep = lane < keff && d[0] <= eps && wv > 1e-12;
+    const uint64_t km = __ballot(keep);
+    const int nkeep = __popcll(~km) == 0 ? 64 : (int)__builtin_ctzll(~km);
+    if (lane < topk) {
+        const bool k2 = lane < nkeep;
+        out_idx[(int64_t)i * topk + lane] = k2 ? ix[0] : -1;
+        out_dist[(int64_t)i * topk + lane] = k2 ? d[0] : __builtin_inf();
+        if (out_w) out_w[(int64_t)i * topk + lane] = k2 ? wv : 0.0;
+    }
+}
+
+inline unsigned grid(int64_t n, int t = 256) {
+    return (unsigned)std::max<int64_t>(1, (n + t - 1) / t);
+}
+
+}  // namespace kcos
+
+static thread_local mn_knn_stats t_cos_stats{};
+
+static int knn_cos_columns_impl(const float *X, int64_t n, int32_t f, const mn_cos_opts *o,
+                                int32_t *out_idx, double *out_dist, double *out_w) {
+    using namespace kcos;
+    clear_error();
+    t_cos_stats = mn_knn_stats{};
+    MN_REQUIRE(o && X && out_idx && out_dist, MN_EINVAL, "mn_knn_cos_columns_f32: NULL argument");
+    MN_REQUIRE(n >= 1 && f >= 2 && f <= FMAXC, MN_EINVAL,
+               "mn_knn_cos_columns_f32: need n >= 1 and 2 <= f <= %d", FMAXC);
+    MN_REQUIRE(o->topk >= 1 && o->topk <= 64, MN_ENOTSUP, "mn_knn_cos_columns_f32: topk in [1,64]");
+    MN_REQUIRE(o->sigma > 0.0, MN_EINVAL, "mn_knn_cos_columns_f32: sigma must be > 0");
+    const int margin = o->margin > 0 ? o->margin : 16;
+    const int L = std::min(std::min(o->topk + margin, LMAXC), f - 1);
+    hipStream_t s = (hipStream_t)o->stream;
+    const int ntile = (f + GT - 1) / GT;
+    const int ntri = ntile * (ntile + 1) / 2;
+    int nchunk = (int)std::max<int64_t>(1, std::min<int64_t>((2048 + ntri - 1) / ntri, (n + 255) / 256));
+    int64_t kchunk = (n + nchunk - 1) / nchunk;
+    kchunk = ((kchunk + GK - 1) / GK) * GK;
+    nchunk = (int)((n + kchunk - 1) / kchunk);
+
+    float *XT = (float *)scratch(kSlotGeneric0, sizeof(float) * (size_t)n * f);
+    char *g = (char *)scratch(kSlotGeneric1, sizeof(double) * ((size_t)f * f + f * 2 + 64) +
+                                                (size_t)f * L * 16 + (size_t)f * 8);
+    MN_REQUIRE(XT && g, MN_ENOMEM, "mn_knn_cos_columns_f32: scratch allocation failed");
+    double *G = (double *)g;
+    double *nrm = G + (size_t)f * f;
+    double *gnext = nrm + f;
+    int *flags = (int *)(gnext + f);
+    int32_t *cand = (int32_t *)(flags + 16);
+    int32_t *pi = cand + (size_t)f * L;
+    int32_t *pj = pi + (size_t)f * L;
+    double *cdist = (double *)(((uintptr_t)(pj + (size_t)f * L) + 15) & ~(uintptr_t)15);
+    int32_t *fb_list = (int32_t *)(cdist + (size_t)f * L);
+
+    Timer tm;
+    tm.start(o->timing != 0, s);
+    MN_HIP_TRY(hipMemsetAsync(G, 0, sizeof(double) * (size_t)f * f, s));
+    MN_HIP_TRY(hipMemsetAsync(flags, 0, 64, s));
+    hipLaunchKernelGGL(k_transpose, dim3(grid(n, 64), (unsigned)((f + 63) / 64)), dim3(256), 0, s,
+                       X, n, f, XT);
+    hipLaunchKernelGGL(k_col_norms, dim3(grid(f, 64)), dim3(64), 0, s, XT, n, f, nrm);
+    hipLaunchKernelGGL(k_gram_f64, dim3((unsigned)(ntri * nchunk)), dim3(256), 0, s, X, n, f, ntile,
+                       kchunk, nchunk, G);
+    MN_HIP_TRY(hipGetLastError());
+    tm.mark();
+    const int nr = (f + 63) / 64;
+#define MN_SEL(NRV) hipLaunchKernelGGL(k_cos_select<NRV>, dim3(grid(f, 4)), dim3(256), 0, s, G, nrm, f, L, cand, gnext)
+    if (nr <= 1) MN_SEL(1); else if (nr <= 2) MN_SEL(2); else if (nr <= 4) MN_SEL(4);
+    else if (nr <= 8) MN_SEL(8); else if (nr <= 16) MN_SEL(16); else if (nr <= 32) MN_SEL(32);
+    else MN_SEL(64);
+#undef MN_SEL
+    hipLaunchKernelGGL(k_cand_pairs, dim3(grid((int64_t)f * L)), dim3(256), 0, s, cand, f, L, pi, pj);
+    hipLaunchKernelGGL(k_cos_exact, dim3(grid((int64_t)f * L)), dim3(256), 0, s, XT, n, pi, pj,
+                       (int64_t)f * L, nrm, cdist);
+    const double delta = 2.0 * ((double)n + 16.0) * 0x1p-53 + 1e-300;
+    hipLaunchKernelGGL(k_cos_finish, dim3(grid(f, 4)), dim3(256), 0, s, cand, cdist, gnext, f, L,
+                       o->topk, o->eps, o->sigma, o->p, delta, out_idx, out_dist, out_w, flags,
+                       fb_list);
+    MN_HIP_TRY(hipGetLastError());
+    tm.mark();
+    int nfb = 0;
+    MN_HIP_TRY(hipMemcpyAsync(&nfb, flags, 4, hipMemcpyDeviceToHost, s));
+    MN_HIP_TRY(hipStreamSynchronize(s));
+    if (nfb > 0) {  // exact all-pairs for the uncertified nodes
+        const int64_t np = (int64_t)nfb * f;
+        int32_t *fpi = nullptr, *fpj = nullptr;
+        double *fd = nullptr;
+        MN_HIP_TRY(hipMalloc(&fpi, 4 * np));
+        MN_HIP_TRY(hipMalloc(&fpj, 4 * np));
+        MN_HIP_TRY(hipMalloc(&fd, 8 * np));
+        hipLaunchKernelGGL(k_fb_pairs, dim3(grid(np)), dim3(256), 0, s, fb_list, flags, f, fpi, fpj);
+        hipLaunchKernelGGL(k_cos_exact, dim3(grid(np)), dim3(256), 0, s, XT, n, fpi, fpj, np, nrm, fd);
+#define MN_FB(NRV) hipLaunchKernelGGL(k_fb_finish<NRV>, dim3(grid(nfb, 4)), dim3(256), 0, s, fb_list, flags, fd, f, o->topk, o->eps, o->sigma, o->p, out_idx, out_dist, out_w)
+        if (nr <= 1) MN_FB(1); else if (nr <= 2) MN_FB(2); else if (nr <= 4) MN_FB(4);
+        else if (nr <= 8) MN_FB(8); else if (nr <= 16) MN_FB(16); else if (nr <= 32) MN_FB(32);
+        else MN_FB(64);
+#undef MN_FB
+        MN_HIP_TRY(hipGetLastError());
+        MN_HIP_TRY(hipStreamSynchronize(s));
+        (void)hipFree(fpi); (void)hipFree(fpj); (void)hipFree(fd);
+    }
+    tm.mark();
+    MN_HIP_TRY(hipStreamSynchronize(s));
+    t_cos_stats.n_queries = f;
+    t_cos_stats.n_uncertified = nfb;
+    t_cos_stats.slices = nchunk;
+    t_cos_stats.list_len = L;
+    if (tm.on) {
+        t_cos_stats.ms_gram = tm.ms(0, 1);
+        t_cos_stats.ms_rerank = tm.ms(1, 2);
+        t_cos_stats.ms_fallback = tm.ms(2, 3);
+        t_cos_stats.ms_total = tm.ms(0, 3);
+    }
+    return MN_OK;
+}
+
+}  // namespace mn
+
+extern "C" {
+
+int mn_knn_cos_columns_f32(const float *X, int64_t n_rows, int32_t f, const mn_cos_opts *opts,
+                           int32_t *out_idx, double *out_dist, double *out_w) {
+    return mn::knn_cos_columns_impl(X, n_rows, f, opts, out_idx, out_dist, out_w);
+}
+
+int mn_cos_last_stats(mn_knn_stats *out) {
+    if (!out) return MN_EINVAL;
+    *out = mn::t_cos_stats;
+    return MN_OK;
+}
+
+}  // extern "C"

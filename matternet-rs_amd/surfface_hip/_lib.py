@@ -65,6 +65,12 @@ class LapStats(C.Structure):
         return {f: getattr(self, f) for f, _ in self._fields_ if f != "reserved0"}
 
 
+class CosOpts(C.Structure):
+    _fields_ = [("topk", C.c_int32), ("margin", C.c_int32), ("eps", C.c_double),
+                ("sigma", C.c_double), ("p", C.c_double), ("timing", C.c_int32),
+                ("reserved0", C.c_int32), ("stream", C.c_void_p)]
+
+
 MN_G_TAUMODE, MN_G_ENERGYMAPS = 0, 1
 MN_TAU_FIXED, MN_TAU_MEDIAN, MN_TAU_MEAN, MN_TAU_PERCENTILE = 0, 1, 2, 3
 
@@ -109,6 +115,8 @@ SIGNATURES = {
     "mn_energy_last_stats": (C.c_int, [C.POINTER(EnergyStats)]),
     "mn_sorted_index": (C.c_int, [P, I64, P, P, P, P]),
     "mn_sparsify_rows": (C.c_int, [P, P, I64, I32, C.c_double, I32, P, P, P, P]),
+    "mn_knn_cos_columns_f32": (C.c_int, [P, I64, I32, C.POINTER(CosOpts), P, P, P]),
+    "mn_cos_last_stats": (C.c_int, [C.POINTER(KnnStats)]),
 }
 MN_SPARSIFY_SFGRASS, MN_SPARSIFY_INLINE = 0, 1
 

@@ -105,3 +105,27 @@ def build_candidate_graph(means, k_neighbors: int,
     if metric == DistanceMetric.Euclidean:
         dist = torch.sqrt(dist)
     return u, v, dist
+
+
+def cos_last_stats() -> dict:
+    st = _lib.KnnStats()
+    _lib.check(_lib.lib().mn_cos_last_stats(C.byref(st)))
+    return st.as_dict()
+
+
+def knn_cos_columns(X: torch.Tensor, topk: int, eps: float = 1.0, sigma: float = 1.0,
+                    p: float = 2.0, margin: int = 16, timing: bool = False, stream=None):
+    """Rectified-cosine kNN of the FEATURE columns of X [n, f] (each column is a
+    node with an n-long profile; graph.rs:214 transposes the centroids).
+    Returns (idx [f, topk] int32, dist [f, topk] f64, w [f, topk] f64, stats);
+    bit-exact vs test_helpers.rs:77-126 semantics."""
+    X = require_cuda(X, torch.float32, "X", 2)
+    n, f = X.shape
+    idx = torch.empty((f, topk), dtype=torch.int32, device=X.device)
+    dist = torch.empty((f, topk), dtype=torch.float64, device=X.device)
+    w = torch.empty((f, topk), dtype=torch.float64, device=X.device)
+    o = _lib.CosOpts(topk=topk, margin=margin, eps=eps, sigma=sigma, p=p,
+                     timing=1 if timing else 0, reserved0=0, stream=stream_handle(stream))
+    _lib.check(_lib.lib().mn_knn_cos_columns_f32(ptr(X), n, f, C.byref(o), ptr(idx), ptr(dist),
+                                                 ptr(w)))
+    return idx, dist, w, cos_last_stats()
