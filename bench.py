@@ -44,6 +44,8 @@ def parse():
     ap.add_argument("--seed", type=int, default=42)
     ap.add_argument("--cpu-seconds", type=float, default=15.0,
                     help="target CPU time of the sampled cpu_baseline leg (0 = skip)")
+    ap.add_argument("--no-c3", dest="c3", action="store_false",
+                    help="skip the C3 legs (Laplacian assembly, energy pass, sorted index)")
     ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_gram_latest.json"),
                     help="PMC-derived HBM bytes per launch of the Gram kernel (optional)")
     return ap.parse_args()
@@ -139,6 +141,12 @@ def main():
             "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": traffic,
             "ms_per_launch": round(gms, 3), "flop_per_launch": flops_launch}
 
+    # C3 legs (configs[2]): Laplacian assembly + energymaps/taumode pass + index,
+    # on this rank's rows (timed individually after the headline step)
+    c3 = None
+    if a.c3:
+        c3 = c3_legs(S, X, out[0], out[1], k)
+
     cpu = None
     parity = None
     if rank == 0 and world == 1 and a.cpu_seconds > 0:
@@ -160,6 +168,8 @@ def main():
             "roofline": roof,
             "cpu_baseline": cpu,
             "parity_sample": parity,
+            "energy_rows_per_sec": (c3 or {}).get("energy_rows_per_sec"),
+            "c3_legs": c3,
             "knn_stats": {"uncertified_rows": st["n_uncertified"], "slices": st["slices"],
                           "list_len": st["list_len"], "ms_norms": st["ms_norms"],
                           "ms_gram": st["ms_gram"], "ms_rerank": st["ms_rerank"],
@@ -169,6 +179,54 @@ def main():
     if dist:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def _timed(fn, reps=3):
+    """median wall ms of fn() (device-synchronised), after one warm call."""
+    fn()
+    torch.cuda.synchronize()
+    ts = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        r = fn()
+        torch.cuda.synchronize()
+        ts.append((time.perf_counter() - t0) * 1e3)
+    return float(np.median(ts)), r
+
+
+def c3_legs(S, X, idx, dist, k):
+    """BASELINE.json configs[2]: on the C2 kNN graph of X (N x F):
+    item-graph Laplacian (legacy UNION, rational weights), the F x F feature
+    graph (rectified-cosine kNN of the columns, topk=4, eps=1, sigma=1, p=2;
+    energymaps.rs:463-471 bootstrap), its Laplacian, the taumode energy pass of
+    all N items against it (Median tau), normalise_lambdas and the sorted index.
+    Algorithmic bytes -> GB/s per leg."""
+    n, f = X.shape
+    out = {}
+    ms, (Lit, _) = _timed(lambda: S.build_laplacian_from_knn(
+        idx, dist, weight_kernel="rational", symmetrise="union", eps=float("inf"), sigma=1.0,
+        p=2.0))
+    byt = n * k * 8 + Lit.nnz * 12 + (n + 1) * 8
+    out["item_laplacian"] = {"ms": round(ms, 3), "nnz": Lit.nnz, "GB_per_s": round(byt / ms / 1e6, 1)}
+    ms, (fi, fd, fw, fst) = _timed(lambda: S.knn_cos_columns(X, 4, eps=1.0, sigma=1.0, p=2.0), 1)
+    out["feature_knn_cos"] = {"ms": round(ms, 3), "uncertified": fst["n_uncertified"],
+                              "gram_tflops": round(2.0 * f * f * n / 2 / (fst["ms_gram"] * 1e9), 2)
+                              if fst["ms_gram"] else None}
+    ms, (Lf, _) = _timed(lambda: S.build_laplacian_from_knn(fi, fw, weight_kernel="given",
+                                                           symmetrise="union"))
+    out["feature_laplacian"] = {"ms": round(ms, 3), "nnz": Lf.nnz}
+    ms, (E, G, lam) = _timed(lambda: S.energy_rows(X, Lf))
+    ebytes = n * f * 4 + Lf.nnz * 12 + (f + 1) * 8 + n * 3 * 8
+    out["energy_rows"] = {"ms": round(ms, 3), "GB_per_s": round(ebytes / ms / 1e6, 1),
+                          "entries_per_row": S.energy.last_stats()["entries"]}
+    out["energy_rows_per_sec"] = n / (ms * 1e-3)
+    lam_n = lam.clone()
+    ms, _ = _timed(lambda: S.normalise_lambdas(lam_n.copy_(lam)))
+    out["normalise_ms"] = round(ms, 3)
+    ms, sl = _timed(lambda: S.SortedLambdas().build_from(lam_n))
+    out["sorted_index"] = {"ms": round(ms, 3), "std_dev": sl.std_dev,
+                           "GB_per_s": round(n * 16 / ms / 1e6, 1)}
+    return out
 
 
 def cpu_baseline(X, idx, dd, k, target_s):
