@@ -77,27 +77,28 @@ def main():
     _lib.check(L.mn_fill_uniform_f32(X.data_ptr(), n_loc, d, a.seed, rank * n_loc,
                                      stream.cuda_stream))
     if world > 1:
-        Xall = torch.empty((n_tot, d), dtype=torch.float32, device=dev)
-        dist.all_gather_into_tensor(Xall, X)
-        recv_i = torch.empty((world, n_loc, k), dtype=torch.int32, device=dev)
-        recv_d = torch.empty((world, n_loc, k), dtype=torch.float32, device=dev)
+        from surfface_hip.dist import sharded_knn
     torch.cuda.synchronize()
 
     gram_ms = []
+
+    last = {}
+
+    def knn_fn(Q, C, kk, c_off):
+        r = S.knn_l2sq_qc(Q, C, kk, q_offset=0, c_offset=c_off, timing=True)
+        gram_ms.append(r.stats["ms_gram"])
+        last["stats"] = r.stats
+        return r.idx, r.dist
 
     def step():
         if world == 1:
             r = S.knn_l2sq(X, k, timing=True)
             gram_ms.append(r.stats["ms_gram"])
             return r.idx, r.dist, r.stats
-        # per-shard exact top-k of ALL queries against this rank's corpus shard
-        r = S.knn_l2sq_qc(Xall, X, k, q_offset=0, c_offset=rank * n_loc, timing=True)
-        gram_ms.append(r.stats["ms_gram"])
-        # owner of query rows [j*n_loc, (j+1)*n_loc) is rank j: all-to-all the lists
-        dist.all_to_all_single(recv_i.view(world, -1), r.idx.view(world, -1))
-        dist.all_to_all_single(recv_d.view(world, -1), r.dist.view(world, -1))
-        idx, dd = S.merge_parts(recv_i, recv_d)
-        return idx, dd, r.stats
+        # all-gather queries, exact per-shard top-k vs the resident shard,
+        # all-to-all of the lists, merge on the owner (surfface_hip/dist.py)
+        idx, dd = sharded_knn(X, k, knn_fn=knn_fn, merge_fn=S.merge_parts)
+        return idx, dd, last["stats"]
 
     for _ in range(a.warmup):
         step()
@@ -164,7 +165,8 @@ def main():
                                     f"C4-style: {n_tot} x {d} f32 exact kNN k={k}, row-sharded"),
                        "n_rows": n_tot, "dim": d, "k": k, "rows_per_gpu": n_loc,
                        "metric_space": "squared L2 (reference sequential f32 fold)",
-                       "parallelism": f"corpus row-shard x{world} + RCCL all-gather/all-to-all"},
+                       "parallelism": (f"corpus row-shard x{world}: RCCL all-gather of queries, "
+                                       "exact per-shard top-k, all-to-all + merge")},
             "roofline": roof,
             "cpu_baseline": cpu,
             "parity_sample": parity,

@@ -1,0 +1,43 @@
+"""Row-sharded multi-GPU kNN graph build, one process per GPU.
+
+Rank r owns rows [r*n_loc, (r+1)*n_loc) of X as its corpus shard (resident).
+1. all-gather the query rows (every row of X) over RCCL/xGMI;
+2. exact per-shard top-k of ALL queries against the local shard
+   (mn_knn_f32_qc with global-id offsets: certified per shard);
+3. one all-to-all: each query's owner receives the R per-shard lists of its rows;
+4. merge by (dist, global id) (mn_knn_merge_f32) -> the owner's rows of the graph.
+Exact: the global top-k is contained in the union of exact per-shard top-k lists and
+a pair's distance is the same arithmetic on every shard.
+
+`knn_fn` / `merge_fn` default to the HIP ops; tests inject CPU stand-ins to check the
+exchange pattern under the `gloo` backend.
+"""
+from __future__ import annotations
+
+import torch
+import torch.distributed as dist
+
+
+def sharded_knn(X_shard: torch.Tensor, k: int, knn_fn=None, merge_fn=None, group=None):
+    """Returns (idx [n_loc, k] int32 global ids, dist [n_loc, k] f32) for this rank's rows."""
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    n_loc, d = X_shard.shape
+    if knn_fn is None or merge_fn is None:
+        from .knn import knn_l2sq_qc, merge_parts
+        knn_fn = knn_fn or (lambda Q, C, kk, c_off: (lambda r: (r.idx, r.dist))(
+            knn_l2sq_qc(Q, C, kk, q_offset=0, c_offset=c_off)))
+        merge_fn = merge_fn or merge_parts
+    sizes = [torch.zeros(1, dtype=torch.int64, device=X_shard.device) for _ in range(world)]
+    dist.all_gather(sizes, torch.tensor([n_loc], dtype=torch.int64, device=X_shard.device),
+                    group=group)
+    if any(int(s.item()) != n_loc for s in sizes):
+        raise ValueError("sharded_knn: every rank must hold the same number of rows")
+    Xall = torch.empty((world * n_loc, d), dtype=X_shard.dtype, device=X_shard.device)
+    dist.all_gather_into_tensor(Xall, X_shard.contiguous(), group=group)
+    part_i, part_d = knn_fn(Xall, X_shard, k, rank * n_loc)   # [world*n_loc, k] each
+    recv_i = torch.empty((world, n_loc, k), dtype=part_i.dtype, device=part_i.device)
+    recv_d = torch.empty((world, n_loc, k), dtype=part_d.dtype, device=part_d.device)
+    dist.all_to_all_single(recv_i.view(world, -1), part_i.contiguous().view(world, -1), group=group)
+    dist.all_to_all_single(recv_d.view(world, -1), part_d.contiguous().view(world, -1), group=group)
+    return merge_fn(recv_i, recv_d)
