@@ -279,6 +279,26 @@ int mn_knn_cos_columns_f32(const float *X, int64_t n_rows, int32_t f, const mn_c
                            int32_t *out_idx, double *out_dist, double *out_w);
 int mn_cos_last_stats(mn_knn_stats *out);
 
+/* C5 item graph (config 5): rectified-cosine kNN over the ROWS of a bf16
+ * matrix X [n][d] (raw bf16 bits, device).  Semantics are those of the legacy
+ * adjacency builder (src_legacy/laplacian.rs:245-290 _build_adjacency /
+ * src_legacy/tests/test_helpers.rs:77-126) evaluated on the exactly widened
+ * values: f64 sequential norms and dots, dist = 1 - max(cos, 0) with cos = 0
+ * when norm_i*norm_j <= 1e-12, keep dist <= eps and w = 1/(1+(dist/sigma)^p)
+ * > 1e-12, order (dist, j), truncate topk.  Outputs [n][topk] (device): idx
+ * (-1 empty), dist (f64), w (f64, may be NULL).  Bit-exact.  topk <= 64.
+ * Candidates come from v_mfma_f32_32x32x16_bf16; every row is certified or
+ * rescanned exactly (n_uncertified in mn_bf16_last_stats). */
+int mn_knn_cos_bf16(const uint16_t *X, int64_t n, int32_t d, const mn_cos_opts *opts,
+                    int32_t *out_idx, double *out_dist, double *out_w);
+/* Row shard form: queries Q [nq][d] with global ids q_offset.., corpus C
+ * [nc][d] with global ids c_offset..; the row whose global id equals the
+ * query's is skipped; returned ids are global. */
+int mn_knn_cos_bf16_qc(const uint16_t *Q, int64_t nq, const uint16_t *C, int64_t nc, int32_t d,
+                       int64_t q_offset, int64_t c_offset, const mn_cos_opts *opts,
+                       int32_t *out_idx, double *out_dist, double *out_w);
+int mn_bf16_last_stats(mn_knn_stats *out);
+
 #ifdef __cplusplus
 }
 #endif

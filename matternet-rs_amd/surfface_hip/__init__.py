@@ -12,10 +12,11 @@ from .energy import (TauMode, compute_taumode_lambdas, energy_rows, node_energy_
                      normalise_lambdas)
 from .laplacian import (CsrMatrix, GraphParams, LaplacianConfig, LaplacianOutput,
                         build_laplacian_from_knn, laplacian_stage_from_edges)
-from .knn import (DistanceMetric, KnnResult, build_candidate_graph, knn_cos_columns, knn_l2sq,
+from .knn import (DistanceMetric, KnnResult, bf16_last_stats, build_candidate_graph, knn_cos_bf16,
+                  knn_cos_bf16_qc, knn_cos_columns, knn_l2sq,
                   knn_l2sq_qc, last_stats, merge_parts)
 
-__all__ = ["MnError", "lib", "knn_cos_columns", "DistanceMetric", "KnnResult", "build_candidate_graph", "knn_l2sq",
+__all__ = ["MnError", "lib", "knn_cos_columns", "knn_cos_bf16", "knn_cos_bf16_qc", "bf16_last_stats", "DistanceMetric", "KnnResult", "build_candidate_graph", "knn_l2sq",
            "knn_l2sq_qc", "last_stats", "merge_parts", "CsrMatrix", "GraphParams",
            "LaplacianConfig", "LaplacianOutput", "build_laplacian_from_knn",
            "laplacian_stage_from_edges", "laplacian", "energy", "TauMode",

@@ -129,3 +129,46 @@ def knn_cos_columns(X: torch.Tensor, topk: int, eps: float = 1.0, sigma: float =
     _lib.check(_lib.lib().mn_knn_cos_columns_f32(ptr(X), n, f, C.byref(o), ptr(idx), ptr(dist),
                                                  ptr(w)))
     return idx, dist, w, cos_last_stats()
+
+
+def bf16_last_stats() -> dict:
+    st = _lib.KnnStats()
+    _lib.check(_lib.lib().mn_bf16_last_stats(C.byref(st)))
+    return st.as_dict()
+
+
+def knn_cos_bf16(X: torch.Tensor, topk: int, eps: float = 1.0, sigma: float = 1.0,
+                 p: float = 2.0, margin: int = 16, timing: bool = False, stream=None):
+    """Item graph of config 5: rectified-cosine kNN over the ROWS of a bf16
+    matrix X [n, d] — the legacy adjacency builder's distance, weight, filter and
+    (dist, j) order (src_legacy/laplacian.rs:245-290, test_helpers.rs:77-126) on
+    the exactly widened values.  Returns (idx [n, topk] int32 (-1 empty),
+    dist [n, topk] f64, w [n, topk] f64, stats); bit-exact."""
+    X = require_cuda(X, torch.bfloat16, "X", 2)
+    n, d = X.shape
+    idx = torch.empty((n, topk), dtype=torch.int32, device=X.device)
+    dist = torch.empty((n, topk), dtype=torch.float64, device=X.device)
+    w = torch.empty((n, topk), dtype=torch.float64, device=X.device)
+    o = _lib.CosOpts(topk=topk, margin=margin, eps=eps, sigma=sigma, p=p,
+                     timing=1 if timing else 0, reserved0=0, stream=stream_handle(stream))
+    _lib.check(_lib.lib().mn_knn_cos_bf16(ptr(X), n, d, C.byref(o), ptr(idx), ptr(dist), ptr(w)))
+    return idx, dist, w, bf16_last_stats()
+
+
+def knn_cos_bf16_qc(Q: torch.Tensor, C_: torch.Tensor, topk: int, q_offset: int = 0,
+                    c_offset: int = 0, eps: float = 1.0, sigma: float = 1.0, p: float = 2.0,
+                    margin: int = 16, timing: bool = False, stream=None):
+    """Row-shard form of knn_cos_bf16 (queries Q vs corpus shard C_, global ids)."""
+    Q = require_cuda(Q, torch.bfloat16, "Q", 2)
+    C_ = require_cuda(C_, torch.bfloat16, "C", 2)
+    if Q.shape[1] != C_.shape[1]:
+        raise ValueError("Q and C must have the same feature dimension")
+    nq, d = Q.shape
+    idx = torch.empty((nq, topk), dtype=torch.int32, device=Q.device)
+    dist = torch.empty((nq, topk), dtype=torch.float64, device=Q.device)
+    w = torch.empty((nq, topk), dtype=torch.float64, device=Q.device)
+    o = _lib.CosOpts(topk=topk, margin=margin, eps=eps, sigma=sigma, p=p,
+                     timing=1 if timing else 0, reserved0=0, stream=stream_handle(stream))
+    _lib.check(_lib.lib().mn_knn_cos_bf16_qc(ptr(Q), nq, ptr(C_), C_.shape[0], d, q_offset,
+                                             c_offset, C.byref(o), ptr(idx), ptr(dist), ptr(w)))
+    return idx, dist, w, bf16_last_stats()

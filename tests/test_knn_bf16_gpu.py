@@ -1,0 +1,122 @@
+"""K1/C5 (bf16 rectified-cosine item graph) parity on the GPU vs the oracle.
+
+Contract: indices, distances (f64) and weights bit-exact vs the reference's
+sequential-f64 rectified-cosine semantics (src_legacy/tests/test_helpers.rs:77-126,
+src_legacy/laplacian.rs:245-290) on the exactly widened bf16 values.  The
+oracle (or_knn_cos_f64) receives the same values as f32 (bf16 -> f32 is exact).
+"""
+import numpy as np
+import pytest
+import torch
+
+import datagen
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+def bf16_rows(X):
+    """(bf16 bits as a cuda bfloat16 tensor, the same values as f32 numpy)."""
+    bits = datagen.to_bf16_bits(np.ascontiguousarray(X, dtype=np.float32))
+    t = torch.from_numpy(bits.view(np.int16)).cuda().view(torch.bfloat16)
+    return t, datagen.bf16_bits_to_f32(bits)
+
+
+def hip(Xt, topk, **kw):
+    import surfface_hip as S
+    i, d, w, st = S.knn_cos_bf16(Xt, topk, **kw)
+    return i.cpu().numpy(), d.cpu().numpy(), w.cpu().numpy(), st
+
+
+def exact(a, b):
+    for x, y in zip(a, b):
+        np.testing.assert_array_equal(np.asarray(x).view(np.uint8), np.asarray(y).view(np.uint8))
+
+
+@pytest.mark.parametrize("n,d,topk", [(3000, 256, 10), (700, 3072, 32), (1500, 100, 8),
+                                      (2000, 64, 64), (257, 24, 5)])
+def test_item_graph_uniform(n, d, topk):
+    Xt, Xf = bf16_rows(datagen.uniform(n, d, seed=11))
+    i, dd, w, st = hip(Xt, topk)
+    exact((i, dd, w), O.knn_cos(Xf, topk))
+    assert st["n_queries"] == n
+
+
+def test_item_graph_clustered_dups_zero_rows_and_filters():
+    X = datagen.clustered(5000, 96, seed=5, blobs=40, sigma=0.05, dup_frac=0.02, zero_frac=0.002)
+    X[10] = -X[11]          # antipodal pair: cos -1 -> rectified dist 1
+    Xt, Xf = bf16_rows(X)
+    kw = dict(eps=0.6, sigma=0.25, p=2.0)
+    exact(hip(Xt, 12, **kw)[:3], O.knn_cos(Xf, 12, **kw))
+
+
+def test_item_graph_pow_weights():
+    Xt, Xf = bf16_rows(datagen.clustered(3000, 128, seed=8, blobs=16))
+    kw = dict(eps=0.95, sigma=0.4, p=3.0)
+    i, d, w, _ = hip(Xt, 7, **kw)
+    ri, rd, rw = O.knn_cos(Xf, 7, **kw)
+    np.testing.assert_array_equal(i, ri)
+    np.testing.assert_array_equal(d, rd)
+    # device pow vs glibc pow: within 2 ulp
+    np.testing.assert_allclose(w, rw, rtol=5e-16, atol=0)
+
+
+def test_ties_force_exact_fallback():
+    X = datagen.uniform(1200, 48, seed=4)
+    X[:100] = X[0]          # 100 identical rows: ties beyond topk + margin
+    Xt, Xf = bf16_rows(X)
+    i, d, w, st = hip(Xt, 8)
+    exact((i, d, w), O.knn_cos(Xf, 8))
+    assert st["n_uncertified"] >= 100
+
+
+def test_tiny_norm_rows_are_exact():
+    X = datagen.uniform(900, 32, seed=6)
+    X[5] *= 1e-7            # norm^2 ~ 1e-13: denom = n_i n_j crosses the 1e-12 switch
+    X[6] *= 3e-7
+    X[7] = 0.0
+    Xt, Xf = bf16_rows(X)
+    exact(hip(Xt, 6)[:3], O.knn_cos(Xf, 6))
+
+
+def test_few_rows():
+    for n in (1, 2, 5):
+        Xt, Xf = bf16_rows(datagen.uniform(n, 16, seed=n))
+        exact(hip(Xt, 4)[:3], O.knn_cos(Xf, 4))
+
+
+def test_query_shard_against_full_corpus():
+    import surfface_hip as S
+    Xt, Xf = bf16_rows(datagen.uniform(4000, 200, seed=21))
+    a, b = 1000, 2300
+    i, d, w, _ = S.knn_cos_bf16_qc(Xt[a:b].contiguous(), Xt, 9, q_offset=a, c_offset=0)
+    ri, rd, rw = O.knn_cos(Xf, 9, q_begin=a, q_end=b)
+    exact((i.cpu().numpy(), d.cpu().numpy(), w.cpu().numpy()), (ri, rd, rw))
+
+
+def test_large_sampled_rows():
+    """Size-independent check at a production-like shape: 120k x 768 bf16, every
+    row certified or rescanned, sampled rows bit-exact vs the oracle."""
+    n, d, k = 120_000, 768, 16
+    Xt, Xf = bf16_rows(datagen.uniform(n, d, seed=77))
+    i, dd, w, st = hip(Xt, k)
+    rows = [0, 1, 4097, 65535, n - 1]
+    for r in rows:
+        ri, rd, rw = O.knn_cos(Xf, k, q_begin=r, q_end=r + 1)
+        exact((i[r:r + 1], dd[r:r + 1], w[r:r + 1]), (ri, rd, rw))
+    # every list is sorted by (dist, idx) and excludes self
+    assert np.all(np.diff(dd, axis=1) >= 0)
+    assert not np.any(i == np.arange(n)[:, None])
+
+
+def test_errors():
+    import surfface_hip as S
+    Xt, _ = bf16_rows(datagen.uniform(100, 16, seed=1))
+    with pytest.raises(S.MnError):
+        S.knn_cos_bf16(Xt, 0)
+    with pytest.raises(S.MnError):
+        S.knn_cos_bf16(Xt, 65)
+    bad = Xt.clone()
+    bad[3, 3] = float("nan")
+    with pytest.raises(S.MnError):
+        S.knn_cos_bf16(bad, 4)
