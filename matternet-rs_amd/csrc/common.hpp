@@ -14,6 +14,9 @@ namespace mn {
 void set_error(const char *fmt, ...);
 void clear_error();
 
+// MN_DEBUG_SYNC=1: synchronise after every launch so a fault names its kernel.
+bool debug_sync();
+
 // Grow-only device scratch, one set of slots per (thread, device).  Growing
 // frees the old block (hipFree synchronises), so never call it while kernels
 // that use that slot are in flight on another stream of this thread.
@@ -54,6 +57,19 @@ struct Timer {
             mn::set_error("%s failed: %s (%s:%d)", #expr, hipGetErrorString(_e),\
                           __FILE__, __LINE__);                                  \
             return MN_EHIP;                                                     \
+        }                                                                       \
+    } while (0)
+
+#define MN_KCHECK(stream, name)                                                 \
+    do {                                                                        \
+        MN_HIP_TRY(hipGetLastError());                                          \
+        if (mn::debug_sync()) {                                                 \
+            hipError_t _e = hipStreamSynchronize(stream);                       \
+            if (_e != hipSuccess) {                                             \
+                mn::set_error("%s: %s (%s:%d)", name, hipGetErrorString(_e),    \
+                              __FILE__, __LINE__);                              \
+                return MN_EHIP;                                                 \
+            }                                                                   \
         }                                                                       \
     } while (0)
 

@@ -35,21 +35,21 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
 constexpr int BM = 256;           // queries per block (4 waves x 64 rows)
-constexpr int BN = 256;           // corpus rows per tile (8 column tiles of 32)
+constexpr int BN = 128;           // corpus rows per tile (4 column blocks of 32)
 constexpr int BK = 32;            // bf16 features per LDS stage (2 x 16-deep MFMA steps)
 constexpr int LDK = BK;           // 64-B rows, 16-B chunks XOR-swizzled by (row >> 2) & 3
-constexpr int NWAVES = 4;         // one wave per SIMD: 256 accumulators in AGPRs
+constexpr int NWAVES = 4;         // one wave per SIMD
 constexpr int WR = BM / NWAVES;   // rows per wave (two 32-row MFMA blocks)
 constexpr int RM = WR / 32;
 constexpr int NT = 64 * NWAVES;
 constexpr int NCT = BN / 32;
-constexpr int QCAP = 40;
-constexpr int QPRE = QCAP - 32;   // merge before a column tile if cnt > QPRE
+constexpr int QCAP = 48;
+constexpr int QPRE = QCAP - 32;   // merge before a 32-column step if cnt > QPRE
 constexpr int LMAX = 128 - QCAP;  // L + QCAP <= 128
 constexpr int KMAX = 64;
 
 struct alignas(16) Smem {
-    uint16_t A[2][BM][LDK];
+    uint16_t A[2][BM][LDK];       // A[1] doubles as the epilogue key slabs
     uint16_t B[2][BN][LDK];
     float qd[BM][QCAP];
     int qi[BM][QCAP];
@@ -60,6 +60,8 @@ struct alignas(16) Smem {
     int lsz[BM];
     int ovf[BM];
 };
+static_assert(sizeof(float) * 32 * 32 * NWAVES <= sizeof(uint16_t) * BM * LDK,
+              "key slabs must fit in A[1]");
 
 __device__ __forceinline__ double bf2d(uint16_t b) {
     return (double)__uint_as_float((uint32_t)b << 16);
@@ -144,6 +146,9 @@ __device__ __forceinline__ void merge_row(Smem &sm, int row, int L, float *__res
 }
 
 __device__ const uint4 g_zero16[1] = {{0u, 0u, 0u, 0u}};
+#ifdef MN_BF16_DEBUG
+__device__ float g_dbg_keys[256 * 256];
+#endif
 
 // physical 16-B chunk of logical chunk c in LDS row r (conflict-free b128 reads
 // for 32 consecutive rows; LDS-DMA writes lane-linearly, so the permutation is
@@ -166,6 +171,98 @@ __device__ __forceinline__ void dma_piece(const uint16_t *__restrict__ X, int64_
                                      (__attribute__((address_space(3))) void *)lds_piece, 16, 0, 0);
 }
 
+struct EpiCtx {
+    int dx, qlim, clim, gc0, par, S, sl, L;
+    int64_t q0;
+    float *list_d;
+    int *list_i;
+};
+
+// Key slab: 32 rows x 32 f32 keys per wave (4 KB) in A[1] (idle during the
+// epilogue).  Row r lives at physical row r ^ ((r >> 2) & 1), so the MFMA-layout
+// writes (rows r and r+4 per half-wave) and the row-pair reads (rows 2i, 2i+1)
+// land in opposite halves of the bank space.
+__device__ __forceinline__ int slab_idx(int row, int col) {
+    return (row ^ ((row >> 2) & 1)) * 32 + col;
+}
+
+// Accumulator block (M, T) -> keys (-cos~; +inf for masked pairs, -2 for
+// forced pairs) in the wave's slab.
+template <int M, int T>
+__device__ __forceinline__ void write_keys(Smem &sm, const EpiCtx &ec, float *slab,
+                                           const f32x16 &v, int lane, int w) {
+    const int h = lane >> 5, cl = lane & 31;
+    const int colr = 32 * T + cl;
+    const bool colok = colr < ec.clim;
+    const float ci = sm.cinv[ec.par][colr];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const int rl = (r & 3) + 8 * (r >> 2) + 4 * h;
+        const int lrow = WR * w + 32 * M + rl;
+        const float qi = sm.qinv[lrow];
+        const bool valid = colok && lrow < ec.qlim && (lrow - colr) != ec.dx;
+        // n_q n_c near the reference's denom > 1e-12 switch: the approximation
+        // cannot tell cos from 0, so the pair becomes a forced candidate (key
+        // below every real key) and the exact re-rank decides.  Exactly-zero
+        // norms give key = -0 = exact.
+        float key = (qi * ci > 5e11f) ? -2.f : -(v[r] * qi) * ci;  // -cos~
+#ifdef MN_BF16_DEBUG
+        if (blockIdx.x == 0 && ec.gc0 == 0) g_dbg_keys[lrow * 256 + colr] = key;
+#endif
+        const bool bad = valid && !(__builtin_fabsf(key) <= 2.f);
+        if (bad) sm.ovf[lrow] = 1;
+        if (!valid || bad) key = __builtin_inff();
+        slab[slab_idx(rl, cl)] = key;
+    }
+}
+
+// Filter the slab (32 rows x 32 columns) against each row's threshold and
+// append survivors to the LDS queues (rows above QPRE are merged first).
+// Lanes 0-31 take row 2i, lanes 32-63 row 2i+1.
+template <int M>
+__device__ __forceinline__ void scan_slab(Smem &sm, const EpiCtx &ec, const float *slab,
+                                          int col0, int lane, int w) {
+    const int h = lane >> 5, cl = lane & 31;
+#pragma unroll 1
+    for (int i = 0; i < 16; ++i) {
+        const int rl = 2 * i + h;
+        const int row = WR * w + 32 * M + rl;
+        const int c = sm.cnt[row];
+        uint64_t need = __ballot(cl == 0 && c > QPRE);
+        while (need) {
+            const int ln = __builtin_ctzll(need);
+            need &= need - 1;
+            const int mrow = WR * w + 32 * M + 2 * i + (ln >> 5);
+            const int64_t base = ((ec.q0 + mrow) * ec.S + ec.sl) * (int64_t)ec.L;
+            merge_row(sm, mrow, ec.L, ec.list_d + base, ec.list_i + base);
+        }
+        const float key = slab[slab_idx(rl, cl)];
+        const bool pass = key < sm.tau[row];
+        const uint64_t pm = __ballot(pass);
+        if (pm) {
+            const uint32_t mh = (uint32_t)(pm >> (32 * h));
+            const int c2 = sm.cnt[row];
+            if (pass) {
+                const int pos = c2 + __popc(mh & ((1u << cl) - 1u));
+                sm.qd[row][pos] = key;
+                sm.qi[row][pos] = ec.gc0 + col0 + cl;
+            }
+            __builtin_amdgcn_wave_barrier();
+            if (cl == 0) sm.cnt[row] = c2 + __popc(mh);
+            __builtin_amdgcn_wave_barrier();
+        }
+    }
+}
+
+// Grid: one block per (query block, corpus slice), 1-D.  Consecutive blocks
+// land on different XCDs, so the linear id is remapped (bijectively) such that
+// the blocks one XCD runs together share query panels and corpus tiles in its
+// L2: all S slices of a query block are adjacent in the remapped order.
+__device__ __forceinline__ int xcd_remap(int orig, int nwg) {
+    const int q = nwg / 8, r = nwg % 8, xcd = orig % 8;
+    return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + orig / 8;
+}
+
 __global__ __launch_bounds__(NT) void k_gram_bf16(
     const uint16_t *__restrict__ Q, int64_t nq, const uint16_t *__restrict__ C, int64_t nc, int d,
     int64_t q_off, int64_t c_off, int excl, const float *__restrict__ qinv,
@@ -174,8 +271,9 @@ __global__ __launch_bounds__(NT) void k_gram_bf16(
     __shared__ Smem sm;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int h = lane >> 5, cl = lane & 31;
-    const int64_t q0 = (int64_t)blockIdx.x * BM;
-    const int sl = blockIdx.y;
+    const int wg = xcd_remap((int)blockIdx.x, (int)gridDim.x);
+    const int64_t q0 = (int64_t)(wg / S) * BM;
+    const int sl = wg % S;
     const int64_t cbeg = (int64_t)sl * chunk, cend = min(nc, cbeg + chunk);
     for (int r = tid; r < BM; r += NT) {
         sm.qinv[r] = (q0 + r < nq) ? qinv[q0 + r] : 0.f;
@@ -186,14 +284,18 @@ __global__ __launch_bounds__(NT) void k_gram_bf16(
     }
     __syncthreads();
     const int nk = (d + BK - 1) / BK;
-    // staging: per stage A and B are 16 pieces each (16 rows x 64 B); wave w
-    // issues pieces 4w..4w+3 of both
+    // staging per stage: A = 16 pieces, B = 8 pieces (16 rows x 64 B each);
+    // wave w issues A pieces 4w..4w+3 and B pieces 2w, 2w+1
     auto stage = [&](int buf, int64_t c0, int kt) {
         const int k0 = kt * BK;
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
             const int pc = 4 * w + u;
             dma_piece(Q, q0 + 16 * pc, nq, d, k0, &sm.A[buf][16 * pc][0], lane);
+        }
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const int pc = 2 * w + u;
             dma_piece(C, c0 + 16 * pc, cend, d, k0, &sm.B[buf][16 * pc][0], lane);
         }
     };
@@ -215,7 +317,7 @@ __global__ __launch_bounds__(NT) void k_gram_bf16(
             if (kt + 1 < nk) stage(cur ^ 1, c0, kt + 1);
 #pragma unroll
             for (int ks = 0; ks < BK / 16; ++ks) {
-                bf16x8 a[RM];
+                bf16x8 a[RM], b[NCT];
 #pragma unroll
                 for (int m = 0; m < RM; ++m) {
                     const int ar = WR * w + 32 * m + cl;
@@ -224,79 +326,50 @@ __global__ __launch_bounds__(NT) void k_gram_bf16(
 #pragma unroll
                 for (int t = 0; t < NCT; ++t) {
                     const int br = 32 * t + cl;
-                    const bf16x8 b = *reinterpret_cast<const bf16x8 *>(
-                        &sm.B[cur][br][8 * swz(br, 2 * ks + h)]);
+                    b[t] = *reinterpret_cast<const bf16x8 *>(&sm.B[cur][br][8 * swz(br, 2 * ks + h)]);
+                }
+#pragma unroll
+                for (int t = 0; t < NCT; ++t)
 #pragma unroll
                     for (int m = 0; m < RM; ++m)
-                        acc[m][t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[m], b, acc[m][t], 0, 0, 0);
-                }
+                        acc[m][t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[m], b[t], acc[m][t], 0, 0, 0);
             }
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __syncthreads();
         }
-        // next tile's first stage flies while the epilogue runs
+        // next tile's first stage flies while the epilogue runs (buffer 0;
+        // the epilogue's key slabs live in A[1])
         if (c0 + BN < cend) stage(0, c0 + BN, 0);
         // ---- epilogue: key = -cos~, filter, queue, merge (64 rows per wave) ----
         // global ids equal  <=>  lrow - col_in_tile == (c_off + c0) - (q_off + q0)
         const int64_t dl = (c_off + c0) - (q_off + q0);
-        const int dx = (excl && dl > -2 * BN && dl < 2 * BN) ? (int)dl : INT_MIN / 2;
-        const int qlim = (int)min<int64_t>(BM, nq - q0);
-        const int clim = (int)min<int64_t>(BN, cend - c0);
-#pragma unroll
-        for (int m = 0; m < RM; ++m)
-#pragma unroll
-        for (int t = 0; t < NCT; ++t) {
-            {
-                const int c = sm.cnt[WR * w + lane];
-                uint64_t need = __ballot(c > QPRE);
-                while (need) {
-                    const int rr = __builtin_ctzll(need);
-                    need &= need - 1;
-                    const int row = WR * w + rr;
-                    const int64_t base = ((q0 + row) * S + sl) * (int64_t)L;
-                    merge_row(sm, row, L, list_d + base, list_i + base);
-                }
-            }
-            const int colr = 32 * t + cl;
-            const bool colok = colr < clim;
-            const float ci = sm.cinv[par][colr];
-            const int gcol = (int)(c_off + c0) + colr;
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int lrow = WR * w + 32 * m + (r & 3) + 8 * (r >> 2) + 4 * h;
-                const float qi = sm.qinv[lrow];
-                const bool valid = colok && lrow < qlim && (lrow - colr) != dx;
-                // n_q n_c near the reference's denom > 1e-12 switch: the
-                // approximation cannot tell cos from 0, so the pair becomes a
-                // forced candidate (key below every real key) and the exact
-                // re-rank decides.  Exactly-zero norms give key = -0 = exact.
-                float key = (qi * ci > 5e11f) ? -2.f : -(acc[m][t][r] * qi) * ci;  // -cos~
-                const bool bad = valid && !(__builtin_fabsf(key) <= 2.f);
-                const bool pass = valid && !bad && key < sm.tau[lrow];
-                if (__builtin_expect(__ballot(bad) != 0, 0)) {
-                    if (bad) sm.ovf[lrow] = 1;
-                    __builtin_amdgcn_wave_barrier();
-                }
-                const uint64_t m = __ballot(pass);
-                if (m) {
-#pragma unroll
-                    for (int hh = 0; hh < 2; ++hh) {
-                        const uint32_t mh = (uint32_t)(m >> (32 * hh));
-                        if (!mh) continue;
-                        const int row = WR * w + 32 * m + (r & 3) + 8 * (r >> 2) + 4 * hh;
-                        const int c = sm.cnt[row];
-                        if (h == hh && pass) {
-                            const int pos = c + __popc(mh & ((1u << cl) - 1u));
-                            sm.qd[row][pos] = key;
-                            sm.qi[row][pos] = gcol;
-                        }
-                        __builtin_amdgcn_wave_barrier();
-                        if (lane == 0) sm.cnt[row] = c + __popc(mh);
-                        __builtin_amdgcn_wave_barrier();
-                    }
-                }
-            }
-        }
+        EpiCtx ec;
+        ec.dx = (excl && dl > -2 * BM && dl < 2 * BM) ? (int)dl : INT_MIN / 2;
+        ec.qlim = (int)min<int64_t>(BM, nq - q0);
+        ec.clim = (int)min<int64_t>(BN, cend - c0);
+        ec.gc0 = (int)(c_off + c0);
+        ec.par = par;
+        ec.q0 = q0;
+        ec.S = S;
+        ec.sl = sl;
+        ec.L = L;
+        ec.list_d = list_d;
+        ec.list_i = list_i;
+        float *slab = reinterpret_cast<float *>(&sm.A[1][0][0]) + 1024 * w;
+        // lane ids re-materialised per block: keeps the compiler from hoisting
+        // every epilogue address out of the tile loop (register pressure)
+#define MN_EPI(M, T)                                                                       \
+    {                                                                                      \
+        int lo = lane;                                                                     \
+        asm volatile("" : "+v"(lo));                                                       \
+        write_keys<M, T>(sm, ec, slab, acc[M][T], lo, w);                                  \
+        __builtin_amdgcn_wave_barrier();                                                   \
+        scan_slab<M>(sm, ec, slab, 32 * T, lo, w);                                         \
+        __builtin_amdgcn_wave_barrier();                                                   \
+    }
+        MN_EPI(0, 0) MN_EPI(0, 1) MN_EPI(0, 2) MN_EPI(0, 3)
+        MN_EPI(1, 0) MN_EPI(1, 1) MN_EPI(1, 2) MN_EPI(1, 3)
+#undef MN_EPI
     }
     for (int rr = 0; rr < WR; ++rr) {
         const int row = WR * w + rr;
@@ -562,7 +635,7 @@ static int knn_cos_bf16_impl(const uint16_t *Q, int64_t nq, const uint16_t *C, i
         if (!same && nc > 0)
             hipLaunchKernelGGL(k_pad_rows, dim3((unsigned)((nc * d8 + 255) / 256)), dim3(256), 0, s,
                                C, nc, d, d8, Cp);
-        MN_HIP_TRY(hipGetLastError());
+        MN_KCHECK(s, "k_pad_rows");
         Q = Qp;
         C = Cp;
         d = d8;
@@ -575,20 +648,20 @@ static int knn_cos_bf16_impl(const uint16_t *Q, int64_t nq, const uint16_t *C, i
     if (!same && nc > 0)
         hipLaunchKernelGGL(k_bf16_norms, dim3((unsigned)((nc + 255) / 256)), dim3(256), 0, s, C, nc,
                            d, cn, cinv, flags + 1);
-    MN_HIP_TRY(hipGetLastError());
+    MN_KCHECK(s, "k_bf16_norms");
     int hf[4] = {0, 0, 0, 0};
     MN_HIP_TRY(hipMemcpyAsync(hf, flags, 16, hipMemcpyDeviceToHost, s));
     MN_HIP_TRY(hipStreamSynchronize(s));
     MN_REQUIRE(hf[1] == 0, MN_ENONFINITE, "mn_knn_cos_bf16: input contains NaN/inf");
     tm.mark();
     if (nc > 0) {
-        hipLaunchKernelGGL(k_gram_bf16, dim3((unsigned)blocks_q, (unsigned)S), dim3(NT), 0, s, Q, nq,
+        hipLaunchKernelGGL(k_gram_bf16, dim3((unsigned)(blocks_q * S)), dim3(NT), 0, s, Q, nq,
                            C, nc, d, q_off, c_off, excl, qinv, cinv, L, (int)S, chunk, list_d,
                            list_i, lsz, ltau);
     } else {
         MN_HIP_TRY(hipMemsetAsync(lsz, 0, sizeof(int) * (size_t)nq * S, s));
     }
-    MN_HIP_TRY(hipGetLastError());
+    MN_KCHECK(s, "k_gram_bf16");
     tm.mark();
     const double delta = 2.0 * ((double)d + 12.0) * 0x1p-24;
     const int64_t nvalid = same ? nc - 1 : nc;  // qc callers: exclusion inside the shard
@@ -600,12 +673,12 @@ static int knn_cos_bf16_impl(const uint16_t *Q, int64_t nq, const uint16_t *C, i
                        fb_list)
     if (NR == 1) MN_RR(1); else if (NR == 2) MN_RR(2); else MN_RR(4);
 #undef MN_RR
-    MN_HIP_TRY(hipGetLastError());
+    MN_KCHECK(s, "k_cos_rerank");
     tm.mark();
     hipLaunchKernelGGL(k_cos_fallback, dim3((unsigned)std::min<int64_t>(nq, 1024)), dim3(FBT), 0, s,
                        Q, C, nc, d, q_off, c_off, excl, qn, cn, o->topk, o->eps, o->sigma, o->p,
                        flags + 2, fb_list, out_idx, out_dist, out_w);
-    MN_HIP_TRY(hipGetLastError());
+    MN_KCHECK(s, "k_cos_fallback");
     tm.mark();
     MN_HIP_TRY(hipMemcpyAsync(hf, flags, 16, hipMemcpyDeviceToHost, s));
     MN_HIP_TRY(hipStreamSynchronize(s));

@@ -4,6 +4,8 @@
 #include <string>
 #include <unordered_map>
 
+#include <cstdlib>
+
 #include "common.hpp"
 
 namespace mn {
@@ -19,6 +21,14 @@ void set_error(const char *fmt, ...) {
     g_err = buf;
 }
 void clear_error() { g_err.clear(); }
+
+bool debug_sync() {
+    static const bool on = [] {
+        const char *e = getenv("MN_DEBUG_SYNC");
+        return e && e[0] && e[0] != '0';
+    }();
+    return on;
+}
 
 namespace {
 struct Block { void *p = nullptr; size_t bytes = 0; };
