@@ -34,23 +34,24 @@ namespace kb16 {
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
-constexpr int BM = 256;           // queries per block (4 waves x 64 rows)
+constexpr int BM = 256;           // queries per block (8 waves x 32 rows)
 constexpr int BN = 128;           // corpus rows per tile (4 column blocks of 32)
 constexpr int BK = 32;            // bf16 features per LDS stage (2 x 16-deep MFMA steps)
 constexpr int LDK = BK;           // 64-B rows, 16-B chunks XOR-swizzled by (row >> 2) & 3
-constexpr int NWAVES = 4;         // one wave per SIMD
-constexpr int WR = BM / NWAVES;   // rows per wave (two 32-row MFMA blocks)
+constexpr int NWAVES = 8;         // two waves per SIMD: one's epilogue/DMA overlaps the other's MFMAs
+constexpr int WR = BM / NWAVES;   // rows per wave (one 32-row MFMA block)
 constexpr int RM = WR / 32;
 constexpr int NT = 64 * NWAVES;
 constexpr int NCT = BN / 32;
-constexpr int QCAP = 48;
-constexpr int QPRE = QCAP - 32;   // merge before a 32-column step if cnt > QPRE
+constexpr int QCAP = 40;
+constexpr int QPRE = QCAP - 32;   // merge before a 32-column block if cnt > QPRE
+constexpr int NSTAGE = 3;         // LDS-DMA ring depth (two stages in flight)
 constexpr int LMAX = 128 - QCAP;  // L + QCAP <= 128
 constexpr int KMAX = 64;
 
 struct alignas(16) Smem {
-    uint16_t A[2][BM][LDK];       // A[1] doubles as the epilogue key slabs
-    uint16_t B[2][BN][LDK];
+    uint16_t A[NSTAGE][BM][LDK];
+    uint16_t B[NSTAGE][BN][LDK];
     float qd[BM][QCAP];
     int qi[BM][QCAP];
     float cinv[2][BN];
@@ -60,8 +61,6 @@ struct alignas(16) Smem {
     int lsz[BM];
     int ovf[BM];
 };
-static_assert(sizeof(float) * 32 * 32 * NWAVES <= sizeof(uint16_t) * BM * LDK,
-              "key slabs must fit in A[1]");
 
 __device__ __forceinline__ double bf2d(uint16_t b) {
     return (double)__uint_as_float((uint32_t)b << 16);
@@ -178,78 +177,65 @@ struct EpiCtx {
     int *list_i;
 };
 
-// Key slab: 32 rows x 32 f32 keys per wave (4 KB) in A[1] (idle during the
-// epilogue).  Row r lives at physical row r ^ ((r >> 2) & 1), so the MFMA-layout
-// writes (rows r and r+4 per half-wave) and the row-pair reads (rows 2i, 2i+1)
-// land in opposite halves of the bank space.
-__device__ __forceinline__ int slab_idx(int row, int col) {
-    return (row ^ ((row >> 2) & 1)) * 32 + col;
-}
-
-// Accumulator block (M, T) -> keys (-cos~; +inf for masked pairs, -2 for
-// forced pairs) in the wave's slab.
+// One 32x32 accumulator block (rows 32M.. of the wave, columns 32T.. of the
+// tile): merge rows whose queue could overflow (a block adds <= 32 entries per
+// row), then filter key < tau and append survivors to the per-row LDS queues.
+// `lane` is passed in opaque (see the call site).
 template <int M, int T>
-__device__ __forceinline__ void write_keys(Smem &sm, const EpiCtx &ec, float *slab,
-                                           const f32x16 &v, int lane, int w) {
+__device__ __forceinline__ void epilogue_block(Smem &sm, const EpiCtx &ec, const f32x16 &v,
+                                               int lane, int w) {
     const int h = lane >> 5, cl = lane & 31;
+    {
+        const int c = lane < WR ? sm.cnt[WR * w + lane] : 0;
+        uint64_t need = __ballot(c > QPRE);
+        while (need) {
+            const int rr = __builtin_ctzll(need);
+            need &= need - 1;
+            const int row = WR * w + rr;
+            const int64_t base = ((ec.q0 + row) * ec.S + ec.sl) * (int64_t)ec.L;
+            merge_row(sm, row, ec.L, ec.list_d + base, ec.list_i + base);
+        }
+    }
     const int colr = 32 * T + cl;
     const bool colok = colr < ec.clim;
     const float ci = sm.cinv[ec.par][colr];
+    const int gcol = ec.gc0 + colr;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-        const int rl = (r & 3) + 8 * (r >> 2) + 4 * h;
-        const int lrow = WR * w + 32 * M + rl;
+        const int lrow = WR * w + 32 * M + (r & 3) + 8 * (r >> 2) + 4 * h;
         const float qi = sm.qinv[lrow];
         const bool valid = colok && lrow < ec.qlim && (lrow - colr) != ec.dx;
         // n_q n_c near the reference's denom > 1e-12 switch: the approximation
         // cannot tell cos from 0, so the pair becomes a forced candidate (key
         // below every real key) and the exact re-rank decides.  Exactly-zero
         // norms give key = -0 = exact.
-        float key = (qi * ci > 5e11f) ? -2.f : -(v[r] * qi) * ci;  // -cos~
+        const float key = (qi * ci > 5e11f) ? -2.f : -(v[r] * qi) * ci;  // -cos~
 #ifdef MN_BF16_DEBUG
         if (blockIdx.x == 0 && ec.gc0 == 0) g_dbg_keys[lrow * 256 + colr] = key;
 #endif
         const bool bad = valid && !(__builtin_fabsf(key) <= 2.f);
-        if (bad) sm.ovf[lrow] = 1;
-        if (!valid || bad) key = __builtin_inff();
-        slab[slab_idx(rl, cl)] = key;
-    }
-}
-
-// Filter the slab (32 rows x 32 columns) against each row's threshold and
-// append survivors to the LDS queues (rows above QPRE are merged first).
-// Lanes 0-31 take row 2i, lanes 32-63 row 2i+1.
-template <int M>
-__device__ __forceinline__ void scan_slab(Smem &sm, const EpiCtx &ec, const float *slab,
-                                          int col0, int lane, int w) {
-    const int h = lane >> 5, cl = lane & 31;
-#pragma unroll 1
-    for (int i = 0; i < 16; ++i) {
-        const int rl = 2 * i + h;
-        const int row = WR * w + 32 * M + rl;
-        const int c = sm.cnt[row];
-        uint64_t need = __ballot(cl == 0 && c > QPRE);
-        while (need) {
-            const int ln = __builtin_ctzll(need);
-            need &= need - 1;
-            const int mrow = WR * w + 32 * M + 2 * i + (ln >> 5);
-            const int64_t base = ((ec.q0 + mrow) * ec.S + ec.sl) * (int64_t)ec.L;
-            merge_row(sm, mrow, ec.L, ec.list_d + base, ec.list_i + base);
+        const bool pass = valid && !bad && key < sm.tau[lrow];
+        if (__builtin_expect(__ballot(bad) != 0, 0)) {
+            if (bad) sm.ovf[lrow] = 1;
+            __builtin_amdgcn_wave_barrier();
         }
-        const float key = slab[slab_idx(rl, cl)];
-        const bool pass = key < sm.tau[row];
         const uint64_t pm = __ballot(pass);
         if (pm) {
-            const uint32_t mh = (uint32_t)(pm >> (32 * h));
-            const int c2 = sm.cnt[row];
-            if (pass) {
-                const int pos = c2 + __popc(mh & ((1u << cl) - 1u));
-                sm.qd[row][pos] = key;
-                sm.qi[row][pos] = ec.gc0 + col0 + cl;
+#pragma unroll
+            for (int hh = 0; hh < 2; ++hh) {
+                const uint32_t mh = (uint32_t)(pm >> (32 * hh));
+                if (!mh) continue;
+                const int row = WR * w + 32 * M + (r & 3) + 8 * (r >> 2) + 4 * hh;
+                const int c = sm.cnt[row];
+                if (h == hh && pass) {
+                    const int pos = c + __popc(mh & ((1u << cl) - 1u));
+                    sm.qd[row][pos] = key;
+                    sm.qi[row][pos] = gcol;
+                }
+                __builtin_amdgcn_wave_barrier();
+                if (lane == 0) sm.cnt[row] = c + __popc(mh);
+                __builtin_amdgcn_wave_barrier();
             }
-            __builtin_amdgcn_wave_barrier();
-            if (cl == 0) sm.cnt[row] = c2 + __popc(mh);
-            __builtin_amdgcn_wave_barrier();
         }
     }
 }
@@ -269,7 +255,8 @@ __global__ __launch_bounds__(NT) void k_gram_bf16(
     const float *__restrict__ cinv, int L, int S, int64_t chunk, float *__restrict__ list_d,
     int *__restrict__ list_i, int *__restrict__ out_lsz, float *__restrict__ out_tau) {
     __shared__ Smem sm;
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: SGPR row math
     const int h = lane >> 5, cl = lane & 31;
     const int wg = xcd_remap((int)blockIdx.x, (int)gridDim.x);
     const int64_t q0 = (int64_t)(wg / S) * BM;
@@ -285,22 +272,35 @@ __global__ __launch_bounds__(NT) void k_gram_bf16(
     __syncthreads();
     const int nk = (d + BK - 1) / BK;
     // staging per stage: A = 16 pieces, B = 8 pieces (16 rows x 64 B each);
-    // wave w issues A pieces 4w..4w+3 and B pieces 2w, 2w+1
+    // wave w issues A pieces 2w, 2w+1 and B piece w
+    static_assert(BM / 16 == 2 * NWAVES && BN / 16 == NWAVES, "staging split");
+    constexpr int kPiecesPerWave = 3;
     auto stage = [&](int buf, int64_t c0, int kt) {
         const int k0 = kt * BK;
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const int pc = 4 * w + u;
-            dma_piece(Q, q0 + 16 * pc, nq, d, k0, &sm.A[buf][16 * pc][0], lane);
-        }
-#pragma unroll
         for (int u = 0; u < 2; ++u) {
             const int pc = 2 * w + u;
-            dma_piece(C, c0 + 16 * pc, cend, d, k0, &sm.B[buf][16 * pc][0], lane);
+            dma_piece(Q, q0 + 16 * pc, nq, d, k0, &sm.A[buf][16 * pc][0], lane);
+        }
+        dma_piece(C, c0 + 16 * w, cend, d, k0, &sm.B[buf][16 * w][0], lane);
+    };
+    // Stage ring over the whole sweep: global stage g = tile * nk + kt lives in
+    // buffer g % NSTAGE; two stages are in flight while one is consumed.  Each
+    // wave issues kPiecesPerWave LDS-DMA pieces per stage, so "stage g landed" is
+    // vmcnt(kPiecesPerWave * stages issued after g).
+    int64_t ic0 = cbeg;  // next stage to issue: tile base, k-step, ring slot
+    int ikt = 0, ibuf = 0;
+    auto issue = [&]() {
+        if (ic0 < cend) {
+            stage(ibuf, ic0, ikt);
+            ibuf = ibuf == NSTAGE - 1 ? 0 : ibuf + 1;
+            if (++ikt == nk) { ikt = 0; ic0 += BN; }
         }
     };
+    issue();
+    issue();
+    int cur = 0;
     int par = 0;
-    if (cbeg < cend) stage(0, cbeg, 0);
     for (int64_t c0 = cbeg; c0 < cend; c0 += BN, par ^= 1) {
         if (tid < BN) sm.cinv[par][tid] = (c0 + tid < cend) ? cinv[c0 + tid] : 0.f;
         f32x16 acc[RM][NCT];
@@ -310,11 +310,14 @@ __global__ __launch_bounds__(NT) void k_gram_bf16(
             for (int t = 0; t < NCT; ++t)
 #pragma unroll
                 for (int r = 0; r < 16; ++r) acc[m][t][r] = 0.f;
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        for (int kt = 0; kt < nk; ++kt) {
-            const int cur = kt & 1;
-            if (kt + 1 < nk) stage(cur ^ 1, c0, kt + 1);
+        for (int kt = 0; kt < nk; ++kt, cur = cur == NSTAGE - 1 ? 0 : cur + 1) {
+            // this stage landed (one stage may stay in flight behind it) ...
+            if (ic0 < cend) asm volatile("s_waitcnt vmcnt(%0)" ::"i"(kPiecesPerWave) : "memory");
+            else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            // ... and is visible to all waves, which are all done with the
+            // previous stage's buffer: the next issue overwrites it
+            __builtin_amdgcn_s_barrier();
+            issue();
 #pragma unroll
             for (int ks = 0; ks < BK / 16; ++ks) {
                 bf16x8 a[RM], b[NCT];
@@ -334,12 +337,8 @@ __global__ __launch_bounds__(NT) void k_gram_bf16(
                     for (int m = 0; m < RM; ++m)
                         acc[m][t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[m], b[t], acc[m][t], 0, 0, 0);
             }
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __syncthreads();
         }
-        // next tile's first stage flies while the epilogue runs (buffer 0;
-        // the epilogue's key slabs live in A[1])
-        if (c0 + BN < cend) stage(0, c0 + BN, 0);
+        __syncthreads();  // cinv[par] written by other waves
         // ---- epilogue: key = -cos~, filter, queue, merge (64 rows per wave) ----
         // global ids equal  <=>  lrow - col_in_tile == (c_off + c0) - (q_off + q0)
         const int64_t dl = (c_off + c0) - (q_off + q0);
@@ -355,21 +354,19 @@ __global__ __launch_bounds__(NT) void k_gram_bf16(
         ec.L = L;
         ec.list_d = list_d;
         ec.list_i = list_i;
-        float *slab = reinterpret_cast<float *>(&sm.A[1][0][0]) + 1024 * w;
-        // lane ids re-materialised per block: keeps the compiler from hoisting
+        // lane id re-materialised per block: keeps the compiler from hoisting
         // every epilogue address out of the tile loop (register pressure)
 #define MN_EPI(M, T)                                                                       \
     {                                                                                      \
-        int lo = lane;                                                                     \
-        asm volatile("" : "+v"(lo));                                                       \
-        write_keys<M, T>(sm, ec, slab, acc[M][T], lo, w);                                  \
-        __builtin_amdgcn_wave_barrier();                                                   \
-        scan_slab<M>(sm, ec, slab, 32 * T, lo, w);                                         \
-        __builtin_amdgcn_wave_barrier();                                                   \
+        int lo = lane, wo = w;                                                             \
+        asm volatile("" : "+v"(lo), "+s"(wo));                                             \
+        epilogue_block<M, T>(sm, ec, acc[M][T], lo, wo);                                   \
     }
         MN_EPI(0, 0) MN_EPI(0, 1) MN_EPI(0, 2) MN_EPI(0, 3)
-        MN_EPI(1, 0) MN_EPI(1, 1) MN_EPI(1, 2) MN_EPI(1, 3)
 #undef MN_EPI
+        // the epilogue's list stores must not satisfy the next counted vmcnt
+        // ahead of an older LDS-DMA piece: drain them here (once per tile)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     for (int rr = 0; rr < WR; ++rr) {
         const int row = WR * w + rr;

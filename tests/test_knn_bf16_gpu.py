@@ -104,6 +104,8 @@ def test_large_sampled_rows():
     for r in rows:
         ri, rd, rw = O.knn_cos(Xf, k, q_begin=r, q_end=r + 1)
         exact((i[r:r + 1], dd[r:r + 1], w[r:r + 1]), (ri, rd, rw))
+    # uniform data: the candidate bound certifies every row
+    assert st["n_uncertified"] == 0
     # every list is sorted by (dist, idx) and excludes self
     assert np.all(np.diff(dd, axis=1) >= 0)
     assert not np.any(i == np.arange(n)[:, None])
