@@ -152,4 +152,42 @@ __device__ __forceinline__ T wave_elem(const T (&d)[NR], int pos) {
     return __shfl(v, l);
 }
 
+// Keys-only ascending bitonic sort of 64*NR floats (element e = lane + 64*r),
+// min/max exchanges (no tie-break needed).  NaN-free inputs.  Whole wave.
+template <int NR>
+__device__ __forceinline__ void wave_sort_f32(float (&d)[NR]) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int k = 2; k <= 64 * NR; k <<= 1) {
+#pragma unroll
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            if (j >= 64) {
+#pragma unroll
+                for (int r = 0; r < NR; ++r) {
+                    const int pr = r ^ (j >> 6);
+                    if (pr > r) {
+                        const bool asc = ((lane + 64 * r) & k) == 0;
+                        const float lo = fminf(d[r], d[pr]), hi = fmaxf(d[r], d[pr]);
+                        d[r] = asc ? lo : hi;
+                        d[pr] = asc ? hi : lo;
+                    }
+                }
+            } else {
+#pragma unroll
+                for (int r = 0; r < NR; ++r) {
+                    const int e = lane + 64 * r;
+                    const float pd = __shfl_xor(d[r], j);
+                    const bool keep_min = (((e & k) == 0) == ((e & j) == 0));
+                    d[r] = keep_min ? fminf(d[r], pd) : fmaxf(d[r], pd);
+                }
+            }
+        }
+    }
+}
+
+template <int NR>
+__device__ __forceinline__ float wave_elem_f32(const float (&d)[NR], int pos) {
+    return wave_elem<NR, float>(d, pos);
+}
+
 }  // namespace mn

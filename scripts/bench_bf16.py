@@ -1,6 +1,8 @@
 """Quick C5 item-graph timing: knn_cos_bf16 on n x d uniform bf16 rows."""
 import argparse, json, sys, time
-sys.path.insert(0, "matternet-rs_amd")
+import os
+_R = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(_R, "matternet-rs_amd"))
 import torch
 import surfface_hip as S
 

@@ -1,5 +1,7 @@
 import sys, numpy as np, torch
-sys.path.insert(0, "matternet-rs_amd"); sys.path.insert(0, "tests"); sys.path.insert(0, ".")
+import os
+_R = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(_R, "matternet-rs_amd")); sys.path.insert(0, os.path.join(_R, "tests")); sys.path.insert(0, _R)
 import datagen
 from oracle import oracle as O
 import surfface_hip as S
