@@ -103,15 +103,15 @@ __global__ __launch_bounds__(256) void k_bf16_norms(const uint16_t *__restrict__
                 const double a = bf2d((uint16_t)(w[u] & 0xFFFFu));
                 const double b = bf2d((uint16_t)(w[u] >> 16));
                 bad |= !isfinite(a) || !isfinite(b);
-                acc = acc + a * a;
-                acc = acc + b * b;
+                acc = __builtin_fma(a, a, acc);  // exact square: same rounding as acc + a*a
+                acc = __builtin_fma(b, b, acc);
             }
         }
     } else {
         for (; t < d; ++t) {
             const double a = bf2d(p[t]);
             bad |= !isfinite(a);
-            acc = acc + a * a;
+            acc = __builtin_fma(a, a, acc);
         }
     }
     const double nv = __builtin_sqrt(acc);
@@ -473,6 +473,8 @@ __global__ __launch_bounds__(NT) void k_gram_bf16(
 }
 
 // ---- exact re-rank / certification / filter --------------------------------------
+// The reference's `acc + a * b` in f64: a bf16 x bf16 product is exact in f64
+// (8 + 8 significant bits), so one fused multiply-add rounds identically.
 __device__ __forceinline__ double exact_dot(const uint16_t *__restrict__ a,
                                             const uint16_t *__restrict__ b, int d) {
     double acc = -0.0;
@@ -483,12 +485,14 @@ __device__ __forceinline__ double exact_dot(const uint16_t *__restrict__ a,
             const uint32_t wa[4] = {va.x, va.y, va.z, va.w}, wb[4] = {vb.x, vb.y, vb.z, vb.w};
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
-                acc = acc + bf2d((uint16_t)(wa[u] & 0xFFFFu)) * bf2d((uint16_t)(wb[u] & 0xFFFFu));
-                acc = acc + bf2d((uint16_t)(wa[u] >> 16)) * bf2d((uint16_t)(wb[u] >> 16));
+                acc = __builtin_fma(bf2d((uint16_t)(wa[u] & 0xFFFFu)),
+                                    bf2d((uint16_t)(wb[u] & 0xFFFFu)), acc);
+                acc = __builtin_fma(bf2d((uint16_t)(wa[u] >> 16)), bf2d((uint16_t)(wb[u] >> 16)),
+                                    acc);
             }
         }
     } else {
-        for (int t = 0; t < d; ++t) acc = acc + bf2d(a[t]) * bf2d(b[t]);
+        for (int t = 0; t < d; ++t) acc = __builtin_fma(bf2d(a[t]), bf2d(b[t]), acc);
     }
     return acc;
 }
@@ -518,6 +522,7 @@ __global__ __launch_bounds__(256) void k_cos_rerank(
     int32_t *__restrict__ out_idx, double *__restrict__ out_dist, double *__restrict__ out_w,
     int *__restrict__ fb_count, int *__restrict__ fb_list) {
     __shared__ int cand[4][64 * NR];
+    __shared__ float candk[4][64 * NR];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const int64_t q = (int64_t)blockIdx.x * 4 + wid;
     if (q >= nq) return;
@@ -539,29 +544,58 @@ __global__ __launch_bounds__(256) void k_cos_rerank(
             const bool pass = e < cnt && __uint_as_float(v.x) <= ts;
             const uint64_t pm = __ballot(pass);
             const int pos = M + (int)__popcll(pm & ((1ull << lane) - 1ull));
-            if (pass && pos < 64 * NR) cand[wid][pos] = (int)v.y;
+            if (pass && pos < 64 * NR) {
+                cand[wid][pos] = (int)v.y;
+                candk[wid][pos] = __uint_as_float(v.x);
+            }
             M += (int)__popcll(pm);
         }
     }
     forced |= M > 64 * NR;
     M = min(M, 64 * NR);
     __builtin_amdgcn_wave_barrier();
-    double dd[NR];
+    // candidates in approximate order (key, id)
+    float kk[NR];
     int ix[NR];
 #pragma unroll
     for (int r = 0; r < NR; ++r) {
         const int e = lane + 64 * r;
-        ix[r] = e < M ? cand[wid][e] : -1;
+        kk[r] = e < M ? candk[wid][e] : __builtin_inff();
+        ix[r] = e < M ? cand[wid][e] : INT_MAX;
     }
+    wave_bitonic_sort<NR>(kk, ix);
+    // exact distances, pruned: the kq best by key first; their largest exact
+    // distance Dp bounds the k-th.  A candidate with key kappa has exact
+    // distance >= 1 - max(-kappa + delta, 0) (|cos~ - cos| <= delta); above
+    // Dp it cannot reach the top k and is skipped (its distance stays +inf,
+    // strictly beyond D_k, so the certification below is unaffected).
     const uint16_t *qrow = Q + q * (int64_t)d;
+    const int kq = min(topk, M);
+    double dd[NR];
 #pragma unroll
     for (int r = 0; r < NR; ++r) {
-        if (ix[r] >= 0) {
+        const int e = lane + 64 * r;
+        dd[r] = __builtin_inf();
+        if (e < kq) {
             const int64_t c = (int64_t)ix[r] - c_off;
             dd[r] = cos_dist(exact_dot(qrow, C + c * d, d), qn[q], cn[c]);
-        } else {
-            dd[r] = __builtin_inf();
-            ix[r] = INT_MAX;
+        }
+    }
+    double Dp = -__builtin_inf();
+#pragma unroll
+    for (int r = 0; r < NR; ++r) Dp = fmax(Dp, (lane + 64 * r) < kq ? dd[r] : -__builtin_inf());
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) Dp = fmax(Dp, __shfl_xor(Dp, o));
+#pragma unroll
+    for (int r = 0; r < NR; ++r) {
+        const int e = lane + 64 * r;
+        if (e >= kq && e < M) {
+            const double cub = -(double)kk[r] + delta;
+            const double lb = 1.0 - (cub > 0.0 ? cub : 0.0);
+            if (lb <= Dp) {
+                const int64_t c = (int64_t)ix[r] - c_off;
+                dd[r] = cos_dist(exact_dot(qrow, C + c * d, d), qn[q], cn[c]);
+            }
         }
     }
     wave_bitonic_sort<NR>(dd, ix);
