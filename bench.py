@@ -44,6 +44,12 @@ def parse():
     ap.add_argument("--seed", type=int, default=42)
     ap.add_argument("--cpu-seconds", type=float, default=15.0,
                     help="target CPU time of the sampled cpu_baseline leg (0 = skip)")
+    ap.add_argument("--no-c5", dest="c5", action="store_false",
+                    help="skip the configs[4] leg (1M x 3072 bf16 cosine item graph + SF-GRASS)")
+    ap.add_argument("--c5-rows", type=int, default=1_048_576)
+    ap.add_argument("--c5-dim", type=int, default=3072)
+    ap.add_argument("--c5-parity-rows", type=int, default=3,
+                    help="rows of the C5 graph checked bit-exact against the oracle (0 = off)")
     ap.add_argument("--no-c3", dest="c3", action="store_false",
                     help="skip the C3 legs (Laplacian assembly, energy pass, sorted index)")
     ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_gram_latest.json"),
@@ -148,6 +154,10 @@ def main():
     if a.c3:
         c3 = c3_legs(S, X, out[0], out[1], k)
 
+    c5 = None
+    if a.c5 and world == 1:
+        c5 = c5_leg(S, _lib, L, a, dev, stream)
+
     cpu = None
     parity = None
     if rank == 0 and world == 1 and a.cpu_seconds > 0:
@@ -172,6 +182,7 @@ def main():
             "parity_sample": parity,
             "energy_rows_per_sec": (c3 or {}).get("energy_rows_per_sec"),
             "c3_legs": c3,
+            "c5_leg": c5,
             "knn_stats": {"uncertified_rows": st["n_uncertified"], "slices": st["slices"],
                           "list_len": st["list_len"], "ms_norms": st["ms_norms"],
                           "ms_gram": st["ms_gram"], "ms_rerank": st["ms_rerank"],
@@ -228,6 +239,61 @@ def c3_legs(S, X, idx, dist, k):
     ms, sl = _timed(lambda: S.SortedLambdas().build_from(lam_n))
     out["sorted_index"] = {"ms": round(ms, 3), "std_dev": sl.std_dev,
                            "GB_per_s": round(n * 16 / ms / 1e6, 1)}
+    return out
+
+
+BF16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X dense bf16 (MI355X_MICROARCH.md), no sparsity
+
+
+def c5_leg(S, _lib, L, a, dev, stream):
+    """BASELINE.json configs[4]: 1M x 3072 bf16 rectified-cosine item graph
+    (topk=32, eps=1, sigma=1, p=2; legacy _build_adjacency semantics) on the
+    bf16 MFMA path, then SF-GRASS (sparsification.rs, ratio 0.5) on its rows.
+    One timed run (the Gram alone is ~10 s), parity rows vs the oracle."""
+    n, d, k = a.c5_rows, a.c5_dim, a.k
+    Xb = torch.empty((n, d), dtype=torch.bfloat16, device=dev)
+    ch = 1 << 17
+    tmp = torch.empty((min(ch, n), d), dtype=torch.float32, device=dev)
+    for r0 in range(0, n, ch):
+        m = min(ch, n - r0)
+        _lib.check(L.mn_fill_uniform_f32(tmp.data_ptr(), m, d, a.seed + 5, r0, stream.cuda_stream))
+        Xb[r0:r0 + m].copy_(tmp[:m])  # round-to-nearest-even
+    del tmp
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    idx, dist, w, st = S.knn_cos_bf16(Xb, k, eps=1.0, sigma=1.0, p=2.0, timing=True)
+    torch.cuda.synchronize()
+    ms = (time.perf_counter() - t0) * 1e3
+    ms_sp, (sidx, sw, applied) = _timed(lambda: S.sparsify_rows(idx, w, 0.5))
+    kept = int((sidx >= 0).sum().item())
+    flops = 2.0 * n * n * d
+    ach = flops / (st["ms_gram"] * 1e-3) / 1e12
+    out = {"workload": f"C5: {n} x {d} bf16 rectified-cosine item graph k={k} + SF-GRASS 0.5",
+           "ms_total": round(ms, 1), "pairs_per_s": n * n / (ms * 1e-3),
+           "roofline": {"bound": "mfma", "kernel": "k_gram_bf16", "achieved": round(ach, 1),
+                        "peak": BF16_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                        "frac": round(ach / BF16_MFMA_PEAK_TFLOPS, 4), "flop_per_launch": flops,
+                        "ms_per_launch": round(st["ms_gram"], 1)},
+           "knn_stats": {kk: (round(v, 3) if isinstance(v, float) else v) for kk, v in st.items()},
+           "sfgrass": {"ms": round(ms_sp, 3), "applied": applied, "edges_kept": kept,
+                       "edges_in": int((idx >= 0).sum().item())}}
+    if a.c5_parity_rows > 0:
+        import oracle.oracle as O
+        rows = np.unique(np.linspace(0, n - 1, a.c5_parity_rows).astype(np.int64))
+        bits = Xb.view(torch.int16).cpu().numpy().view(np.uint16)
+        t1 = time.perf_counter()
+        ri, rd, rw = O.knn_cos_bf16_rows(bits, k, rows, nthreads=16)
+        oms = (time.perf_counter() - t1) * 1e3
+        gi = idx[torch.from_numpy(rows).to(dev)].cpu().numpy()
+        gd = dist[torch.from_numpy(rows).to(dev)].cpu().numpy()
+        gw = w[torch.from_numpy(rows).to(dev)].cpu().numpy()
+        same = (np.array_equal(gi, ri) and np.array_equal(gd.view(np.uint64), rd.view(np.uint64))
+                and np.array_equal(gw.view(np.uint64), rw.view(np.uint64)))
+        out["parity_sample"] = {"rows": rows.tolist(), "bit_exact": bool(same),
+                                "oracle_ms": round(oms, 1), "oracle_threads": 16}
+        del bits
+    del Xb, idx, dist, w, sidx, sw
+    torch.cuda.empty_cache()
     return out
 
 

@@ -735,7 +735,7 @@ static int knn_cos_bf16_impl(const uint16_t *Q, int64_t nq, const uint16_t *C, i
     // corpus slices: enough blocks to fill the chip, and at least kMinSlices
     // so the co-scheduled slices of one query block share its query panel in
     // the XCD's L2 (each block re-reads it once per corpus tile)
-    const int64_t kMinSlices = (int64_t)getenv_int("MN_BF16_MIN_SLICES", 4);
+    const int64_t kMinSlices = (int64_t)getenv_int("MN_BF16_MIN_SLICES", 2);
     int64_t S = std::max<int64_t>(kMinSlices, (512 + blocks_q - 1) / blocks_q);
     S = std::min<int64_t>(S, 256 / L);
     S = std::min<int64_t>(S, std::max<int64_t>(1, (nc + BN - 1) / BN));

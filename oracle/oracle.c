@@ -266,6 +266,94 @@ int or_knn_cos_f64(const float *X, int64_t n, int32_t d, int32_t topk,
     return err;
 }
 
+/* A.1c on bf16 rows (config 5), explicit query rows: the same arithmetic as
+ * or_knn_cos_f64 on the exactly widened values (bf16 -> f32 is a 16-bit
+ * shift).  Used for full-size parity samples without a 4x host copy. */
+static inline double bf16_to_f64(uint16_t b) {
+    uint32_t u = (uint32_t)b << 16;
+    float f;
+    memcpy(&f, &u, 4);
+    return (double)f;
+}
+
+int or_knn_cos_bf16_rows(const uint16_t *X, int64_t n, int32_t d, int32_t topk,
+                         double eps, double sigma, double p,
+                         const int64_t *rows, int64_t nrows, int nthreads,
+                         int32_t *out_idx, double *out_dist, double *out_w) {
+    if (!X || !rows || !out_idx || !out_dist || n < 1 || d < 1 || topk < 1 || nrows < 0)
+        return OR_EINVAL;
+    for (int64_t r = 0; r < nrows; ++r)
+        if (rows[r] < 0 || rows[r] >= n) return OR_EINVAL;
+    double *norms = (double *)malloc(sizeof(double) * (size_t)n);
+    if (!norms) return OR_ENOMEM;
+    set_threads(nthreads);
+    int err = 0;
+#pragma omp parallel for schedule(static)
+    for (int64_t i = 0; i < n; ++i) {
+        const uint16_t *x = X + i * (int64_t)d;
+        double acc = -0.0;
+        for (int32_t t = 0; t < d; ++t) {
+            const double v = bf16_to_f64(x[t]);
+            acc = acc + v * v;
+        }
+        norms[i] = sqrt(acc);
+    }
+#pragma omp parallel
+    {
+        cand_f64 *buf = (cand_f64 *)malloc(sizeof(cand_f64) * (size_t)topk);
+        double *xi = (double *)malloc(sizeof(double) * (size_t)d);
+        if (!buf || !xi) {
+#pragma omp atomic write
+            err = OR_ENOMEM;
+        }
+#pragma omp for schedule(dynamic, 1)
+        for (int64_t r = 0; r < nrows; ++r) {
+            if (!buf || !xi) continue;
+            const int64_t i = rows[r];
+            for (int32_t t = 0; t < d; ++t) xi[t] = bf16_to_f64(X[i * (int64_t)d + t]);
+            int32_t cnt = 0;
+            for (int64_t j = 0; j < n; ++j) {
+                if (j == i) continue;
+                double denom = norms[i] * norms[j];
+                double cs;
+                if (denom > 1e-12) {
+                    const uint16_t *xj = X + j * (int64_t)d;
+                    double dot = -0.0;
+                    for (int32_t t = 0; t < d; ++t) dot = dot + xi[t] * bf16_to_f64(xj[t]);
+                    cs = dot / denom;
+                    cs = cs < -1.0 ? -1.0 : (cs > 1.0 ? 1.0 : cs);
+                } else {
+                    cs = 0.0;
+                }
+                double dist = 1.0 - (cs > 0.0 ? cs : 0.0);
+                if (!(dist <= eps)) continue;
+                double nd = dist / sigma;
+                double wgt = 1.0 / (1.0 + (p == 2.0 ? nd * nd : pow(nd, p)));
+                if (!(wgt > 1e-12)) continue;
+                if (cnt < topk) {
+                    buf[cnt].d = dist; buf[cnt].w = wgt; buf[cnt].j = (int32_t)j;
+                    heap64_up(buf, cnt); ++cnt;
+                } else if (lt_f64(dist, (int32_t)j, buf[0].d, buf[0].j)) {
+                    buf[0].d = dist; buf[0].w = wgt; buf[0].j = (int32_t)j;
+                    heap64_down(buf, cnt, 0);
+                }
+            }
+            qsort(buf, (size_t)cnt, sizeof(cand_f64), cmp_cand_f64);
+            int32_t *oi = out_idx + r * (int64_t)topk;
+            double *od = out_dist + r * (int64_t)topk;
+            double *ow = out_w ? out_w + r * (int64_t)topk : NULL;
+            for (int32_t q = 0; q < topk; ++q) {
+                if (q < cnt) { oi[q] = buf[q].j; od[q] = buf[q].d; if (ow) ow[q] = buf[q].w; }
+                else { oi[q] = -1; od[q] = INFINITY; if (ow) ow[q] = 0.0; }
+            }
+        }
+        free(buf);
+        free(xi);
+    }
+    free(norms);
+    return err;
+}
+
 /* ------------------------------------------------------------------------ */
 /* K2 — A.2 UNION / unnormalised                                             */
 /* ------------------------------------------------------------------------ */

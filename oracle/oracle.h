@@ -67,6 +67,13 @@ int or_knn_cos_f64(const float *X, int64_t n, int32_t d, int32_t topk,
                    int64_t q_begin, int64_t q_end, int nthreads,
                    int32_t *out_idx, double *out_dist, double *out_w);
 
+/* A.1c on bf16 rows (bf16 bits, row-major [n][d]) for explicit query rows
+ * (config 5 parity samples); outputs [nrows][topk]. */
+int or_knn_cos_bf16_rows(const uint16_t *X, int64_t n, int32_t d, int32_t topk,
+                         double eps, double sigma, double p,
+                         const int64_t *rows, int64_t nrows, int nthreads,
+                         int32_t *out_idx, double *out_dist, double *out_w);
+
 /* ---- K2: Laplacian assembly --------------------------------------------- */
 
 /* A.2 UNION / unnormalised (legacy).

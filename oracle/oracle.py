@@ -49,6 +49,7 @@ def _declare(L):
     L.or_knn_l2sq_f32.argtypes = [P, I64, I32, I32, I64, I64, C.c_int, C.c_int, P, P]
     L.or_knn_l2sq_rows_f32.argtypes = [P, I64, I32, I32, P, I64, C.c_int, P, P]
     L.or_knn_cos_f64.argtypes = [P, I64, I32, I32, D, D, D, I64, I64, C.c_int, P, P, P]
+    L.or_knn_cos_bf16_rows.argtypes = [P, I64, I32, I32, D, D, D, P, I64, C.c_int, P, P, P]
     L.or_laplacian_union.argtypes = [I64, I32, P, P, I64, P, P, P, P]
     L.or_laplacian_max.argtypes = [I64, I64, P, P, P, F, C.c_int, I64, P, P, P, P, P, P]
     L.or_select_tau.argtypes = [P, I64, C.c_int, D]
@@ -102,6 +103,20 @@ def knn_cos(X, topk, eps=1.0, sigma=1.0, p=2.0, q_begin=0, q_end=None, nthreads=
     w = np.empty((m, topk), np.float64)
     _check(lib().or_knn_cos_f64(_p(X), n, d, topk, eps, sigma, p, q_begin, q_end, nthreads,
                                 _p(idx), _p(dist), _p(w)), "knn_cos")
+    return idx, dist, w
+
+
+def knn_cos_bf16_rows(Xbits, topk, rows, eps=1.0, sigma=1.0, p=2.0, nthreads=0):
+    """A.1c on bf16 rows given as uint16 bits [n, d], for explicit query rows."""
+    Xbits = np.ascontiguousarray(Xbits, dtype=np.uint16)
+    n, d = Xbits.shape
+    rows = np.ascontiguousarray(rows, dtype=np.int64)
+    m = rows.shape[0]
+    idx = np.empty((m, topk), np.int32)
+    dist = np.empty((m, topk), np.float64)
+    w = np.empty((m, topk), np.float64)
+    _check(lib().or_knn_cos_bf16_rows(_p(Xbits), n, d, topk, eps, sigma, p, _p(rows), m,
+                                      nthreads, _p(idx), _p(dist), _p(w)), "knn_cos_bf16_rows")
     return idx, dist, w
 
 

@@ -16,6 +16,8 @@ import pytest
 
 from oracle import oracle as O
 
+import datagen
+
 HERE = os.path.dirname(os.path.abspath(__file__))
 KA = json.load(open(os.path.join(HERE, "golden", "reference_known_answers.json")))
 GS = np.load(os.path.join(HERE, "golden", "golden_small.npz"))
@@ -237,3 +239,18 @@ def test_knn_rows_variant_matches_full():
     i_r, d_r = O.knn_l2sq_rows(X, 7, rows)
     np.testing.assert_array_equal(i_r, i_all[rows])
     np.testing.assert_array_equal(d_r, d_all[rows])
+
+
+def test_knn_cos_bf16_rows_matches_widened_f32():
+    """The bf16-row oracle (config 5 parity samples) is the f32 oracle on the
+    exactly widened values, row for row, bit for bit."""
+    X = datagen.uniform(600, 40, seed=3)
+    X[5] = 0.0
+    X[9] = X[10]
+    bits = datagen.to_bf16_bits(X)
+    Xf = datagen.bf16_bits_to_f32(bits)
+    full = O.knn_cos(Xf, 7, eps=0.9, sigma=0.5)
+    rows = np.array([0, 5, 9, 17, 599])
+    part = O.knn_cos_bf16_rows(bits, 7, rows, eps=0.9, sigma=0.5)
+    for a, b in zip(full, part):
+        np.testing.assert_array_equal(a[rows].view(np.uint8), b.view(np.uint8))
