@@ -68,9 +68,17 @@ typedef struct mn_knn_opts {
     int32_t exclude_self; /* 1 = the reference behaviour (mst.rs:336 j != i)       */
     int32_t margin;       /* candidate margin m (list length L = k + m); 0 => 16   */
     int32_t timing;       /* 1 = record per-kernel HIP-event times in mn_knn_stats */
-    int32_t reserved0;
+    int32_t algo;         /* enum mn_knn_algo: candidate generator (results are
+                             identical; only speed differs)                       */
     void *stream;         /* hipStream_t or NULL                                   */
 } mn_knn_opts;
+
+enum mn_knn_algo {
+    MN_KNN_AUTO = 0,   /* bf16-split when k + margin <= 64, else f32                */
+    MN_KNN_F32 = 1,    /* v_mfma_f32_16x16x4_f32 Gram (exact f32 products)          */
+    MN_KNN_BF16X3 = 2  /* f32 rows split into bf16 hi + lo; hi.hi + hi.lo + lo.hi on
+                          v_mfma_f32_32x32x16_bf16 (16x the rate per instruction)   */
+};
 
 typedef struct mn_knn_stats {
     int64_t n_queries;

@@ -31,8 +31,10 @@
 //                       recomputed by an exact brute-force scan.
 #include <algorithm>
 #include <climits>
+#include <cstdlib>
 
 #include "common.hpp"
+#include "gram_bf16.hpp"
 
 namespace mn {
 namespace knn {
@@ -420,6 +422,157 @@ __global__ __launch_bounds__(256) void k_rerank(
 }
 
 // ---------------------------------------------------------------------------
+// 2b. bf16-split candidate path (default): split + buffer-based exact re-rank.
+//     The Gram runs on bf16 MFMA (gram_bf16.hpp, GM_L2) at 16x the f32 MFMA
+//     rate per instruction, three instructions per 16 features.
+// ---------------------------------------------------------------------------
+
+// f32 -> bf16, round to nearest even (finite inputs; values beyond the bf16
+// range round to +-inf, which the Gram epilogue flags as unusable).
+__device__ __forceinline__ uint32_t bf16_rne(float x) {
+    const uint32_t u = __float_as_uint(x);
+    return (u + 0x7FFFu + ((u >> 16) & 1u)) >> 16;
+}
+
+// X [n][d] f32 -> XS [n][2 dp] bf16, per 32-feature group [hi 32 | lo 32]:
+// hi = bf16(x), lo = bf16(x - hi) (x - hi is exact in f32), so
+// |x - hi - lo| <= 2^-16 |x|.  Subnormal parts are flushed here (the bf16
+// MFMA may flush them anyway), which adds at most 2^-126 per term: covered by
+// the absolute slack of the certification bound.  Features d..dp-1 are 0.
+__global__ __launch_bounds__(256) void k_split_bf16(const float *__restrict__ X, int64_t n, int d,
+                                                    int dp, uint16_t *__restrict__ XS) {
+    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int per = dp >> 3;
+    if (e >= n * per) return;
+    const int64_t row = e / per;
+    const int f0 = (int)(e - row * per) * 8;
+    uint32_t hw[4], lw[4];
+#pragma unroll
+    for (int u = 0; u < 8; u += 2) {
+        uint32_t hp[2], lp[2];
+#pragma unroll
+        for (int v = 0; v < 2; ++v) {
+            const int f = f0 + u + v;
+            const float x = f < d ? X[row * (int64_t)d + f] : 0.f;
+            uint32_t hb = 0, lb = 0;
+            if (__builtin_fabsf(x) >= 0x1p-126f) {
+                hb = bf16_rne(x);
+                const float r = x - __uint_as_float(hb << 16);
+                lb = __builtin_fabsf(r) >= 0x1p-126f ? bf16_rne(r) : 0u;
+            }
+            hp[v] = hb;
+            lp[v] = lb;
+        }
+        hw[u >> 1] = hp[0] | (hp[1] << 16);
+        lw[u >> 1] = lp[0] | (lp[1] << 16);
+    }
+    uint16_t *o = XS + row * (int64_t)(2 * dp) + 64 * (f0 >> 5) + (f0 & 31);
+    *reinterpret_cast<uint4 *>(o) = make_uint4(hw[0], hw[1], hw[2], hw[3]);
+    *reinterpret_cast<uint4 *>(o + 32) = make_uint4(lw[0], lw[1], lw[2], lw[3]);
+}
+
+// One wave per query: gather the buffered candidates of every slice (key <=
+// the slice's final tau), order them by key, evaluate the reference fold for
+// the best kq and then for every other candidate whose lower bound key - delta
+// does not exceed the worst of those (the rest cannot enter the top k), sort by
+// (dist, idx) and certify: every pair never buffered (or dropped) had key >=
+// T = min_s tau_s, so T - delta > D_k proves the top k exact.
+//   delta = cert_c (|q|^2 + max|c|^2) + 2^-100 bounds |d~ - d| (split
+//   residuals and the dropped lo.lo term <= 3 2^-16 sum|q_t c_t|, f32
+//   accumulation of 3 dp exact products, the two norms, the final fma; sum
+//   |q_t c_t| <= (|q|^2 + |c|^2)/2; 2^-100 covers flushed subnormal parts).
+template <int NR, bool VEC4>
+__global__ __launch_bounds__(256) void k_rerank_buf(
+    const float *__restrict__ Q, int64_t nq, const float *__restrict__ C, int d, int64_t c_off,
+    const float *__restrict__ qnrm, const unsigned *__restrict__ cmax_bits, int S, int cap,
+    const uint2 *__restrict__ buf, const int *__restrict__ bcnt, const float *__restrict__ btau,
+    int k, int64_t nvalid_max, float cert_c, int32_t *__restrict__ out_idx,
+    float *__restrict__ out_dist, int *__restrict__ fb_count, int *__restrict__ fb_list) {
+    __shared__ int cand[4][64 * NR];
+    __shared__ float candk[4][64 * NR];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int64_t q = (int64_t)blockIdx.x * 4 + wid;
+    if (q >= nq) return;
+    int M = 0;
+    float T = __builtin_inff();
+    bool forced = false;
+    for (int s = 0; s < S; ++s) {
+        const int cnt = bcnt[q * S + s];
+        const float ts = btau[q * S + s];
+        forced |= (ts == -__builtin_inff());
+        T = fminf(T, ts);
+        const uint2 *bp = buf + (q * S + s) * (int64_t)cap;
+        for (int e0 = 0; e0 < cnt; e0 += 64) {
+            const int e = e0 + lane;
+            const uint2 v = e < cnt ? bp[e] : make_uint2(0x7f800000u, 0u);
+            const bool pass = e < cnt && __uint_as_float(v.x) <= ts;
+            const uint64_t pm = __ballot(pass);
+            const int pos = M + (int)__popcll(pm & ((1ull << lane) - 1ull));
+            if (pass && pos < 64 * NR) {
+                cand[wid][pos] = (int)v.y;
+                candk[wid][pos] = __uint_as_float(v.x);
+            }
+            M += (int)__popcll(pm);
+        }
+    }
+    forced |= M > 64 * NR;
+    M = min(M, 64 * NR);
+    __builtin_amdgcn_wave_barrier();
+    float kk[NR];
+    int ix[NR];
+#pragma unroll
+    for (int r = 0; r < NR; ++r) {
+        const int e = lane + 64 * r;
+        kk[r] = e < M ? candk[wid][e] : __builtin_inff();
+        ix[r] = e < M ? cand[wid][e] : INT_MAX;
+    }
+    wave_bitonic_sort<NR>(kk, ix);
+    const float delta = cert_c * (qnrm[q] + __uint_as_float(*cmax_bits)) + 0x1p-100f;
+    const float *qrow = Q + q * (int64_t)d;
+    const int kq = min(k, M);
+    float dd[NR];
+#pragma unroll
+    for (int r = 0; r < NR; ++r) {
+        const int e = lane + 64 * r;
+        dd[r] = __builtin_inff();
+        if (e < kq) dd[r] = exact_l2sq<VEC4>(qrow, C + ((int64_t)ix[r] - c_off) * d, d);
+    }
+    float Dp = -__builtin_inff();
+#pragma unroll
+    for (int r = 0; r < NR; ++r) Dp = fmaxf(Dp, (lane + 64 * r) < kq ? dd[r] : -__builtin_inff());
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) Dp = fmaxf(Dp, __shfl_xor(Dp, o));
+#pragma unroll
+    for (int r = 0; r < NR; ++r) {
+        const int e = lane + 64 * r;
+        // NaN-safe: evaluated unless the lower bound provably exceeds Dp
+        if (e >= kq && e < M && !(kk[r] - delta > Dp))
+            dd[r] = exact_l2sq<VEC4>(qrow, C + ((int64_t)ix[r] - c_off) * d, d);
+    }
+    // skipped candidates keep +inf: strictly beyond D_k, so neither the order
+    // of the top k nor the certification below can see them
+#pragma unroll
+    for (int r = 0; r < NR; ++r)
+        if (lane + 64 * r >= M) ix[r] = INT_MAX;
+    wave_bitonic_sort<NR>(dd, ix);
+    const int keff = (int)min((int64_t)min(k, M), nvalid_max);
+    bool cert = !forced;
+    if (cert && T < __builtin_inff() && keff > 0) {
+        const float Dk = wave_elem<NR>(dd, keff - 1);
+        cert = (T - delta) > Dk;  // NaN/inf-safe: false => exact rescan
+    }
+    if (!cert) {
+        if (lane == 0) fb_list[atomicAdd(fb_count, 1)] = (int)q;
+        return;
+    }
+    if (lane < k) {
+        const bool ok = lane < keff;
+        out_idx[q * k + lane] = ok ? ix[0] : -1;
+        out_dist[q * k + lane] = ok ? dd[0] : __builtin_inff();
+    }
+}
+
+// ---------------------------------------------------------------------------
 // 4. exact fallback scan for uncertified rows
 // ---------------------------------------------------------------------------
 struct alignas(16) FallbackSmem {
@@ -559,6 +712,14 @@ static int knn_f32_impl(const float *Q, int64_t nq, const float *C, int64_t nc, 
     const int margin = opts->margin > 0 ? opts->margin : 16;
     const int L = k + margin;
     MN_REQUIRE(L <= LMAX, MN_ENOTSUP, "mn_knn: k+margin=%d exceeds %d", L, LMAX);
+    // candidate generator: bf16-split MFMA (default) or f32 MFMA; both are
+    // followed by the same exact re-rank / certification / fallback contract
+    const int algo = opts->algo;
+    MN_REQUIRE(algo >= MN_KNN_AUTO && algo <= MN_KNN_BF16X3, MN_EINVAL, "mn_knn: bad algo %d",
+               algo);
+    MN_REQUIRE(!(algo == MN_KNN_BF16X3 && L > kb16::LMAX), MN_ENOTSUP,
+               "mn_knn: bf16-split candidates need k+margin <= %d", kb16::LMAX);
+    const bool split = algo == MN_KNN_BF16X3 || (algo == MN_KNN_AUTO && L <= kb16::LMAX);
     MN_REQUIRE(q_off >= 0 && c_off >= 0 && q_off + nq <= INT_MAX && c_off + nc <= INT_MAX,
                MN_EINVAL, "mn_knn: global ids must fit int32");
     const int excl = opts->exclude_self ? 1 : 0;
@@ -629,38 +790,100 @@ static int knn_f32_impl(const float *Q, int64_t nq, const float *C, int64_t nc, 
                "mn_knn: input contains NaN/inf (the reference panics in partial_cmp().unwrap())");
     tm.mark();
 
-    if (nc > 0) {
-        dim3 grid((unsigned)blocks_q, (unsigned)S);
-        if (vec4)
-            hipLaunchKernelGGL(k_gram_topk<true>, grid, dim3(NT), 0, s, Q, nq, C, nc, d, q_off,
-                               c_off, excl, qn, cn, L, (int)S, chunk, list_d, list_i, lsz, ltau);
-        else
-            hipLaunchKernelGGL(k_gram_topk<false>, grid, dim3(NT), 0, s, Q, nq, C, nc, d, q_off,
-                               c_off, excl, qn, cn, L, (int)S, chunk, list_d, list_i, lsz, ltau);
-        MN_HIP_TRY(hipGetLastError());
+    if (split) {
+        // ---- bf16-split candidates (gram_bf16.hpp GM_L2) + buffer re-rank ----
+        const int dp = (d + 127) / 128 * 128;  // 2 dp bf16 per row: a multiple of DALIGN
+        uint16_t *XSq = (uint16_t *)scratch(kSlotGeneric0, (size_t)nq * dp * 4 + 64);
+        uint16_t *XSc = same ? XSq : (uint16_t *)scratch(kSlotGeneric1, (size_t)nc * dp * 4 + 64);
+        MN_REQUIRE(XSq && XSc, MN_ENOMEM, "mn_knn: split copy allocation failed");
+        auto split_rows = [&](const float *X, int64_t n, uint16_t *XS) {
+            const int64_t th = n * (dp / 8);
+            if (th > 0)
+                hipLaunchKernelGGL(k_split_bf16, dim3((unsigned)((th + 255) / 256)), dim3(256), 0, s,
+                                   X, n, d, dp, XS);
+        };
+        split_rows(Q, nq, XSq);
+        if (!same) split_rows(C, nc, XSc);
+        MN_KCHECK(s, "k_split_bf16");
+        tm.mark();
+        const char *ms = getenv("MN_L2_MIN_SLICES");
+        const kb16::GramPlan pl = kb16::plan_gram(nq, nc, L, (ms && *ms) ? atoi(ms) : 2);
+        t_stats.slices = (int)pl.S;
+        const size_t nbuf = (size_t)nq * pl.S * pl.cap;
+        uint2 *cbuf = (uint2 *)scratch(kSlotLists, nbuf * sizeof(uint2) + 64);
+        char *bmeta = (char *)scratch(kSlotListMeta, (size_t)nq * pl.S * 8 + 64);
+        MN_REQUIRE(cbuf && bmeta, MN_ENOMEM, "mn_knn: candidate buffer allocation failed (%zu MB)",
+                   (nbuf * sizeof(uint2)) >> 20);
+        int *bcnt = (int *)bmeta;
+        float *btau = (float *)(bmeta + (size_t)nq * pl.S * 4);
+        if (nc > 0) {
+            const int64_t bq = (nq + kb16::BM - 1) / kb16::BM;
+            hipLaunchKernelGGL((kb16::k_gram_bf16<kb16::GM_L2, 0>), dim3((unsigned)(bq * pl.S)),
+                               dim3(kb16::NT), 0, s, XSq, nq, XSc, nc, 2 * dp, q_off, c_off, excl, qn,
+                               cn, L, (int)pl.S, pl.chunk, pl.cap, cbuf, bcnt, btau);
+        } else {
+            MN_HIP_TRY(hipMemsetAsync(bcnt, 0, sizeof(int) * (size_t)nq * pl.S, s));
+        }
+        MN_KCHECK(s, "k_gram_bf16<L2>");
+        tm.mark();
+        // |d~ - d| bound per unit of (|q|^2 + max|c|^2); generous constants
+        const float cert_c =
+            2.0f * (3.0f * 0x1p-16f + (4.0f * (float)dp + 32.0f) * 0x1p-24f);
+        const int64_t nvalid = same ? nc - 1 : nc;
+        const dim3 rgrid((unsigned)((nq + 3) / 4));
+#define MN_RRB(NRV, V)                                                                          \
+    hipLaunchKernelGGL((k_rerank_buf<NRV, V>), rgrid, dim3(256), 0, s, Q, nq, C, d, c_off, qn,   \
+                       maxbits, (int)pl.S, pl.cap, cbuf, bcnt, btau, k,                         \
+                       std::max<int64_t>(nvalid, 0), cert_c, out_idx, out_dist, fb_count, fb_list)
+        if (vec4) {
+            if (pl.NR == 1) MN_RRB(1, true);
+            else if (pl.NR == 2) MN_RRB(2, true);
+            else if (pl.NR == 4) MN_RRB(4, true);
+            else MN_RRB(8, true);
+        } else {
+            if (pl.NR == 1) MN_RRB(1, false);
+            else if (pl.NR == 2) MN_RRB(2, false);
+            else if (pl.NR == 4) MN_RRB(4, false);
+            else MN_RRB(8, false);
+        }
+#undef MN_RRB
+        MN_KCHECK(s, "k_rerank_buf");
+        tm.mark();
     } else {
-        MN_HIP_TRY(hipMemsetAsync(lsz, 0, sizeof(int) * (size_t)nq * S, s));
-    }
-    tm.mark();
+        tm.mark();  // no split phase
+        if (nc > 0) {
+            dim3 grid((unsigned)blocks_q, (unsigned)S);
+            if (vec4)
+                hipLaunchKernelGGL(k_gram_topk<true>, grid, dim3(NT), 0, s, Q, nq, C, nc, d, q_off,
+                                   c_off, excl, qn, cn, L, (int)S, chunk, list_d, list_i, lsz, ltau);
+            else
+                hipLaunchKernelGGL(k_gram_topk<false>, grid, dim3(NT), 0, s, Q, nq, C, nc, d, q_off,
+                                   c_off, excl, qn, cn, L, (int)S, chunk, list_d, list_i, lsz, ltau);
+            MN_HIP_TRY(hipGetLastError());
+        } else {
+            MN_HIP_TRY(hipMemsetAsync(lsz, 0, sizeof(int) * (size_t)nq * S, s));
+        }
+        tm.mark();
 
-    const float cert_c = 2.0f * (4.0f * (float)d + 16.0f) * 0x1p-24f;
-    const dim3 rgrid((unsigned)((nq + 3) / 4));
-#define MN_RERANK(NRV, V)                                                                       \
-    hipLaunchKernelGGL((k_rerank<NRV, V>), rgrid, dim3(256), 0, s, Q, nq, C, nc, d, c_off, qn,   \
-                       maxbits, (int)S, L, list_d, list_i, lsz, ltau, k, cert_c, out_idx,        \
-                       out_dist, fb_count, fb_list)
-    if (vec4) {
-        if (NR == 1) MN_RERANK(1, true);
-        else if (NR == 2) MN_RERANK(2, true);
-        else MN_RERANK(4, true);
-    } else {
-        if (NR == 1) MN_RERANK(1, false);
-        else if (NR == 2) MN_RERANK(2, false);
-        else MN_RERANK(4, false);
+        const float cert_c = 2.0f * (4.0f * (float)d + 16.0f) * 0x1p-24f;
+        const dim3 rgrid((unsigned)((nq + 3) / 4));
+    #define MN_RERANK(NRV, V)                                                                       \
+        hipLaunchKernelGGL((k_rerank<NRV, V>), rgrid, dim3(256), 0, s, Q, nq, C, nc, d, c_off, qn,   \
+                           maxbits, (int)S, L, list_d, list_i, lsz, ltau, k, cert_c, out_idx,        \
+                           out_dist, fb_count, fb_list)
+        if (vec4) {
+            if (NR == 1) MN_RERANK(1, true);
+            else if (NR == 2) MN_RERANK(2, true);
+            else MN_RERANK(4, true);
+        } else {
+            if (NR == 1) MN_RERANK(1, false);
+            else if (NR == 2) MN_RERANK(2, false);
+            else MN_RERANK(4, false);
+        }
+    #undef MN_RERANK
+        MN_HIP_TRY(hipGetLastError());
+        tm.mark();
     }
-#undef MN_RERANK
-    MN_HIP_TRY(hipGetLastError());
-    tm.mark();
 
     const unsigned fgrid = (unsigned)std::min<int64_t>(nq, 1024);
     if (vec4)
@@ -675,11 +898,11 @@ static int knn_f32_impl(const float *Q, int64_t nq, const float *C, int64_t nc, 
     MN_HIP_TRY(hipStreamSynchronize(s));
     t_stats.n_uncertified = hflags[2];
     if (tm.on) {
-        t_stats.ms_norms = tm.ms(0, 1);
-        t_stats.ms_gram = tm.ms(1, 2);
-        t_stats.ms_rerank = tm.ms(2, 3);
-        t_stats.ms_fallback = tm.ms(3, 4);
-        t_stats.ms_total = tm.ms(0, 4);
+        t_stats.ms_norms = tm.ms(0, 2);  // norms (+ bf16 split)
+        t_stats.ms_gram = tm.ms(2, 3);
+        t_stats.ms_rerank = tm.ms(3, 4);
+        t_stats.ms_fallback = tm.ms(4, 5);
+        t_stats.ms_total = tm.ms(0, 5);
     }
     return MN_OK;
 }

@@ -27,8 +27,12 @@ class MnError(RuntimeError):
 
 class KnnOpts(C.Structure):
     _fields_ = [("k", C.c_int32), ("metric", C.c_int32), ("exclude_self", C.c_int32),
-                ("margin", C.c_int32), ("timing", C.c_int32), ("reserved0", C.c_int32),
+                ("margin", C.c_int32), ("timing", C.c_int32), ("algo", C.c_int32),
                 ("stream", C.c_void_p)]
+
+
+# enum mn_knn_algo: candidate generator of mn_knn_f32 (outputs are identical)
+MN_KNN_AUTO, MN_KNN_F32, MN_KNN_BF16X3 = 0, 1, 2
 
 
 class KnnStats(C.Structure):

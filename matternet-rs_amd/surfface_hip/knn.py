@@ -31,9 +31,12 @@ class KnnResult:
     stats: dict
 
 
-def _opts(k, margin, timing, stream, exclude_self=True, metric=_lib.MN_L2SQ):
+ALGOS = {"auto": _lib.MN_KNN_AUTO, "f32": _lib.MN_KNN_F32, "bf16x3": _lib.MN_KNN_BF16X3}
+
+
+def _opts(k, margin, timing, stream, exclude_self=True, metric=_lib.MN_L2SQ, algo="auto"):
     return _lib.KnnOpts(k=k, metric=metric, exclude_self=1 if exclude_self else 0,
-                        margin=margin, timing=1 if timing else 0, reserved0=0,
+                        margin=margin, timing=1 if timing else 0, algo=ALGOS[algo],
                         stream=stream_handle(stream))
 
 
@@ -44,20 +47,22 @@ def last_stats() -> dict:
 
 
 def knn_l2sq(X: torch.Tensor, k: int, margin: int = 16, timing: bool = False,
-             stream=None, out_idx=None, out_dist=None) -> KnnResult:
-    """Exact kNN of every row of X [n, d] (f32, on device) by squared L2."""
+             stream=None, out_idx=None, out_dist=None, algo: str = "auto") -> KnnResult:
+    """Exact kNN of every row of X [n, d] (f32, on device) by squared L2.
+    algo picks the candidate generator ("auto" = "bf16x3" when k + margin <= 64,
+    "f32"); the result is the same bit for bit."""
     X = require_cuda(X, torch.float32, "X", 2)
     n, d = X.shape
     idx = out_idx if out_idx is not None else torch.empty((n, k), dtype=torch.int32, device=X.device)
     dist = out_dist if out_dist is not None else torch.empty((n, k), dtype=torch.float32, device=X.device)
-    o = _opts(k, margin, timing, stream)
+    o = _opts(k, margin, timing, stream, algo=algo)
     _lib.check(_lib.lib().mn_knn_f32(ptr(X), n, d, C.byref(o), ptr(idx), ptr(dist)))
     return KnnResult(idx, dist, last_stats())
 
 
 def knn_l2sq_qc(Qm: torch.Tensor, Cm: torch.Tensor, k: int, q_offset: int = 0, c_offset: int = 0,
                 exclude_self: bool = True, margin: int = 16, timing: bool = False,
-                stream=None) -> KnnResult:
+                stream=None, algo: str = "auto") -> KnnResult:
     """Exact per-shard top-k of queries Q against corpus C (global-id offsets)."""
     Qm = require_cuda(Qm, torch.float32, "Q", 2)
     Cm = require_cuda(Cm, torch.float32, "C", 2)
@@ -67,7 +72,7 @@ def knn_l2sq_qc(Qm: torch.Tensor, Cm: torch.Tensor, k: int, q_offset: int = 0, c
         raise ValueError("Q and C must have the same feature dimension")
     idx = torch.empty((nq, k), dtype=torch.int32, device=Qm.device)
     dist = torch.empty((nq, k), dtype=torch.float32, device=Qm.device)
-    o = _opts(k, margin, timing, stream, exclude_self)
+    o = _opts(k, margin, timing, stream, exclude_self, algo=algo)
     _lib.check(_lib.lib().mn_knn_f32_qc(ptr(Qm), nq, ptr(Cm), nc, d, q_offset, c_offset,
                                         C.byref(o), ptr(idx), ptr(dist)))
     return KnnResult(idx, dist, last_stats())

@@ -2,6 +2,8 @@
 
 Contract: neighbour indices bit-exact and distances bit-exact
 (the re-rank IS the reference's sequential f32 fold), ties by ascending index.
+Every case runs with both candidate generators: the bf16-split MFMA Gram (the
+default, algo "bf16x3") and the f32 MFMA Gram (algo "f32").
 """
 import numpy as np
 import pytest
@@ -14,6 +16,11 @@ pytestmark = pytest.mark.gpu
 
 GS = np.load(__import__("os").path.join(__import__("os").path.dirname(__file__), "golden",
                                         "golden_small.npz"))
+
+
+@pytest.fixture(params=["bf16x3", "f32"])
+def algo(request):
+    return request.param
 
 
 def hip_knn(X, k, **kw):
@@ -29,68 +36,68 @@ def assert_exact(idx, dist, ridx, rdist):
 
 
 @pytest.mark.parametrize("name,k", [("l2_uniform", 5), ("l2_clustered", 7), ("l2_grid", 6)])
-def test_golden_fixtures(name, k):
-    idx, dist, _ = hip_knn(GS[name + "_X"], k)
+def test_golden_fixtures(name, k, algo):
+    idx, dist, _ = hip_knn(GS[name + "_X"], k, algo=algo)
     assert_exact(idx, dist, GS[name + "_idx"], GS[name + "_dist"])
 
 
-def test_config1_shape_10k_x_64_k10():
+def test_config1_shape_10k_x_64_k10(algo):
     X = datagen.uniform(10_000, 64, seed=42)
-    idx, dist, st = hip_knn(X, 10)
+    idx, dist, st = hip_knn(X, 10, algo=algo)
     ridx, rdist = O.knn_l2sq(X, 10)
     assert_exact(idx, dist, ridx, rdist)
 
 
 @pytest.mark.parametrize("n,d,k", [(3000, 96, 32), (2500, 17, 10), (1000, 5, 3), (700, 768, 32)])
-def test_clustered_duplicates_and_zero_rows(n, d, k):
+def test_clustered_duplicates_and_zero_rows(n, d, k, algo):
     X = datagen.clustered(n, d, seed=7, blobs=8, dup_frac=0.03, zero_frac=0.01)
-    idx, dist, st = hip_knn(X, k)
+    idx, dist, st = hip_knn(X, k, algo=algo)
     ridx, rdist = O.knn_l2sq(X, k)
     assert_exact(idx, dist, ridx, rdist)
 
 
-def test_small_n_and_k_clamp():
+def test_small_n_and_k_clamp(algo):
     X = datagen.uniform(5, 8, seed=3)
-    idx, dist, _ = hip_knn(X, 10)
+    idx, dist, _ = hip_knn(X, 10, algo=algo)
     ridx, rdist = O.knn_l2sq(X, 10)
     assert_exact(idx, dist, ridx, rdist)
     assert (idx[:, 4:] == -1).all()
 
 
-def test_all_identical_rows_tie_by_index():
+def test_all_identical_rows_tie_by_index(algo):
     X = np.ones((300, 12), np.float32)
-    idx, dist, st = hip_knn(X, 8)
+    idx, dist, st = hip_knn(X, 8, algo=algo)
     ridx, rdist = O.knn_l2sq(X, 8)
     assert_exact(idx, dist, ridx, rdist)
     assert st["n_uncertified"] == 300  # every row ties beyond L -> exact fallback path
 
 
-def test_zero_rows_tie_beyond_candidate_list():
+def test_zero_rows_tie_beyond_candidate_list(algo):
     X = datagen.uniform(2000, 32, seed=4)
     X[::7] = 0.0  # 286 identical zero rows: ties far beyond k + margin
-    idx, dist, st = hip_knn(X, 16)
+    idx, dist, st = hip_knn(X, 16, algo=algo)
     ridx, rdist = O.knn_l2sq(X, 16)
     assert_exact(idx, dist, ridx, rdist)
     assert st["n_uncertified"] >= 286
 
 
-def test_huge_values_overflow_to_inf():
+def test_huge_values_overflow_to_inf(algo):
     X = datagen.uniform(400, 8, seed=9)
     X[17] *= 3e19  # its distances overflow to +inf in the f32 fold
-    idx, dist, st = hip_knn(X, 6)
+    idx, dist, st = hip_knn(X, 6, algo=algo)
     ridx, rdist = O.knn_l2sq(X, 6)
     assert_exact(idx, dist, ridx, rdist)
 
 
-def test_nonfinite_input_is_an_error():
+def test_nonfinite_input_is_an_error(algo):
     import surfface_hip as S
     X = datagen.uniform(100, 8, seed=1)
     X[5, 3] = np.nan
     with pytest.raises(S.MnError):
-        hip_knn(X, 4)
+        hip_knn(X, 4, algo=algo)
 
 
-def test_query_corpus_offsets_and_shard_merge():
+def test_query_corpus_offsets_and_shard_merge(algo):
     import surfface_hip as S
     X = datagen.uniform(6000, 64, seed=5)
     Xd = torch.from_numpy(X).cuda()
@@ -98,7 +105,7 @@ def test_query_corpus_offsets_and_shard_merge():
     parts_i, parts_d = [], []
     bounds = [0, 1500, 3100, 6000]
     for a, b in zip(bounds[:-1], bounds[1:]):
-        r = S.knn_l2sq_qc(Xd, Xd[a:b], k, q_offset=0, c_offset=a)
+        r = S.knn_l2sq_qc(Xd, Xd[a:b], k, q_offset=0, c_offset=a, algo=algo)
         parts_i.append(r.idx)
         parts_d.append(r.dist)
     idx, dist = S.merge_parts(torch.stack(parts_i), torch.stack(parts_d))
@@ -106,11 +113,11 @@ def test_query_corpus_offsets_and_shard_merge():
     assert_exact(idx.cpu().numpy(), dist.cpu().numpy(), ridx, rdist)
 
 
-def test_large_n_sampled_rows_d768():
+def test_large_n_sampled_rows_d768(algo):
     """200k x 768, k=32: full GPU run, oracle on a sample of 192 query rows."""
     n, d, k = 200_000, 768, 32
     X = datagen.uniform(n, d, seed=42)
-    idx, dist, st = hip_knn(X, k)
+    idx, dist, st = hip_knn(X, k, algo=algo)
     rows = np.random.default_rng(0).choice(n, 192, replace=False)
     ridx, rdist = O.knn_l2sq_rows(X, k, rows)
     assert_exact(idx[rows], dist[rows], ridx, rdist)
@@ -118,3 +125,46 @@ def test_large_n_sampled_rows_d768():
     assert (np.diff(dist, axis=1) >= 0).all()
     assert (idx != np.arange(n)[:, None]).all()
     assert st["n_uncertified"] == 0
+
+
+def test_tiny_values_flush_to_exact_path(algo):
+    """Values near the f32 subnormal range: the split flushes subnormal parts,
+    the certification's absolute slack then sends rows to the exact scan."""
+    X = datagen.uniform(600, 24, seed=11) * np.float32(1e-30)
+    X[::5] *= np.float32(1e-8)
+    idx, dist, st = hip_knn(X, 8, algo=algo)
+    ridx, rdist = O.knn_l2sq(X, 8)
+    assert_exact(idx, dist, ridx, rdist)
+
+
+def test_mixed_row_scales(algo):
+    """Rows whose norms differ by many orders of magnitude (the bound scales
+    with |q|^2 + max|c|^2)."""
+    X = datagen.clustered(1500, 40, seed=13, blobs=6, dup_frac=0.02, zero_frac=0.0)
+    scale = np.float32(10.0) ** np.random.default_rng(2).integers(-6, 7, size=(1500, 1))
+    X = (X * scale.astype(np.float32)).astype(np.float32)
+    idx, dist, st = hip_knn(X, 12, algo=algo)
+    ridx, rdist = O.knn_l2sq(X, 12)
+    assert_exact(idx, dist, ridx, rdist)
+
+
+def test_bf16_range_overflow_in_split():
+    """|x| beyond the bf16 range: the split's hi term rounds to inf, the row is
+    flagged and rescanned exactly (f32 fold: those distances are +inf too)."""
+    X = datagen.uniform(300, 16, seed=21)
+    X[7, 3] = np.float32(3.3999e38)
+    idx, dist, st = hip_knn(X, 5, algo="bf16x3")
+    ridx, rdist = O.knn_l2sq(X, 5)
+    assert_exact(idx, dist, ridx, rdist)
+
+
+def test_k64_uses_f32_generator_in_auto():
+    """k + margin > 64 exceeds the bf16 kernel's list width: auto picks f32,
+    an explicit bf16x3 request is an error."""
+    import surfface_hip as S
+    X = datagen.uniform(500, 16, seed=1)
+    idx, dist, _ = hip_knn(X, 60, algo="auto")
+    ridx, rdist = O.knn_l2sq(X, 60)
+    assert_exact(idx, dist, ridx, rdist)
+    with pytest.raises(S.MnError):
+        hip_knn(X, 60, algo="bf16x3")
