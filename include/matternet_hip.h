@@ -86,6 +86,7 @@ typedef struct mn_knn_stats {
     int32_t slices;         /* corpus split factor used                         */
     int32_t list_len;       /* L = k + margin                                   */
     float ms_norms, ms_gram, ms_rerank, ms_fallback, ms_total; /* timing == 1   */
+    int32_t algo;           /* candidate generator used (enum mn_knn_algo)      */
 } mn_knn_stats;
 
 /* Self kNN over the rows of X [n][d] f32 (device, row-major): replaces

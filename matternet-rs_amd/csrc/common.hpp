@@ -36,6 +36,13 @@ enum ScratchSlot {
     kNumSlots
 };
 
+// The calling thread's non-blocking side stream on the current device
+// (library-owned, created on first use) for work that runs concurrently with
+// the caller's stream; nullptr on failure.
+hipStream_t side_stream();
+// Make `waiter` wait for all work issued so far on `on`.
+hipError_t stream_wait(hipStream_t waiter, hipStream_t on);
+
 // Per-call HIP-event timer (active only when requested).
 struct Timer {
     bool on = false;

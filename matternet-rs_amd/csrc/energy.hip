@@ -17,13 +17,18 @@
 // in rayon par_bridge order.  Here: G = Q/S^2 with Q = sum e^2 (one pass,
 // algebraically identical to sum (e/S)^2, within ~nnz*u relative).
 //
-// GPU design: one wave per item row; the row is staged in LDS (f32) for the
-// x_j gathers and held in registers for the order statistics.  The Laplacian
-// is flattened once per call into an entry list (i, j, v, multiplicity): for
-// an exactly symmetric L only the upper triangle is kept with multiplicity 2
-// (half the gathers and f64 flops); the list lives in LDS, shared by the
-// block's waves.  tau = median via an exact wave-level radix select on the
-// sortable f32 keys (no sort).  f64 accumulation throughout.
+// GPU design.  The Laplacian is flattened once per call into two entry lists
+// (entry_class below): A = the dispersion's edges (w = -L_ij > 0), which feed
+// the Rayleigh numerator, S and Q; B = everything that feeds only the
+// numerator.  For an exactly symmetric L only the upper triangle is listed
+// (multiplicity 2, applied once per row).  Both lists live in LDS, shared by
+// the block's waves.  A wave takes TWO item rows at a time: they are staged
+// in LDS (f32) for the x_i / x_j gathers, and each entry read from LDS serves
+// both rows (per entry and row: 7 f64 VALU ops, 2 LDS gathers, half an entry
+// read).  tau = median via an exact wave-level radix select on the sortable
+// f32 keys (no sort).  f64 accumulation throughout.  This orientation is
+// compute-bound (F^2-ish entries per F-long row), not HBM-bound: the roofline
+// that applies is the f64 VALU rate.
 #include <algorithm>
 #include <climits>
 #include <cmath>
@@ -34,11 +39,12 @@
 namespace mn {
 namespace energy {
 
-constexpr int WAVES = 4;
-constexpr int FMAX = 4096;            // row length limit (registers: FMAX/64 per lane)
-constexpr int EDGE_LDS_CAP = 4096;    // entries kept in LDS (12 B each => 48 KB)
+constexpr int FMAX = 4096;             // row length limit (registers: FMAX/64 per lane)
+constexpr int ROWS = 2;                // item rows per wave per pass
+constexpr size_t LDS_BUDGET = 160 * 1024;
+constexpr size_t EDGE_LDS_MAX = 96 * 1024;  // entry lists kept in LDS up to this size
 
-// ---- build the entry list from CSR --------------------------------------
+// ---- build the entry lists from CSR --------------------------------------
 __global__ void k_check_sym(const int64_t *__restrict__ ip, const int32_t *__restrict__ ix,
                             const double *__restrict__ v, int f, int *__restrict__ asym) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -59,31 +65,52 @@ __global__ void k_check_sym(const int64_t *__restrict__ ip, const int32_t *__res
     }
 }
 
-__global__ void k_count_entries(const int64_t *__restrict__ ip, const int32_t *__restrict__ ix,
-                                int f, int sym, int32_t *__restrict__ cnt) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= f) return;
-    int c = 0;
-    for (int64_t p = ip[i]; p < ip[i + 1]; ++p)
-        if (!sym || ix[p] >= i) ++c;
-    cnt[i] = c;
+// Every stored CSR entry (i, j, v) the reduction needs goes to one list,
+// packed (i | j << 16) + an f64 value:
+//   A (0)  off-diagonal, w = -v > 0, in the dispersion's pair set: value w;
+//          feeds num (as -w), S and Q with the uniform multiplicities
+//          (mA_num, mA_g) applied once to the row's sums;
+//   B (1)  everything else (the diagonal, v >= 0, pairs outside the
+//          dispersion's set): value m * v, feeds num only.
+// Symmetric L: only j >= i is listed, off-diagonal multiplicity 2.  Pair set:
+// taumode = ordered pairs i != j (taumode.rs:366-408), energymaps = j > i
+// (energymaps.rs:990-1030).
+__device__ __forceinline__ int entry_class(int i, int j, double v, int sym, int g_mode) {
+    if (sym && j < i) return -1;  // covered by (j, i)
+    if (i == j) return 1;
+    const bool counts = (g_mode == MN_G_TAUMODE) || sym || j > i;
+    return (counts && -v > 0.0) ? 0 : 1;
 }
 
-// entry list: packed (i | j << 16) + value; multiplicity is implied:
-// 2 for off-diagonal entries of the symmetric (upper-triangle) list, else 1
+__global__ void k_count_entries(const int64_t *__restrict__ ip, const int32_t *__restrict__ ix,
+                                const double *__restrict__ v, int f, int sym, int g_mode,
+                                int32_t *__restrict__ cnt) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= f) return;
+    int ca = 0, cb = 0;
+    for (int64_t p = ip[i]; p < ip[i + 1]; ++p) {
+        const int c = entry_class(i, ix[p], v[p], sym, g_mode);
+        ca += c == 0;
+        cb += c == 1;
+    }
+    cnt[i] = ca;
+    cnt[f + i] = cb;
+}
+
 __global__ void k_fill_entries(const int64_t *__restrict__ ip, const int32_t *__restrict__ ix,
-                               const double *__restrict__ v, int f, int sym,
+                               const double *__restrict__ v, int f, int sym, int g_mode,
                                const int64_t *__restrict__ off, uint32_t *__restrict__ eij,
                                double *__restrict__ ev) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= f) return;
-    int64_t q = off[i];
+    int64_t qa = off[i], qb = off[f + i];
     for (int64_t p = ip[i]; p < ip[i + 1]; ++p) {
         const int j = ix[p];
-        if (sym && j < i) continue;
+        const int c = entry_class(i, j, v[p], sym, g_mode);
+        if (c < 0) continue;
+        const int64_t q = c == 0 ? qa++ : qb++;
         eij[q] = (uint32_t)i | ((uint32_t)j << 16);
-        ev[q] = v[p];
-        ++q;
+        ev[q] = c == 0 ? -v[p] : ((sym && i != j) ? 2.0 * v[p] : v[p]);
     }
 }
 
@@ -149,133 +176,153 @@ __device__ __forceinline__ double wave_sum(double x) {
     return x;
 }
 
+// tau of one row (taumode.rs:29-70) from its keys
 template <int NR>
-struct alignas(16) EnergySmem {
-    double ev[EDGE_LDS_CAP];
-    uint32_t eij[EDGE_LDS_CAP];
-    float xs[WAVES][NR * 64];
-    int hist[WAVES][256];
-};
-
-template <int NR>
-__global__ __launch_bounds__(64 * WAVES) void k_energy_rows(
-    const float *__restrict__ X, int64_t n, int f, int64_t ne, int sym,
-    const uint32_t *__restrict__ geij, const double *__restrict__ gev, int g_mode, int tau_mode,
-    double tau_param, int pct_rank, double *__restrict__ Eo, double *__restrict__ Go,
-    double *__restrict__ Lo) {
-    __shared__ EnergySmem<NR> sm;
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const bool in_lds = ne <= EDGE_LDS_CAP;
-    if (in_lds) {
-        for (int64_t p = threadIdx.x; p < ne; p += blockDim.x) {
-            sm.eij[p] = geij[p];
-            sm.ev[p] = gev[p];
-        }
-    }
-    __syncthreads();
-    const uint32_t *EIJ = in_lds ? sm.eij : geij;
-    const double *EV = in_lds ? sm.ev : gev;
-    float *xs = sm.xs[w];
-    const int64_t nw = (int64_t)gridDim.x * WAVES;
-    for (int64_t row = (int64_t)blockIdx.x * WAVES + w; row < n; row += nw) {
-        const float *xr = X + row * (int64_t)f;
-        float xv[NR];
-        uint32_t keys[NR];
-        double den = 0.0, msum = 0.0;
-        bool nonzero = false;
+__device__ double row_tau(const uint32_t (&keys)[NR], int f, double msum, int tau_mode,
+                          double tau_param, int pct_rank, int *hist) {
+    if (tau_mode == MN_TAU_FIXED)
+        return (isfinite(tau_param) && tau_param > 0.0) ? tau_param : 1e-10;
+    if (tau_mode == MN_TAU_MEAN) return fmax(wave_sum(msum) / (double)f, 1e-10);
+    const int lane = threadIdx.x & 63;
+    const int rank = (tau_mode == MN_TAU_PERCENTILE) ? pct_rank : ((f % 2 == 1) ? f / 2 : f / 2 - 1);
+    const uint32_t ka = wave_select<NR>(keys, NR, rank, hist);
+    double med = (double)key2f(ka);
+    if (tau_mode == MN_TAU_MEDIAN && f % 2 == 0) {
+        // element rank+1: equal to ka if >= rank+2 keys are <= ka, else min{key > ka}
+        int le = 0;
+        uint32_t nxt = 0xFFFFFFFFu;
 #pragma unroll
         for (int r = 0; r < NR; ++r) {
             const int t = lane + 64 * r;
-            const float x = t < f ? xr[t] : 0.f;
-            xv[r] = x;
             if (t < f) {
-                xs[t] = x;
-                const double xd = (double)x;
-                den += xd * xd;
-                msum += xd;
-                nonzero |= !(fabs(xd) <= 1e-10);
+                le += keys[r] <= ka ? 1 : 0;
+                if (keys[r] > ka && keys[r] < nxt) nxt = keys[r];
             }
-            keys[r] = t < f ? f2key(x) : 0xFFFFFFFFu;
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            le += __shfl_xor(le, o);
+            const uint32_t on = __shfl_xor(nxt, o);
+            nxt = on < nxt ? on : nxt;
+        }
+        const double b = (le >= rank + 2) ? med : (double)key2f(nxt);
+        med = 0.5 * (med + b);
+    }
+    return fmax(med, 1e-10);
+}
+
+// LDS: [ev f64 x ne | eij u32 x ne] (when in_lds) | xs f32 [waves][ROWS][fpad]
+//      | hist int [waves][256]
+template <int NR>
+__global__ __launch_bounds__(NR <= 16 ? 1024 : 256) void k_energy_rows(
+    const float *__restrict__ X, int64_t n, int f, int64_t na, int64_t ne, int in_lds,
+    const uint32_t *__restrict__ geij, const double *__restrict__ gev, double mA_num,
+    double mA_g, int g_mode, int tau_mode, double tau_param, int pct_rank,
+    double *__restrict__ Eo, double *__restrict__ Go, double *__restrict__ Lo) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char dsm[];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    const int fpad = (f + 3) & ~3;
+    const size_t eb = in_lds ? (((size_t)ne * 12 + 15) & ~(size_t)15) : 0;
+    double *sev = (double *)dsm;
+    uint32_t *seij = (uint32_t *)(dsm + (size_t)ne * 8);
+    float *xs = (float *)(dsm + eb) + (size_t)w * ROWS * fpad;
+    int *hist = (int *)(dsm + eb + (size_t)nw * ROWS * fpad * 4) + w * 256;
+    if (in_lds) {
+        for (int64_t p = threadIdx.x; p < ne; p += blockDim.x) {
+            seij[p] = geij[p];
+            sev[p] = gev[p];
+        }
+    }
+    __syncthreads();
+    const uint32_t *EIJ = in_lds ? seij : geij;
+    const double *EV = in_lds ? sev : gev;
+    const int64_t npass = (n + ROWS - 1) / ROWS;
+    for (int64_t ps = (int64_t)blockIdx.x * nw + w; ps < npass; ps += (int64_t)gridDim.x * nw) {
+        const int64_t r0 = ps * ROWS;
+        uint32_t keys[ROWS][NR];
+        double den[ROWS], msum[ROWS];
+        bool nonzero[ROWS];
+#pragma unroll
+        for (int t = 0; t < ROWS; ++t) {
+            // a missing last row repeats the previous one (computed, not written)
+            const float *xr = X + min(r0 + t, n - 1) * (int64_t)f;
+            double dn = 0.0, ms = 0.0;
+            bool nz = false;
+#pragma unroll
+            for (int r = 0; r < NR; ++r) {
+                const int c = lane + 64 * r;
+                const float x = c < f ? xr[c] : 0.f;
+                if (c < f) {
+                    xs[t * fpad + c] = x;
+                    const double xd = (double)x;
+                    dn += xd * xd;
+                    ms += xd;
+                    nz |= !(fabs(xd) <= 1e-10);
+                }
+                keys[t][r] = c < f ? f2key(x) : 0xFFFFFFFFu;
+            }
+            den[t] = wave_sum(dn);
+            msum[t] = ms;
+            nonzero[t] = __any(nz) != 0;
         }
         __builtin_amdgcn_wave_barrier();
-        den = wave_sum(den);
-        const bool any_nonzero = __any(nonzero);
-        double e_raw = 0.0, g_raw = 0.0, lam = 0.0;
-        if (g_mode == MN_G_TAUMODE && !any_nonzero) {
-            // zero vector (taumode.rs:268-274): lambda = 0
-        } else {
-            double num = 0.0, S = 0.0, Q = 0.0;
-            for (int64_t p = lane; p < ne; p += 64) {
-                const uint32_t ij = EIJ[p];
-                const int i = (int)(ij & 0xFFFFu), j = (int)(ij >> 16);
-                const double v = EV[p];
-                const double m = (sym && i != j) ? 2.0 : 1.0;
-                const double xi = (double)xs[i], xj = (double)xs[j];
-                num += m * ((xi * v) * xj);
-                const bool counts = (g_mode == MN_G_TAUMODE) ? (i != j) : (j > i);
-                const double wgt = -v;
-                if (counts && wgt > 0.0) {
-                    const double dd = xi - xj;
-                    const double e = wgt * dd * dd;
-                    const double sm_ = (g_mode == MN_G_TAUMODE) ? m : 1.0;
-                    S += sm_ * e;
-                    Q += sm_ * (e * e);
-                }
-            }
-            num = wave_sum(num);
-            S = wave_sum(S);
-            Q = wave_sum(Q);
-            e_raw = den > 1e-12 ? fmax(num / den, 0.0) : 0.0;
-            if (S > 1e-12) {
-                const double g = Q / (S * S);
-                g_raw = g < 0.0 ? 0.0 : (g > 1.0 ? 1.0 : g);
-            }
-            if (g_mode == MN_G_TAUMODE) {
-                double tau = 1e-10;
-                if (tau_mode == MN_TAU_FIXED) {
-                    tau = (isfinite(tau_param) && tau_param > 0.0) ? tau_param : 1e-10;
-                } else if (tau_mode == MN_TAU_MEAN) {
-                    const double mean = wave_sum(msum) / (double)f;
-                    tau = fmax(mean, 1e-10);
-                } else {
-                    int rank;
-                    if (tau_mode == MN_TAU_PERCENTILE) rank = pct_rank;
-                    else rank = (f % 2 == 1) ? f / 2 : f / 2 - 1;
-                    const uint32_t ka = wave_select<NR>(keys, NR, rank, sm.hist[w]);
-                    double med = (double)key2f(ka);
-                    if (tau_mode == MN_TAU_MEDIAN && f % 2 == 0) {
-                        // element rank+1: equal to a if >= rank+2 keys are <= ka, else min{key > ka}
-                        int le = 0;
-                        uint32_t nxt = 0xFFFFFFFFu;
+        double nA[ROWS], nB[ROWS], S[ROWS], Q[ROWS];
 #pragma unroll
-                        for (int r = 0; r < NR; ++r) {
-                            const int t = lane + 64 * r;
-                            if (t < f) {
-                                le += keys[r] <= ka ? 1 : 0;
-                                if (keys[r] > ka && keys[r] < nxt) nxt = keys[r];
-                            }
-                        }
+        for (int t = 0; t < ROWS; ++t) nA[t] = nB[t] = S[t] = Q[t] = 0.0;
+        // list A: num += v x_i x_j (v = -w), S += e, Q += e^2, e = w (x_i - x_j)^2
+#pragma unroll 2
+        for (int64_t p = lane; p < na; p += 64) {
+            const uint32_t ij = EIJ[p];
+            const double wv = EV[p];
+            const int i = (int)(ij & 0xFFFFu), j = (int)(ij >> 16);
 #pragma unroll
-                        for (int o = 32; o > 0; o >>= 1) {
-                            le += __shfl_xor(le, o);
-                            const uint32_t on = __shfl_xor(nxt, o);
-                            nxt = on < nxt ? on : nxt;
-                        }
-                        const double b = (le >= rank + 2) ? med : (double)key2f(nxt);
-                        med = 0.5 * (med + b);
-                    }
-                    tau = fmax(med, 1e-10);
-                }
-                const double eb = e_raw / (e_raw + tau);
-                lam = tau * eb + (1.0 - tau) * g_raw;
-            } else {
-                lam = e_raw;
+            for (int t = 0; t < ROWS; ++t) {
+                const double xi = (double)xs[t * fpad + i], xj = (double)xs[t * fpad + j];
+                nA[t] = __builtin_fma(-wv, xi * xj, nA[t]);
+                const double dd = xi - xj;
+                const double e = (dd * dd) * wv;
+                S[t] += e;
+                Q[t] = __builtin_fma(e, e, Q[t]);
             }
         }
-        if (lane == 0) {
-            if (Eo) Eo[row] = e_raw;
-            if (Go) Go[row] = g_raw;
-            if (Lo) Lo[row] = lam;
+        // list B: num only
+#pragma unroll 2
+        for (int64_t p = na + lane; p < ne; p += 64) {
+            const uint32_t ij = EIJ[p];
+            const double v = EV[p];
+            const int i = (int)(ij & 0xFFFFu), j = (int)(ij >> 16);
+#pragma unroll
+            for (int t = 0; t < ROWS; ++t) {
+                const double xi = (double)xs[t * fpad + i], xj = (double)xs[t * fpad + j];
+                nB[t] = __builtin_fma(v, xi * xj, nB[t]);
+            }
+        }
+#pragma unroll
+        for (int t = 0; t < ROWS; ++t) {
+            const double num = wave_sum(mA_num * nA[t] + nB[t]);
+            const double Ss = mA_g * wave_sum(S[t]);
+            const double Qs = mA_g * wave_sum(Q[t]);
+            double e_raw = 0.0, g_raw = 0.0, lam = 0.0;
+            if (!(g_mode == MN_G_TAUMODE && !nonzero[t])) {  // zero vector: lambda 0
+                e_raw = den[t] > 1e-12 ? fmax(num / den[t], 0.0) : 0.0;
+                if (Ss > 1e-12) {
+                    const double g = Qs / (Ss * Ss);
+                    g_raw = g < 0.0 ? 0.0 : (g > 1.0 ? 1.0 : g);
+                }
+                if (g_mode == MN_G_TAUMODE) {
+                    const double tau =
+                        row_tau<NR>(keys[t], f, msum[t], tau_mode, tau_param, pct_rank, hist);
+                    const double ebv = e_raw / (e_raw + tau);
+                    lam = tau * ebv + (1.0 - tau) * g_raw;
+                } else {
+                    lam = e_raw;
+                }
+            }
+            if (lane == 0 && r0 + t < n) {
+                if (Eo) Eo[r0 + t] = e_raw;
+                if (Go) Go[r0 + t] = g_raw;
+                if (Lo) Lo[r0 + t] = lam;
+            }
         }
         __builtin_amdgcn_wave_barrier();
     }
@@ -350,13 +397,14 @@ static int energy_impl(const mn_csr *L, const float *X, int64_t n, int32_t f,
     hipStream_t s = (hipStream_t)opts->stream;
     if (n == 0) return MN_OK;
     const int64_t nnz = L->nnz;
-    char *g = (char *)scratch(kSlotGeneric0, (size_t)nnz * 12 + (size_t)(f + 1) * 12 + 256);
+    char *g = (char *)scratch(kSlotGeneric0, (size_t)nnz * 12 + (size_t)f * 8 +
+                                                 (size_t)(2 * f + 1) * 8 + 256);
     MN_REQUIRE(g, MN_ENOMEM, "mn_energy_rows: scratch allocation failed");
     uint32_t *eij = (uint32_t *)g;
     int32_t *cnt = (int32_t *)(eij + nnz);
-    double *ev = (double *)(((uintptr_t)(cnt + f) + 15) & ~(uintptr_t)15);
+    double *ev = (double *)(((uintptr_t)(cnt + 2 * f) + 15) & ~(uintptr_t)15);
     int64_t *off = (int64_t *)(ev + nnz);
-    int *flag = (int *)(off + (f + 1));
+    int *flag = (int *)(off + 2 * f);
 
     Timer tm;
     tm.start(opts->timing != 0, s);
@@ -369,21 +417,22 @@ static int energy_impl(const mn_csr *L, const float *X, int64_t n, int32_t f,
     MN_HIP_TRY(hipStreamSynchronize(s));
     MN_REQUIRE(!(hflag & 2), MN_EINVAL, "mn_energy_rows: Laplacian column index out of range");
     const int sym = (hflag & 1) ? 0 : 1;
-    hipLaunchKernelGGL(k_count_entries, dim3(fb), dim3(256), 0, s, L->indptr, L->indices, f, sym,
-                       cnt);
-    // tiny scan on the host side of the stream (f <= 4096)
-    std::vector<int32_t> hc(f);
-    std::vector<int64_t> ho(f + 1);
-    MN_HIP_TRY(hipMemcpyAsync(hc.data(), cnt, 4 * (size_t)f, hipMemcpyDeviceToHost, s));
+    hipLaunchKernelGGL(k_count_entries, dim3(fb), dim3(256), 0, s, L->indptr, L->indices,
+                       (const double *)L->values, f, sym, opts->g_mode, cnt);
+    // tiny scan on the host side of the stream (f <= 4096): list A, then B
+    std::vector<int32_t> hc(2 * (size_t)f);
+    std::vector<int64_t> ho(2 * (size_t)f);
+    MN_HIP_TRY(hipMemcpyAsync(hc.data(), cnt, 8 * (size_t)f, hipMemcpyDeviceToHost, s));
     MN_HIP_TRY(hipStreamSynchronize(s));
-    ho[0] = 0;
-    for (int i = 0; i < f; ++i) ho[i + 1] = ho[i] + hc[i];
-    const int64_t ne = ho[f];
-    MN_HIP_TRY(hipMemcpyAsync(off, ho.data(), 8 * (size_t)(f + 1), hipMemcpyHostToDevice, s));
+    int64_t acc = 0;
+    for (int i = 0; i < 2 * f; ++i) {
+        ho[i] = acc;
+        acc += hc[i];
+    }
+    const int64_t na = ho[f], ne = acc;
+    MN_HIP_TRY(hipMemcpyAsync(off, ho.data(), 16 * (size_t)f, hipMemcpyHostToDevice, s));
     hipLaunchKernelGGL(k_fill_entries, dim3(fb), dim3(256), 0, s, L->indptr, L->indices,
-                       (const double *)L->values, f, sym, off, eij, ev);
-    // finite check of X (the reference's order statistics filter non-finite
-    // values; a NaN/inf item is rejected here instead)
+                       (const double *)L->values, f, sym, opts->g_mode, off, eij, ev);
     int pct_rank = 0;
     if (opts->tau_mode == MN_TAU_PERCENTILE) {
         double pp = opts->tau_param;
@@ -391,13 +440,31 @@ static int energy_impl(const mn_csr *L, const float *X, int64_t n, int32_t f,
         const double fi = std::round((double)(f - 1) * pp);  // f64::round
         pct_rank = (fi != fi || fi < 0) ? 0 : (int)std::min<double>(fi, f - 1);
     }
+    // multiplicities of list A: num (2 for the upper-triangle list), dispersion
+    // (taumode counts each undirected edge twice, energymaps once)
+    const double mA_num = sym ? 2.0 : 1.0;
+    const double mA_g = (sym && opts->g_mode == MN_G_TAUMODE) ? 2.0 : 1.0;
     tm.mark();
-    const int64_t blocks = std::min<int64_t>((n + WAVES - 1) / WAVES, 2048);
     const int nr = (f + 63) / 64;
+    const int fpad = (f + 3) & ~3;
+    const size_t ebytes = (((size_t)ne * 12) + 15) & ~(size_t)15;
+    const int in_lds = ebytes <= EDGE_LDS_MAX ? 1 : 0;
+    const size_t per_wave = (size_t)ROWS * fpad * 4 + 256 * 4;
+    const size_t avail = LDS_BUDGET - (in_lds ? ebytes : 0);
+    const int wmax = nr <= 16 ? 16 : 4;
+    const int nw = (int)std::min<size_t>((size_t)wmax, avail / per_wave);
+    MN_REQUIRE(nw >= 1, MN_ENOTSUP, "mn_energy_rows: f=%d does not fit the LDS plan", f);
+    const size_t shmem = (in_lds ? ebytes : 0) + (size_t)nw * per_wave;
+    const int64_t npass = (n + ROWS - 1) / ROWS;
+    const int64_t blocks = std::min<int64_t>((npass + nw - 1) / nw, 1024);
 #define MN_ER(NRV)                                                                              \
-    hipLaunchKernelGGL(k_energy_rows<NRV>, dim3((unsigned)blocks), dim3(64 * WAVES), 0, s, X,   \
-                       n, f, ne, sym, eij, ev, opts->g_mode, opts->tau_mode, opts->tau_param,   \
-                       pct_rank, E, G, lam)
+    do {                                                                                        \
+        MN_HIP_TRY(hipFuncSetAttribute((const void *)k_energy_rows<NRV>,                        \
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)shmem)); \
+        hipLaunchKernelGGL(k_energy_rows<NRV>, dim3((unsigned)blocks), dim3(64 * nw), shmem, s, \
+                           X, n, f, na, ne, in_lds, eij, ev, mA_num, mA_g, opts->g_mode,        \
+                           opts->tau_mode, opts->tau_param, pct_rank, E, G, lam);               \
+    } while (0)
     if (nr <= 4) MN_ER(4);
     else if (nr <= 8) MN_ER(8);
     else if (nr <= 12) MN_ER(12);
@@ -405,7 +472,7 @@ static int energy_impl(const mn_csr *L, const float *X, int64_t n, int32_t f,
     else if (nr <= 32) MN_ER(32);
     else MN_ER(64);  // f <= 4096
 #undef MN_ER
-    MN_HIP_TRY(hipGetLastError());
+    MN_KCHECK(s, "k_energy_rows");
     tm.mark();
     MN_HIP_TRY(hipStreamSynchronize(s));
     t_energy_stats.entries = ne;

@@ -720,6 +720,7 @@ static int knn_f32_impl(const float *Q, int64_t nq, const float *C, int64_t nc, 
     MN_REQUIRE(!(algo == MN_KNN_BF16X3 && L > kb16::LMAX), MN_ENOTSUP,
                "mn_knn: bf16-split candidates need k+margin <= %d", kb16::LMAX);
     const bool split = algo == MN_KNN_BF16X3 || (algo == MN_KNN_AUTO && L <= kb16::LMAX);
+    t_stats.algo = split ? MN_KNN_BF16X3 : MN_KNN_F32;
     MN_REQUIRE(q_off >= 0 && c_off >= 0 && q_off + nq <= INT_MAX && c_off + nc <= INT_MAX,
                MN_EINVAL, "mn_knn: global ids must fit int32");
     const int excl = opts->exclude_self ? 1 : 0;

@@ -11,18 +11,24 @@
 //     key with the max weight, w <= thr dropped, degrees in f32, optional
 //     L_sym = I - D^-1/2 W D^-1/2) and :209-219 (dense -> CSR keeps |v|>1e-9).
 //
-// GPU design: an O(E) counting-sort CSR build, no global sort —
-//   1. k_lap_weights     per row: weight kernel + validity, in-degree atomics
-//   2. scan              row capacity = out + in  -> segment offsets
-//   3. k_lap_scatter     forward entries in slot order, reverse entries by
-//                        atomic fill (order fixed by step 4)
-//   4. row sort+dedupe   (col asc, w desc) then unique col (keeps the max):
-//                        one wave per row (<=256 entries, bitonic in
-//                        registers), one 1024-thread block per row (<=8192,
-//                        bitonic in LDS), dense column map for hub rows
-//   5. degrees/values    one thread per row, sequential ascending-column sums
-//                        (exactly the reference order for the legacy path)
-//   6. scan + write      CSR with the diagonal at its sorted position.
+// GPU design: an O(E) counting-sort CSR build, no global sort, every pass
+// coalesced (one thread per kNN slot, one wave per graph row):
+//   1. k_lap_slots      per slot: weight kernel + validity, in-degree atomics
+//   2. scan             row segment = k forward slots + in-degree reverse slots
+//   3. k_lap_scatter    forward slot r -> segment position r (an invalid slot
+//                       holds a sentinel column), reverse entries by atomic
+//                       fill (their order is fixed by step 4); the weight is
+//                       recomputed rather than staged through HBM
+//   4. row sort+dedupe  (col asc, w desc), a unique col keeps the max weight;
+//                       one wave per row (<= 256 entries, bitonic in
+//                       registers, sized 64/128/256 per row) fused with the
+//                       row's degree: a sequential ascending-column fold (the
+//                       reference's order on the legacy path) over the kept
+//                       entries, lane values read in order by v_readlane; one
+//                       1024-thread block per row <= 8192 (bitonic in LDS); a
+//                       dense column map for hub rows
+//   5. (MAX) kept count per row (needs every degree), one wave per row
+//   6. scan + CSR write, one wave per row, diagonal at its sorted position.
 #include <algorithm>
 #include <climits>
 #include <vector>
@@ -42,6 +48,7 @@ struct Params {
 
 constexpr int WAVE_CAP = 256;
 constexpr int BLOCK_CAP = 8192;
+constexpr int EMPTY = INT_MAX;  // sentinel column of an invalid forward slot
 
 __device__ __forceinline__ double pw(double x, double p) {
     if (p == 2.0) return x * x;
@@ -49,64 +56,67 @@ __device__ __forceinline__ double pw(double x, double p) {
     return pow(x, p);
 }
 
-__global__ __launch_bounds__(256) void k_lap_weights(const int32_t *__restrict__ nbr,
-                                                     const void *__restrict__ val, int val_f64,
-                                                     int64_t n, int k, Params P,
-                                                     int32_t *__restrict__ vidx,
-                                                     double *__restrict__ vw,
-                                                     int32_t *__restrict__ outcnt,
-                                                     int32_t *__restrict__ indeg,
-                                                     int *__restrict__ bad) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    int cnt = 0;
-    for (int r = 0; r < k; ++r) {
-        const int64_t s = i * k + r;
-        const int32_t j = nbr[s];
-        const double x = val_f64 ? ((const double *)val)[s] : (double)((const float *)val)[s];
-        bool valid = j >= 0 && (int64_t)j != i;
-        if (j >= (int64_t)n) { atomicOr(bad, 1); valid = false; }
-        double w = x;
-        if (valid && P.kernel == MN_W_RATIONAL) {
-            valid = x <= P.eps;  // laplacian.rs:252 (NaN fails)
-            w = 1.0 / (1.0 + pw(x / P.sigma, P.p));
-            valid = valid && (w > 1e-12);
-        }
-        if (valid && P.sym == MN_SYM_MAX) valid = w > P.thr;  // laplacian.rs:324
-        vidx[s] = valid ? j : -1;
-        vw[s] = w;
-        if (valid) {
-            ++cnt;
-            atomicAdd(&indeg[j], 1);
-        }
+// Slot s = i*k + r of the kNN rows: neighbour j and edge weight w; false if
+// the slot carries no edge (empty, self loop, filtered).  laplacian.rs:245-260
+// (rational kernel), surfface-core/src/laplacian.rs:324 (MAX threshold).
+__device__ __forceinline__ bool slot_edge(const int32_t *__restrict__ nbr,
+                                          const void *__restrict__ val, int val_f64, int64_t n,
+                                          int64_t i, int64_t s, const Params &P, int32_t &j,
+                                          double &w, bool &bad) {
+    j = nbr[s];
+    const double x = val_f64 ? ((const double *)val)[s] : (double)((const float *)val)[s];
+    bad = j >= n;
+    bool valid = j >= 0 && (int64_t)j != i && !bad;
+    w = x;
+    if (valid && P.kernel == MN_W_RATIONAL) {
+        valid = x <= P.eps;  // laplacian.rs:252 (NaN fails)
+        w = 1.0 / (1.0 + pw(x / P.sigma, P.p));
+        valid = valid && (w > 1e-12);
     }
-    outcnt[i] = cnt;
+    if (valid && P.sym == MN_SYM_MAX) valid = w > P.thr;
+    return valid;
 }
 
-__global__ void k_add_i32(const int32_t *__restrict__ a, const int32_t *__restrict__ b, int64_t n,
+__global__ __launch_bounds__(256) void k_lap_slots(const int32_t *__restrict__ nbr,
+                                                   const void *__restrict__ val, int val_f64,
+                                                   int64_t n, int k, Params P,
+                                                   int32_t *__restrict__ indeg,
+                                                   int *__restrict__ bad) {
+    const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= n * k) return;
+    int32_t j;
+    double w;
+    bool b;
+    if (slot_edge(nbr, val, val_f64, n, s / k, s, P, j, w, b)) atomicAdd(&indeg[j], 1);
+    if (b) atomicOr(bad, 1);
+}
+
+__global__ void k_seg_len(const int32_t *__restrict__ indeg, int64_t n, int k,
                           int32_t *__restrict__ out) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) out[i] = a[i] + b[i];
+    if (i < n) out[i] = k + indeg[i];
 }
 
-__global__ __launch_bounds__(256) void k_lap_scatter(const int32_t *__restrict__ vidx,
-                                                     const double *__restrict__ vw, int64_t n,
-                                                     int k, const int64_t *__restrict__ offs,
-                                                     const int32_t *__restrict__ outcnt,
+__global__ __launch_bounds__(256) void k_lap_scatter(const int32_t *__restrict__ nbr,
+                                                     const void *__restrict__ val, int val_f64,
+                                                     int64_t n, int k, Params P,
+                                                     const int64_t *__restrict__ offs,
                                                      int32_t *__restrict__ fill,
                                                      int32_t *__restrict__ col,
                                                      double *__restrict__ wt) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    int64_t pos = offs[i];
-    for (int r = 0; r < k; ++r) {
-        const int32_t j = vidx[i * k + r];
-        if (j < 0) continue;
-        const double w = vw[i * k + r];
-        col[pos] = j;
-        wt[pos] = w;
-        ++pos;
-        const int64_t q = offs[j] + outcnt[j] + atomicAdd(&fill[j], 1);
+    const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= n * k) return;
+    const int64_t i = s / k;
+    const int r = (int)(s - i * k);
+    int32_t j;
+    double w;
+    bool b;
+    const bool valid = slot_edge(nbr, val, val_f64, n, i, s, P, j, w, b);
+    const int64_t f = offs[i] + r;
+    col[f] = valid ? j : EMPTY;
+    wt[f] = w;
+    if (valid) {
+        const int64_t q = offs[j] + k + atomicAdd(&fill[j], 1);
         col[q] = (int32_t)i;
         wt[q] = w;
     }
@@ -117,29 +127,28 @@ __device__ __forceinline__ bool cw_less(int ca, double wa, int cb, double wb) {
     return ca < cb || (ca == cb && wa > wb);
 }
 
-// one wave per row with m <= WAVE_CAP entries
-__global__ __launch_bounds__(256) void k_row_sort_wave(const int64_t *__restrict__ offs,
-                                                       int64_t n, int32_t *__restrict__ col,
-                                                       double *__restrict__ wt,
-                                                       int32_t *__restrict__ uniq,
-                                                       int32_t *__restrict__ big_list,
-                                                       int *__restrict__ big_count) {
-    constexpr int NR = WAVE_CAP / 64;
+__device__ __forceinline__ double readlane_f64(double x, int l) {
+    const long long u = __double_as_longlong(x);
+    const int lo = __builtin_amdgcn_readlane((int)(u & 0xFFFFFFFFll), l);
+    const int hi = __builtin_amdgcn_readlane((int)(u >> 32), l);
+    return __longlong_as_double(((long long)hi << 32) | (long long)(unsigned)lo);
+}
+
+// Sort, dedupe and fold one row of m <= 64*NR entries held by one wave.
+template <int NR>
+__device__ __forceinline__ void row_sort_fold(int64_t i, int64_t o, int m, int sym,
+                                              int32_t *__restrict__ col, double *__restrict__ wt,
+                                              int32_t *__restrict__ uniq,
+                                              int32_t *__restrict__ kept,
+                                              double *__restrict__ deg64,
+                                              float *__restrict__ deg32) {
     const int lane = threadIdx.x & 63;
-    const int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-    if (i >= n) return;
-    const int64_t o = offs[i];
-    const int m = (int)(offs[i + 1] - o);
-    if (m > WAVE_CAP) {
-        if (lane == 0) big_list[atomicAdd(big_count, 1)] = (int32_t)i;
-        return;
-    }
     int c[NR];
     double w[NR];
 #pragma unroll
     for (int r = 0; r < NR; ++r) {
         const int e = lane + 64 * r;
-        c[r] = e < m ? col[o + e] : INT_MAX;
+        c[r] = e < m ? col[o + e] : EMPTY;
         w[r] = e < m ? wt[o + e] : 0.0;
     }
 #pragma unroll
@@ -176,24 +185,73 @@ __global__ __launch_bounds__(256) void k_row_sort_wave(const int64_t *__restrict
             }
         }
     }
-    // dedupe: keep e if e < m and (e == 0 or col[e] != col[e-1])
+    // dedupe: keep e if it holds a column (not the sentinel) that differs from
+    // its predecessor's; kept entries are compacted in place and folded in
+    // ascending column order (lane values read one by one: the chain of adds
+    // is the reference's sequential sum)
     int base = 0;
+    double s64 = -0.0;  // laplacian.rs:367 s.iter().map(w).sum() in ascending j
+    float s32 = 0.0f;   // surfface-core/src/laplacian.rs:331-340 (order: ascending column)
 #pragma unroll
     for (int r = 0; r < NR; ++r) {
         const int e = lane + 64 * r;
         int prev = __shfl_up(c[r], 1);
         const int last_prev = (r > 0) ? __shfl(c[r > 0 ? r - 1 : 0], 63) : INT_MIN;
         if (lane == 0) prev = (r == 0) ? INT_MIN : last_prev;
-        const bool keep = e < m && c[r] != prev;
-        const uint64_t mk = __ballot(keep);
+        const bool keep = e < m && c[r] != EMPTY && c[r] != prev;
+        uint64_t mk = __ballot(keep);
         if (keep) {
             const int pos = base + (int)__popcll(mk & ((1ull << lane) - 1ull));
             col[o + pos] = c[r];
             wt[o + pos] = w[r];
         }
         base += (int)__popcll(mk);
+        if (sym == MN_SYM_UNION) {
+            while (mk) {
+                const int l = __builtin_ctzll(mk);
+                mk &= mk - 1;
+                s64 = s64 + readlane_f64(w[r], l);
+            }
+        } else {
+            while (mk) {
+                const int l = __builtin_ctzll(mk);
+                mk &= mk - 1;
+                s32 = s32 + (float)readlane_f64(w[r], l);
+            }
+        }
     }
-    if (lane == 0) uniq[i] = base;
+    if (lane == 0) {
+        uniq[i] = base;
+        if (sym == MN_SYM_UNION) {
+            deg64[i] = s64;
+            kept[i] = base + 1;  // + the diagonal, stored for every row
+        } else {
+            deg32[i] = s32;
+        }
+    }
+}
+
+// one wave per row; rows with more than WAVE_CAP entries are listed for the
+// block kernel
+__global__ __launch_bounds__(256) void k_row_sort_wave(const int64_t *__restrict__ offs,
+                                                       int64_t n, int sym,
+                                                       int32_t *__restrict__ col,
+                                                       double *__restrict__ wt,
+                                                       int32_t *__restrict__ uniq,
+                                                       int32_t *__restrict__ kept,
+                                                       double *__restrict__ deg64,
+                                                       float *__restrict__ deg32,
+                                                       int32_t *__restrict__ big_list,
+                                                       int *__restrict__ big_count) {
+    const int lane = threadIdx.x & 63;
+    const int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    if (i >= n) return;
+    const int64_t o = offs[i];
+    const int m = (int)(offs[i + 1] - o);
+    if (m <= 64) row_sort_fold<1>(i, o, m, sym, col, wt, uniq, kept, deg64, deg32);
+    else if (m <= 128) row_sort_fold<2>(i, o, m, sym, col, wt, uniq, kept, deg64, deg32);
+    else if (m <= WAVE_CAP) row_sort_fold<4>(i, o, m, sym, col, wt, uniq, kept, deg64, deg32);
+    else if (lane == 0) big_list[atomicAdd(big_count, 1)] = (int32_t)i;
 }
 
 // one 1024-thread block per row with WAVE_CAP < m <= BLOCK_CAP (bitonic in LDS)
@@ -207,9 +265,12 @@ struct alignas(16) BigSmem {
 __global__ __launch_bounds__(1024) void k_row_sort_block(const int64_t *__restrict__ offs,
                                                          const int32_t *__restrict__ big_list,
                                                          const int *__restrict__ big_count,
-                                                         int32_t *__restrict__ col,
+                                                         int sym, int32_t *__restrict__ col,
                                                          double *__restrict__ wt,
                                                          int32_t *__restrict__ uniq,
+                                                         int32_t *__restrict__ kept,
+                                                         double *__restrict__ deg64,
+                                                         float *__restrict__ deg32,
                                                          int32_t *__restrict__ huge_list,
                                                          int *__restrict__ huge_count) {
     __shared__ BigSmem sm;
@@ -225,7 +286,7 @@ __global__ __launch_bounds__(1024) void k_row_sort_block(const int64_t *__restri
         int P = 1;
         while (P < m) P <<= 1;
         for (int e = threadIdx.x; e < P; e += blockDim.x) {
-            sm.c[e] = e < m ? col[o + e] : INT_MAX;
+            sm.c[e] = e < m ? col[o + e] : EMPTY;
             sm.w[e] = e < m ? wt[o + e] : 0.0;
         }
         __syncthreads();
@@ -250,7 +311,8 @@ __global__ __launch_bounds__(1024) void k_row_sort_block(const int64_t *__restri
         int base = 0;
         for (int c0 = 0; c0 < m; c0 += 1024) {
             const int e = c0 + threadIdx.x;
-            const bool keep = e < m && (e == 0 || sm.c[e] != sm.c[e - 1]);
+            const bool keep =
+                e < m && sm.c[e] != EMPTY && (e == 0 || sm.c[e] != sm.c[e - 1]);
             const uint64_t mk = __ballot(keep);
             const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
             if (lane == 0) sm.wsum[wv] = (int)__popcll(mk);
@@ -271,7 +333,19 @@ __global__ __launch_bounds__(1024) void k_row_sort_block(const int64_t *__restri
             col[o + q] = sm.c[sm.flag[q]];
             wt[o + q] = sm.w[sm.flag[q]];
         }
-        if (threadIdx.x == 0) uniq[i] = base;
+        if (threadIdx.x == 0) {
+            uniq[i] = base;
+            if (sym == MN_SYM_UNION) {
+                double s = -0.0;
+                for (int q = 0; q < base; ++q) s = s + sm.w[sm.flag[q]];
+                deg64[i] = s;
+                kept[i] = base + 1;
+            } else {
+                float s = 0.0f;
+                for (int q = 0; q < base; ++q) s = s + (float)sm.w[sm.flag[q]];
+                deg32[i] = s;
+            }
+        }
         __syncthreads();
     }
 }
@@ -286,6 +360,7 @@ __global__ void k_dense_scatter(const int32_t *__restrict__ col, const double *_
     const int e = blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= m) return;
     const int c = col[o + e];
+    if (c == EMPTY) return;
     const double w = wt[o + e];
     unsigned long long *p = (unsigned long long *)&dense[c];
     unsigned long long old = *p, assumed;
@@ -308,66 +383,68 @@ __global__ void k_dense_compact(const double *__restrict__ dense, const int32_t 
     col[o + pos[c]] = (int32_t)c;
     wt[o + pos[c]] = dense[c];
 }
-__global__ void k_set_uniq(int32_t *uniq, int64_t i, const int64_t *total) {
-    uniq[i] = (int32_t)*total;
-}
-
-// ---- per-row degrees, kept counts, CSR write ----------------------------
-
-__global__ __launch_bounds__(256) void k_degrees(const int64_t *__restrict__ offs,
-                                                 const int32_t *__restrict__ uniq, int64_t n,
-                                                 const double *__restrict__ wt, int sym,
-                                                 double *__restrict__ deg64,
-                                                 float *__restrict__ deg32) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const int64_t o = offs[i];
-    const int u = uniq[i];
+// the hub row's count and degree (sequential, ascending column; rare)
+__global__ void k_hub_finish(int64_t i, int64_t o, const int64_t *__restrict__ total, int sym,
+                             const double *__restrict__ wt, int32_t *__restrict__ uniq,
+                             int32_t *__restrict__ kept, double *__restrict__ deg64,
+                             float *__restrict__ deg32) {
+    if (threadIdx.x != 0) return;
+    const int u = (int)*total;
+    uniq[i] = u;
     if (sym == MN_SYM_UNION) {
-        double s = -0.0;  // laplacian.rs:367: s.iter().map(w).sum() in ascending j
+        double s = -0.0;
         for (int e = 0; e < u; ++e) s = s + wt[o + e];
         deg64[i] = s;
+        kept[i] = u + 1;
     } else {
-        float s = 0.0f;  // laplacian.rs:331-340 (order: ascending column here)
+        float s = 0.0f;
         for (int e = 0; e < u; ++e) s = s + (float)wt[o + e];
         deg32[i] = s;
     }
 }
 
+// ---- MAX: kept counts; CSR write ------------------------------------------
+
 __device__ __forceinline__ float max_offdiag(float w, float di, float dj, int normalize) {
     return normalize ? -w / sqrt_rn_f32(di * dj) : -w;
 }
 
-__global__ __launch_bounds__(256) void k_kept(const int64_t *__restrict__ offs,
-                                              const int32_t *__restrict__ col,
-                                              const double *__restrict__ wt,
-                                              const int32_t *__restrict__ uniq, int64_t n,
-                                              Params P, const float *__restrict__ deg32,
-                                              int32_t *__restrict__ kept) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const int u = uniq[i];
-    if (P.sym == MN_SYM_UNION) {
-        kept[i] = u + 1;
-        return;
-    }
-    const float thr = (float)P.thr, di = deg32[i];
-    int c = 0;
-    if (di > thr) {
-        const float v = P.normalize ? 1.0f : di;
-        if (fabsf(v) > 1e-9f) ++c;
-    }
-    const int64_t o = offs[i];
-    for (int e = 0; e < u; ++e) {
-        const int j = col[o + e];
-        const float dj = deg32[j];
-        if (P.normalize && (di <= thr || dj <= thr)) continue;
-        const float v = max_offdiag((float)wt[o + e], di, dj, P.normalize);
-        if (fabsf(v) > 1e-9f) ++c;
-    }
-    kept[i] = c;
+// does the MAX entry (i, j) survive (surfface-core/src/laplacian.rs:355-394, 215)
+__device__ __forceinline__ bool max_entry(const Params &P, float di, float dj, double w,
+                                          float &v) {
+    const float thr = (float)P.thr;
+    if (P.normalize && (di <= thr || dj <= thr)) return false;
+    v = max_offdiag((float)w, di, dj, P.normalize);
+    return fabsf(v) > 1e-9f;
 }
 
+__device__ __forceinline__ bool max_has_diag(const Params &P, float di) {
+    return di > (float)P.thr && fabsf(P.normalize ? 1.0f : di) > 1e-9f;
+}
+
+__global__ __launch_bounds__(256) void k_kept_max(const int64_t *__restrict__ offs,
+                                                  const int32_t *__restrict__ col,
+                                                  const double *__restrict__ wt,
+                                                  const int32_t *__restrict__ uniq, int64_t n,
+                                                  Params P, const float *__restrict__ deg32,
+                                                  int32_t *__restrict__ kept) {
+    const int lane = threadIdx.x & 63;
+    const int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    if (i >= n) return;
+    const int64_t o = offs[i];
+    const int u = uniq[i];
+    const float di = deg32[i];
+    int c = 0;
+    for (int e0 = 0; e0 < u; e0 += 64) {
+        const int e = e0 + lane;
+        float v = 0.f;
+        const bool keep = e < u && max_entry(P, di, deg32[col[o + e]], wt[o + e], v);
+        c += (int)__popcll(__ballot(keep));
+    }
+    if (lane == 0) kept[i] = c + (max_has_diag(P, di) ? 1 : 0);
+}
+
+// one wave per row: the row's entries (ascending columns) and its diagonal
 __global__ __launch_bounds__(256) void k_write_csr(const int64_t *__restrict__ offs,
                                                    const int32_t *__restrict__ col,
                                                    const double *__restrict__ wt,
@@ -378,42 +455,58 @@ __global__ __launch_bounds__(256) void k_write_csr(const int64_t *__restrict__ o
                                                    int32_t *__restrict__ out_col,
                                                    double *__restrict__ out_v64,
                                                    float *__restrict__ out_v32) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int lane = threadIdx.x & 63;
+    const int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     if (i >= n) return;
     const int64_t o = offs[i];
     const int u = uniq[i];
-    int64_t q = indptr[i];
+    const int64_t q0 = indptr[i];
+    const uint64_t below = (1ull << lane) - 1ull;
     if (P.sym == MN_SYM_UNION) {
-        bool diag = false;
-        for (int e = 0; e < u; ++e) {
-            const int j = col[o + e];
-            if (!diag && j > i) {
-                out_col[q] = (int32_t)i; out_v64[q] = deg64[i]; ++q; diag = true;
+        int nlt = 0;  // entries left of the diagonal
+        for (int e0 = 0; e0 < u; e0 += 64) {
+            const int e = e0 + lane;
+            const bool ok = e < u;
+            const int j = ok ? col[o + e] : 0;
+            nlt += (int)__popcll(__ballot(ok && j < i));
+            if (ok) {
+                const int64_t q = q0 + e + (j > i ? 1 : 0);
+                out_col[q] = j;
+                out_v64[q] = -wt[o + e];
             }
-            out_col[q] = j;
-            out_v64[q] = -wt[o + e];
-            ++q;
         }
-        if (!diag) { out_col[q] = (int32_t)i; out_v64[q] = deg64[i]; }
+        if (lane == 0) {
+            out_col[q0 + nlt] = (int32_t)i;
+            out_v64[q0 + nlt] = deg64[i];
+        }
         return;
     }
-    const float thr = (float)P.thr, di = deg32[i];
-    const bool has_diag = di > thr && fabsf(P.normalize ? 1.0f : di) > 1e-9f;
-    bool diag = !has_diag;
-    for (int e = 0; e < u; ++e) {
-        const int j = col[o + e];
-        if (!diag && j > i) {
-            out_col[q] = (int32_t)i; out_v32[q] = P.normalize ? 1.0f : di; ++q; diag = true;
+    const float di = deg32[i];
+    const bool has_diag = max_has_diag(P, di);
+    int base = 0, nlt = 0;
+    for (int e0 = 0; e0 < u; e0 += 64) {
+        const int e = e0 + lane;
+        float v = 0.f;
+        int j = 0;
+        bool keep = false;
+        if (e < u) {
+            j = col[o + e];
+            keep = max_entry(P, di, deg32[j], wt[o + e], v);
         }
-        const float dj = deg32[j];
-        if (P.normalize && (di <= thr || dj <= thr)) continue;
-        const float v = max_offdiag((float)wt[o + e], di, dj, P.normalize);
-        if (!(fabsf(v) > 1e-9f)) continue;
-        out_col[q] = j;
-        out_v32[q] = v;
-        ++q;
+        const uint64_t mk = __ballot(keep);
+        nlt += (int)__popcll(__ballot(keep && j < i));
+        if (keep) {
+            const int64_t q =
+                q0 + base + (int)__popcll(mk & below) + ((has_diag && j > i) ? 1 : 0);
+            out_col[q] = j;
+            out_v32[q] = v;
+        }
+        base += (int)__popcll(mk);
     }
-    if (!diag) { out_col[q] = (int32_t)i; out_v32[q] = P.normalize ? 1.0f : di; }
+    if (lane == 0 && has_diag) {
+        out_col[q0 + nlt] = (int32_t)i;
+        out_v32[q0 + nlt] = P.normalize ? 1.0f : di;
+    }
 }
 
 inline unsigned grid_for(int64_t n, int t = 256) { return (unsigned)std::max<int64_t>(1, (n + t - 1) / t); }
@@ -431,7 +524,7 @@ static int laplacian_impl(const int32_t *nbr, const void *val, int32_t val_f64, 
     *out = mn_csr{};
     MN_REQUIRE(n >= 1 && k >= 0 && (k == 0 || (nbr && val)), MN_EINVAL,
                "mn_laplacian_from_knn: bad shape n=%lld k=%d", (long long)n, k);
-    MN_REQUIRE(n <= INT_MAX, MN_EINVAL, "mn_laplacian_from_knn: n must fit int32");
+    MN_REQUIRE(n < INT_MAX, MN_EINVAL, "mn_laplacian_from_knn: n must fit int32");
     MN_REQUIRE(opts->weight_kernel == MN_W_GIVEN || opts->weight_kernel == MN_W_RATIONAL,
                MN_EINVAL, "mn_laplacian_from_knn: unknown weight_kernel");
     MN_REQUIRE(opts->symmetrise == MN_SYM_UNION || opts->symmetrise == MN_SYM_MAX, MN_EINVAL,
@@ -445,47 +538,51 @@ static int laplacian_impl(const int32_t *nbr, const void *val, int32_t val_f64, 
     hipStream_t s = (hipStream_t)opts->stream;
     const int64_t nk = n * (int64_t)k;
 
-    // scratch layout
-    char *g0 = (char *)scratch(kSlotGeneric0, (size_t)nk * 12 + 64);                 // vidx, vw
-    char *g1 = (char *)scratch(kSlotGeneric1, (size_t)n * 4 * 6 + (size_t)(n + 1) * 8 * 2 + 64 +
+    // scratch: per-row ints + offsets; row segments (k + in-degree per row)
+    char *g1 = (char *)scratch(kSlotGeneric1, (size_t)n * 4 * 5 + (size_t)(n + 1) * 8 + 64 +
                                                ((size_t)n / scan::SB + 2) * 8);
-    char *g2 = (char *)scratch(kSlotGeneric2, (size_t)(2 * nk + 1) * 12);             // col, w
-    MN_REQUIRE(g0 && g1 && g2, MN_ENOMEM, "mn_laplacian_from_knn: scratch allocation failed");
-    int32_t *vidx = (int32_t *)g0;
-    double *vw = (double *)(g0 + (((size_t)nk * 4 + 15) & ~(size_t)15));
-    int32_t *outcnt = (int32_t *)g1;
-    int32_t *indeg = outcnt + n;
-    int32_t *capv = indeg + n;
-    int32_t *fill = capv + n;
+    char *g2 = (char *)scratch(kSlotGeneric2, (size_t)(2 * nk + 1) * 12 + 64);
+    int *flags = (int *)scratch(kSlotFlags, 64);
+    int32_t *lists = (int32_t *)scratch(kSlotGeneric3, (size_t)n * 8 + 64);
+    MN_REQUIRE(g1 && g2 && flags && lists, MN_ENOMEM,
+               "mn_laplacian_from_knn: scratch allocation failed");
+    int32_t *indeg = (int32_t *)g1;
+    int32_t *seg = indeg + n;
+    int32_t *fill = seg + n;
     int32_t *uniq = fill + n;
     int32_t *kept = uniq + n;
     int64_t *offs = (int64_t *)(((uintptr_t)(kept + n) + 15) & ~(uintptr_t)15);
     int64_t *part = offs + (n + 1);
-    int *flags = (int *)(part + (n / scan::SB + 2));
     const int64_t E2 = 2 * nk;
     int32_t *col = (int32_t *)g2;
     double *wt = (double *)(g2 + (((size_t)E2 * 4 + 15) & ~(size_t)15));
-    int32_t *lists = (int32_t *)scratch(kSlotGeneric3, (size_t)n * 8 + 64);
-    MN_REQUIRE(lists, MN_ENOMEM, "mn_laplacian_from_knn: scratch allocation failed");
     int32_t *big_list = lists, *huge_list = lists + n;
+    // degrees (into degrees_out when given, else scratch)
+    void *degbuf = degrees_out;
+    if (!degbuf) {
+        degbuf = scratch(kSlotNorms2, (size_t)n * 8);
+        MN_REQUIRE(degbuf, MN_ENOMEM, "mn_laplacian_from_knn: scratch allocation failed");
+    }
+    double *deg64 = P.sym == MN_SYM_UNION ? (double *)degbuf : nullptr;
+    float *deg32 = P.sym == MN_SYM_UNION ? nullptr : (float *)degbuf;
 
     Timer tm;
     tm.start(true, s);
-    MN_HIP_TRY(hipMemsetAsync(outcnt, 0, (size_t)n * 4 * 6, s));
+    MN_HIP_TRY(hipMemsetAsync(indeg, 0, (size_t)n * 4 * 5, s));
     MN_HIP_TRY(hipMemsetAsync(flags, 0, 16, s));
     if (k > 0)
-        hipLaunchKernelGGL(k_lap_weights, dim3(grid_for(n)), dim3(256), 0, s, nbr, val, val_f64,
-                           n, k, P, vidx, vw, outcnt, indeg, flags);
-    hipLaunchKernelGGL(k_add_i32, dim3(grid_for(n)), dim3(256), 0, s, outcnt, indeg, n, capv);
-    MN_HIP_TRY(scan::exclusive_scan(capv, n, offs, part, s));
+        hipLaunchKernelGGL(k_lap_slots, dim3(grid_for(nk)), dim3(256), 0, s, nbr, val, val_f64, n,
+                           k, P, indeg, flags);
+    hipLaunchKernelGGL(k_seg_len, dim3(grid_for(n)), dim3(256), 0, s, indeg, n, k, seg);
+    MN_HIP_TRY(scan::exclusive_scan(seg, n, offs, part, s));
     if (k > 0)
-        hipLaunchKernelGGL(k_lap_scatter, dim3(grid_for(n)), dim3(256), 0, s, vidx, vw, n, k, offs,
-                           outcnt, fill, col, wt);
-    hipLaunchKernelGGL(k_row_sort_wave, dim3(grid_for(n * 64)), dim3(256), 0, s, offs, n, col, wt,
-                       uniq, big_list, flags + 1);
+        hipLaunchKernelGGL(k_lap_scatter, dim3(grid_for(nk)), dim3(256), 0, s, nbr, val, val_f64,
+                           n, k, P, offs, fill, col, wt);
+    hipLaunchKernelGGL(k_row_sort_wave, dim3(grid_for(n * 64)), dim3(256), 0, s, offs, n, P.sym,
+                       col, wt, uniq, kept, deg64, deg32, big_list, flags + 1);
     hipLaunchKernelGGL(k_row_sort_block, dim3(256), dim3(1024), 0, s, offs, big_list, flags + 1,
-                       col, wt, uniq, huge_list, flags + 2);
-    MN_HIP_TRY(hipGetLastError());
+                       P.sym, col, wt, uniq, kept, deg64, deg32, huge_list, flags + 2);
+    MN_KCHECK(s, "k_row_sort");
     int hf[4] = {0, 0, 0, 0};
     MN_HIP_TRY(hipMemcpyAsync(hf, flags, 16, hipMemcpyDeviceToHost, s));
     MN_HIP_TRY(hipStreamSynchronize(s));
@@ -517,24 +614,15 @@ static int laplacian_impl(const int32_t *nbr, const void *val, int32_t val_f64, 
             MN_HIP_TRY(scan::exclusive_scan(dflag, n, dpos, dpart, s));
             hipLaunchKernelGGL(k_dense_compact, dim3(grid_for(n)), dim3(256), 0, s, dense, dflag,
                                dpos, n, o, col, wt);
-            hipLaunchKernelGGL(k_set_uniq, dim3(1), dim3(1), 0, s, uniq, i, dpos + n);
+            hipLaunchKernelGGL(k_hub_finish, dim3(1), dim3(64), 0, s, i, o, dpos + n, P.sym, wt,
+                               uniq, kept, deg64, deg32);
         }
         MN_HIP_TRY(hipStreamSynchronize(s));
         (void)hipFree(dense); (void)hipFree(dflag); (void)hipFree(dpos); (void)hipFree(dpart);
     }
-    // degrees (into degrees_out when given, else scratch)
-    double *deg64 = nullptr;
-    float *deg32 = nullptr;
-    void *degbuf = degrees_out;
-    if (!degbuf) {
-        degbuf = scratch(kSlotNorms2, (size_t)n * 8);
-        MN_REQUIRE(degbuf, MN_ENOMEM, "mn_laplacian_from_knn: scratch allocation failed");
-    }
-    if (P.sym == MN_SYM_UNION) deg64 = (double *)degbuf; else deg32 = (float *)degbuf;
-    hipLaunchKernelGGL(k_degrees, dim3(grid_for(n)), dim3(256), 0, s, offs, uniq, n, wt, P.sym,
-                       deg64, deg32);
-    hipLaunchKernelGGL(k_kept, dim3(grid_for(n)), dim3(256), 0, s, offs, col, wt, uniq, n, P,
-                       deg32, kept);
+    if (P.sym == MN_SYM_MAX)
+        hipLaunchKernelGGL(k_kept_max, dim3(grid_for(n * 64)), dim3(256), 0, s, offs, col, wt,
+                           uniq, n, P, deg32, kept);
     int64_t *indptr = nullptr;
     MN_HIP_TRY(hipMalloc(&indptr, sizeof(int64_t) * (n + 1)));
     MN_HIP_TRY(scan::exclusive_scan(kept, n, indptr, part, s));
@@ -550,8 +638,8 @@ static int laplacian_impl(const int32_t *nbr, const void *val, int32_t val_f64, 
         set_error("mn_laplacian_from_knn: output allocation (nnz=%lld) failed", (long long)nnz);
         return MN_ENOMEM;
     }
-    hipLaunchKernelGGL(k_write_csr, dim3(grid_for(n)), dim3(256), 0, s, offs, col, wt, uniq, n, P,
-                       deg64, deg32, indptr, ocol, (double *)oval, (float *)oval);
+    hipLaunchKernelGGL(k_write_csr, dim3(grid_for(n * 64)), dim3(256), 0, s, offs, col, wt, uniq,
+                       n, P, deg64, deg32, indptr, ocol, (double *)oval, (float *)oval);
     MN_HIP_TRY(hipGetLastError());
     tm.mark();
     MN_HIP_TRY(hipStreamSynchronize(s));

@@ -60,6 +60,39 @@ void *scratch(int slot, size_t bytes) {
     return b.p;
 }
 
+namespace {
+struct ThreadStreams {
+    std::unordered_map<int, hipStream_t> side;
+    std::unordered_map<int, hipEvent_t> ev;
+    ~ThreadStreams() {
+        for (auto &kv : side) (void)hipStreamDestroy(kv.second);
+        for (auto &kv : ev) (void)hipEventDestroy(kv.second);
+    }
+};
+thread_local ThreadStreams t_streams;
+}  // namespace
+
+hipStream_t side_stream() {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+    auto it = t_streams.side.find(dev);
+    if (it != t_streams.side.end()) return it->second;
+    hipStream_t st = nullptr;
+    if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) return nullptr;
+    t_streams.side[dev] = st;
+    return st;
+}
+
+hipError_t stream_wait(hipStream_t waiter, hipStream_t on) {
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    hipEvent_t &ev = t_streams.ev[dev];
+    if (!ev && (e = hipEventCreateWithFlags(&ev, hipEventDisableTiming)) != hipSuccess) return e;
+    if ((e = hipEventRecord(ev, on)) != hipSuccess) return e;
+    return hipStreamWaitEvent(waiter, ev, 0);
+}
+
 void Timer::start(bool enable, hipStream_t stream) {
     on = enable;
     s = stream;

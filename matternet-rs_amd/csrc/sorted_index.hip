@@ -163,38 +163,73 @@ __global__ __launch_bounds__(256) void k_emit(const Key *__restrict__ keys, int6
 
 // laplacian.rs:421-448 std_deviation, reproduced bit-for-bit: the reference
 // folds sequentially (f64 sum -> f32 mean, then an f32 sum of squared
-// deviations), and no parallel order reproduces that rounding, so one thread
-// walks the array (loads unrolled ahead of the dependent adds).
+// deviations), and no parallel order reproduces that rounding, so the adds
+// stay one dependent chain.  What is NOT sequential is everything around it:
+// one wave streams 256-value chunks (4 consecutive values per lane, the next
+// chunk in flight) into LDS, and the chain reads them back as broadcast
+// ds_read_b128 (all lanes, same address: conflict-free), so the VALU issues
+// little but the chain's adds (pass 2: the squared deviations are formed
+// lane-parallel before the chain).  The host runs it on a side stream,
+// concurrent with the sort.
+constexpr int STD_CHUNK = 256;  // values per chunk: 64 lanes x 4
+
 __global__ __launch_bounds__(64) void k_std_exact(const double *__restrict__ lam, int64_t n,
                                                   float *__restrict__ out) {
-    if (threadIdx.x != 0) return;
+    __shared__ double b64[2][STD_CHUNK];
+    __shared__ float b32[2][STD_CHUNK];
+    const int lane = threadIdx.x;
+    const int64_t nfull = n / STD_CHUNK;
+    double p[4];
+    auto fetch = [&](int64_t c) {
+#pragma unroll
+        for (int t = 0; t < 4; ++t) p[t] = lam[c * STD_CHUNK + 4 * lane + t];
+    };
+    // ---- pass 1: s = sum(lam) in index order (f64) ----
     double s = -0.0;
-    int64_t i = 0;
-    for (; i + 8 <= n; i += 8) {
-        double v[8];
+    if (nfull > 0) fetch(0);
+    for (int64_t c = 0; c < nfull; ++c) {
+        double *bb = b64[c & 1];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) v[u] = lam[i + u];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) s = s + v[u];
-    }
-    for (; i < n; ++i) s = s + lam[i];
-    const float mean = __fdiv_rn((float)s, (float)n);
-    float var = -0.0f;
-    for (i = 0; i + 8 <= n; i += 8) {
-        double v[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) v[u] = lam[i + u];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-            const float d = mean - (float)v[u];
-            var = var + d * d;
+        for (int t = 0; t < 4; ++t) bb[4 * lane + t] = p[t];
+        if (c + 1 < nfull) fetch(c + 1);
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll 32
+        for (int e = 0; e < STD_CHUNK; e += 2) {
+            const double2 v = *reinterpret_cast<const double2 *>(bb + e);
+            s = s + v.x;
+            s = s + v.y;
         }
+        __builtin_amdgcn_wave_barrier();
     }
-    for (; i < n; ++i) {
-        const float d = mean - (float)lam[i];
-        var = var + d * d;
+    for (int64_t i = nfull * STD_CHUNK; i < n; ++i) s = s + lam[i];
+    const float mean = __fdiv_rn((float)s, (float)n);
+    // ---- pass 2: var = sum((mean - (f32)lam)^2) in index order (f32) ----
+    float var = -0.0f;
+    if (nfull > 0) fetch(0);
+    for (int64_t c = 0; c < nfull; ++c) {
+        float *bb = b32[c & 1];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            const float dv = mean - (float)p[t];
+            bb[4 * lane + t] = dv * dv;
+        }
+        if (c + 1 < nfull) fetch(c + 1);
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll 16
+        for (int e = 0; e < STD_CHUNK; e += 4) {
+            const float4 v = *reinterpret_cast<const float4 *>(bb + e);
+            var = var + v.x;
+            var = var + v.y;
+            var = var + v.z;
+            var = var + v.w;
+        }
+        __builtin_amdgcn_wave_barrier();
     }
-    *out = sqrt_rn_f32(__fdiv_rn(var, (float)n));
+    for (int64_t i = nfull * STD_CHUNK; i < n; ++i) {
+        const float dv = mean - (float)lam[i];
+        var = var + dv * dv;
+    }
+    if (lane == 0) *out = sqrt_rn_f32(__fdiv_rn(var, (float)n));
 }
 
 inline unsigned grid(int64_t n, int t = 256) {
@@ -223,6 +258,16 @@ static int sorted_index_impl(const double *lam, int64_t n, int64_t *order, doubl
     double *sums = (double *)scratch(kSlotFlags, 64);
     MN_REQUIRE(sums, MN_ENOMEM, "mn_sorted_index: scratch allocation failed");
 
+    // std_deviation is a sequential fold independent of the sort: it runs on
+    // the library's side stream (ordered after the caller's prior work on s)
+    hipStream_t side = nullptr;
+    if (std_host) {
+        side = side_stream();
+        MN_REQUIRE(side, MN_EHIP, "mn_sorted_index: side stream creation failed");
+        MN_HIP_TRY(stream_wait(side, s));
+        hipLaunchKernelGGL(k_std_exact, dim3(1), dim3(64), 0, side, lam, n, (float *)sums);
+        MN_KCHECK(side, "k_std_exact");
+    }
     hipLaunchKernelGGL(k_make_keys, dim3(grid(P)), dim3(256), 0, s, lam, n, P, keys);
     // local sort of every TILE, then merge levels: global stages j >= TILE, local j < TILE
     hipLaunchKernelGGL(k_bitonic_local, dim3((unsigned)(P / TILE)), dim3(1024), 0, s, keys, P,
@@ -242,7 +287,7 @@ static int sorted_index_impl(const double *lam, int64_t n, int64_t *order, doubl
     hipLaunchKernelGGL(k_emit, dim3(grid(n)), dim3(256), 0, s, keys, n, start, pos, run_min, lam,
                        order, key_out);
     if (std_host) {
-        hipLaunchKernelGGL(k_std_exact, dim3(1), dim3(64), 0, s, lam, n, (float *)sums);
+        MN_HIP_TRY(stream_wait(s, side));
         float sd = 0.f;
         MN_HIP_TRY(hipMemcpyAsync(&sd, sums, 4, hipMemcpyDeviceToHost, s));
         MN_HIP_TRY(hipStreamSynchronize(s));

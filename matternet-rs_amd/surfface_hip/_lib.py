@@ -38,7 +38,8 @@ MN_KNN_AUTO, MN_KNN_F32, MN_KNN_BF16X3 = 0, 1, 2
 class KnnStats(C.Structure):
     _fields_ = [("n_queries", C.c_int64), ("n_uncertified", C.c_int64), ("slices", C.c_int32),
                 ("list_len", C.c_int32), ("ms_norms", C.c_float), ("ms_gram", C.c_float),
-                ("ms_rerank", C.c_float), ("ms_fallback", C.c_float), ("ms_total", C.c_float)]
+                ("ms_rerank", C.c_float), ("ms_fallback", C.c_float), ("ms_total", C.c_float),
+                ("algo", C.c_int32)]
 
     def as_dict(self):
         return {f: getattr(self, f) for f, _ in self._fields_}

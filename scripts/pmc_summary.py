@@ -29,7 +29,11 @@ def main():
     ks = os.path.join(src, "kt", "run_kernel_stats.csv")
     shutil.copy(ks, os.path.join(dst, f"{tag}_kernel_stats.csv"))
     stats = {r["Name"]: r for r in rows(ks)}
-    out = {"tag": tag, "rows_per_gpu": n, "dim": d, "kernels": {}}
+    # the dominant kernel (largest total time) is the one the roofline is about
+    dom = max(stats, key=lambda k: float(stats[k]["TotalDurationNs"]))
+    dshort = dom.split("(")[0].replace("void ", "")
+    out = {"tag": tag, "rows_per_gpu": n, "dim": d, "kernel": dshort.split("::")[-1],
+           "kernel_full": dshort, "kernels": {}}
     for name, r in stats.items():
         short = name.split("(")[0].replace("void ", "")
         out["kernels"][short] = {"calls": int(r["Calls"]), "avg_ms": float(r["AverageNs"]) / 1e6,
@@ -41,12 +45,17 @@ def main():
             continue
         shutil.copy(p, os.path.join(dst, f"{tag}_pmc_{pas}.csv"))
         for r in rows(p):
-            if "k_gram_topk" in r["Kernel_Name"] and r["Counter_Name"] == ctr:
-                pm[ctr] = float(r["Counter_Value"])
+            if r["Kernel_Name"].split("(")[0].replace("void ", "") == dshort \
+                    and r["Counter_Name"] == ctr:
+                pm[ctr] = pm.get(ctr, 0.0) + float(r["Counter_Value"])
+                pm[ctr + "_n"] = pm.get(ctr + "_n", 0) + 1
+    for ctr in ("FETCH_SIZE", "WRITE_SIZE"):  # per launch
+        if ctr in pm:
+            pm[ctr] /= pm[ctr + "_n"]
     if "FETCH_SIZE" in pm and "WRITE_SIZE" in pm:
         fetch_b = pm["FETCH_SIZE"] * 1024 * 2  # gfx950: FETCH_SIZE = 1/2 of wide reads
         write_b = pm["WRITE_SIZE"] * 1024
-        out["gram_pmc"] = {"FETCH_SIZE_KiB": pm["FETCH_SIZE"], "WRITE_SIZE_KiB": pm["WRITE_SIZE"],
+        out["dominant_pmc"] = {"FETCH_SIZE_KiB": pm["FETCH_SIZE"], "WRITE_SIZE_KiB": pm["WRITE_SIZE"],
                            "fetch_bytes_corrected": fetch_b, "write_bytes": write_b}
         out["hbm_bytes_per_launch"] = fetch_b + write_b
         out["algorithmic_bytes_per_launch"] = 2 * n * d * 4

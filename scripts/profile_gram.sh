@@ -10,7 +10,7 @@ OUT=$ROOT/gpurun_out/prof_$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 cd /tmp || exit 1
-ARGS=(--cpu-seconds 0 --warmup 0 --steps 1 "$@")
+ARGS=(--cpu-seconds 0 --warmup 0 --steps 1 --no-c3 --no-c5 "$@")
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/kt" -o run -- \
     python3 "$ROOT/bench.py" "${ARGS[@]}" > "$OUT/kt.log" 2>&1 || { echo "kt pass failed rc=$?"; exit 1; }
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/fetch" -o run -- \

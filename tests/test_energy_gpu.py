@@ -116,3 +116,42 @@ def test_normalise_lambdas_vs_oracle():
     t = torch.tensor([-1.0, -3.0, -2.0], dtype=torch.float64).cuda()
     S.normalise_lambdas(t)
     np.testing.assert_allclose(t.cpu().numpy(), [2 / 3, 0.0, 1 / 3], atol=1e-15)
+
+
+def test_odd_rows_and_positive_offdiagonals():
+    """n odd (the last two-row pass holds one row) and positive off-diagonal
+    entries (they feed the Rayleigh numerator, never the dispersion), both
+    dispersion modes."""
+    import scipy.sparse as sp
+    import surfface_hip as S
+    ip, ix, iv = feature_laplacian(f=301, profile=800, topk=5, seed=4)
+    M = sp.csr_matrix((iv, ix, ip), shape=(301, 301)).tolil()
+    rng = np.random.default_rng(3)
+    rows, cols = sp.triu(M.tocsr(), k=1).nonzero()
+    for t in rng.choice(len(rows), 40, replace=False):
+        M[rows[t], cols[t]] = M[cols[t], rows[t]] = 0.3
+    M = M.tocsr()
+    M.sort_indices()
+    ip2, ix2, iv2 = M.indptr.astype(np.int64), M.indices.astype(np.int32), M.data
+    X = datagen.clustered(1001, 301, seed=5, blobs=3)
+    for gm, og in ((0, O.G_TAUMODE), (1, O.G_ENERGYMAPS)):
+        E, G, lam = run(X, ip2, ix2, iv2, gm, S.TauMode.Median)
+        assert S.energy.last_stats()["symmetric"] == 1
+        rE, rG, rl = O.energy_rows(X, ip2, ix2, iv2, og, O.TAU_MEDIAN)
+        np.testing.assert_allclose(E, rE, rtol=RTOL, atol=ATOL)
+        np.testing.assert_allclose(G, rG, rtol=RTOL, atol=ATOL)
+        np.testing.assert_allclose(lam, rl, rtol=RTOL, atol=ATOL)
+
+
+def test_entry_list_beyond_lds_and_wide_rows():
+    """f = 2048 with topk 24: the entry list (~50k entries) exceeds the LDS
+    budget and is read from L2; rows of 2048 values (NR = 32 registers)."""
+    import surfface_hip as S
+    ip, ix, iv = feature_laplacian(f=2048, profile=300, topk=24, seed=6)
+    X = datagen.uniform(333, 2048, seed=12)
+    E, G, lam = run(X, ip, ix, iv, 0, S.TauMode.Median)
+    rE, rG, rl = O.energy_rows(X, ip, ix, iv, O.G_TAUMODE, O.TAU_MEDIAN)
+    np.testing.assert_allclose(E, rE, rtol=RTOL, atol=ATOL)
+    np.testing.assert_allclose(G, rG, rtol=RTOL, atol=ATOL)
+    np.testing.assert_allclose(lam, rl, rtol=RTOL, atol=ATOL)
+    assert S.energy.last_stats()["entries"] * 12 > 96 * 1024
