@@ -240,7 +240,9 @@ def c3_legs(S, X, idx, dist, k):
         idx, dist, weight_kernel="rational", symmetrise="union", eps=float("inf"), sigma=1.0,
         p=2.0))
     byt = n * k * 8 + Lit.nnz * 12 + (n + 1) * 8
-    out["item_laplacian"] = {"ms": round(ms, 3), "nnz": Lit.nnz, "GB_per_s": round(byt / ms / 1e6, 1)}
+    lst = S.laplacian.last_stats()
+    out["item_laplacian"] = {"ms": round(ms, 3), "nnz": Lit.nnz, "GB_per_s": round(byt / ms / 1e6, 1),
+                             "rows_block_sorted": lst["big_rows"], "hub_rows": lst["hub_rows"]}
     ms, (fi, fd, fw, fst) = _timed(lambda: S.knn_cos_columns(X, 4, eps=1.0, sigma=1.0, p=2.0), 1)
     out["feature_knn_cos"] = {"ms": round(ms, 3), "uncertified": fst["n_uncertified"],
                               "gram_tflops": round(2.0 * f * f * n / 2 / (fst["ms_gram"] * 1e9), 2)

@@ -149,14 +149,18 @@ typedef struct mn_lap_opts {
     void *stream;
 } mn_lap_opts;
 
-/* CSR matrix; library-allocated device buffers, release with mn_csr_free. */
+/* CSR matrix.  As an output: library-allocated device buffers (release with
+ * mn_csr_free), or, when caller_owned == 1 on entry, the caller's device
+ * buffers indptr [n_rows + 1], indices / values [nnz = capacity] of the
+ * mode's value_type; a capacity that is too small returns MN_ECAP with nnz =
+ * the entries needed.  n(2k + 1) entries always suffice for kNN rows. */
 typedef struct mn_csr {
     int64_t n_rows, n_cols, nnz;
     int64_t *indptr;   /* [n_rows + 1] */
     int32_t *indices;  /* [nnz], ascending within a row */
     void *values;      /* [nnz] of value_type */
     int32_t value_type;
-    int32_t reserved0;
+    int32_t caller_owned;
 } mn_csr;
 
 typedef struct mn_lap_stats {
@@ -189,7 +193,12 @@ int mn_lap_last_stats(mn_lap_stats *out);
 enum mn_g_mode {
     MN_G_TAUMODE = 0,    /* ordered pairs, lambda = tau*E/(E+tau)+(1-tau)G
                             (src_legacy/taumode.rs:261-408)                      */
-    MN_G_ENERGYMAPS = 1  /* j > i pairs, lambda = E (energymaps.rs:923-1045)     */
+    MN_G_ENERGYMAPS = 1, /* j > i pairs, lambda = E (energymaps.rs:923-1045)     */
+    MN_G_SPECTRAL = 2    /* Stage D device lambdas (surfface-core/src/spectral/
+                            mod.rs:69-181): E = clamp(num/(den+1e-9), +-1e6),
+                            G = D = clamp(row/(sum_rows row + 1e-12), 0, 1) with
+                            row = sum_f max(0, sum_j w_fj (x_f - x_j)^2),
+                            lambda = E + D; f32 or f64 Laplacian values        */
 };
 enum mn_tau_mode { MN_TAU_FIXED = 0, MN_TAU_MEDIAN = 1, MN_TAU_MEAN = 2, MN_TAU_PERCENTILE = 3 };
 
@@ -215,7 +224,11 @@ typedef struct mn_energy_stats {
  * TauMode::compute_taumode_lambdas_parallel's per-item work
  * (src_legacy/taumode.rs:117-250, 261-408) and node_energy_and_dispersion
  * (src_legacy/energymaps.rs:923-1045).  Tolerance 1e-9 relative (the
- * reference sums in rayon order).  f <= 4096. */
+ * reference sums in rayon order).  MN_G_SPECTRAL replaces compute_lambdas_gpu
+ * / compute_tau_mode_gpu (surfface-core/src/spectral/mod.rs:158-181,
+ * bridge.rs:27-69) and also takes the Stage C f32 Laplacian (MN_SYM_MAX
+ * output); the reference computes in f32 (Burn matmuls), this in f64:
+ * tolerance 1e-4 relative.  f <= 4096. */
 int mn_energy_rows(const mn_csr *L, const float *X, int64_t n, int32_t f,
                    const mn_energy_opts *opts, double *E, double *G, double *lambda);
 

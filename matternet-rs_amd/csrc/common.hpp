@@ -149,6 +149,66 @@ __device__ __forceinline__ void wave_bitonic_sort(T (&d)[NR], int (&ix)[NR]) {
 // the double rounding is innocuous) and matches Rust's IEEE f32::sqrt.
 __device__ __forceinline__ float sqrt_rn_f32(float x) { return (float)__builtin_sqrt((double)x); }
 
+// Ordered fold acc = (((acc + b[0]) + b[1]) + ...) over N values in LDS that
+// every lane reads as broadcasts (same address: conflict-free).  The loads
+// go out in register batches of 32 values, the next batch issued before the
+// current batch's adds, so the chain waits on the add latency only.
+template <int N>
+__device__ __forceinline__ double lds_chain_f64(double acc, const double *b) {
+    static_assert(N % 64 == 0, "chain length must be a multiple of 64");
+    constexpr int NB = N / 32;  // batches of 16 double2
+    const double2 *b2 = reinterpret_cast<const double2 *>(b);
+    double2 v[2][16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) v[0][q] = b2[q];
+    __builtin_amdgcn_sched_group_barrier(0x100, 16, 0);
+#pragma unroll
+    for (int bt = 0; bt < NB; ++bt) {
+        // the next batch's 16 reads go out before this batch's 32 adds (the
+        // scheduler would otherwise interleave them and expose the LDS
+        // latency on the chain)
+        if (bt + 1 < NB) {
+#pragma unroll
+            for (int q = 0; q < 16; ++q) v[(bt + 1) & 1][q] = b2[16 * (bt + 1) + q];
+            __builtin_amdgcn_sched_group_barrier(0x100, 16, 0);
+        }
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+            acc = acc + v[bt & 1][q].x;
+            acc = acc + v[bt & 1][q].y;
+        }
+        __builtin_amdgcn_sched_group_barrier(0x002, 32, 0);
+    }
+    return acc;
+}
+template <int N>
+__device__ __forceinline__ float lds_chain_f32(float acc, const float *b) {
+    static_assert(N % 128 == 0, "chain length must be a multiple of 128");
+    constexpr int NB = N / 32;  // batches of 8 float4
+    const float4 *b4 = reinterpret_cast<const float4 *>(b);
+    float4 v[2][8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) v[0][q] = b4[q];
+    __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);
+#pragma unroll
+    for (int bt = 0; bt < NB; ++bt) {
+        if (bt + 1 < NB) {
+#pragma unroll
+            for (int q = 0; q < 8; ++q) v[(bt + 1) & 1][q] = b4[8 * (bt + 1) + q];
+            __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);
+        }
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            acc = acc + v[bt & 1][q].x;
+            acc = acc + v[bt & 1][q].y;
+            acc = acc + v[bt & 1][q].z;
+            acc = acc + v[bt & 1][q].w;
+        }
+        __builtin_amdgcn_sched_group_barrier(0x002, 32, 0);
+    }
+    return acc;
+}
+
 // Read element `pos` of a register-distributed array (wave-uniform pos).
 template <int NR, typename T>
 __device__ __forceinline__ T wave_elem(const T (&d)[NR], int pos) {

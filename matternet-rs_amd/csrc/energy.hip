@@ -45,8 +45,17 @@ constexpr size_t LDS_BUDGET = 160 * 1024;
 constexpr size_t EDGE_LDS_MAX = 96 * 1024;  // entry lists kept in LDS up to this size
 
 // ---- build the entry lists from CSR --------------------------------------
+// Laplacian values: f64 (legacy GraphLaplacian) or f32 (Stage C CsMat<f32>)
+struct Vals {
+    const void *p;
+    int f32;
+    __device__ __forceinline__ double operator[](int64_t i) const {
+        return f32 ? (double)((const float *)p)[i] : ((const double *)p)[i];
+    }
+};
+
 __global__ void k_check_sym(const int64_t *__restrict__ ip, const int32_t *__restrict__ ix,
-                            const double *__restrict__ v, int f, int *__restrict__ asym) {
+                            Vals v, int f, int *__restrict__ asym) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= f) return;
     for (int64_t p = ip[i]; p < ip[i + 1]; ++p) {
@@ -74,16 +83,17 @@ __global__ void k_check_sym(const int64_t *__restrict__ ip, const int32_t *__res
 //          dispersion's set): value m * v, feeds num only.
 // Symmetric L: only j >= i is listed, off-diagonal multiplicity 2.  Pair set:
 // taumode = ordered pairs i != j (taumode.rs:366-408), energymaps = j > i
-// (energymaps.rs:990-1030).
+// (energymaps.rs:990-1030), spectral = ordered pairs with W = max(0, -L)
+// (spectral/mod.rs:115-140: the diagonal's (x_f - x_f)^2 term is 0).
 __device__ __forceinline__ int entry_class(int i, int j, double v, int sym, int g_mode) {
     if (sym && j < i) return -1;  // covered by (j, i)
     if (i == j) return 1;
-    const bool counts = (g_mode == MN_G_TAUMODE) || sym || j > i;
+    const bool counts = (g_mode != MN_G_ENERGYMAPS) || sym || j > i;
     return (counts && -v > 0.0) ? 0 : 1;
 }
 
 __global__ void k_count_entries(const int64_t *__restrict__ ip, const int32_t *__restrict__ ix,
-                                const double *__restrict__ v, int f, int sym, int g_mode,
+                                Vals v, int f, int sym, int g_mode,
                                 int32_t *__restrict__ cnt) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= f) return;
@@ -98,7 +108,7 @@ __global__ void k_count_entries(const int64_t *__restrict__ ip, const int32_t *_
 }
 
 __global__ void k_fill_entries(const int64_t *__restrict__ ip, const int32_t *__restrict__ ix,
-                               const double *__restrict__ v, int f, int sym, int g_mode,
+                               Vals v, int f, int sym, int g_mode,
                                const int64_t *__restrict__ off, uint32_t *__restrict__ eij,
                                double *__restrict__ ev) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -303,7 +313,14 @@ __global__ __launch_bounds__(NR <= 16 ? 1024 : 256) void k_energy_rows(
             const double Ss = mA_g * wave_sum(S[t]);
             const double Qs = mA_g * wave_sum(Q[t]);
             double e_raw = 0.0, g_raw = 0.0, lam = 0.0;
-            if (!(g_mode == MN_G_TAUMODE && !nonzero[t])) {  // zero vector: lambda 0
+            if (g_mode == MN_G_SPECTRAL) {
+                // spectral/mod.rs:89: clamp(num / (den + 1e-9), -1e6, 1e6); the
+                // row energy is kept raw (G) until the global total is known
+                const double r = num / (den[t] + 1e-9);
+                e_raw = r < -1e6 ? -1e6 : (r > 1e6 ? 1e6 : r);
+                g_raw = Ss;
+                lam = e_raw;
+            } else if (!(g_mode == MN_G_TAUMODE && !nonzero[t])) {  // zero vector: lambda 0
                 e_raw = den[t] > 1e-12 ? fmax(num / den[t], 0.0) : 0.0;
                 if (Ss > 1e-12) {
                     const double g = Qs / (Ss * Ss);
@@ -325,6 +342,44 @@ __global__ __launch_bounds__(NR <= 16 ? 1024 : 256) void k_energy_rows(
             }
         }
         __builtin_amdgcn_wave_barrier();
+    }
+}
+
+// ---- Stage D global normalisation (spectral/mod.rs:137-145, 177) ------------
+// total = sum of the row energies: fixed-order two-level reduction
+// (deterministic); then D = clamp(row / (total + 1e-12), 0, 1), lambda = R + D.
+constexpr int SUM_BLOCKS = 256;
+__global__ __launch_bounds__(256) void k_sum_partials(const double *__restrict__ x, int64_t n,
+                                                      double *__restrict__ part) {
+    __shared__ double red[4];
+    const int64_t per = (n + SUM_BLOCKS - 1) / SUM_BLOCKS;
+    const int64_t b0 = (int64_t)blockIdx.x * per, b1 = min(n, b0 + per);
+    double s = 0.0;
+    for (int64_t i = b0 + threadIdx.x; i < b1; i += blockDim.x) s += x[i];
+    s = wave_sum(s);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) part[blockIdx.x] = ((red[0] + red[1]) + red[2]) + red[3];
+}
+__global__ __launch_bounds__(256) void k_spectral_finish(const double *__restrict__ part,
+                                                         int64_t n, const double *__restrict__ E,
+                                                         double *__restrict__ G,
+                                                         double *__restrict__ lam) {
+    __shared__ double tot;
+    if (threadIdx.x < 64) {
+        double s = 0.0;
+        for (int q = threadIdx.x; q < SUM_BLOCKS; q += 64) s += part[q];
+        s = wave_sum(s);
+        if (threadIdx.x == 0) tot = s;
+    }
+    __syncthreads();
+    const double total = tot;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        double d = G[i] / (total + 1e-12);
+        d = d < 0.0 ? 0.0 : (d > 1.0 ? 1.0 : d);
+        G[i] = d;
+        if (lam) lam[i] = E[i] + d;
     }
 }
 
@@ -388,17 +443,28 @@ static int energy_impl(const mn_csr *L, const float *X, int64_t n, int32_t f,
     MN_REQUIRE(L->n_rows == f && L->n_cols == f, MN_EINVAL,
                "mn_energy_rows: Laplacian must be f x f (feature space), got %lld x %lld",
                (long long)L->n_rows, (long long)L->n_cols);
-    MN_REQUIRE(L->value_type == MN_F64, MN_ENOTSUP,
-               "mn_energy_rows: Laplacian values must be f64 (legacy GraphLaplacian)");
-    MN_REQUIRE(opts->g_mode == MN_G_TAUMODE || opts->g_mode == MN_G_ENERGYMAPS, MN_EINVAL,
-               "mn_energy_rows: unknown g_mode");
+    MN_REQUIRE(opts->g_mode == MN_G_TAUMODE || opts->g_mode == MN_G_ENERGYMAPS ||
+                   opts->g_mode == MN_G_SPECTRAL,
+               MN_EINVAL, "mn_energy_rows: unknown g_mode");
+    MN_REQUIRE(L->value_type == MN_F64 || (L->value_type == MN_F32 && opts->g_mode == MN_G_SPECTRAL),
+               MN_ENOTSUP,
+               "mn_energy_rows: Laplacian values must be f64 (legacy GraphLaplacian); f32 only "
+               "for MN_G_SPECTRAL (Stage C output)");
     MN_REQUIRE(opts->tau_mode >= MN_TAU_FIXED && opts->tau_mode <= MN_TAU_PERCENTILE, MN_EINVAL,
                "mn_energy_rows: unknown tau_mode");
     hipStream_t s = (hipStream_t)opts->stream;
     if (n == 0) return MN_OK;
     const int64_t nnz = L->nnz;
+    const bool spec = opts->g_mode == MN_G_SPECTRAL;
+    const Vals vals{L->values, L->value_type == MN_F32 ? 1 : 0};
     char *g = (char *)scratch(kSlotGeneric0, (size_t)nnz * 12 + (size_t)f * 8 +
                                                  (size_t)(2 * f + 1) * 8 + 256);
+    if (spec) {  // E and the raw row energies are needed for the global pass
+        double *sc = (double *)scratch(kSlotNorms2, (size_t)n * 16 + 8 * SUM_BLOCKS + 64);
+        MN_REQUIRE(sc, MN_ENOMEM, "mn_energy_rows: scratch allocation failed");
+        if (!E) E = sc;
+        if (!G) G = sc + n;
+    }
     MN_REQUIRE(g, MN_ENOMEM, "mn_energy_rows: scratch allocation failed");
     uint32_t *eij = (uint32_t *)g;
     int32_t *cnt = (int32_t *)(eij + nnz);
@@ -410,15 +476,15 @@ static int energy_impl(const mn_csr *L, const float *X, int64_t n, int32_t f,
     tm.start(opts->timing != 0, s);
     MN_HIP_TRY(hipMemsetAsync(flag, 0, 8, s));
     const unsigned fb = (unsigned)((f + 255) / 256);
-    hipLaunchKernelGGL(k_check_sym, dim3(fb), dim3(256), 0, s, L->indptr, L->indices,
-                       (const double *)L->values, f, flag);
+    hipLaunchKernelGGL(k_check_sym, dim3(fb), dim3(256), 0, s, L->indptr, L->indices, vals, f,
+                       flag);
     int hflag = 0;
     MN_HIP_TRY(hipMemcpyAsync(&hflag, flag, 4, hipMemcpyDeviceToHost, s));
     MN_HIP_TRY(hipStreamSynchronize(s));
     MN_REQUIRE(!(hflag & 2), MN_EINVAL, "mn_energy_rows: Laplacian column index out of range");
     const int sym = (hflag & 1) ? 0 : 1;
-    hipLaunchKernelGGL(k_count_entries, dim3(fb), dim3(256), 0, s, L->indptr, L->indices,
-                       (const double *)L->values, f, sym, opts->g_mode, cnt);
+    hipLaunchKernelGGL(k_count_entries, dim3(fb), dim3(256), 0, s, L->indptr, L->indices, vals,
+                       f, sym, opts->g_mode, cnt);
     // tiny scan on the host side of the stream (f <= 4096): list A, then B
     std::vector<int32_t> hc(2 * (size_t)f);
     std::vector<int64_t> ho(2 * (size_t)f);
@@ -431,8 +497,8 @@ static int energy_impl(const mn_csr *L, const float *X, int64_t n, int32_t f,
     }
     const int64_t na = ho[f], ne = acc;
     MN_HIP_TRY(hipMemcpyAsync(off, ho.data(), 16 * (size_t)f, hipMemcpyHostToDevice, s));
-    hipLaunchKernelGGL(k_fill_entries, dim3(fb), dim3(256), 0, s, L->indptr, L->indices,
-                       (const double *)L->values, f, sym, opts->g_mode, off, eij, ev);
+    hipLaunchKernelGGL(k_fill_entries, dim3(fb), dim3(256), 0, s, L->indptr, L->indices, vals, f,
+                       sym, opts->g_mode, off, eij, ev);
     int pct_rank = 0;
     if (opts->tau_mode == MN_TAU_PERCENTILE) {
         double pp = opts->tau_param;
@@ -443,7 +509,7 @@ static int energy_impl(const mn_csr *L, const float *X, int64_t n, int32_t f,
     // multiplicities of list A: num (2 for the upper-triangle list), dispersion
     // (taumode counts each undirected edge twice, energymaps once)
     const double mA_num = sym ? 2.0 : 1.0;
-    const double mA_g = (sym && opts->g_mode == MN_G_TAUMODE) ? 2.0 : 1.0;
+    const double mA_g = (sym && opts->g_mode != MN_G_ENERGYMAPS) ? 2.0 : 1.0;
     tm.mark();
     const int nr = (f + 63) / 64;
     const int fpad = (f + 3) & ~3;
@@ -473,6 +539,14 @@ static int energy_impl(const mn_csr *L, const float *X, int64_t n, int32_t f,
     else MN_ER(64);  // f <= 4096
 #undef MN_ER
     MN_KCHECK(s, "k_energy_rows");
+    if (spec) {
+        double *part = (double *)scratch(kSlotNorms2, (size_t)n * 16 + 8 * SUM_BLOCKS + 64) + 2 * n;
+        hipLaunchKernelGGL(k_sum_partials, dim3(SUM_BLOCKS), dim3(256), 0, s, G, n, part);
+        hipLaunchKernelGGL(k_spectral_finish,
+                           dim3((unsigned)std::min<int64_t>((n + 255) / 256, 4096)), dim3(256), 0,
+                           s, part, n, E, G, lam);
+        MN_KCHECK(s, "k_spectral_finish");
+    }
     tm.mark();
     MN_HIP_TRY(hipStreamSynchronize(s));
     t_energy_stats.entries = ne;

@@ -13,14 +13,21 @@
 //
 // MI355X design (profiles are long: n ~ 1e6, f ~ 768):
 //   1. k_transpose        X -> XT [f][n] (LDS-tiled) so every profile streams.
-//   2. k_col_norms        exact sequential f64 norms (one lane per column).
+//   2. k_col_norms        exact sequential f64 norms (one wave per column:
+//                         squares formed lane-parallel, the ordered chain of
+//                         adds reads them back from LDS as broadcasts).
 //   3. k_gram_f64         G = X^T X on MFMA v_mfma_f64_16x16x4_f64 (f32 inputs
 //                         widened: products exact), upper 64x64 block tiles,
 //                         split-K over rows, f64 atomics into G.
 //   4. k_cos_select       per node (one wave): approximate distances from G,
 //                         wave bitonic sort, top-L candidates + the (L+1)-th.
-//   5. k_cos_exact        per (node, candidate) thread: the reference's
-//                         sequential f64 dot over the full profile.
+//   5. k_cos_exact_wave   per (node, candidate) wave: the reference's
+//                         sequential f64 dot over the full profile (products
+//                         exact and lane-parallel, the chain of adds ordered).
+//                         Only candidates that can reach the top k are
+//                         evaluated: the first topk by approximate distance,
+//                         then those whose lower bound d~ - delta does not
+//                         exceed the worst of those (k_extra_pairs).
 //   6. k_cos_finish       per node: sort exact (dist, j), certify
 //                         (|d~ - d| <= 2(n+16)2^-53), filter, write; nodes
 //                         that fail go to the exact all-pairs fallback.
@@ -58,29 +65,65 @@ __global__ __launch_bounds__(256) void k_transpose(const float *__restrict__ X, 
     }
 }
 
-// ---- 2. exact sequential norms --------------------------------------------
-__global__ __launch_bounds__(64) void k_col_norms(const float *__restrict__ XT, int64_t n, int f,
-                                                  double *__restrict__ nrm) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= f) return;
-    const float *p = XT + (int64_t)i * n;
+// ---- 2. exact sequential norms / dots (one wave per ordered f64 chain) ------
+// The reference folds sum_t a_t b_t in t order (f64, products exact for f32
+// inputs).  One wave streams 256-element chunks of both profiles (float4 per
+// lane, the next chunk in flight), forms the 256 products lane-parallel into
+// LDS, and the ordered chain of adds reads them back as broadcast
+// ds_read_b128: the VALU issues little but the adds.
+constexpr int CH = 256;
+
+constexpr int PF = 4;  // chunks in flight ahead of the chain
+
+__device__ __forceinline__ double ordered_dot(const float *__restrict__ a,
+                                              const float *__restrict__ b, int64_t n,
+                                              double (*buf)[CH]) {
+    const int lane = threadIdx.x & 63;
+    const int64_t nfull = n / CH;
+    const bool vec = ((((uintptr_t)a) | ((uintptr_t)b)) & 15) == 0;
+    float4 ra[PF], rb[PF];
+    auto fetch = [&](int64_t c, float4 &pa, float4 &pb) {
+        const int64_t o = c * CH + 4 * lane;
+        if (vec) {
+            pa = *reinterpret_cast<const float4 *>(a + o);
+            pb = *reinterpret_cast<const float4 *>(b + o);
+        } else {
+            pa = make_float4(a[o], a[o + 1], a[o + 2], a[o + 3]);
+            pb = make_float4(b[o], b[o + 1], b[o + 2], b[o + 3]);
+        }
+    };
+#pragma unroll
+    for (int u = 0; u < PF; ++u)
+        if (u < nfull) fetch(u, ra[u], rb[u]);
     double acc = -0.0;
-    int64_t t = 0;
-    for (; t + 8 <= n; t += 8) {
-        float v[8];
+    for (int64_t c0 = 0; c0 < nfull; c0 += PF) {
 #pragma unroll
-        for (int u = 0; u < 8; ++u) v[u] = p[t + u];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-            const double x = (double)v[u];
-            acc = acc + x * x;
+        for (int u = 0; u < PF; ++u) {
+            const int64_t c = c0 + u;
+            if (c >= nfull) break;
+            double *bb = buf[u & 1];
+            bb[4 * lane + 0] = (double)ra[u].x * (double)rb[u].x;
+            bb[4 * lane + 1] = (double)ra[u].y * (double)rb[u].y;
+            bb[4 * lane + 2] = (double)ra[u].z * (double)rb[u].z;
+            bb[4 * lane + 3] = (double)ra[u].w * (double)rb[u].w;
+            if (c + PF < nfull) fetch(c + PF, ra[u], rb[u]);
+            __builtin_amdgcn_wave_barrier();
+            acc = lds_chain_f64<CH>(acc, bb);
+            __builtin_amdgcn_wave_barrier();
         }
     }
-    for (; t < n; ++t) {
-        const double x = (double)p[t];
-        acc = acc + x * x;
-    }
-    nrm[i] = __builtin_sqrt(acc);
+    for (int64_t t = nfull * CH; t < n; ++t) acc = acc + (double)a[t] * (double)b[t];
+    return acc;
+}
+
+__global__ __launch_bounds__(64) void k_col_norms(const float *__restrict__ XT, int64_t n, int f,
+                                                  double *__restrict__ nrm) {
+    __shared__ double buf[2][CH];
+    const int i = blockIdx.x;
+    if (i >= f) return;
+    const float *p = XT + (int64_t)i * n;
+    const double acc = ordered_dot(p, p, n, buf);
+    if (threadIdx.x == 0) nrm[i] = __builtin_sqrt(acc);
 }
 
 // ---- 3. Gram on f64 MFMA --------------------------------------------------
@@ -178,6 +221,7 @@ template <int NR>
 __global__ __launch_bounds__(256) void k_cos_select(const double *__restrict__ G,
                                                     const double *__restrict__ nrm, int f, int L,
                                                     int32_t *__restrict__ cand,
+                                                    double *__restrict__ capx,
                                                     double *__restrict__ gnext) {
     const int lane = threadIdx.x & 63;
     const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -200,7 +244,10 @@ __global__ __launch_bounds__(256) void k_cos_select(const double *__restrict__ G
     }
     const bool any_nan = __any(nan);
     wave_bitonic_sort<NR>(d, ix);
-    if (lane < L) cand[(int64_t)i * L + lane] = ix[0];
+    if (lane < L) {
+        cand[(int64_t)i * L + lane] = ix[0];
+        capx[(int64_t)i * L + lane] = any_nan ? -__builtin_inf() : d[0];
+    }
     double gn = (L < f - 1) ? wave_elem<NR>(d, L) : __builtin_inf();
     if (any_nan) gn = -__builtin_inf();  // the bound argument fails: exact path
     if (lane == 0) gnext[i] = gn;
@@ -231,6 +278,58 @@ __global__ __launch_bounds__(256) void k_cos_exact(const float *__restrict__ XT,
     }
     for (; t < n; ++t) acc = acc + (double)a[t] * (double)b[t];
     dist[q] = cos_dist(acc, nrm[i], nrm[j]);
+}
+
+// one wave per listed pair q: (node i = pi[q], candidate slot) -> dist[slot]
+__global__ __launch_bounds__(256) void k_cos_exact_wave(const float *__restrict__ XT, int64_t n,
+                                                        const int32_t *__restrict__ plist,
+                                                        const int *__restrict__ pcount,
+                                                        int64_t pmax, const int32_t *__restrict__ cand,
+                                                        int L, const double *__restrict__ nrm,
+                                                        double *__restrict__ dist) {
+    __shared__ double buf[4][2][CH];
+    const int w = threadIdx.x >> 6;
+    const int64_t q = (int64_t)blockIdx.x * 4 + w;
+    const int64_t np = pcount ? (int64_t)*pcount : pmax;
+    if (q >= np) return;
+    const int slot = plist ? plist[q] : (int)q;  // slot = i * L + r
+    const int i = slot / L, j = cand[slot];
+    if (j == INT_MAX) return;
+    const double denom = nrm[i] * nrm[j];
+    double d = 1.0;  // cos = 0 without a dot
+    if (denom > 1e-12) d = cos_dist(ordered_dot(XT + (int64_t)i * n, XT + (int64_t)j * n, n, buf[w]),
+                                    nrm[i], nrm[j]);
+    if ((threadIdx.x & 63) == 0) dist[slot] = d;
+}
+
+// slots of the first kq candidates of every node (they are always evaluated)
+__global__ void k_first_pairs(int f, int L, int kq, int32_t *__restrict__ plist) {
+    const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= (int64_t)f * kq) return;
+    plist[q] = (int32_t)((q / kq) * L + q % kq);
+}
+
+// the other candidates of node i that can still reach its top k: their lower
+// bound d~ - delta does not exceed Dp <= d~_{kq-1} + delta, the upper bound of
+// the worst exact distance among the first kq (NaN-safe: -inf approximate
+// distances flag non-finite data, everything is evaluated then)
+__global__ void k_extra_pairs(const int32_t *__restrict__ cand, const double *__restrict__ capx,
+                              int f, int L, int kq, double delta, int32_t *__restrict__ plist,
+                              int *__restrict__ pcount) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= f) return;
+    const double ak = capx[(int64_t)i * L + kq - 1];
+    const double Dp = (ak == -__builtin_inf()) ? __builtin_inf() : ak + delta;
+    for (int r = kq; r < L; ++r) {
+        const int64_t slot = (int64_t)i * L + r;
+        if (cand[slot] == INT_MAX) continue;
+        if (!(capx[slot] - delta > Dp)) plist[atomicAdd(pcount, 1)] = (int32_t)slot;
+    }
+}
+
+__global__ void k_fill_f64(double *__restrict__ p, int64_t n, double v) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) p[i] = v;
 }
 
 __global__ void k_cand_pairs(const int32_t *__restrict__ cand, int f, int L,
@@ -369,7 +468,7 @@ static int knn_cos_columns_impl(const float *X, int64_t n, int32_t f, const mn_c
 
     float *XT = (float *)scratch(kSlotGeneric0, sizeof(float) * (size_t)n * f);
     char *g = (char *)scratch(kSlotGeneric1, sizeof(double) * ((size_t)f * f + f * 2 + 64) +
-                                                (size_t)f * L * 16 + (size_t)f * 8);
+                                                (size_t)f * L * 24 + (size_t)f * 8 + 64);
     MN_REQUIRE(XT && g, MN_ENOMEM, "mn_knn_cos_columns_f32: scratch allocation failed");
     double *G = (double *)g;
     double *nrm = G + (size_t)f * f;
@@ -379,7 +478,8 @@ static int knn_cos_columns_impl(const float *X, int64_t n, int32_t f, const mn_c
     int32_t *pi = cand + (size_t)f * L;
     int32_t *pj = pi + (size_t)f * L;
     double *cdist = (double *)(((uintptr_t)(pj + (size_t)f * L) + 15) & ~(uintptr_t)15);
-    int32_t *fb_list = (int32_t *)(cdist + (size_t)f * L);
+    double *capx = cdist + (size_t)f * L;
+    int32_t *fb_list = (int32_t *)(capx + (size_t)f * L);
 
     Timer tm;
     tm.start(o->timing != 0, s);
@@ -387,21 +487,40 @@ static int knn_cos_columns_impl(const float *X, int64_t n, int32_t f, const mn_c
     MN_HIP_TRY(hipMemsetAsync(flags, 0, 64, s));
     hipLaunchKernelGGL(k_transpose, dim3(grid(n, 64), (unsigned)((f + 63) / 64)), dim3(256), 0, s,
                        X, n, f, XT);
-    hipLaunchKernelGGL(k_col_norms, dim3(grid(f, 64)), dim3(64), 0, s, XT, n, f, nrm);
+    // the exact norms (768 latency-bound chains) run on the side stream while
+    // the Gram occupies the MFMAs
+    hipStream_t side = side_stream();
+    MN_REQUIRE(side, MN_EHIP, "mn_knn_cos_columns_f32: side stream creation failed");
+    MN_HIP_TRY(stream_wait(side, s));
+    hipLaunchKernelGGL(k_col_norms, dim3((unsigned)f), dim3(64), 0, side, XT, n, f, nrm);
+    MN_KCHECK(side, "k_col_norms");
     hipLaunchKernelGGL(k_gram_f64, dim3((unsigned)(ntri * nchunk)), dim3(256), 0, s, X, n, f, ntile,
                        kchunk, nchunk, G);
     MN_HIP_TRY(hipGetLastError());
+    MN_HIP_TRY(stream_wait(s, side));
     tm.mark();
     const int nr = (f + 63) / 64;
-#define MN_SEL(NRV) hipLaunchKernelGGL(k_cos_select<NRV>, dim3(grid(f, 4)), dim3(256), 0, s, G, nrm, f, L, cand, gnext)
+#define MN_SEL(NRV) hipLaunchKernelGGL(k_cos_select<NRV>, dim3(grid(f, 4)), dim3(256), 0, s, G, nrm, f, L, cand, capx, gnext)
     if (nr <= 1) MN_SEL(1); else if (nr <= 2) MN_SEL(2); else if (nr <= 4) MN_SEL(4);
     else if (nr <= 8) MN_SEL(8); else if (nr <= 16) MN_SEL(16); else if (nr <= 32) MN_SEL(32);
     else MN_SEL(64);
 #undef MN_SEL
-    hipLaunchKernelGGL(k_cand_pairs, dim3(grid((int64_t)f * L)), dim3(256), 0, s, cand, f, L, pi, pj);
-    hipLaunchKernelGGL(k_cos_exact, dim3(grid((int64_t)f * L)), dim3(256), 0, s, XT, n, pi, pj,
-                       (int64_t)f * L, nrm, cdist);
+    // exact distances: the first kq candidates of every node, then the ones
+    // whose lower bound can still reach the top k (the rest stay +inf)
     const double delta = 2.0 * ((double)n + 16.0) * 0x1p-53 + 1e-300;
+    const int kq = std::min(o->topk, L);
+    const int fkq = f * kq;
+    hipLaunchKernelGGL(k_fill_f64, dim3(grid((int64_t)f * L)), dim3(256), 0, s, cdist,
+                       (int64_t)f * L, __builtin_inf());
+    // one pass over one list: [first kq of every node | near ties], the
+    // count of the latter appended on the device (flags[1])
+    hipLaunchKernelGGL(k_first_pairs, dim3(grid((int64_t)f * kq)), dim3(256), 0, s, f, L, kq, pi);
+    MN_HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)(flags + 1), fkq, 1, s));
+    if (L > kq)
+        hipLaunchKernelGGL(k_extra_pairs, dim3(grid(f)), dim3(256), 0, s, cand, capx, f, L, kq,
+                           delta, pi, flags + 1);
+    hipLaunchKernelGGL(k_cos_exact_wave, dim3(grid((int64_t)f * L, 4)), dim3(256), 0, s, XT, n, pi,
+                       flags + 1, (int64_t)f * L, cand, L, nrm, cdist);
     hipLaunchKernelGGL(k_cos_finish, dim3(grid(f, 4)), dim3(256), 0, s, cand, cdist, gnext, f, L,
                        o->topk, o->eps, o->sigma, o->p, delta, out_idx, out_dist, out_w, flags,
                        fb_list);

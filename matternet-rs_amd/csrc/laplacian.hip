@@ -20,8 +20,8 @@
 //                       fill (their order is fixed by step 4); the weight is
 //                       recomputed rather than staged through HBM
 //   4. row sort+dedupe  (col asc, w desc), a unique col keeps the max weight;
-//                       one wave per row (<= 256 entries, bitonic in
-//                       registers, sized 64/128/256 per row) fused with the
+//                       one wave per row (<= 512 entries, bitonic in
+//                       registers, sized 64/128/256/512 per row) fused with the
 //                       row's degree: a sequential ascending-column fold (the
 //                       reference's order on the legacy path) over the kept
 //                       entries, lane values read in order by v_readlane; one
@@ -46,7 +46,7 @@ struct Params {
     double eps, sigma, p, thr;
 };
 
-constexpr int WAVE_CAP = 256;
+constexpr int WAVE_CAP = 512;
 constexpr int BLOCK_CAP = 8192;
 constexpr int EMPTY = INT_MAX;  // sentinel column of an invalid forward slot
 
@@ -250,7 +250,8 @@ __global__ __launch_bounds__(256) void k_row_sort_wave(const int64_t *__restrict
     const int m = (int)(offs[i + 1] - o);
     if (m <= 64) row_sort_fold<1>(i, o, m, sym, col, wt, uniq, kept, deg64, deg32);
     else if (m <= 128) row_sort_fold<2>(i, o, m, sym, col, wt, uniq, kept, deg64, deg32);
-    else if (m <= WAVE_CAP) row_sort_fold<4>(i, o, m, sym, col, wt, uniq, kept, deg64, deg32);
+    else if (m <= 256) row_sort_fold<4>(i, o, m, sym, col, wt, uniq, kept, deg64, deg32);
+    else if (m <= WAVE_CAP) row_sort_fold<8>(i, o, m, sym, col, wt, uniq, kept, deg64, deg32);
     else if (lane == 0) big_list[atomicAdd(big_count, 1)] = (int32_t)i;
 }
 
@@ -383,23 +384,56 @@ __global__ void k_dense_compact(const double *__restrict__ dense, const int32_t 
     col[o + pos[c]] = (int32_t)c;
     wt[o + pos[c]] = dense[c];
 }
-// the hub row's count and degree (sequential, ascending column; rare)
-__global__ void k_hub_finish(int64_t i, int64_t o, const int64_t *__restrict__ total, int sym,
-                             const double *__restrict__ wt, int32_t *__restrict__ uniq,
-                             int32_t *__restrict__ kept, double *__restrict__ deg64,
-                             float *__restrict__ deg32) {
-    if (threadIdx.x != 0) return;
+// the hub row's count and degree: one wave, coalesced 64-entry chunks, the
+// ascending-column fold reads the lanes in order (v_readlane)
+__global__ __launch_bounds__(64) void k_hub_finish(int64_t i, int64_t o,
+                                                   const int64_t *__restrict__ total, int sym,
+                                                   const double *__restrict__ wt,
+                                                   int32_t *__restrict__ uniq,
+                                                   int32_t *__restrict__ kept,
+                                                   double *__restrict__ deg64,
+                                                   float *__restrict__ deg32) {
+    constexpr int PF = 8;  // 64-entry chunks in flight ahead of the fold
+    __shared__ double cb[2][64];
+    const int lane = threadIdx.x;
     const int u = (int)*total;
-    uniq[i] = u;
-    if (sym == MN_SYM_UNION) {
-        double s = -0.0;
-        for (int e = 0; e < u; ++e) s = s + wt[o + e];
-        deg64[i] = s;
-        kept[i] = u + 1;
-    } else {
-        float s = 0.0f;
-        for (int e = 0; e < u; ++e) s = s + (float)wt[o + e];
-        deg32[i] = s;
+    const int nch = (u + 63) / 64;
+    double ring[PF];
+#pragma unroll
+    for (int q = 0; q < PF; ++q) ring[q] = (64 * q + lane < u) ? wt[o + 64 * q + lane] : 0.0;
+    double s64 = -0.0;
+    float s32 = 0.0f;
+    for (int c0 = 0; c0 < nch; c0 += PF) {
+#pragma unroll
+        for (int q = 0; q < PF; ++q) {
+            const int c = c0 + q;
+            if (c >= nch) break;
+            const double w = ring[q];
+            const int nx = 64 * (c + PF) + lane;
+            ring[q] = nx < u ? wt[o + nx] : 0.0;
+            const int m = min(64, u - 64 * c);
+            if (sym == MN_SYM_UNION && m == 64) {  // full chunk: LDS broadcast chain
+                cb[c & 1][lane] = w;
+                __builtin_amdgcn_wave_barrier();
+                s64 = lds_chain_f64<64>(s64, cb[c & 1]);
+                __builtin_amdgcn_wave_barrier();
+            } else {
+                for (int l = 0; l < m; ++l) {
+                    const double v = readlane_f64(w, l);
+                    if (sym == MN_SYM_UNION) s64 = s64 + v;
+                    else s32 = s32 + (float)v;
+                }
+            }
+        }
+    }
+    if (lane == 0) {
+        uniq[i] = u;
+        if (sym == MN_SYM_UNION) {
+            deg64[i] = s64;
+            kept[i] = u + 1;
+        } else {
+            deg32[i] = s32;
+        }
     }
 }
 
@@ -521,7 +555,17 @@ static int laplacian_impl(const int32_t *nbr, const void *val, int32_t val_f64, 
     clear_error();
     t_lap_stats = mn_lap_stats{};
     MN_REQUIRE(opts && out, MN_EINVAL, "mn_laplacian_from_knn: NULL opts/out");
+    const mn_csr given = *out;
+    const bool caller = given.caller_owned == 1;
     *out = mn_csr{};
+    if (caller) {
+        MN_REQUIRE(given.indptr && given.indices && given.values && given.nnz >= 0, MN_EINVAL,
+                   "mn_laplacian_from_knn: caller-owned output needs indptr/indices/values");
+        const int want = opts->symmetrise == MN_SYM_UNION ? MN_F64 : MN_F32;
+        MN_REQUIRE(given.value_type == want, MN_EINVAL,
+                   "mn_laplacian_from_knn: caller-owned values must be %s",
+                   want == MN_F64 ? "f64 (UNION)" : "f32 (MAX)");
+    }
     MN_REQUIRE(n >= 1 && k >= 0 && (k == 0 || (nbr && val)), MN_EINVAL,
                "mn_laplacian_from_knn: bad shape n=%lld k=%d", (long long)n, k);
     MN_REQUIRE(n < INT_MAX, MN_EINVAL, "mn_laplacian_from_knn: n must fit int32");
@@ -593,20 +637,23 @@ static int laplacian_impl(const int32_t *nbr, const void *val, int32_t val_f64, 
         std::vector<int32_t> hubs(hf[2]);
         MN_HIP_TRY(hipMemcpyAsync(hubs.data(), huge_list, sizeof(int32_t) * hf[2],
                                   hipMemcpyDeviceToHost, s));
-        std::vector<int64_t> hoffs(n + 1);
-        MN_HIP_TRY(hipMemcpyAsync(hoffs.data(), offs, sizeof(int64_t) * (n + 1),
-                                  hipMemcpyDeviceToHost, s));
         MN_HIP_TRY(hipStreamSynchronize(s));
-        double *dense = nullptr;
-        int32_t *dflag = nullptr;
-        int64_t *dpos = nullptr, *dpart = nullptr;
-        MN_HIP_TRY(hipMalloc(&dense, sizeof(double) * n));
-        MN_HIP_TRY(hipMalloc(&dflag, sizeof(int32_t) * n));
-        MN_HIP_TRY(hipMalloc(&dpos, sizeof(int64_t) * (n + 1)));
-        MN_HIP_TRY(hipMalloc(&dpart, sizeof(int64_t) * (n / scan::SB + 2)));
+        // persistent scratch (no per-call hipMalloc/hipFree: hipFree synchronises)
+        char *hb = (char *)scratch(kSlotLists, (size_t)n * 8 + 64);
+        char *hm = (char *)scratch(kSlotListMeta, (size_t)n * 4 + (size_t)(n + 1) * 8 +
+                                                      ((size_t)n / scan::SB + 2) * 8 + 64);
+        MN_REQUIRE(hb && hm, MN_ENOMEM, "mn_laplacian_from_knn: hub scratch allocation failed");
+        double *dense = (double *)hb;
+        int32_t *dflag = (int32_t *)hm;
+        int64_t *dpos = (int64_t *)(((uintptr_t)(dflag + n) + 15) & ~(uintptr_t)15);
+        int64_t *dpart = dpos + (n + 1);
         for (int h = 0; h < hf[2]; ++h) {
-            const int64_t i = hubs[h], o = hoffs[i];
-            const int m = (int)(hoffs[i + 1] - o);
+            const int64_t i = hubs[h];
+            int64_t oo[2];
+            MN_HIP_TRY(hipMemcpyAsync(oo, offs + i, 16, hipMemcpyDeviceToHost, s));
+            MN_HIP_TRY(hipStreamSynchronize(s));
+            const int64_t o = oo[0];
+            const int m = (int)(oo[1] - o);
             hipLaunchKernelGGL(k_dense_fill, dim3(grid_for(n)), dim3(256), 0, s, dense, n);
             hipLaunchKernelGGL(k_dense_scatter, dim3(grid_for(m)), dim3(256), 0, s, col, wt, o, m,
                                dense);
@@ -617,23 +664,28 @@ static int laplacian_impl(const int32_t *nbr, const void *val, int32_t val_f64, 
             hipLaunchKernelGGL(k_hub_finish, dim3(1), dim3(64), 0, s, i, o, dpos + n, P.sym, wt,
                                uniq, kept, deg64, deg32);
         }
-        MN_HIP_TRY(hipStreamSynchronize(s));
-        (void)hipFree(dense); (void)hipFree(dflag); (void)hipFree(dpos); (void)hipFree(dpart);
+        MN_KCHECK(s, "k_hub_finish");
     }
     if (P.sym == MN_SYM_MAX)
         hipLaunchKernelGGL(k_kept_max, dim3(grid_for(n * 64)), dim3(256), 0, s, offs, col, wt,
                            uniq, n, P, deg32, kept);
-    int64_t *indptr = nullptr;
-    MN_HIP_TRY(hipMalloc(&indptr, sizeof(int64_t) * (n + 1)));
+    int64_t *indptr = caller ? given.indptr : nullptr;
+    if (!caller) MN_HIP_TRY(hipMalloc(&indptr, sizeof(int64_t) * (n + 1)));
     MN_HIP_TRY(scan::exclusive_scan(kept, n, indptr, part, s));
     int64_t nnz = 0;
     MN_HIP_TRY(hipMemcpyAsync(&nnz, indptr + n, 8, hipMemcpyDeviceToHost, s));
     MN_HIP_TRY(hipStreamSynchronize(s));
-    int32_t *ocol = nullptr;
-    void *oval = nullptr;
+    int32_t *ocol = caller ? given.indices : nullptr;
+    void *oval = caller ? given.values : nullptr;
     const size_t vsz = P.sym == MN_SYM_UNION ? 8 : 4;
-    if (hipMalloc(&ocol, sizeof(int32_t) * std::max<int64_t>(nnz, 1)) != hipSuccess ||
-        hipMalloc(&oval, vsz * std::max<int64_t>(nnz, 1)) != hipSuccess) {
+    if (caller && nnz > given.nnz) {
+        out->nnz = nnz;
+        set_error("mn_laplacian_from_knn: output capacity %lld < nnz %lld", (long long)given.nnz,
+                  (long long)nnz);
+        return MN_ECAP;
+    }
+    if (!caller && (hipMalloc(&ocol, sizeof(int32_t) * std::max<int64_t>(nnz, 1)) != hipSuccess ||
+                    hipMalloc(&oval, vsz * std::max<int64_t>(nnz, 1)) != hipSuccess)) {
         (void)hipFree(indptr); (void)hipFree(ocol);
         set_error("mn_laplacian_from_knn: output allocation (nnz=%lld) failed", (long long)nnz);
         return MN_ENOMEM;
@@ -652,6 +704,7 @@ static int laplacian_impl(const int32_t *nbr, const void *val, int32_t val_f64, 
     out->indices = ocol;
     out->values = oval;
     out->value_type = P.sym == MN_SYM_UNION ? MN_F64 : MN_F32;
+    out->caller_owned = caller ? 1 : 0;
     return MN_OK;
 }
 
@@ -667,6 +720,10 @@ int mn_laplacian_from_knn(const int32_t *nbr_idx, const void *nbr_val, int32_t v
 
 int mn_csr_free(mn_csr *m) {
     if (!m) return MN_OK;
+    if (m->caller_owned) {  // not ours to free
+        *m = mn_csr{};
+        return MN_OK;
+    }
     if (m->indptr) (void)hipFree(m->indptr);
     if (m->indices) (void)hipFree(m->indices);
     if (m->values) (void)hipFree(m->values);

@@ -173,57 +173,61 @@ __global__ __launch_bounds__(256) void k_emit(const Key *__restrict__ keys, int6
 // concurrent with the sort.
 constexpr int STD_CHUNK = 256;  // values per chunk: 64 lanes x 4
 
+constexpr int STD_PF = 4;  // chunks in flight ahead of the chain
+
 __global__ __launch_bounds__(64) void k_std_exact(const double *__restrict__ lam, int64_t n,
                                                   float *__restrict__ out) {
     __shared__ double b64[2][STD_CHUNK];
     __shared__ float b32[2][STD_CHUNK];
     const int lane = threadIdx.x;
     const int64_t nfull = n / STD_CHUNK;
-    double p[4];
-    auto fetch = [&](int64_t c) {
+    double ring[STD_PF][4];
+    auto fetch = [&](int64_t c, double (&p)[4]) {
 #pragma unroll
         for (int t = 0; t < 4; ++t) p[t] = lam[c * STD_CHUNK + 4 * lane + t];
     };
     // ---- pass 1: s = sum(lam) in index order (f64) ----
     double s = -0.0;
-    if (nfull > 0) fetch(0);
-    for (int64_t c = 0; c < nfull; ++c) {
-        double *bb = b64[c & 1];
 #pragma unroll
-        for (int t = 0; t < 4; ++t) bb[4 * lane + t] = p[t];
-        if (c + 1 < nfull) fetch(c + 1);
-        __builtin_amdgcn_wave_barrier();
-#pragma unroll 32
-        for (int e = 0; e < STD_CHUNK; e += 2) {
-            const double2 v = *reinterpret_cast<const double2 *>(bb + e);
-            s = s + v.x;
-            s = s + v.y;
+    for (int u = 0; u < STD_PF; ++u)
+        if (u < nfull) fetch(u, ring[u]);
+    for (int64_t c0 = 0; c0 < nfull; c0 += STD_PF) {
+#pragma unroll
+        for (int u = 0; u < STD_PF; ++u) {
+            const int64_t c = c0 + u;
+            if (c >= nfull) break;
+            double *bb = b64[u & 1];
+#pragma unroll
+            for (int t = 0; t < 4; ++t) bb[4 * lane + t] = ring[u][t];
+            if (c + STD_PF < nfull) fetch(c + STD_PF, ring[u]);
+            __builtin_amdgcn_wave_barrier();
+            s = lds_chain_f64<STD_CHUNK>(s, bb);
+            __builtin_amdgcn_wave_barrier();
         }
-        __builtin_amdgcn_wave_barrier();
     }
     for (int64_t i = nfull * STD_CHUNK; i < n; ++i) s = s + lam[i];
     const float mean = __fdiv_rn((float)s, (float)n);
     // ---- pass 2: var = sum((mean - (f32)lam)^2) in index order (f32) ----
     float var = -0.0f;
-    if (nfull > 0) fetch(0);
-    for (int64_t c = 0; c < nfull; ++c) {
-        float *bb = b32[c & 1];
 #pragma unroll
-        for (int t = 0; t < 4; ++t) {
-            const float dv = mean - (float)p[t];
-            bb[4 * lane + t] = dv * dv;
+    for (int u = 0; u < STD_PF; ++u)
+        if (u < nfull) fetch(u, ring[u]);
+    for (int64_t c0 = 0; c0 < nfull; c0 += STD_PF) {
+#pragma unroll
+        for (int u = 0; u < STD_PF; ++u) {
+            const int64_t c = c0 + u;
+            if (c >= nfull) break;
+            float *bb = b32[u & 1];
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                const float dv = mean - (float)ring[u][t];
+                bb[4 * lane + t] = dv * dv;
+            }
+            if (c + STD_PF < nfull) fetch(c + STD_PF, ring[u]);
+            __builtin_amdgcn_wave_barrier();
+            var = lds_chain_f32<STD_CHUNK>(var, bb);
+            __builtin_amdgcn_wave_barrier();
         }
-        if (c + 1 < nfull) fetch(c + 1);
-        __builtin_amdgcn_wave_barrier();
-#pragma unroll 16
-        for (int e = 0; e < STD_CHUNK; e += 4) {
-            const float4 v = *reinterpret_cast<const float4 *>(bb + e);
-            var = var + v.x;
-            var = var + v.y;
-            var = var + v.z;
-            var = var + v.w;
-        }
-        __builtin_amdgcn_wave_barrier();
     }
     for (int64_t i = nfull * STD_CHUNK; i < n; ++i) {
         const float dv = mean - (float)lam[i];

@@ -59,7 +59,7 @@ class LapOpts(C.Structure):
 class Csr(C.Structure):
     _fields_ = [("n_rows", C.c_int64), ("n_cols", C.c_int64), ("nnz", C.c_int64),
                 ("indptr", C.c_void_p), ("indices", C.c_void_p), ("values", C.c_void_p),
-                ("value_type", C.c_int32), ("reserved0", C.c_int32)]
+                ("value_type", C.c_int32), ("caller_owned", C.c_int32)]
 
 
 class LapStats(C.Structure):
@@ -76,7 +76,7 @@ class CosOpts(C.Structure):
                 ("reserved0", C.c_int32), ("stream", C.c_void_p)]
 
 
-MN_G_TAUMODE, MN_G_ENERGYMAPS = 0, 1
+MN_G_TAUMODE, MN_G_ENERGYMAPS, MN_G_SPECTRAL = 0, 1, 2
 MN_TAU_FIXED, MN_TAU_MEDIAN, MN_TAU_MEAN, MN_TAU_PERCENTILE = 0, 1, 2, 3
 
 

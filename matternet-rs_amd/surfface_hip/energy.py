@@ -7,7 +7,11 @@ Host-side mirror of:
       -> compute_taumode_lambdas()
   * node_energy_and_dispersion (energymaps.rs:923-1045) -> node_energy_and_dispersion()
   * ArrowSpace::normalise_lambdas                       -> normalise_lambdas()
-Values within 1e-9 relative of the reference (it sums in rayon order).
+  * Stage D compute_lambdas_gpu / compute_tau_mode_gpu
+    (surfface-core/src/spectral/mod.rs:158-181, bridge.rs:27-69)
+      -> compute_lambdas_gpu() / compute_tau_mode_gpu()
+Values within 1e-9 relative of the reference (it sums in rayon order); Stage D
+within 1e-4 (the reference computes in f32 through Burn matmuls, this in f64).
 """
 from __future__ import annotations
 
@@ -42,12 +46,17 @@ TauMode.Mean = TauMode(_lib.MN_TAU_MEAN)
 TAU_FLOOR = 1e-10
 
 
-def _csr_struct(L: CsrMatrix) -> _lib.Csr:
-    if L.values.dtype != torch.float64:
-        raise TypeError("the feature Laplacian must hold f64 values (legacy GraphLaplacian)")
+def _csr_struct(L: CsrMatrix, allow_f32: bool = False) -> _lib.Csr:
+    if L.values.dtype == torch.float32 and allow_f32:
+        vt = _lib.MN_F32
+    elif L.values.dtype == torch.float64:
+        vt = _lib.MN_F64
+    else:
+        raise TypeError("the feature Laplacian must hold f64 values (legacy GraphLaplacian); "
+                        "f32 (Stage C) only for the spectral lambdas")
     return _lib.Csr(n_rows=L.shape[0], n_cols=L.shape[1], nnz=L.nnz, indptr=ptr(L.indptr).value,
                     indices=ptr(L.indices).value, values=ptr(L.values).value,
-                    value_type=_lib.MN_F64, reserved0=0)
+                    value_type=vt, caller_owned=1)
 
 
 def last_stats() -> dict:
@@ -66,7 +75,7 @@ def energy_rows(X: torch.Tensor, L: CsrMatrix, g_mode: int = _lib.MN_G_TAUMODE,
     lam = torch.empty(n, dtype=torch.float64, device=X.device)
     o = _lib.EnergyOpts(g_mode=g_mode, tau_mode=taumode.kind, tau_param=taumode.param,
                         timing=1 if timing else 0, reserved0=0, stream=stream_handle(stream))
-    csr = _csr_struct(L)
+    csr = _csr_struct(L, allow_f32=(g_mode == _lib.MN_G_SPECTRAL))
     _lib.check(_lib.lib().mn_energy_rows(C.byref(csr), ptr(X), n, f, C.byref(o), ptr(E), ptr(G),
                                          ptr(lam)))
     return E, G, lam
@@ -95,3 +104,22 @@ def node_energy_and_dispersion(X: torch.Tensor, L: CsrMatrix):
     """(lambda = Rayleigh E, G over j > i) per row (energymaps.rs:923-1045)."""
     E, G, _ = energy_rows(X, L, _lib.MN_G_ENERGYMAPS)
     return E, G
+
+
+def compute_lambdas_gpu(L: CsrMatrix, X: torch.Tensor):
+    """Stage D device lambdas (spectral/mod.rs:158-181): per item the clamped
+    Rayleigh quotient plus the globally normalised Dirichlet dispersion.
+    Returns (lambda, rayleigh, dirichlet) as f64 device tensors."""
+    R, D, lam = energy_rows(X, L, _lib.MN_G_SPECTRAL)
+    return lam, R, D
+
+
+def compute_tau_mode_gpu(laplacian, data: torch.Tensor, n_items: int = None,
+                         n_features: int = None):
+    """bridge.rs:27-69: Stage C output (LaplacianOutput or CsrMatrix, f32
+    values) + the N x F item matrix -> f64 lambdas (no normalisation, as in
+    the reference)."""
+    L = getattr(laplacian, "matrix", laplacian)
+    X = data if data.dim() == 2 else data.view(n_items, n_features)
+    lam, _, _ = compute_lambdas_gpu(L, X)
+    return lam

@@ -116,13 +116,24 @@ def build_laplacian_from_knn(nbr_idx: torch.Tensor, nbr_val: torch.Tensor, *,
     o = _lib.LapOpts(weight_kernel=wk, symmetrise=sy, normalize=1 if normalize else 0,
                      reserved0=0, eps=eps, sigma=sigma, p=p, weight_threshold=weight_threshold,
                      stream=stream_handle(stream))
-    deg = torch.empty(n, dtype=torch.float64 if sy == _lib.MN_SYM_UNION else torch.float32,
-                      device=nbr_idx.device)
-    csr = _lib.Csr()
+    vdt = torch.float64 if sy == _lib.MN_SYM_UNION else torch.float32
+    dev = nbr_idx.device
+    deg = torch.empty(n, dtype=vdt, device=dev)
+    # the library writes straight into torch-owned buffers sized for the
+    # worst case (every row: k forward + k reverse entries + the diagonal)
+    cap = n * (2 * k + 1)
+    indptr = torch.empty(n + 1, dtype=torch.int64, device=dev)
+    indices = torch.empty(max(cap, 1), dtype=torch.int32, device=dev)
+    values = torch.empty(max(cap, 1), dtype=vdt, device=dev)
+    csr = _lib.Csr(n_rows=n, n_cols=n, nnz=cap, indptr=ptr(indptr).value,
+                   indices=ptr(indices).value, values=ptr(values).value,
+                   value_type=_lib.MN_F64 if sy == _lib.MN_SYM_UNION else _lib.MN_F32,
+                   caller_owned=1)
     _lib.check(_lib.lib().mn_laplacian_from_knn(
         ptr(nbr_idx), ptr(nbr_val), 1 if nbr_val.dtype == torch.float64 else 0, n, k,
         C.byref(o), C.byref(csr), ptr(deg)))
-    return _adopt(csr, nbr_idx.device), deg
+    nnz = csr.nnz
+    return CsrMatrix(indptr, indices[:nnz], values[:nnz], (n, n)), deg
 
 
 def laplacian_stage_from_edges(nbr_idx: torch.Tensor, weights: torch.Tensor,

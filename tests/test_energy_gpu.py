@@ -155,3 +155,29 @@ def test_entry_list_beyond_lds_and_wide_rows():
     np.testing.assert_allclose(G, rG, rtol=RTOL, atol=ATOL)
     np.testing.assert_allclose(lam, rl, rtol=RTOL, atol=ATOL)
     assert S.energy.last_stats()["entries"] * 12 > 96 * 1024
+
+
+def test_stage_d_spectral_lambdas_vs_oracle():
+    """compute_tau_mode_gpu (spectral/bridge.rs:27-69) on a Stage C Laplacian
+    (MAX, L_sym, f32 values) and on a legacy f64 Laplacian.  The reference
+    computes in f32 through Burn matmuls; this path in f64: tolerance 1e-4."""
+    import surfface_hip as S
+    P = datagen.uniform(400, 300, seed=31).T.copy()  # 300 feature nodes, profile 400
+    idx, dist = O.knn_l2sq(P, 10)
+    w = (1.0 / (1.0 + dist)).astype(np.float32)
+    out = S.laplacian_stage_from_edges(torch.from_numpy(idx).cuda(), torch.from_numpy(w).cuda(),
+                                       S.LaplacianConfig(k_neighbors=10))
+    ip, ix, iv = out.matrix.to_numpy()
+    X = datagen.uniform(5001, 300, seed=32)
+    X[7] = 0.0  # zero row: R = 0 / (0 + 1e-9) = 0
+    lam = S.compute_tau_mode_gpu(out, torch.from_numpy(X).cuda()).cpu().numpy()
+    ref = O.spectral_lambdas(X, ip, ix, iv.astype(np.float32))
+    np.testing.assert_allclose(lam, ref, rtol=1e-4, atol=1e-7)
+    lam2, R, D = S.compute_lambdas_gpu(out.matrix, torch.from_numpy(X).cuda())
+    D = D.cpu().numpy()
+    assert (D >= 0).all() and (D <= 1).all() and abs(D.sum() - 1.0) < 1e-9
+    # legacy f64 feature Laplacian (unnormalised D - W)
+    lip, lix, liv = feature_laplacian(f=300, profile=500, topk=5, seed=33)
+    lam3, _, _ = S.compute_lambdas_gpu(csr_dev(lip, lix, liv), torch.from_numpy(X).cuda())
+    ref3 = O.spectral_lambdas(X, lip, lix, liv.astype(np.float32))
+    np.testing.assert_allclose(lam3.cpu().numpy(), ref3, rtol=1e-4, atol=1e-7)

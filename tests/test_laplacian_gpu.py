@@ -112,3 +112,40 @@ def test_laplacian_stage_output_properties():
     assert out.nnz <= 800 * (2 * 15 + 1)
     # null space L D^{1/2} 1 = 0 (surfface-core tests/test_laplacian.rs invariant)
     assert np.abs(L @ np.sqrt(out.degrees.cpu().numpy().astype(np.float64))).max() < 1e-4
+
+
+def test_library_owned_output_and_capacity_error():
+    """The C ABI's two output modes: library-allocated CSR (mn_csr_free) and
+    caller-owned buffers; a too-small caller capacity is MN_ECAP with nnz =
+    the entries needed."""
+    import ctypes as C
+    import surfface_hip as S
+    from surfface_hip import _lib
+    from surfface_hip._torch import ptr
+    X = datagen.uniform(3000, 16, seed=2)
+    idx, dist = O.knn_l2sq(X, 8)
+    ref = S.build_laplacian_from_knn(torch.from_numpy(idx).cuda(), torch.from_numpy(dist).cuda(),
+                                     eps=1e30, sigma=2.0)[0].to_numpy()
+    L = _lib.lib()
+    di, dd = torch.from_numpy(idx).cuda(), torch.from_numpy(dist).cuda()
+    o = _lib.LapOpts(weight_kernel=_lib.MN_W_RATIONAL, symmetrise=_lib.MN_SYM_UNION, normalize=0,
+                     reserved0=0, eps=1e30, sigma=2.0, p=2.0, weight_threshold=1e-9, stream=None)
+    csr = _lib.Csr()
+    _lib.check(L.mn_laplacian_from_knn(ptr(di), ptr(dd), 0, 3000, 8, C.byref(o), C.byref(csr),
+                                       None))
+    assert csr.caller_owned == 0 and csr.nnz == len(ref[1])
+    ip = torch.empty(3001, dtype=torch.int64, device="cuda")
+    ix = torch.empty(csr.nnz, dtype=torch.int32, device="cuda")
+    iv = torch.empty(csr.nnz, dtype=torch.float64, device="cuda")
+    for dst, src, nb in ((ip, csr.indptr, 8 * 3001), (ix, csr.indices, 4 * csr.nnz),
+                         (iv, csr.values, 8 * csr.nnz)):
+        _lib.check(L.mn_memcpy_d2d(ptr(dst), src, nb, None))
+    _lib.check(L.mn_csr_free(C.byref(csr)))
+    np.testing.assert_array_equal(ip.cpu().numpy(), ref[0])
+    np.testing.assert_array_equal(ix.cpu().numpy(), ref[1])
+    np.testing.assert_array_equal(iv.cpu().numpy().view(np.uint64), ref[2].view(np.uint64))
+    small = _lib.Csr(n_rows=3000, n_cols=3000, nnz=100, indptr=ptr(ip).value,
+                     indices=ptr(ix).value, values=ptr(iv).value, value_type=_lib.MN_F64,
+                     caller_owned=1)
+    rc = L.mn_laplacian_from_knn(ptr(di), ptr(dd), 0, 3000, 8, C.byref(o), C.byref(small), None)
+    assert rc == -4 and small.nnz == len(ref[1])
