@@ -116,14 +116,69 @@ __device__ __forceinline__ double ordered_dot(const float *__restrict__ a,
     return acc;
 }
 
+// Four ordered chains per wave (lanes 16g..16g+15 run chain g): each group
+// loads its 256-element chunk of both profiles (16 per lane, next chunk in
+// flight), forms the products lane-parallel into its LDS buffer, and folds it
+// with group-broadcast LDS reads — one VALU add serves four chains, so the
+// redundant-lane issue cost of a single-chain wave is cut by four.
+constexpr int CHP = CH + 2;  // buffer stride (16 B pad: the 4 groups hit different banks)
+
+__device__ __forceinline__ double ordered_dot4(const float *__restrict__ a,
+                                               const float *__restrict__ b, int64_t n,
+                                               double (*buf)[4][CHP]) {
+    const int lane = threadIdx.x & 63, g = lane >> 4, gl = lane & 15;
+    const int64_t nfull = n / CH;
+    const bool vec = ((((uintptr_t)a) | ((uintptr_t)b)) & 15) == 0;
+    float4 ra[2][4], rb[2][4];
+    auto fetch = [&](int64_t c, float4 (&pa)[4], float4 (&pb)[4]) {
+        const int64_t o = c * CH + 16 * gl;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            if (vec) {
+                pa[u] = *reinterpret_cast<const float4 *>(a + o + 4 * u);
+                pb[u] = *reinterpret_cast<const float4 *>(b + o + 4 * u);
+            } else {
+                const float *x = a + o + 4 * u, *y = b + o + 4 * u;
+                pa[u] = make_float4(x[0], x[1], x[2], x[3]);
+                pb[u] = make_float4(y[0], y[1], y[2], y[3]);
+            }
+        }
+    };
+    if (nfull > 0) fetch(0, ra[0], rb[0]);
+    if (nfull > 1) fetch(1, ra[1], rb[1]);
+    double acc = -0.0;
+    for (int64_t c0 = 0; c0 < nfull; c0 += 2) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int64_t c = c0 + h;
+            if (c >= nfull) break;
+            double *bb = buf[h][g];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                bb[16 * gl + 4 * u + 0] = (double)ra[h][u].x * (double)rb[h][u].x;
+                bb[16 * gl + 4 * u + 1] = (double)ra[h][u].y * (double)rb[h][u].y;
+                bb[16 * gl + 4 * u + 2] = (double)ra[h][u].z * (double)rb[h][u].z;
+                bb[16 * gl + 4 * u + 3] = (double)ra[h][u].w * (double)rb[h][u].w;
+            }
+            if (c + 2 < nfull) fetch(c + 2, ra[h], rb[h]);
+            __builtin_amdgcn_wave_barrier();
+            acc = lds_chain_f64<CH>(acc, bb);
+            __builtin_amdgcn_wave_barrier();
+        }
+    }
+    for (int64_t t = nfull * CH; t < n; ++t) acc = acc + (double)a[t] * (double)b[t];
+    return acc;
+}
+
+// four columns per wave
 __global__ __launch_bounds__(64) void k_col_norms(const float *__restrict__ XT, int64_t n, int f,
                                                   double *__restrict__ nrm) {
-    __shared__ double buf[2][CH];
-    const int i = blockIdx.x;
-    if (i >= f) return;
-    const float *p = XT + (int64_t)i * n;
-    const double acc = ordered_dot(p, p, n, buf);
-    if (threadIdx.x == 0) nrm[i] = __builtin_sqrt(acc);
+    __shared__ double buf[2][4][CHP];
+    const int g = threadIdx.x >> 4;
+    const int i = blockIdx.x * 4 + g;
+    const float *p = XT + (int64_t)min(i, f - 1) * n;
+    const double acc = ordered_dot4(p, p, n, buf);
+    if ((threadIdx.x & 15) == 0 && i < f) nrm[i] = __builtin_sqrt(acc);
 }
 
 // ---- 3. Gram on f64 MFMA --------------------------------------------------
@@ -281,25 +336,35 @@ __global__ __launch_bounds__(256) void k_cos_exact(const float *__restrict__ XT,
 }
 
 // one wave per listed pair q: (node i = pi[q], candidate slot) -> dist[slot]
+// four listed pairs per wave, pair q = (node i, candidate slot) -> dist[slot]
 __global__ __launch_bounds__(256) void k_cos_exact_wave(const float *__restrict__ XT, int64_t n,
                                                         const int32_t *__restrict__ plist,
                                                         const int *__restrict__ pcount,
                                                         int64_t pmax, const int32_t *__restrict__ cand,
                                                         int L, const double *__restrict__ nrm,
                                                         double *__restrict__ dist) {
-    __shared__ double buf[4][2][CH];
-    const int w = threadIdx.x >> 6;
-    const int64_t q = (int64_t)blockIdx.x * 4 + w;
+    __shared__ double buf[4][2][4][CHP];
+    const int w = threadIdx.x >> 6, g = (threadIdx.x & 63) >> 4;
     const int64_t np = pcount ? (int64_t)*pcount : pmax;
-    if (q >= np) return;
-    const int slot = plist ? plist[q] : (int)q;  // slot = i * L + r
-    const int i = slot / L, j = cand[slot];
-    if (j == INT_MAX) return;
-    const double denom = nrm[i] * nrm[j];
-    double d = 1.0;  // cos = 0 without a dot
-    if (denom > 1e-12) d = cos_dist(ordered_dot(XT + (int64_t)i * n, XT + (int64_t)j * n, n, buf[w]),
-                                    nrm[i], nrm[j]);
-    if ((threadIdx.x & 63) == 0) dist[slot] = d;
+    const int64_t wq = ((int64_t)blockIdx.x * 4 + w) * 4;
+    if (wq >= np) return;  // wave-uniform
+    const int64_t q = wq + g;
+    int slot = -1, i = 0, j = 0;
+    bool act = false;
+    double denom = 0.0;
+    if (q < np) {
+        slot = plist ? plist[q] : (int)q;  // slot = i * L + r
+        i = slot / L;
+        j = cand[slot];
+        if (j != INT_MAX) {
+            denom = nrm[i] * nrm[j];
+            act = true;
+        }
+    }
+    const bool dot = act && denom > 1e-12;  // else cos = 0 without a dot
+    const float *pa = XT + (int64_t)(dot ? i : 0) * n, *pb = XT + (int64_t)(dot ? j : 0) * n;
+    const double acc = ordered_dot4(pa, pb, n, buf[w]);
+    if ((threadIdx.x & 15) == 0 && act) dist[slot] = dot ? cos_dist(acc, nrm[i], nrm[j]) : 1.0;
 }
 
 // slots of the first kq candidates of every node (they are always evaluated)
@@ -492,7 +557,7 @@ static int knn_cos_columns_impl(const float *X, int64_t n, int32_t f, const mn_c
     hipStream_t side = side_stream();
     MN_REQUIRE(side, MN_EHIP, "mn_knn_cos_columns_f32: side stream creation failed");
     MN_HIP_TRY(stream_wait(side, s));
-    hipLaunchKernelGGL(k_col_norms, dim3((unsigned)f), dim3(64), 0, side, XT, n, f, nrm);
+    hipLaunchKernelGGL(k_col_norms, dim3((unsigned)((f + 3) / 4)), dim3(64), 0, side, XT, n, f, nrm);
     MN_KCHECK(side, "k_col_norms");
     hipLaunchKernelGGL(k_gram_f64, dim3((unsigned)(ntri * nchunk)), dim3(256), 0, s, X, n, f, ntile,
                        kchunk, nchunk, G);
@@ -519,7 +584,7 @@ static int knn_cos_columns_impl(const float *X, int64_t n, int32_t f, const mn_c
     if (L > kq)
         hipLaunchKernelGGL(k_extra_pairs, dim3(grid(f)), dim3(256), 0, s, cand, capx, f, L, kq,
                            delta, pi, flags + 1);
-    hipLaunchKernelGGL(k_cos_exact_wave, dim3(grid((int64_t)f * L, 4)), dim3(256), 0, s, XT, n, pi,
+    hipLaunchKernelGGL(k_cos_exact_wave, dim3(grid((int64_t)f * L, 16)), dim3(256), 0, s, XT, n, pi,
                        flags + 1, (int64_t)f * L, cand, L, nrm, cdist);
     hipLaunchKernelGGL(k_cos_finish, dim3(grid(f, 4)), dim3(256), 0, s, cand, cdist, gnext, f, L,
                        o->topk, o->eps, o->sigma, o->p, delta, out_idx, out_dist, out_w, flags,
