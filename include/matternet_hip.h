@@ -255,6 +255,34 @@ int mn_sorted_index(const double *lambda, int64_t n, int64_t *order_out, double 
                     double *std_out_host, void *stream);
 
 
+/* Lambda-aware lookups on a built index (keys / order = mn_sorted_index
+ * outputs, device, n items), batched over nq query lambdas (device).  Per
+ * query t: out_idx [t][k] item indices (int64, -1 padded), out_lambda [t][k]
+ * their bucket keys (f64), out_count [t] = entries written, or -1 where the
+ * reference panics (BTreeMap::range with start > end; partial_cmp().unwrap()
+ * on NaN distances).  Bit-exact. */
+
+/* SortedLambdas::range_bylambda (src_legacy/sorted_index.rs:64-80): band =
+ * std_dev / 2^p; the items whose key lies in [lq - band, lq + band]
+ * (OrderedFloat order) in index order, the first k. */
+int mn_sorted_range_bylambda(const double *keys, const int64_t *order, int64_t n,
+                             double std_dev, const double *lambda_q, int64_t nq, int32_t k,
+                             double p, int64_t *out_idx, double *out_lambda, int32_t *out_count,
+                             void *stream);
+
+/* SortedLambdas::k_nearest_by_lambda (src_legacy/sorted_index.rs:85-140):
+ * window [max(lq - delta, 0), min(lq + delta, 1)] from delta = |base_delta|
+ * (has_base_delta) or max(std_dev * lambda_p, 1e-9), grown by `growth` (> 1
+ * and finite, else 1.7) up to min(delta * max(max_multiplier, 1), 1) until it
+ * holds k items; then the k smallest |lambda - lq|.  The reference sorts
+ * unstably (tie order unspecified): ties here keep index order. */
+int mn_sorted_k_nearest_by_lambda(const double *keys, const int64_t *order, int64_t n,
+                                  double std_dev, const double *lambda_q, int64_t nq, int32_t k,
+                                  double lambda_p, int32_t has_base_delta, double base_delta,
+                                  double growth, double max_multiplier, int64_t *out_idx,
+                                  double *out_lambda, int32_t *out_count, void *stream);
+
+
 /* ---------------------------------------------------------------------- */
 /* K5 — sparsification of directed neighbour rows                         */
 /* ---------------------------------------------------------------------- */

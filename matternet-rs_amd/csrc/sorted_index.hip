@@ -19,6 +19,7 @@
 //   Bit-exact order given identical lambdas.
 #include <algorithm>
 #include <climits>
+#include <cmath>
 
 #include "common.hpp"
 #include "scan.hpp"
@@ -236,6 +237,127 @@ __global__ __launch_bounds__(64) void k_std_exact(const double *__restrict__ lam
     if (lane == 0) *out = sqrt_rn_f32(__fdiv_rn(var, (float)n));
 }
 
+// ---- lambda-aware lookups (sorted_index.rs:64-140) ---------------------------
+// keys[] is non-decreasing in OrderedFloat order; searches run on of_key().
+__device__ __forceinline__ int64_t lower_rank(const double *keys, int64_t n, unsigned long long kv) {
+    int64_t lo = 0, hi = n;  // first rank with key >= kv
+    while (lo < hi) {
+        const int64_t mid = (lo + hi) >> 1;
+        if (of_key(keys[mid]) < kv) lo = mid + 1; else hi = mid;
+    }
+    return lo;
+}
+__device__ __forceinline__ int64_t upper_rank(const double *keys, int64_t n, unsigned long long kv) {
+    int64_t lo = 0, hi = n;  // first rank with key > kv
+    while (lo < hi) {
+        const int64_t mid = (lo + hi) >> 1;
+        if (of_key(keys[mid]) <= kv) lo = mid + 1; else hi = mid;
+    }
+    return lo;
+}
+
+__global__ __launch_bounds__(256) void k_range_bylambda(const double *__restrict__ keys,
+                                                        const int64_t *__restrict__ order,
+                                                        int64_t n, double band,
+                                                        const double *__restrict__ lq, int64_t nq,
+                                                        int k, int64_t *__restrict__ oi,
+                                                        double *__restrict__ ol,
+                                                        int32_t *__restrict__ oc) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= nq) return;
+    const double q = lq[t];
+    const unsigned long long klo = of_key(q - band), khi = of_key(q + band);
+    int cnt = 0;
+    if (klo > khi) {
+        cnt = -1;  // BTreeMap::range panics: start > end
+    } else {
+        const int64_t r0 = lower_rank(keys, n, klo), r1 = upper_rank(keys, n, khi);
+        cnt = (int)min<int64_t>(k, max<int64_t>(0, r1 - r0));
+        for (int e = 0; e < cnt; ++e) {
+            oi[t * k + e] = order[r0 + e];
+            ol[t * k + e] = keys[r0 + e];
+        }
+    }
+    for (int e = max(cnt, 0); e < k; ++e) {
+        oi[t * k + e] = -1;
+        ol[t * k + e] = __builtin_nan("");
+    }
+    oc[t] = cnt;
+}
+
+__global__ __launch_bounds__(256) void k_nearest_bylambda(
+    const double *__restrict__ keys, const int64_t *__restrict__ order, int64_t n, double delta0,
+    double growth, double max_delta, const double *__restrict__ lq, int64_t nq, int k,
+    int64_t *__restrict__ oi, double *__restrict__ ol, int32_t *__restrict__ oc) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= nq) return;
+    const double q = lq[t];
+    double delta = delta0;
+    int64_t r0 = 0, r1 = 0;
+    int cnt = 0;
+    for (;;) {  // sorted_index.rs:110-126 (f64::max / f64::min ignore NaN, like fmax / fmin)
+        const double lo = fmax(q - delta, 0.0), hi = fmin(q + delta, 1.0);
+        const unsigned long long klo = of_key(lo), khi = of_key(hi);
+        if (klo > khi) { cnt = -1; break; }  // BTreeMap::range panics
+        r0 = lower_rank(keys, n, klo);
+        r1 = upper_rank(keys, n, khi);
+        if (r1 - r0 >= k || delta >= max_delta) break;
+        delta = fmin(delta * growth, max_delta);
+    }
+    if (cnt == 0 && r1 > r0) {
+        const int64_t m = r1 - r0;
+        if (q != q && m >= 2) {
+            cnt = -1;  // |lambda - NaN| is NaN: partial_cmp().unwrap() panics
+        } else {
+            // k smallest |key - q| with ties in rank order: the distance is
+            // non-increasing toward q from the left and non-decreasing from the
+            // right, so merge outward from q's position, run by run
+            auto dist = [&](int64_t r) { return fabs(keys[r] - q); };
+            int64_t L = lower_rank(keys, n, of_key(q));
+            L = min(max(L, r0), r1) - 1;  // left pointer (descending)
+            int64_t R = L + 1;           // right pointer (ascending)
+            while (cnt < k && (L >= r0 || R < r1)) {
+                const double dl = L >= r0 ? dist(L) : __builtin_inf();
+                const double dr = R < r1 ? dist(R) : __builtin_inf();
+                const bool take_left = L >= r0 && (R >= r1 || dl <= dr);
+                const double d = take_left ? dl : dr;
+                if (take_left) {
+                    // left run: ranks [Ls, L] with distance d (first rank <= L
+                    // whose distance is <= d, by bisection)
+                    int64_t a = r0, b = L;
+                    while (a < b) {
+                        const int64_t mid = (a + b) >> 1;
+                        if (dist(mid) <= d) b = mid; else a = mid + 1;
+                    }
+                    for (int64_t r = a; r <= L && cnt < k; ++r, ++cnt) {
+                        oi[t * k + cnt] = order[r];
+                        ol[t * k + cnt] = keys[r];
+                    }
+                    L = a - 1;
+                }
+                if (R < r1 && (!take_left || dr == d)) {
+                    // right run: ranks [R, Re] with distance d
+                    int64_t a = R, b = r1 - 1;
+                    while (a < b) {
+                        const int64_t mid = (a + b + 1) >> 1;
+                        if (dist(mid) <= d) a = mid; else b = mid - 1;
+                    }
+                    for (int64_t r = R; r <= a && cnt < k; ++r, ++cnt) {
+                        oi[t * k + cnt] = order[r];
+                        ol[t * k + cnt] = keys[r];
+                    }
+                    R = a + 1;
+                }
+            }
+        }
+    }
+    for (int e = max(cnt, 0); e < k; ++e) {
+        oi[t * k + e] = -1;
+        ol[t * k + e] = __builtin_nan("");
+    }
+    oc[t] = cnt;
+}
+
 inline unsigned grid(int64_t n, int t = 256) {
     return (unsigned)std::max<int64_t>(1, (n + t - 1) / t);
 }
@@ -307,4 +429,53 @@ static int sorted_index_impl(const double *lam, int64_t n, int64_t *order, doubl
 extern "C" int mn_sorted_index(const double *lambda, int64_t n, int64_t *order_out,
                                double *key_out, double *std_out_host, void *stream) {
     return mn::sorted_index_impl(lambda, n, order_out, key_out, std_out_host, stream);
+}
+
+extern "C" int mn_sorted_range_bylambda(const double *keys, const int64_t *order, int64_t n,
+                                        double std_dev, const double *lambda_q, int64_t nq,
+                                        int32_t k, double p, int64_t *out_idx, double *out_lambda,
+                                        int32_t *out_count, void *stream) {
+    using namespace mn::sidx;
+    mn::clear_error();
+    MN_REQUIRE(n >= 0 && nq >= 0 && k >= 0, MN_EINVAL, "mn_sorted_range_bylambda: bad sizes");
+    MN_REQUIRE(nq == 0 || (lambda_q && out_idx && out_lambda && out_count && (n == 0 || (keys && order))),
+               MN_EINVAL, "mn_sorted_range_bylambda: NULL pointer");
+    if (nq == 0) return MN_OK;
+    hipStream_t s = (hipStream_t)stream;
+    const double band = std_dev / pow(2.0, p);  // sorted_index.rs:65
+    hipLaunchKernelGGL(k_range_bylambda, dim3(grid(nq)), dim3(256), 0, s, keys, order, n, band,
+                       lambda_q, nq, k, out_idx, out_lambda, out_count);
+    MN_HIP_TRY(hipGetLastError());
+    MN_HIP_TRY(hipStreamSynchronize(s));
+    return MN_OK;
+}
+
+extern "C" int mn_sorted_k_nearest_by_lambda(const double *keys, const int64_t *order, int64_t n,
+                                             double std_dev, const double *lambda_q, int64_t nq,
+                                             int32_t k, double lambda_p, int32_t has_base_delta,
+                                             double base_delta, double growth,
+                                             double max_multiplier, int64_t *out_idx,
+                                             double *out_lambda, int32_t *out_count,
+                                             void *stream) {
+    using namespace mn::sidx;
+    mn::clear_error();
+    MN_REQUIRE(n >= 0 && nq >= 0 && k >= 0, MN_EINVAL, "mn_sorted_k_nearest_by_lambda: bad sizes");
+    MN_REQUIRE(nq == 0 || (lambda_q && out_idx && out_lambda && out_count && (n == 0 || (keys && order))),
+               MN_EINVAL, "mn_sorted_k_nearest_by_lambda: NULL pointer");
+    if (nq == 0) return MN_OK;
+    hipStream_t s = (hipStream_t)stream;
+    if (k == 0 || n == 0) {  // sorted_index.rs:94-96: empty result
+        MN_HIP_TRY(hipMemsetAsync(out_count, 0, sizeof(int32_t) * (size_t)nq, s));
+        MN_HIP_TRY(hipStreamSynchronize(s));
+        return MN_OK;
+    }
+    // sorted_index.rs:97-106 (f64::max / min: fmax / fmin; abs after unwrap)
+    const double delta0 = fabs(has_base_delta ? base_delta : fmax(std_dev * lambda_p, 1e-9));
+    const double g = (std::isfinite(growth) && growth > 1.0) ? growth : 1.7;
+    const double max_delta = fmin(delta0 * fmax(max_multiplier, 1.0), 1.0);
+    hipLaunchKernelGGL(k_nearest_bylambda, dim3(grid(nq)), dim3(256), 0, s, keys, order, n, delta0,
+                       g, max_delta, lambda_q, nq, k, out_idx, out_lambda, out_count);
+    MN_HIP_TRY(hipGetLastError());
+    MN_HIP_TRY(hipStreamSynchronize(s));
+    return MN_OK;
 }

@@ -119,6 +119,11 @@ SIGNATURES = {
     "mn_normalise_lambdas": (C.c_int, [P, I64, P, P]),
     "mn_energy_last_stats": (C.c_int, [C.POINTER(EnergyStats)]),
     "mn_sorted_index": (C.c_int, [P, I64, P, P, P, P]),
+    "mn_sorted_range_bylambda": (C.c_int, [P, P, I64, C.c_double, P, I64, C.c_int32, C.c_double,
+                                           P, P, P, P]),
+    "mn_sorted_k_nearest_by_lambda": (C.c_int, [P, P, I64, C.c_double, P, I64, C.c_int32,
+                                                C.c_double, C.c_int32, C.c_double, C.c_double,
+                                                C.c_double, P, P, P, P]),
     "mn_sparsify_rows": (C.c_int, [P, P, I64, I32, C.c_double, I32, P, P, P, P]),
     "mn_knn_cos_columns_f32": (C.c_int, [P, I64, I32, C.POINTER(CosOpts), P, P, P]),
     "mn_cos_last_stats": (C.c_int, [C.POINTER(KnnStats)]),

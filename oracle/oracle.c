@@ -784,6 +784,71 @@ int or_sorted_index(const double *lam, int64_t n, int64_t *order_out,
     return 0;
 }
 
+/* sorted_index.rs:64-80: BTreeMap::range(OrderedFloat(lo)..=OrderedFloat(hi)) */
+int64_t or_range_bylambda(const double *keys, const int64_t *order, int64_t n, double std_dev,
+                          double lq, int64_t k, double p, int64_t *out_idx, double *out_key) {
+    double band = std_dev / pow(2.0, p);
+    double lo = lq - band, hi = lq + band;
+    if (cmp_ordered_float(lo, hi) > 0) return -1; /* range start > end: panic */
+    int64_t cnt = 0;
+    for (int64_t r = 0; r < n && cnt < k; ++r)
+        if (cmp_ordered_float(keys[r], lo) >= 0 && cmp_ordered_float(keys[r], hi) <= 0) {
+            out_idx[cnt] = order[r];
+            out_key[cnt] = keys[r];
+            ++cnt;
+        }
+    return cnt;
+}
+
+typedef struct { double d; int64_t rank; } nkey;
+static int cmp_nkey(const void *pa, const void *pb) {
+    const nkey *a = (const nkey *)pa, *b = (const nkey *)pb;
+    if (a->d < b->d) return -1;
+    if (a->d > b->d) return 1;
+    return a->rank < b->rank ? -1 : (a->rank > b->rank ? 1 : 0);
+}
+
+/* sorted_index.rs:85-140 */
+int64_t or_k_nearest_by_lambda(const double *keys, const int64_t *order, int64_t n,
+                               double std_dev, double lq, int64_t k, double lambda_p,
+                               int has_base_delta, double base_delta, double growth,
+                               double max_multiplier, int64_t *out_idx, double *out_key) {
+    if (k == 0 || n == 0) return 0;
+    double delta = fabs(has_base_delta ? base_delta : fmax(std_dev * lambda_p, 1e-9));
+    if (!(isfinite(growth) && growth > 1.0)) growth = 1.7;
+    double max_delta = fmin(delta * fmax(max_multiplier, 1.0), 1.0);
+    int64_t r0 = 0, r1 = 0;
+    for (;;) {
+        double lo = fmax(lq - delta, 0.0), hi = fmin(lq + delta, 1.0); /* f64::max / min */
+        if (cmp_ordered_float(lo, hi) > 0) return -1;
+        r0 = n; r1 = 0;
+        int64_t c = 0;
+        for (int64_t r = 0; r < n; ++r)
+            if (cmp_ordered_float(keys[r], lo) >= 0 && cmp_ordered_float(keys[r], hi) <= 0) {
+                if (c == 0) r0 = r;
+                r1 = r + 1;
+                ++c;
+            }
+        if (c == 0) r0 = r1 = 0;
+        if (c >= k || delta >= max_delta) break;
+        delta = fmin(delta * growth, max_delta);
+    }
+    int64_t m = r1 - r0;
+    if (m <= 0) return 0;
+    if (lq != lq && m >= 2) return -1; /* NaN distances: partial_cmp().unwrap() panics */
+    nkey *c = (nkey *)malloc(sizeof(nkey) * (size_t)m);
+    if (!c) return -2;
+    for (int64_t r = r0; r < r1; ++r) { c[r - r0].d = fabs(keys[r] - lq); c[r - r0].rank = r; }
+    qsort(c, (size_t)m, sizeof(nkey), cmp_nkey);
+    int64_t cnt = m < k ? m : k;
+    for (int64_t e = 0; e < cnt; ++e) {
+        out_idx[e] = order[c[e].rank];
+        out_key[e] = keys[c[e].rank];
+    }
+    free(c);
+    return cnt;
+}
+
 /* ------------------------------------------------------------------------ */
 /* K5 — SF-GRASS                                                             */
 /* ------------------------------------------------------------------------ */

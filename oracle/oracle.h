@@ -161,6 +161,21 @@ int or_spectral_lambdas_f32(const float *X, int64_t n, int32_t f,
 int or_sorted_index(const double *lam, int64_t n, int64_t *order_out,
                     double *key_out, double *std_out);
 
+/* src_legacy/sorted_index.rs:64-80 range_bylambda and :85-140
+ * k_nearest_by_lambda over a built index (keys/order as or_sorted_index
+ * returns them: the BTreeMap flattened in key order), one query lambda.
+ * Writes up to k (idx, key) pairs, returns the count, or -1 where the
+ * reference panics (range start > end; NaN distance compare).
+ * k_nearest: candidates = every item in the final window, sorted stably by
+ * |key - lq| (the reference's sort_unstable leaves tie order unspecified;
+ * the contract is index order), truncated to k. */
+int64_t or_range_bylambda(const double *keys, const int64_t *order, int64_t n, double std_dev,
+                          double lq, int64_t k, double p, int64_t *out_idx, double *out_key);
+int64_t or_k_nearest_by_lambda(const double *keys, const int64_t *order, int64_t n,
+                               double std_dev, double lq, int64_t k, double lambda_p,
+                               int has_base_delta, double base_delta, double growth,
+                               double max_multiplier, int64_t *out_idx, double *out_key);
+
 /* ---- K5: SF-GRASS ------------------------------------------------------- */
 
 /* src_legacy/sparsification.rs:32-113: avg = sum len / n; avg < 10 => copy;

@@ -58,6 +58,11 @@ def _declare(L):
     L.or_normalise_lambdas.argtypes = [P, I64, P, P, P]
     L.or_spectral_lambdas_f32.argtypes = [P, I64, I32, P, P, P, P]
     L.or_sorted_index.argtypes = [P, I64, P, P, P]
+    L.or_range_bylambda.argtypes = [P, P, I64, C.c_double, C.c_double, I64, C.c_double, P, P]
+    L.or_range_bylambda.restype = I64
+    L.or_k_nearest_by_lambda.argtypes = [P, P, I64, C.c_double, C.c_double, I64, C.c_double,
+                                         C.c_int, C.c_double, C.c_double, C.c_double, P, P]
+    L.or_k_nearest_by_lambda.restype = I64
     L.or_sfgrass.argtypes = [I64, P, P, P, D, P, P, P]
 
 
@@ -201,6 +206,29 @@ def sorted_index(lam):
     std = np.zeros(1)
     _check(lib().or_sorted_index(_p(lam), n, _p(order), _p(keys), _p(std)), "sorted_index")
     return order, keys, float(std[0])
+
+
+def range_bylambda(keys, order, std_dev, lq, k, p):
+    """sorted_index.rs:64-80 for one query; None where the reference panics."""
+    oi, ok = np.empty(max(k, 1), np.int64), np.empty(max(k, 1), np.float64)
+    c = lib().or_range_bylambda(_p(np.ascontiguousarray(keys, np.float64)),
+                                _p(np.ascontiguousarray(order, np.int64)), len(keys), std_dev,
+                                lq, k, p, _p(oi), _p(ok))
+    return None if c < 0 else (oi[:c], ok[:c])
+
+
+def k_nearest_by_lambda(keys, order, std_dev, lq, k, lambda_p, base_delta=None, growth=1.7,
+                        max_multiplier=10.0):
+    """sorted_index.rs:85-140 for one query; None where the reference panics."""
+    oi, ok = np.empty(max(k, 1), np.int64), np.empty(max(k, 1), np.float64)
+    c = lib().or_k_nearest_by_lambda(_p(np.ascontiguousarray(keys, np.float64)),
+                                     _p(np.ascontiguousarray(order, np.int64)), len(keys),
+                                     std_dev, lq, k, lambda_p, 0 if base_delta is None else 1,
+                                     0.0 if base_delta is None else base_delta, growth,
+                                     max_multiplier, _p(oi), _p(ok))
+    if c == -2:
+        raise MemoryError("or_k_nearest_by_lambda")
+    return None if c < 0 else (oi[:c], ok[:c])
 
 
 def sfgrass(indptr, indices, w, ratio=0.5):

@@ -254,3 +254,27 @@ def test_knn_cos_bf16_rows_matches_widened_f32():
     part = O.knn_cos_bf16_rows(bits, 7, rows, eps=0.9, sigma=0.5)
     for a, b in zip(full, part):
         np.testing.assert_array_equal(a[rows].view(np.uint8), b.view(np.uint8))
+
+
+def test_lambda_lookups_known_answers():
+    """sorted_index.rs:64-140 on a hand-checked 6-item index (binary-exact
+    lambdas): keys in OrderedFloat order with string-id ties; range band =
+    std / 2^p (std = 0.2357 here); k_nearest grows its window x1.7 from
+    base_delta and ranks by |lambda - lq| (ties: index order)."""
+    lam = np.array([0.5, 0.125, 0.5, 0.875, 0.25, 0.5])
+    order, keys, std = O.sorted_index(lam)
+    assert order.tolist() == [1, 4, 0, 2, 5, 3] and abs(std - 0.23570226) < 1e-7
+    idx, key = O.range_bylambda(keys, order, std, 0.5, 3, 0.0)      # [0.264, 0.736]
+    assert idx.tolist() == [0, 2, 5] and key.tolist() == [0.5, 0.5, 0.5]
+    idx, _ = O.range_bylambda(keys, order, std, 0.5, 3, -1.0)       # [0.029, 0.971]
+    assert idx.tolist() == [1, 4, 0]
+    r = O.range_bylambda(keys, order, std, float("nan"), 3, 0.0)   # lo = hi = NaN bucket
+    assert r is not None and len(r[0]) == 0
+    # windows around 0.3: 0.05 -> 0.085 -> 0.1445 -> 0.24565 holds 5 >= 3 items
+    idx, key = O.k_nearest_by_lambda(keys, order, std, 0.3, 3, 1.0, base_delta=0.05)
+    assert idx.tolist() == [4, 1, 0] and key.tolist() == [0.25, 0.125, 0.5]
+    # 0.25 and 0.5 are both exactly 0.125 from 0.375: index (rank) order
+    idx, _ = O.k_nearest_by_lambda(keys, order, std, 0.375, 2, 1.0, base_delta=0.2)
+    assert idx.tolist() == [4, 0]
+    # window lo > hi (lq far above 1): the reference panics in BTreeMap::range
+    assert O.k_nearest_by_lambda(keys, order, std, 5.0, 2, 1.0, base_delta=0.1) is None

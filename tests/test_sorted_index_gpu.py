@@ -51,3 +51,47 @@ def test_random_unique_and_special_values():
     lam[9::7000] = np.inf
     lam[11::7000] = -np.inf
     check(lam)
+
+
+def _lookup_case(lam, queries, k, p, lambda_p, base_delta, growth=1.7, mult=10.0):
+    import surfface_hip as S
+    sl = S.SortedLambdas().build_from(torch.from_numpy(np.ascontiguousarray(lam)).cuda())
+    ro, rk, rsd = O.sorted_index(lam)
+    q = torch.from_numpy(np.ascontiguousarray(queries, np.float64)).cuda()
+    for kind in ("range", "nearest"):
+        if kind == "range":
+            oi, ol, oc = sl.range_bylambda(q, k, p)
+        else:
+            oi, ol, oc = sl.k_nearest_by_lambda(q, k, lambda_p, base_delta, growth, mult)
+        oi, ol, oc = oi.cpu().numpy(), ol.cpu().numpy(), oc.cpu().numpy()
+        for t, lq in enumerate(queries):
+            ref = (O.range_bylambda(rk, ro, rsd, lq, k, p) if kind == "range" else
+                   O.k_nearest_by_lambda(rk, ro, rsd, lq, k, lambda_p, base_delta, growth, mult))
+            if ref is None:
+                assert oc[t] == -1, (kind, t, lq)
+                continue
+            c = len(ref[0])
+            assert oc[t] == c, (kind, t, lq, oc[t], c)
+            np.testing.assert_array_equal(oi[t, :c], ref[0])
+            np.testing.assert_array_equal(ol[t, :c].view(np.uint64), ref[1].view(np.uint64))
+
+
+def test_lambda_lookups_vs_oracle_massive_ties():
+    """range_bylambda / k_nearest_by_lambda (sorted_index.rs:64-140) batched on
+    the GPU: 200k items in 9 lambda buckets (ties in string-id order)."""
+    rng = np.random.default_rng(4)
+    lam = rng.integers(0, 9, size=200_000).astype(np.float64) / 8.0
+    qs = np.concatenate([rng.uniform(-0.1, 1.1, 60), [0.0, 0.5, 1.0, 0.0625, np.nan, 3.0, -2.0]])
+    _lookup_case(lam, qs, 25, 1.0, 0.5, None)
+    _lookup_case(lam, qs, 7, 3.0, 0.01, 0.001, growth=2.0, mult=50.0)
+
+
+def test_lambda_lookups_vs_oracle_unique_and_edges():
+    rng = np.random.default_rng(6)
+    lam = rng.uniform(0.0, 1.0, 50_001)
+    lam[::97] = 0.25  # equal distances on both sides of 0.3 / 0.2 queries
+    lam[1::97] = 0.35
+    qs = np.concatenate([rng.uniform(0, 1, 80), [0.3, 0.2, 0.25, 1.5, -0.5, np.nan]])
+    _lookup_case(lam, qs, 40, 2.0, 0.001, None)
+    _lookup_case(lam, qs, 1, 0.0, 1.0, 0.0)     # base_delta 0: one window
+    _lookup_case(lam[:1], qs[:10], 3, 1.0, 0.5, None)  # a single item
