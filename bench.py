@@ -255,6 +255,12 @@ def c3_legs(S, X, idx, dist, k):
     out["energy_rows"] = {"ms": round(ms, 3), "GB_per_s": round(ebytes / ms / 1e6, 1),
                           "entries_per_row": S.energy.last_stats()["entries"]}
     out["energy_rows_per_sec"] = n / (ms * 1e-3)
+    # energymaps diffusion pre-pass (eta 0.1, 4 steps; energymaps.rs:518-546) on
+    # the same rows: f32 in, f64 out; bytes = N F (4 + 8)
+    Xd = torch.empty((n, f), dtype=torch.float64, device=X.device)
+    ms, _ = _timed(lambda: S.diffuse_rows(X, Lf, 0.1, 4, out=Xd))
+    out["diffusion_4_steps"] = {"ms": round(ms, 3), "GB_per_s": round(n * f * 12 / ms / 1e6, 1)}
+    del Xd
     lam_n = lam.clone()
     ms, _ = _timed(lambda: S.normalise_lambdas(lam_n.copy_(lam)))
     out["normalise_ms"] = round(ms, 3)

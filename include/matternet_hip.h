@@ -239,6 +239,18 @@ int mn_normalise_lambdas(double *lambda, int64_t n, double *out_min_max_range_ho
                          void *stream);
 int mn_energy_last_stats(mn_energy_stats *out);
 
+/* EnergyMaps diffusion pre-pass (src_legacy/energymaps.rs:518-546): `steps`
+ * times every row x (length f) becomes x - eta * (L x), where (L x)_i is the
+ * CSR row fold sum += L[i,p] * x[col[p]] from +0.0 in stored order
+ * (GraphLaplacian::multiply_vector, src_legacy/graph.rs:464-501).  X [n][f]
+ * f32 or f64 (x_is_f64, device), X_out [n][f] f64 (device; may alias X when
+ * it is f64), L the f x f f64 CSR.  Bit-exact (f64, no contraction). */
+int mn_diffuse_rows(const mn_csr *L, const void *X, int32_t x_is_f64, int64_t n, int32_t f,
+                    double eta, int32_t steps, double *X_out, void *stream);
+/* Y = L x per row (GraphLaplacian::multiply_vector), same conventions. */
+int mn_laplacian_matvec_rows(const mn_csr *L, const void *X, int32_t x_is_f64, int64_t n,
+                             int32_t f, double *Y, void *stream);
+
 
 /* ---------------------------------------------------------------------- */
 /* K4 — lambda-sorted index                                               */

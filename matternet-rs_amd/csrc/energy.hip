@@ -428,6 +428,60 @@ __global__ __launch_bounds__(256) void k_normalise(double *__restrict__ lam, int
     if (i == 0 && out3) { out3[0] = mnv; out3[1] = mxv; out3[2] = range; }
 }
 
+// ---- diffusion pre-pass / Laplacian matvec (energymaps.rs:518-546,
+//      GraphLaplacian::multiply_vector graph.rs:464-501) ----------------------
+// Per row x (f64): steps times x <- x - eta * (L x), (L x)_i = the CSR row
+// fold sum += L[i,p] * x[col[p]] from +0.0 in stored order (no FMA), or, in
+// matvec mode, y = L x once.  One wave per row, the row double-buffered in
+// LDS; L (CSR) in LDS when it fits.  Lane-parallel over features i: every
+// fold is its own sequential chain, so the result is bit-exact.
+template <bool XF64>
+__global__ __launch_bounds__(512) void k_diffuse_rows(
+    const void *__restrict__ Xin, int64_t n, int f, const int64_t *__restrict__ gip,
+    const int32_t *__restrict__ gix, const double *__restrict__ gv, int64_t nnz, int l_in_lds,
+    double eta, int steps, int matvec, double *__restrict__ Xout) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char dsm[];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    // LDS: [val f64 x nnz | col i32 x nnz | ptr i32 x (f+1)] | x [waves][2][f] f64
+    double *lv = (double *)dsm;
+    int32_t *lc = (int32_t *)(dsm + (size_t)nnz * 8);
+    int32_t *lp = lc + nnz;
+    const size_t lb = l_in_lds ? ((((size_t)nnz * 12 + (size_t)(f + 1) * 4) + 15) & ~(size_t)15) : 0;
+    double *xb = (double *)(dsm + lb) + (size_t)w * 2 * f;
+    if (l_in_lds) {
+        for (int64_t p = threadIdx.x; p < nnz; p += blockDim.x) {
+            lv[p] = gv[p];
+            lc[p] = gix[p];
+        }
+        for (int i = threadIdx.x; i <= f; i += blockDim.x) lp[i] = (int32_t)gip[i];
+    }
+    __syncthreads();
+    for (int64_t row = (int64_t)blockIdx.x * nw + w; row < n; row += (int64_t)gridDim.x * nw) {
+        double *x = xb, *y = xb + f;
+        for (int i = lane; i < f; i += 64)
+            x[i] = XF64 ? ((const double *)Xin)[row * f + i]
+                        : (double)((const float *)Xin)[row * f + i];
+        __builtin_amdgcn_wave_barrier();
+        const int ns = matvec ? 1 : steps;
+        for (int st = 0; st < ns; ++st) {
+            for (int i = lane; i < f; i += 64) {
+                const int64_t p0 = l_in_lds ? lp[i] : gip[i], p1 = l_in_lds ? lp[i + 1] : gip[i + 1];
+                double sum = 0.0;
+                for (int64_t p = p0; p < p1; ++p) {
+                    const double v = l_in_lds ? lv[p] : gv[p];
+                    const int c = l_in_lds ? lc[p] : gix[p];
+                    sum = sum + v * x[c];
+                }
+                y[i] = matvec ? sum : x[i] - eta * sum;
+            }
+            __builtin_amdgcn_wave_barrier();
+            double *t = x; x = y; y = t;
+        }
+        for (int i = lane; i < f; i += 64) Xout[row * f + i] = x[i];
+        __builtin_amdgcn_wave_barrier();
+    }
+}
+
 }  // namespace energy
 
 static thread_local mn_energy_stats t_energy_stats{};
@@ -556,9 +610,58 @@ static int energy_impl(const mn_csr *L, const float *X, int64_t n, int32_t f,
     return MN_OK;
 }
 
+static int diffuse_impl(const mn_csr *L, const void *X, int32_t x_is_f64, int64_t n, int32_t f,
+                        double eta, int32_t steps, int matvec, double *out, void *stream) {
+    using namespace energy;
+    clear_error();
+    MN_REQUIRE(L && X && out, MN_EINVAL, "mn_diffuse_rows: NULL argument");
+    MN_REQUIRE(n >= 0 && f >= 1 && steps >= 0, MN_EINVAL, "mn_diffuse_rows: bad sizes");
+    MN_REQUIRE(L->n_rows == f && L->n_cols == f && L->value_type == MN_F64, MN_EINVAL,
+               "mn_diffuse_rows: L must be the f x f f64 GraphLaplacian CSR");
+    MN_REQUIRE(x_is_f64 || (const void *)out != X, MN_EINVAL,
+               "mn_diffuse_rows: an f32 input cannot alias the f64 output");
+    hipStream_t s = (hipStream_t)stream;
+    if (n == 0) return MN_OK;
+    const int64_t nnz = L->nnz;
+    const size_t lbytes = ((size_t)nnz * 12 + (size_t)(f + 1) * 4 + 15) & ~(size_t)15;
+    const size_t per_wave = (size_t)2 * f * 8;
+    const int l_in_lds = lbytes + per_wave <= LDS_BUDGET ? 1 : 0;
+    const size_t avail = LDS_BUDGET - (l_in_lds ? lbytes : 0);
+    const int nw = (int)std::min<size_t>(8, avail / per_wave);
+    MN_REQUIRE(nw >= 1, MN_ENOTSUP, "mn_diffuse_rows: f=%d too large for the LDS plan", f);
+    const size_t shmem = (l_in_lds ? lbytes : 0) + (size_t)nw * per_wave;
+    const int64_t blocks = std::min<int64_t>((n + nw - 1) / nw, 2048);
+    if (x_is_f64) {
+        MN_HIP_TRY(hipFuncSetAttribute((const void *)k_diffuse_rows<true>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)shmem));
+        hipLaunchKernelGGL(k_diffuse_rows<true>, dim3((unsigned)blocks), dim3(64 * nw), shmem, s,
+                           X, n, f, L->indptr, L->indices, (const double *)L->values, nnz, l_in_lds,
+                           eta, steps, matvec, out);
+    } else {
+        MN_HIP_TRY(hipFuncSetAttribute((const void *)k_diffuse_rows<false>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)shmem));
+        hipLaunchKernelGGL(k_diffuse_rows<false>, dim3((unsigned)blocks), dim3(64 * nw), shmem, s,
+                           X, n, f, L->indptr, L->indices, (const double *)L->values, nnz, l_in_lds,
+                           eta, steps, matvec, out);
+    }
+    MN_KCHECK(s, "k_diffuse_rows");
+    MN_HIP_TRY(hipStreamSynchronize(s));
+    return MN_OK;
+}
+
 }  // namespace mn
 
 extern "C" {
+
+int mn_diffuse_rows(const mn_csr *L, const void *X, int32_t x_is_f64, int64_t n, int32_t f,
+                    double eta, int32_t steps, double *X_out, void *stream) {
+    return mn::diffuse_impl(L, X, x_is_f64, n, f, eta, steps, 0, X_out, stream);
+}
+
+int mn_laplacian_matvec_rows(const mn_csr *L, const void *X, int32_t x_is_f64, int64_t n,
+                             int32_t f, double *Y, void *stream) {
+    return mn::diffuse_impl(L, X, x_is_f64, n, f, 0.0, 1, 1, Y, stream);
+}
 
 int mn_energy_rows(const mn_csr *L, const float *X, int64_t n, int32_t f,
                    const mn_energy_opts *opts, double *E, double *G, double *lambda) {

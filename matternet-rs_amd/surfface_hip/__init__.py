@@ -9,7 +9,8 @@ from . import energy, laplacian, sorted_index, sparsification
 from .sparsification import SfGrassSparsifier, sparsify_rows
 from .sorted_index import SortedLambdas
 from .energy import (TauMode, compute_lambdas_gpu, compute_tau_mode_gpu, compute_taumode_lambdas,
-                     energy_rows, node_energy_and_dispersion,
+                     diffuse_rows, energy_rows, laplacian_matvec_rows,
+                     node_energy_and_dispersion,
                      normalise_lambdas)
 from .laplacian import (CsrMatrix, GraphParams, LaplacianConfig, LaplacianOutput,
                         build_laplacian_from_knn, laplacian_stage_from_edges)
@@ -22,6 +23,7 @@ __all__ = ["MnError", "lib", "knn_cos_columns", "knn_cos_bf16", "knn_cos_bf16_qc
            "LaplacianConfig", "LaplacianOutput", "build_laplacian_from_knn",
            "laplacian_stage_from_edges", "laplacian", "energy", "TauMode",
            "compute_taumode_lambdas", "energy_rows", "node_energy_and_dispersion",
-           "compute_lambdas_gpu", "compute_tau_mode_gpu",
+           "compute_lambdas_gpu", "compute_tau_mode_gpu", "diffuse_rows",
+           "laplacian_matvec_rows",
            "normalise_lambdas", "sorted_index", "SortedLambdas", "sparsification",
            "SfGrassSparsifier", "sparsify_rows"]

@@ -116,6 +116,8 @@ SIGNATURES = {
     "mn_csr_free": (C.c_int, [C.POINTER(Csr)]),
     "mn_lap_last_stats": (C.c_int, [C.POINTER(LapStats)]),
     "mn_energy_rows": (C.c_int, [C.POINTER(Csr), P, I64, I32, C.POINTER(EnergyOpts), P, P, P]),
+    "mn_diffuse_rows": (C.c_int, [C.POINTER(Csr), P, I32, I64, I32, C.c_double, I32, P, P]),
+    "mn_laplacian_matvec_rows": (C.c_int, [C.POINTER(Csr), P, I32, I64, I32, P, P]),
     "mn_normalise_lambdas": (C.c_int, [P, I64, P, P]),
     "mn_energy_last_stats": (C.c_int, [C.POINTER(EnergyStats)]),
     "mn_sorted_index": (C.c_int, [P, I64, P, P, P, P]),

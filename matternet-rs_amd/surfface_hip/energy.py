@@ -7,6 +7,9 @@ Host-side mirror of:
       -> compute_taumode_lambdas()
   * node_energy_and_dispersion (energymaps.rs:923-1045) -> node_energy_and_dispersion()
   * ArrowSpace::normalise_lambdas                       -> normalise_lambdas()
+  * EnergyMaps diffusion pre-pass (energymaps.rs:518-546)   -> diffuse_rows()
+  * GraphLaplacian::multiply_vector (graph.rs:464-501)       -> laplacian_matvec_rows()
+    (both bit-exact: f64 CSR row folds in stored order)
   * Stage D compute_lambdas_gpu / compute_tau_mode_gpu
     (surfface-core/src/spectral/mod.rs:158-181, bridge.rs:27-69)
       -> compute_lambdas_gpu() / compute_tau_mode_gpu()
@@ -123,3 +126,34 @@ def compute_tau_mode_gpu(laplacian, data: torch.Tensor, n_items: int = None,
     X = data if data.dim() == 2 else data.view(n_items, n_features)
     lam, _, _ = compute_lambdas_gpu(L, X)
     return lam
+
+
+def _rows_in(X: torch.Tensor):
+    if X.dtype not in (torch.float32, torch.float64):
+        raise TypeError("X must be float32 or float64")
+    X = require_cuda(X, X.dtype, "X", 2)
+    return X, 1 if X.dtype == torch.float64 else 0
+
+
+def diffuse_rows(X: torch.Tensor, L: CsrMatrix, eta: float = 0.1, steps: int = 4,
+                 out: torch.Tensor = None, stream=None) -> torch.Tensor:
+    """`steps` x [x <- x - eta * L x] per row (EnergyParams defaults eta 0.1,
+    steps 4, energymaps.rs:59-60); f64 result."""
+    X, xf64 = _rows_in(X)
+    n, f = X.shape
+    out = torch.empty((n, f), dtype=torch.float64, device=X.device) if out is None else out
+    csr = _csr_struct(L)
+    _lib.check(_lib.lib().mn_diffuse_rows(C.byref(csr), ptr(X), xf64, n, f, eta, steps, ptr(out),
+                                          stream_handle(stream)))
+    return out
+
+
+def laplacian_matvec_rows(X: torch.Tensor, L: CsrMatrix, stream=None) -> torch.Tensor:
+    """Y = L x per row (GraphLaplacian::multiply_vector); f64 result."""
+    X, xf64 = _rows_in(X)
+    n, f = X.shape
+    Y = torch.empty((n, f), dtype=torch.float64, device=X.device)
+    csr = _csr_struct(L)
+    _lib.check(_lib.lib().mn_laplacian_matvec_rows(C.byref(csr), ptr(X), xf64, n, f, ptr(Y),
+                                                   stream_handle(stream)))
+    return Y

@@ -849,6 +849,41 @@ int64_t or_k_nearest_by_lambda(const double *keys, const int64_t *order, int64_t
     return cnt;
 }
 
+int or_diffuse_rows(const double *X, int64_t n, int32_t f, const int64_t *indptr,
+                    const int32_t *indices, const double *values, double eta, int32_t steps,
+                    int matvec, double *out) {
+    if (!X || !out || n < 0 || f < 1 || steps < 0) return OR_EINVAL;
+    int err = 0;
+#pragma omp parallel
+    {
+        double *x = (double *)malloc(sizeof(double) * (size_t)f);
+        double *lx = (double *)malloc(sizeof(double) * (size_t)f);
+        if (!x || !lx) {
+#pragma omp atomic write
+            err = OR_ENOMEM;
+        }
+#pragma omp for schedule(static)
+        for (int64_t r = 0; r < n; ++r) {
+            if (!x || !lx) continue;
+            memcpy(x, X + r * (int64_t)f, sizeof(double) * (size_t)f);
+            int ns = matvec ? 1 : steps;
+            for (int st = 0; st < ns; ++st) {
+                for (int32_t i = 0; i < f; ++i) { /* multiply_vector */
+                    double sum = 0.0;
+                    for (int64_t p = indptr[i]; p < indptr[i + 1]; ++p)
+                        sum += values[p] * x[indices[p]];
+                    lx[i] = sum;
+                }
+                for (int32_t i = 0; i < f; ++i) x[i] = matvec ? lx[i] : x[i] - eta * lx[i];
+            }
+            memcpy(out + r * (int64_t)f, x, sizeof(double) * (size_t)f);
+        }
+        free(x);
+        free(lx);
+    }
+    return err;
+}
+
 /* ------------------------------------------------------------------------ */
 /* K5 — SF-GRASS                                                             */
 /* ------------------------------------------------------------------------ */

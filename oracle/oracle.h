@@ -176,6 +176,13 @@ int64_t or_k_nearest_by_lambda(const double *keys, const int64_t *order, int64_t
                                int has_base_delta, double base_delta, double growth,
                                double max_multiplier, int64_t *out_idx, double *out_key);
 
+/* src_legacy/energymaps.rs:518-546 (diffusion: steps x [x <- x - eta L x])
+ * and graph.rs:464-501 (multiply_vector: y = L x, CSR row fold from +0.0 in
+ * stored order), per row of X [n][f] (f64).  matvec != 0: out = L x. */
+int or_diffuse_rows(const double *X, int64_t n, int32_t f, const int64_t *indptr,
+                    const int32_t *indices, const double *values, double eta, int32_t steps,
+                    int matvec, double *out);
+
 /* ---- K5: SF-GRASS ------------------------------------------------------- */
 
 /* src_legacy/sparsification.rs:32-113: avg = sum len / n; avg < 10 => copy;

@@ -58,6 +58,7 @@ def _declare(L):
     L.or_normalise_lambdas.argtypes = [P, I64, P, P, P]
     L.or_spectral_lambdas_f32.argtypes = [P, I64, I32, P, P, P, P]
     L.or_sorted_index.argtypes = [P, I64, P, P, P]
+    L.or_diffuse_rows.argtypes = [P, I64, I32, P, P, P, C.c_double, I32, C.c_int, P]
     L.or_range_bylambda.argtypes = [P, P, I64, C.c_double, C.c_double, I64, C.c_double, P, P]
     L.or_range_bylambda.restype = I64
     L.or_k_nearest_by_lambda.argtypes = [P, P, I64, C.c_double, C.c_double, I64, C.c_double,
@@ -206,6 +207,18 @@ def sorted_index(lam):
     std = np.zeros(1)
     _check(lib().or_sorted_index(_p(lam), n, _p(order), _p(keys), _p(std)), "sorted_index")
     return order, keys, float(std[0])
+
+
+def diffuse_rows(X, indptr, indices, values, eta=0.1, steps=4, matvec=False):
+    """energymaps.rs:518-546 diffusion (or graph.rs:464-501 L x) per row, f64."""
+    X = np.ascontiguousarray(X, dtype=np.float64)
+    n, f = X.shape
+    out = np.empty_like(X)
+    _check(lib().or_diffuse_rows(_p(X), n, f, _p(np.ascontiguousarray(indptr, np.int64)),
+                                 _p(np.ascontiguousarray(indices, np.int32)),
+                                 _p(np.ascontiguousarray(values, np.float64)), eta, steps,
+                                 1 if matvec else 0, _p(out)), "diffuse")
+    return out
 
 
 def range_bylambda(keys, order, std_dev, lq, k, p):

@@ -181,3 +181,30 @@ def test_stage_d_spectral_lambdas_vs_oracle():
     lam3, _, _ = S.compute_lambdas_gpu(csr_dev(lip, lix, liv), torch.from_numpy(X).cuda())
     ref3 = O.spectral_lambdas(X, lip, lix, liv.astype(np.float32))
     np.testing.assert_allclose(lam3.cpu().numpy(), ref3, rtol=1e-4, atol=1e-7)
+
+
+@pytest.mark.parametrize("x64", [False, True])
+def test_diffusion_and_matvec_bit_exact(x64):
+    """EnergyMaps diffusion (energymaps.rs:518-546, eta 0.1 x 4 steps) and
+    GraphLaplacian::multiply_vector (graph.rs:464-501): f64 CSR row folds in
+    stored order — bit-exact vs the oracle, f32 or f64 rows, odd sizes."""
+    import surfface_hip as S
+    ip, ix, iv = feature_laplacian(f=301, profile=700, topk=6, seed=41)
+    X = datagen.clustered(1003, 301, seed=42, blobs=5)
+    Xd = torch.from_numpy(X).cuda()
+    if x64:
+        Xd = Xd.double()
+    L = csr_dev(ip, ix, iv)
+    out = S.diffuse_rows(Xd, L, 0.1, 4).cpu().numpy()
+    ref = O.diffuse_rows(X.astype(np.float64), ip, ix, iv, 0.1, 4)
+    np.testing.assert_array_equal(out.view(np.uint64), ref.view(np.uint64))
+    Y = S.laplacian_matvec_rows(Xd, L).cpu().numpy()
+    refY = O.diffuse_rows(X.astype(np.float64), ip, ix, iv, matvec=True)
+    np.testing.assert_array_equal(Y.view(np.uint64), refY.view(np.uint64))
+    # the reference's row sums: L 1 = 0 for the unnormalised union Laplacian
+    ones = S.laplacian_matvec_rows(torch.ones((2, 301), dtype=torch.float64, device="cuda"), L)
+    assert float(ones.abs().max()) < 1e-12
+    # in place (f64 input aliasing the output)
+    if x64:
+        S.diffuse_rows(Xd, L, 0.1, 4, out=Xd)
+        np.testing.assert_array_equal(Xd.cpu().numpy().view(np.uint64), ref.view(np.uint64))
