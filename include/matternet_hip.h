@@ -121,6 +121,22 @@ int mn_knn_merge_f32(const int32_t *part_idx, const float *part_dist,
 int mn_knn_last_stats(mn_knn_stats *out);
 
 
+/* Stage C feature kNN by Bhattacharyya coefficient: replaces
+ * LaplacianStage::compute_bhattacharyya_weights (surfface-core/src/
+ * laplacian.rs:254-298) with bhattacharyya_coefficient (distance.rs:260-290).
+ * Nodes = the f feature columns of means / vars [c][f] (f32, device; the
+ * CentroidState [C, F] tensors).  Per node the k' = min(k, f-1) largest
+ * BC > weight_thr over j != i, ordered (BC desc, j asc; the reference's
+ * sort_unstable leaves ties unspecified): out_idx [f][k] (int32, -1 pad),
+ * out_w [f][k] (f32, 0 pad) — the directed edges the Stage C Laplacian
+ * (mn_laplacian_from_knn, MN_SYM_MAX) symmetrises.  f32 arithmetic and fold
+ * order as the reference; ln / exp are the device's (<= 2 ulp): weights within
+ * 1e-5 relative, neighbour sets equal up to near-ties.  2 <= f <= 4096,
+ * k >= 1.  MN_ENONFINITE on NaN coefficients (the reference panics). */
+int mn_bc_knn_f32(const float *means, const float *vars, int64_t c, int32_t f, int32_t k,
+                  float var_reg, float weight_thr, int32_t *out_idx, float *out_w, void *stream);
+
+
 /* ---------------------------------------------------------------------- */
 /* K2 — Laplacian assembly from kNN rows (CSR)                            */
 /* ---------------------------------------------------------------------- */

@@ -12,8 +12,9 @@ from .energy import (TauMode, compute_lambdas_gpu, compute_tau_mode_gpu, compute
                      diffuse_rows, energy_rows, laplacian_matvec_rows,
                      node_energy_and_dispersion,
                      normalise_lambdas)
-from .laplacian import (CsrMatrix, GraphParams, LaplacianConfig, LaplacianOutput,
-                        build_laplacian_from_knn, laplacian_stage_from_edges)
+from .laplacian import (CsrMatrix, GraphParams, LaplacianConfig, LaplacianOutput, LaplacianStage,
+                        build_laplacian_from_knn, compute_bhattacharyya_weights,
+                        laplacian_stage_from_edges)
 from .knn import (DistanceMetric, KnnResult, bf16_last_stats, build_candidate_graph, knn_cos_bf16,
                   knn_cos_bf16_qc, knn_cos_columns, knn_l2sq,
                   knn_l2sq_qc, last_stats, merge_parts)
@@ -21,7 +22,7 @@ from .knn import (DistanceMetric, KnnResult, bf16_last_stats, build_candidate_gr
 __all__ = ["MnError", "lib", "knn_cos_columns", "knn_cos_bf16", "knn_cos_bf16_qc", "bf16_last_stats", "DistanceMetric", "KnnResult", "build_candidate_graph", "knn_l2sq",
            "knn_l2sq_qc", "last_stats", "merge_parts", "CsrMatrix", "GraphParams",
            "LaplacianConfig", "LaplacianOutput", "build_laplacian_from_knn",
-           "laplacian_stage_from_edges", "laplacian", "energy", "TauMode",
+           "laplacian_stage_from_edges", "LaplacianStage", "compute_bhattacharyya_weights", "laplacian", "energy", "TauMode",
            "compute_taumode_lambdas", "energy_rows", "node_energy_and_dispersion",
            "compute_lambdas_gpu", "compute_tau_mode_gpu", "diffuse_rows",
            "laplacian_matvec_rows",

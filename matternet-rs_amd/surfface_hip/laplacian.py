@@ -8,6 +8,9 @@ Host-side mirror of the reference types/entry points:
   * LaplacianConfig / LaplacianOutput / laplacian_stage_from_edges
     surfface-core/src/laplacian.rs:49-99, 312-394: MAX symmetrisation,
     optional L_sym = I - D^-1/2 W D^-1/2, f32 values
+  * compute_bhattacharyya_weights / LaplacianStage.execute
+    surfface-core/src/laplacian.rs:135-298, distance.rs:260-290: the whole
+    Stage C on the GPU (BC kNN of the feature columns -> MAX Laplacian)
 """
 from __future__ import annotations
 
@@ -146,3 +149,34 @@ def laplacian_stage_from_edges(nbr_idx: torch.Tensor, weights: torch.Tensor,
     f = nbr_idx.shape[0]
     return LaplacianOutput(matrix=m, n_features=f, nnz=m.nnz, degrees=deg,
                            sparsity=1.0 - m.nnz / float(f * f))
+
+
+def compute_bhattacharyya_weights(means: torch.Tensor, variances: torch.Tensor,
+                                  config: LaplacianConfig = LaplacianConfig(), stream=None):
+    """laplacian.rs:254-298: per feature node the k = min(k, F-1) largest
+    Bhattacharyya coefficients > weight_threshold (BC desc, j asc).
+    means/variances [C, F] (CentroidState layout) -> (idx [F, k] int32 (-1 pad),
+    w [F, k] f32)."""
+    means = require_cuda(means, torch.float32, "means", 2)
+    variances = require_cuda(variances, torch.float32, "variances", 2)
+    if means.shape != variances.shape:
+        raise ValueError("means and variances must have the same [C, F] shape")
+    c, f = means.shape
+    k = config.k_neighbors
+    idx = torch.empty((f, k), dtype=torch.int32, device=means.device)
+    w = torch.empty((f, k), dtype=torch.float32, device=means.device)
+    _lib.check(_lib.lib().mn_bc_knn_f32(ptr(means), ptr(variances), c, f, k,
+                                        config.variance_regularizer, config.weight_threshold,
+                                        ptr(idx), ptr(w), stream_handle(stream)))
+    return idx, w
+
+
+class LaplacianStage:
+    """surfface-core/src/laplacian.rs:113-228 — Stage C, feature-space Laplacian."""
+
+    def __init__(self, config: LaplacianConfig = LaplacianConfig()):
+        self.config = config
+
+    def execute(self, means: torch.Tensor, variances: torch.Tensor) -> LaplacianOutput:
+        idx, w = compute_bhattacharyya_weights(means, variances, self.config)
+        return laplacian_stage_from_edges(idx, w, self.config)

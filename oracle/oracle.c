@@ -884,6 +884,57 @@ int or_diffuse_rows(const double *X, int64_t n, int32_t f, const int64_t *indptr
     return err;
 }
 
+typedef struct { float w; int32_t j; } bcent;
+static int cmp_bcent(const void *pa, const void *pb) {
+    const bcent *a = (const bcent *)pa, *b = (const bcent *)pb;
+    if (a->w > b->w) return -1;
+    if (a->w < b->w) return 1;
+    return a->j < b->j ? -1 : (a->j > b->j ? 1 : 0);
+}
+
+int or_bc_knn(const float *means, const float *vars, int64_t c, int32_t f, int32_t k,
+              float reg, float thr, int32_t *out_idx, float *out_w) {
+    if (!means || !vars || !out_idx || !out_w || c < 1 || f < 2 || k < 1) return OR_EINVAL;
+    int err = 0;
+#pragma omp parallel
+    {
+        bcent *sc = (bcent *)malloc(sizeof(bcent) * (size_t)f);
+        if (!sc) {
+#pragma omp atomic write
+            err = OR_ENOMEM;
+        }
+#pragma omp for schedule(dynamic, 4)
+        for (int32_t i = 0; i < f; ++i) {
+            if (!sc) continue;
+            int32_t m = 0;
+            for (int32_t j = 0; j < f; ++j) {
+                if (j == i) continue;
+                float db = 0.0f; /* distance.rs:271-286 */
+                for (int64_t t = 0; t < c; ++t) {
+                    float vi = fmaxf(vars[t * f + i], reg), vj = fmaxf(vars[t * f + j], reg);
+                    float vs = vi + vj;
+                    float d = means[t * f + i] - means[t * f + j];
+                    float mean_term = (d * d) / (4.0f * vs);
+                    float log_term = 0.5f * logf(vs / (2.0f * sqrtf(vi * vj)));
+                    db += mean_term + log_term;
+                }
+                float w = expf(-db);
+                w = w < 0.0f ? 0.0f : (w > 1.0f ? 1.0f : w);
+                if (w > thr) { sc[m].w = w; sc[m].j = j; ++m; } /* laplacian.rs:282 */
+            }
+            qsort(sc, (size_t)m, sizeof(bcent), cmp_bcent);
+            int32_t kk = k < f - 1 ? k : f - 1;
+            for (int32_t r = 0; r < k; ++r) {
+                int ok = r < kk && r < m;
+                out_idx[(int64_t)i * k + r] = ok ? sc[r].j : -1;
+                out_w[(int64_t)i * k + r] = ok ? sc[r].w : 0.0f;
+            }
+        }
+        free(sc);
+    }
+    return err;
+}
+
 /* ------------------------------------------------------------------------ */
 /* K5 — SF-GRASS                                                             */
 /* ------------------------------------------------------------------------ */

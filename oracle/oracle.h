@@ -183,6 +183,14 @@ int or_diffuse_rows(const double *X, int64_t n, int32_t f, const int64_t *indptr
                     const int32_t *indices, const double *values, double eta, int32_t steps,
                     int matvec, double *out);
 
+/* surfface-core/src/laplacian.rs:254-298 compute_bhattacharyya_weights with
+ * distance.rs:260-290 bhattacharyya_coefficient (f32, host libm logf/expf,
+ * as the Rust reference links them): means/vars [c][f] (feature columns are
+ * the nodes), per node the k' = min(k, f-1) largest BC > thr over j != i,
+ * (BC desc, j asc).  out_idx/out_w [f][k] (-1 / 0 padded). */
+int or_bc_knn(const float *means, const float *vars, int64_t c, int32_t f, int32_t k,
+              float reg, float thr, int32_t *out_idx, float *out_w);
+
 /* ---- K5: SF-GRASS ------------------------------------------------------- */
 
 /* src_legacy/sparsification.rs:32-113: avg = sum len / n; avg < 10 => copy;

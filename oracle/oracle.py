@@ -58,6 +58,7 @@ def _declare(L):
     L.or_normalise_lambdas.argtypes = [P, I64, P, P, P]
     L.or_spectral_lambdas_f32.argtypes = [P, I64, I32, P, P, P, P]
     L.or_sorted_index.argtypes = [P, I64, P, P, P]
+    L.or_bc_knn.argtypes = [P, P, I64, I32, I32, C.c_float, C.c_float, P, P]
     L.or_diffuse_rows.argtypes = [P, I64, I32, P, P, P, C.c_double, I32, C.c_int, P]
     L.or_range_bylambda.argtypes = [P, P, I64, C.c_double, C.c_double, I64, C.c_double, P, P]
     L.or_range_bylambda.restype = I64
@@ -207,6 +208,18 @@ def sorted_index(lam):
     std = np.zeros(1)
     _check(lib().or_sorted_index(_p(lam), n, _p(order), _p(keys), _p(std)), "sorted_index")
     return order, keys, float(std[0])
+
+
+def bc_knn(means, variances, k, reg=1e-6, thr=1e-9):
+    """compute_bhattacharyya_weights (surfface-core/src/laplacian.rs:254-298):
+    means/variances [C, F] -> (idx [F, k] int32, w [F, k] f32)."""
+    means = np.ascontiguousarray(means, np.float32)
+    variances = np.ascontiguousarray(variances, np.float32)
+    c, f = means.shape
+    idx = np.empty((f, k), np.int32)
+    w = np.empty((f, k), np.float32)
+    _check(lib().or_bc_knn(_p(means), _p(variances), c, f, k, reg, thr, _p(idx), _p(w)), "bc_knn")
+    return idx, w
 
 
 def diffuse_rows(X, indptr, indices, values, eta=0.1, steps=4, matvec=False):

@@ -149,3 +149,70 @@ def test_library_owned_output_and_capacity_error():
                      caller_owned=1)
     rc = L.mn_laplacian_from_knn(ptr(di), ptr(dd), 0, 3000, 8, C.byref(o), C.byref(small), None)
     assert rc == -4 and small.nnz == len(ref[1])
+
+
+def _centroids(c, f, seed, group=5):
+    """[C, F] centroid means / variances in the spirit of the surfface-core
+    tests' centroids_from_gaussian_blobs (test_laplacian.rs:257-275): feature
+    columns come in groups of near-identical profiles (so Bhattacharyya
+    coefficients span (0, 1] and the top-k are meaningful), U(0.05, 0.3)
+    variances, some below the variance floor."""
+    rng = np.random.default_rng(seed)
+    base = rng.uniform(-1, 1, size=(c, (f + group - 1) // group))
+    means = (base[:, np.arange(f) // group] + rng.normal(0, 0.05, size=(c, f))).astype(np.float32)
+    var = rng.uniform(0.05, 0.3, size=(c, f)).astype(np.float32)
+    var[:, ::17] = 0.0  # below the variance floor: max(var, reg)
+    return means, var
+
+
+@pytest.mark.parametrize("c,f,k", [(64, 200, 15), (300, 129, 8), (7, 70, 69)])
+def test_bhattacharyya_stage_c_knn_vs_oracle(c, f, k):
+    """compute_bhattacharyya_weights (laplacian.rs:254-298): weights within
+    1e-5 relative (device ln/exp vs host libm, everything else identical);
+    neighbour lists equal except at near-ties (|BC_a - BC_b| < 1e-5 rel)."""
+    import surfface_hip as S
+    means, var = _centroids(c, f, seed=c + f)
+    cfg = S.LaplacianConfig(k_neighbors=k)
+    gi, gw = S.compute_bhattacharyya_weights(torch.from_numpy(means).cuda(),
+                                             torch.from_numpy(var).cuda(), cfg)
+    gi, gw = gi.cpu().numpy(), gw.cpu().numpy()
+    ri, rw = O.bc_knn(means, var, k)
+    assert (ri >= 0).mean() > 0.2  # a real neighbourhood, not an empty graph
+    np.testing.assert_array_equal(gi < 0, ri < 0)
+    np.testing.assert_allclose(gw, rw, rtol=1e-5, atol=1e-30)
+    mism = gi != ri
+    if mism.any():  # only swaps between (near-)equal coefficients
+        np.testing.assert_allclose(gw[mism], rw[mism], rtol=1e-5)
+    assert mism.mean() < 0.01
+
+
+def test_laplacian_stage_execute_end_to_end():
+    """LaplacianStage::execute (laplacian.rs:135-228) on the GPU: BC kNN ->
+    MAX symmetrisation -> L_sym; invariants of surfface-core tests/test_laplacian.rs
+    (symmetric, unit diagonal, off-diagonals <= 0, nnz <= F(2k+1))."""
+    import surfface_hip as S
+    means, var = _centroids(96, 150, seed=5)
+    out = S.LaplacianStage(S.LaplacianConfig(k_neighbors=10)).execute(
+        torch.from_numpy(means).cuda(), torch.from_numpy(var).cuda())
+    L = out.matrix.to_dense().astype(np.float64)
+    assert np.allclose(L, L.T, atol=1e-6)
+    deg = out.degrees.cpu().numpy()
+    # unit diagonal where the node has edges (L_ii = 1 iff d_i > thr, laplacian.rs:355-365);
+    # the floored-variance features (every 17th) are isolated
+    assert np.allclose(np.diag(L)[deg > 1e-9], 1.0) and (np.diag(L)[deg <= 1e-9] == 0).all()
+    assert (deg[::17] <= 1e-9).all() and (deg > 1e-9).mean() > 0.9
+    assert (L - np.diag(np.diag(L)) <= 0).all()
+    assert out.nnz <= 150 * (2 * 10 + 1)
+    ri, rw = O.bc_knn(means, var, 10)
+    src = np.repeat(np.arange(150), 10)
+    rip, rix, riv, rdeg, _ = O.laplacian_max(150, src, ri.ravel(), rw.ravel(), thr=1e-9,
+                                              normalize=True)
+    ip, ix, iv = out.matrix.to_numpy()
+    np.testing.assert_allclose(L, _dense(rip, rix, riv, 150), rtol=1e-4, atol=1e-6)
+
+
+def _dense(ip, ix, iv, n):
+    M = np.zeros((n, n))
+    for i in range(n):
+        M[i, ix[ip[i]:ip[i + 1]]] = iv[ip[i]:ip[i + 1]]
+    return M
