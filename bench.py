@@ -261,6 +261,17 @@ def c3_legs(S, X, idx, dist, k):
     ms, _ = _timed(lambda: S.diffuse_rows(X, Lf, 0.1, 4, out=Xd))
     out["diffusion_4_steps"] = {"ms": round(ms, 3), "GB_per_s": round(n * f * 12 / ms / 1e6, 1)}
     del Xd
+    # item-graph orientation: the F feature signals against
+    # the n x n item Laplacian; bytes = one x_j row gather per stored entry
+    ms, _ = _timed(lambda: S.signal_energy_and_dispersion(X, Lit))
+    out["item_graph_signals"] = {"ms": round(ms, 3),
+                                 "GB_per_s": round((Lit.nnz // 2 + n) * f * 4 / ms / 1e6, 1)}
+    # Stage C Bhattacharyya feature kNN (§8(f) rank 3) on 2048 centroid rows of X
+    cm = X[:2048].contiguous()
+    cv = (X[2048:4096].abs() * 0.3 + 0.05).contiguous()
+    ms, _ = _timed(lambda: S.compute_bhattacharyya_weights(cm, cv, S.LaplacianConfig(k_neighbors=15)))
+    out["stage_c_bc_knn"] = {"ms": round(ms, 3), "centroids": 2048, "features": f,
+                             "pair_terms_per_s": round(f * (f + 1) / 2 * 2048 / (ms * 1e-3), 1)}
     lam_n = lam.clone()
     ms, _ = _timed(lambda: S.normalise_lambdas(lam_n.copy_(lam)))
     out["normalise_ms"] = round(ms, 3)

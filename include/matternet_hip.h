@@ -255,6 +255,17 @@ int mn_normalise_lambdas(double *lambda, int64_t n, double *out_min_max_range_ho
                          void *stream);
 int mn_energy_last_stats(mn_energy_stats *out);
 
+/* Item-graph orientation: node_energy_and_dispersion
+ * applied to the F feature SIGNALS (columns of X [n][f], length n, f32,
+ * device) against the n x n item Laplacian L (f64 CSR, e.g. the C3 item
+ * graph from mn_laplacian_from_knn UNION) (src_legacy/energymaps.rs:923-1045
+ * with x = X^T): E[f] = max(0, s^T L s / s^T s) (den > 1e-12), G[f] =
+ * clamp(sum (e/S)^2, 0, 1) over ordered pairs (MN_G_TAUMODE) or j > i
+ * (MN_G_ENERGYMAPS).  E, G [f] f64 device (may be NULL).  Tolerance 1e-9
+ * relative (the reference sums in rayon order).  f <= 4096. */
+int mn_energy_signals(const mn_csr *L, const float *X, int64_t n, int32_t f, int32_t g_mode,
+                      double *E, double *G, void *stream);
+
 /* EnergyMaps diffusion pre-pass (src_legacy/energymaps.rs:518-546): `steps`
  * times every row x (length f) becomes x - eta * (L x), where (L x)_i is the
  * CSR row fold sum += L[i,p] * x[col[p]] from +0.0 in stored order

@@ -482,6 +482,93 @@ __global__ __launch_bounds__(512) void k_diffuse_rows(
     }
 }
 
+// ---- item-graph orientation: energy of the F feature signals (length n) ----
+// node_energy_and_dispersion(X^T, L_items) (energymaps.rs:923-1045 with the
+// n x n item Laplacian; SURVEY §8(d) orientation (ii)): per signal s_f =
+// X[:, f], E_f = max(0, s^T L s / s^T s) and G_f = sum (e/S)^2 over the
+// dispersion's pairs.  One block per contiguous range of graph rows i, 256
+// threads over the signals (coalesced row loads of X); per stored entry
+// (i, j, v) the row x_j is gathered once and serves every signal.  Block
+// partials [block][4][f] (num, den, S, Q) are summed in a fixed order.
+template <int FPT>
+__global__ __launch_bounds__(256) void k_energy_signals(
+    const float *__restrict__ X, int64_t n, int f, const int64_t *__restrict__ ip,
+    const int32_t *__restrict__ ix, const double *__restrict__ v, int sym, int g_mode,
+    int64_t rows_per_block, double *__restrict__ part) {
+    const int t = threadIdx.x;
+    const int64_t r0 = (int64_t)blockIdx.x * rows_per_block, r1 = min(n, r0 + rows_per_block);
+    double num[FPT], den[FPT], S[FPT], Q[FPT];
+#pragma unroll
+    for (int u = 0; u < FPT; ++u) num[u] = den[u] = S[u] = Q[u] = 0.0;
+    const double mnum = sym ? 2.0 : 1.0;
+    const double mg = (sym && g_mode == MN_G_TAUMODE) ? 2.0 : 1.0;
+    for (int64_t i = r0; i < r1; ++i) {
+        double xi[FPT];
+#pragma unroll
+        for (int u = 0; u < FPT; ++u) {
+            const int c = t + 256 * u;
+            xi[u] = c < f ? (double)X[i * f + c] : 0.0;
+            den[u] += xi[u] * xi[u];
+        }
+        const int64_t p0 = ip[i], p1 = ip[i + 1];
+        for (int64_t p = p0; p < p1; ++p) {
+            const int j = ix[p];
+            if (sym && j < i) continue;  // covered by (j, i)
+            const double vv = v[p];
+            const bool g = j != i && -vv > 0.0 && (g_mode == MN_G_TAUMODE || sym || j > i);
+            const double m = (j != i) ? mnum : 1.0;
+#pragma unroll
+            for (int u = 0; u < FPT; ++u) {
+                const int c = t + 256 * u;
+                const double xj = c < f ? (double)X[(int64_t)j * f + c] : 0.0;
+                num[u] += m * (vv * (xi[u] * xj));
+                if (g) {
+                    const double dd = xi[u] - xj;
+                    const double e = (dd * dd) * (-vv);
+                    S[u] += mg * e;
+                    Q[u] += mg * (e * e);
+                }
+            }
+        }
+    }
+    double *pb = part + (size_t)blockIdx.x * 4 * f;
+#pragma unroll
+    for (int u = 0; u < FPT; ++u) {
+        const int c = t + 256 * u;
+        if (c < f) {
+            pb[c] = num[u];
+            pb[f + c] = den[u];
+            pb[2 * f + c] = S[u];
+            pb[3 * f + c] = Q[u];
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void k_energy_signals_finish(const double *__restrict__ part,
+                                                               int nb, int f,
+                                                               double *__restrict__ E,
+                                                               double *__restrict__ G) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= f) return;
+    double num = 0.0, den = 0.0, S = 0.0, Q = 0.0;
+    for (int b = 0; b < nb; ++b) {  // fixed order: deterministic
+        const double *pb = part + (size_t)b * 4 * f;
+        num += pb[c];
+        den += pb[f + c];
+        S += pb[2 * f + c];
+        Q += pb[3 * f + c];
+    }
+    if (E) E[c] = den > 1e-12 ? fmax(num / den, 0.0) : 0.0;
+    if (G) {
+        double g = 0.0;
+        if (S > 1e-12) {
+            g = Q / (S * S);
+            g = g < 0.0 ? 0.0 : (g > 1.0 ? 1.0 : g);
+        }
+        G[c] = g;
+    }
+}
+
 }  // namespace energy
 
 static thread_local mn_energy_stats t_energy_stats{};
@@ -610,6 +697,46 @@ static int energy_impl(const mn_csr *L, const float *X, int64_t n, int32_t f,
     return MN_OK;
 }
 
+static int energy_signals_impl(const mn_csr *L, const float *X, int64_t n, int32_t f,
+                               int32_t g_mode, double *E, double *G, void *stream) {
+    using namespace energy;
+    clear_error();
+    MN_REQUIRE(L && X, MN_EINVAL, "mn_energy_signals: NULL argument");
+    MN_REQUIRE(n >= 1 && f >= 1 && f <= FMAX, MN_EINVAL, "mn_energy_signals: bad sizes");
+    MN_REQUIRE(L->n_rows == n && L->n_cols == n && L->value_type == MN_F64, MN_EINVAL,
+               "mn_energy_signals: L must be the n x n f64 item Laplacian");
+    MN_REQUIRE(g_mode == MN_G_TAUMODE || g_mode == MN_G_ENERGYMAPS, MN_EINVAL,
+               "mn_energy_signals: g_mode must be MN_G_TAUMODE or MN_G_ENERGYMAPS");
+    hipStream_t s = (hipStream_t)stream;
+    int *flag = (int *)scratch(kSlotFlags, 64);
+    const int64_t nb = std::min<int64_t>(n, 4096);
+    const int64_t rpb = (n + nb - 1) / nb;
+    const int64_t nbu = (n + rpb - 1) / rpb;
+    double *part = (double *)scratch(kSlotGeneric0, sizeof(double) * (size_t)nbu * 4 * f + 64);
+    MN_REQUIRE(flag && part, MN_ENOMEM, "mn_energy_signals: scratch allocation failed");
+    MN_HIP_TRY(hipMemsetAsync(flag, 0, 8, s));
+    hipLaunchKernelGGL(k_check_sym, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, L->indptr,
+                       L->indices, Vals{L->values, 0}, (int)n, flag);
+    int hflag = 0;
+    MN_HIP_TRY(hipMemcpyAsync(&hflag, flag, 4, hipMemcpyDeviceToHost, s));
+    MN_HIP_TRY(hipStreamSynchronize(s));
+    MN_REQUIRE(!(hflag & 2), MN_EINVAL, "mn_energy_signals: Laplacian column index out of range");
+    const int sym = (hflag & 1) ? 0 : 1;
+    const int fpt = (f + 255) / 256;
+#define MN_ES(FP)                                                                               \
+    hipLaunchKernelGGL(k_energy_signals<FP>, dim3((unsigned)nbu), dim3(256), 0, s, X, n, f,     \
+                       L->indptr, L->indices, (const double *)L->values, sym, g_mode, rpb, part)
+    if (fpt <= 1) MN_ES(1); else if (fpt <= 2) MN_ES(2); else if (fpt <= 4) MN_ES(4);
+    else if (fpt <= 8) MN_ES(8); else MN_ES(16);
+#undef MN_ES
+    MN_KCHECK(s, "k_energy_signals");
+    hipLaunchKernelGGL(k_energy_signals_finish, dim3((unsigned)((f + 255) / 256)), dim3(256), 0, s,
+                       part, (int)nbu, f, E, G);
+    MN_KCHECK(s, "k_energy_signals_finish");
+    MN_HIP_TRY(hipStreamSynchronize(s));
+    return MN_OK;
+}
+
 static int diffuse_impl(const mn_csr *L, const void *X, int32_t x_is_f64, int64_t n, int32_t f,
                         double eta, int32_t steps, int matvec, double *out, void *stream) {
     using namespace energy;
@@ -656,6 +783,11 @@ extern "C" {
 int mn_diffuse_rows(const mn_csr *L, const void *X, int32_t x_is_f64, int64_t n, int32_t f,
                     double eta, int32_t steps, double *X_out, void *stream) {
     return mn::diffuse_impl(L, X, x_is_f64, n, f, eta, steps, 0, X_out, stream);
+}
+
+int mn_energy_signals(const mn_csr *L, const float *X, int64_t n, int32_t f, int32_t g_mode,
+                      double *E, double *G, void *stream) {
+    return mn::energy_signals_impl(L, X, n, f, g_mode, E, G, stream);
 }
 
 int mn_laplacian_matvec_rows(const mn_csr *L, const void *X, int32_t x_is_f64, int64_t n,

@@ -10,7 +10,7 @@ from .sparsification import SfGrassSparsifier, sparsify_rows
 from .sorted_index import SortedLambdas
 from .energy import (TauMode, compute_lambdas_gpu, compute_tau_mode_gpu, compute_taumode_lambdas,
                      diffuse_rows, energy_rows, laplacian_matvec_rows,
-                     node_energy_and_dispersion,
+                     node_energy_and_dispersion, signal_energy_and_dispersion,
                      normalise_lambdas)
 from .laplacian import (CsrMatrix, GraphParams, LaplacianConfig, LaplacianOutput, LaplacianStage,
                         build_laplacian_from_knn, compute_bhattacharyya_weights,
@@ -25,6 +25,6 @@ __all__ = ["MnError", "lib", "knn_cos_columns", "knn_cos_bf16", "knn_cos_bf16_qc
            "laplacian_stage_from_edges", "LaplacianStage", "compute_bhattacharyya_weights", "laplacian", "energy", "TauMode",
            "compute_taumode_lambdas", "energy_rows", "node_energy_and_dispersion",
            "compute_lambdas_gpu", "compute_tau_mode_gpu", "diffuse_rows",
-           "laplacian_matvec_rows",
+           "laplacian_matvec_rows", "signal_energy_and_dispersion",
            "normalise_lambdas", "sorted_index", "SortedLambdas", "sparsification",
            "SfGrassSparsifier", "sparsify_rows"]

@@ -7,6 +7,8 @@ Host-side mirror of:
       -> compute_taumode_lambdas()
   * node_energy_and_dispersion (energymaps.rs:923-1045) -> node_energy_and_dispersion()
   * ArrowSpace::normalise_lambdas                       -> normalise_lambdas()
+  * node_energy_and_dispersion on the item graph (X^T vs the n x n item
+    Laplacian, SURVEY §8(d) orientation (ii))             -> signal_energy_and_dispersion()
   * EnergyMaps diffusion pre-pass (energymaps.rs:518-546)   -> diffuse_rows()
   * GraphLaplacian::multiply_vector (graph.rs:464-501)       -> laplacian_matvec_rows()
     (both bit-exact: f64 CSR row folds in stored order)
@@ -157,3 +159,17 @@ def laplacian_matvec_rows(X: torch.Tensor, L: CsrMatrix, stream=None) -> torch.T
     _lib.check(_lib.lib().mn_laplacian_matvec_rows(C.byref(csr), ptr(X), xf64, n, f, ptr(Y),
                                                    stream_handle(stream)))
     return Y
+
+
+def signal_energy_and_dispersion(X: torch.Tensor, L_items: CsrMatrix,
+                                 g_mode: int = _lib.MN_G_ENERGYMAPS, stream=None):
+    """node_energy_and_dispersion(X^T, L_items): the F feature signals (columns
+    of X [n, F]) against the n x n item Laplacian -> (E [F], G [F]) f64."""
+    X = require_cuda(X, torch.float32, "X", 2)
+    n, f = X.shape
+    E = torch.empty(f, dtype=torch.float64, device=X.device)
+    G = torch.empty(f, dtype=torch.float64, device=X.device)
+    csr = _csr_struct(L_items)
+    _lib.check(_lib.lib().mn_energy_signals(C.byref(csr), ptr(X), n, f, g_mode, ptr(E), ptr(G),
+                                            stream_handle(stream)))
+    return E, G

@@ -208,3 +208,27 @@ def test_diffusion_and_matvec_bit_exact(x64):
     if x64:
         S.diffuse_rows(Xd, L, 0.1, 4, out=Xd)
         np.testing.assert_array_equal(Xd.cpu().numpy().view(np.uint64), ref.view(np.uint64))
+
+
+@pytest.mark.parametrize("gm", [0, 1])
+def test_item_graph_signal_orientation(gm):
+    """node_energy_and_dispersion(X^T, L_items): the 96
+    feature signals of length n = 6000 against the item kNN Laplacian (UNION,
+    rational weights); tolerance 1e-9 relative; a non-symmetric L too."""
+    import surfface_hip as S
+    X = datagen.clustered(6000, 96, seed=51, blobs=6)
+    idx, dist = O.knn_l2sq(X, 10)
+    L, _ = S.build_laplacian_from_knn(torch.from_numpy(idx).cuda(), torch.from_numpy(dist).cuda(),
+                                      eps=1e30, sigma=4.0)
+    ip, ix, iv = L.to_numpy()
+    og = O.G_TAUMODE if gm == 0 else O.G_ENERGYMAPS
+    E, G = S.signal_energy_and_dispersion(torch.from_numpy(X).cuda(), L, gm)
+    rE, rG, _ = O.energy_rows(np.ascontiguousarray(X.T), ip, ix, iv, og, O.TAU_MEDIAN)
+    np.testing.assert_allclose(E.cpu().numpy(), rE, rtol=RTOL, atol=ATOL)
+    np.testing.assert_allclose(G.cpu().numpy(), rG, rtol=RTOL, atol=ATOL)
+    iv2 = iv.copy()
+    iv2[3] *= 1.25  # break symmetry: every stored entry is streamed
+    E2, G2 = S.signal_energy_and_dispersion(torch.from_numpy(X).cuda(), csr_dev(ip, ix, iv2), gm)
+    rE2, rG2, _ = O.energy_rows(np.ascontiguousarray(X.T), ip, ix, iv2, og, O.TAU_MEDIAN)
+    np.testing.assert_allclose(E2.cpu().numpy(), rE2, rtol=RTOL, atol=ATOL)
+    np.testing.assert_allclose(G2.cpu().numpy(), rG2, rtol=RTOL, atol=ATOL)
