@@ -709,7 +709,7 @@ static int energy_signals_impl(const mn_csr *L, const float *X, int64_t n, int32
                "mn_energy_signals: g_mode must be MN_G_TAUMODE or MN_G_ENERGYMAPS");
     hipStream_t s = (hipStream_t)stream;
     int *flag = (int *)scratch(kSlotFlags, 64);
-    const int64_t nb = std::min<int64_t>(n, 4096);
+    const int64_t nb = std::min<int64_t>(n, 16384);
     const int64_t rpb = (n + nb - 1) / nb;
     const int64_t nbu = (n + rpb - 1) / rpb;
     double *part = (double *)scratch(kSlotGeneric0, sizeof(double) * (size_t)nbu * 4 * f + 64);
@@ -726,8 +726,8 @@ static int energy_signals_impl(const mn_csr *L, const float *X, int64_t n, int32
 #define MN_ES(FP)                                                                               \
     hipLaunchKernelGGL(k_energy_signals<FP>, dim3((unsigned)nbu), dim3(256), 0, s, X, n, f,     \
                        L->indptr, L->indices, (const double *)L->values, sym, g_mode, rpb, part)
-    if (fpt <= 1) MN_ES(1); else if (fpt <= 2) MN_ES(2); else if (fpt <= 4) MN_ES(4);
-    else if (fpt <= 8) MN_ES(8); else MN_ES(16);
+    if (fpt <= 1) MN_ES(1); else if (fpt <= 2) MN_ES(2); else if (fpt <= 3) MN_ES(3);
+    else if (fpt <= 4) MN_ES(4); else if (fpt <= 8) MN_ES(8); else MN_ES(16);
 #undef MN_ES
     MN_KCHECK(s, "k_energy_signals");
     hipLaunchKernelGGL(k_energy_signals_finish, dim3((unsigned)((f + 255) / 256)), dim3(256), 0, s,
