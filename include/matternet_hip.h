@@ -321,6 +321,24 @@ int mn_sorted_k_nearest_by_lambda(const double *keys, const int64_t *order, int6
                                   double growth, double max_multiplier, int64_t *out_idx,
                                   double *out_lambda, int32_t *out_count, void *stream);
 
+/* ArrowSpace::search_lambda_aware (src_legacy/core.rs:1156-1193), batched over
+ * nq queries: Q [nq][f] f64 query rows, lambda_q [nq] their (prepared) lambdas,
+ * over the n item rows of X [n][f] (f32, the exactly widened values the
+ * reference's f64 ArrowSpace.data holds, or f64 when x_is_f64) with item
+ * lambdas [n] (f64); all device pointers.  score = alpha*cos(q, x_i) +
+ * (1 - alpha)*(1 - min(|lq - l_i|, 1)) (ArrowItem::lambda_similarity,
+ * core.rs:141-179; cos = dot/(norm*norm), 0 when that product is not > 0,
+ * :196-244: sequential non-contracted f64 folds).  out_idx / out_score
+ * [nq][k] (device): the reference's stable sort by score descending (ties by
+ * ascending i) truncated to k, padded with (-1, NaN) when k > n.  Bit-exact.
+ * MN_EINVAL when some lambda_q == 0.0 (the reference's assert_ne!, :1169),
+ * MN_ENONFINITE on a NaN score (its partial_cmp().unwrap() panics),
+ * MN_ENOTSUP for k > 256. */
+int mn_search_lambda_aware(const void *X, int32_t x_is_f64, int64_t n, int32_t f,
+                           const double *lambdas, const double *Q, const double *lambda_q,
+                           int64_t nq, int32_t k, double alpha, int64_t *out_idx,
+                           double *out_score, void *stream);
+
 
 /* ---------------------------------------------------------------------- */
 /* K5 — sparsification of directed neighbour rows                         */

@@ -134,6 +134,8 @@ SIGNATURES = {
     "mn_knn_cos_bf16": (C.c_int, [P, I64, I32, C.POINTER(CosOpts), P, P, P]),
     "mn_knn_cos_bf16_qc": (C.c_int, [P, I64, P, I64, I32, I64, I64, C.POINTER(CosOpts), P, P, P]),
     "mn_bf16_last_stats": (C.c_int, [C.POINTER(KnnStats)]),
+    "mn_search_lambda_aware": (C.c_int, [P, I32, I64, I32, P, P, P, I64, I32, C.c_double, P,
+                                         P, P]),
 }
 MN_SPARSIFY_SFGRASS, MN_SPARSIFY_INLINE = 0, 1
 

@@ -992,3 +992,71 @@ int or_sfgrass(int64_t n, const int64_t *indptr, const int32_t *indices,
     free(buf);
     return 0;
 }
+
+/* ---- §8(f) rank 2: lambda-aware search (core.rs:1156-1193) ------------- */
+
+typedef struct { double s; int64_t i; } sscore;
+/* sort_by(|a, b| b.1.partial_cmp(&a.1)) over ascending i, stable: score
+ * descending, equal scores (0.0 == -0.0 included) by ascending i. */
+static int cmp_sscore(const void *pa, const void *pb) {
+    const sscore *a = (const sscore *)pa, *b = (const sscore *)pb;
+    if (a->s > b->s) return -1;
+    if (a->s < b->s) return 1;
+    return a->i < b->i ? -1 : (a->i > b->i ? 1 : 0);
+}
+
+/* ArrowItem::norm, core.rs:210-214: sequential f64 sum of x*x, sqrt */
+static double item_norm(const double *a, int32_t f) {
+    double s = 0.0;
+    for (int32_t t = 0; t < f; ++t) s = s + a[t] * a[t];
+    return sqrt(s);
+}
+
+int or_search_lambda_aware(const double *X, int64_t n, int32_t f, const double *lambdas,
+                           const double *Q, const double *lambda_q, int64_t nq, int64_t k,
+                           double alpha, int nthreads, int64_t *out_idx, double *out_score,
+                           int64_t *out_count) {
+    if (n < 0 || f < 0 || nq < 0 || k < 0) return -1;
+    set_threads(nthreads);
+    double *xn = (double *)malloc(sizeof(double) * (size_t)(n > 0 ? n : 1));
+    if (!xn) return -2;
+#pragma omp parallel for schedule(static)
+    for (int64_t i = 0; i < n; ++i) xn[i] = item_norm(X + (size_t)i * f, f);
+    int rc = 0;
+#pragma omp parallel for schedule(dynamic, 1)
+    for (int64_t q = 0; q < nq; ++q) {
+        const double *qv = Q + (size_t)q * f;
+        int64_t *oi = out_idx + (size_t)q * k;
+        double *os = out_score + (size_t)q * k;
+        for (int64_t r = 0; r < k; ++r) { oi[r] = -1; os[r] = NAN; }
+        if (lambda_q[q] == 0.0) { out_count[q] = -1; continue; } /* core.rs:1169-1172 */
+        sscore *sc = (sscore *)malloc(sizeof(sscore) * (size_t)(n > 0 ? n : 1));
+        if (!sc) { rc = -2; continue; }
+        const double qn = item_norm(qv, f);
+        int nan = 0;
+        for (int64_t i = 0; i < n; ++i) {
+            const double *x = X + (size_t)i * f;
+            const double denom = qn * xn[i];
+            double cs = 0.0;
+            if (denom > 0.0) {
+                double dot = 0.0;
+                for (int32_t t = 0; t < f; ++t) dot = dot + qv[t] * x[t];
+                cs = dot / denom;
+            }
+            const double ld = fabs(lambda_q[q] - lambdas[i]);
+            const double ls = 1.0 - fmin(ld, 1.0);
+            const double s = alpha * cs + (1.0 - alpha) * ls;
+            if (isnan(s)) nan = 1;
+            sc[i].s = s;
+            sc[i].i = i;
+        }
+        if (nan) { out_count[q] = -3; free(sc); continue; }
+        qsort(sc, (size_t)n, sizeof(sscore), cmp_sscore);
+        const int64_t c = k < n ? k : n;
+        for (int64_t r = 0; r < c; ++r) { oi[r] = sc[r].i; os[r] = sc[r].s; }
+        out_count[q] = c;
+        free(sc);
+    }
+    free(xn);
+    return rc;
+}

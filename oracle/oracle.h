@@ -202,6 +202,24 @@ int or_sfgrass(int64_t n, const int64_t *indptr, const int32_t *indices,
                const double *w, double ratio, int64_t *out_indptr,
                int32_t *out_indices, double *out_w);
 
+/* ---- §8(f) rank 2: lambda-aware search ---------------------------------- */
+
+/* ArrowSpace::search_lambda_aware (src_legacy/core.rs:1156-1193) for nq
+ * queries over the n item rows of X (f64, row-major, the exactly widened
+ * f32 data): score = alpha*cos + (1-alpha)*(1 - min(|lq - l_i|, 1))
+ * (ArrowItem::lambda_similarity core.rs:162-179, lambda_component_similarity
+ * :141-144); cos = dot/(norm(q)*norm(x_i)) if the product > 0 else 0
+ * (cosine_similarity :233-244, norm :210-214, dot :196-205: sequential
+ * non-contracted f64 folds).  Results sorted by score descending with a
+ * stable sort over ascending i (sort_by is stable), truncated to k.
+ * out_idx/out_score [nq][k], -1 / NaN padded when k > n.  out_count[q] =
+ * min(k, n), or -1 where the reference asserts lambda_q != 0, -3 on a NaN
+ * score (partial_cmp().unwrap() panics). */
+int or_search_lambda_aware(const double *X, int64_t n, int32_t f, const double *lambdas,
+                           const double *Q, const double *lambda_q, int64_t nq, int64_t k,
+                           double alpha, int nthreads, int64_t *out_idx, double *out_score,
+                           int64_t *out_count);
+
 #ifdef __cplusplus
 }
 #endif

@@ -278,3 +278,60 @@ def test_lambda_lookups_known_answers():
     assert idx.tolist() == [4, 0]
     # window lo > hi (lq far above 1): the reference panics in BTreeMap::range
     assert O.k_nearest_by_lambda(keys, order, std, 5.0, 2, 1.0, base_delta=0.1) is None
+
+
+def _py_search(X, lam, q, lq, k, alpha):
+    """Pure-Python restatement of core.rs:1156-1193 (sequential folds)."""
+    def norm(a):
+        s = 0.0
+        for v in a:
+            s = s + v * v
+        return math.sqrt(s)
+    qn = norm(q)
+    out = []
+    for i, x in enumerate(X):
+        denom = qn * norm(x)
+        cs = 0.0
+        if denom > 0.0:
+            d = 0.0
+            for a, b in zip(q, x):
+                d = d + a * b
+            cs = d / denom
+        ls = 1.0 - min(abs(lq - lam[i]), 1.0)
+        out.append((i, alpha * cs + (1.0 - alpha) * ls))
+    out.sort(key=lambda t: -t[1])  # stable: ties keep ascending i
+    return out[:k]
+
+
+def test_search_lambda_aware_known_answers_and_restatement():
+    # ArrowItem::lambda_similarity doctest (core.rs:155-160): a=[1,0] l=.5,
+    # b=[1,0] l=.6, alpha=.7 -> .7*1 + .3*(1-.1) = 0.97 (within [0,1])
+    X = np.array([[1.0, 0.0]])
+    oi, osc, oc = O.search_lambda_aware(X, np.array([0.6]), np.array([[1.0, 0.0]]),
+                                        np.array([0.5]), 1, 0.7)
+    assert oc[0] == 1 and oi[0, 0] == 0
+    assert osc[0, 0] == 0.7 * 1.0 + (1.0 - 0.7) * (1.0 - min(abs(0.5 - 0.6), 1.0))
+    # cosine_similarity doctest (core.rs:226-231): orthogonal -> 0; zero vector -> 0
+    X = np.array([[0.0, 1.0], [0.0, 0.0], [3.0, 0.0]])
+    oi, osc, oc = O.search_lambda_aware(X, np.array([0.5, 0.5, 0.5]), np.array([[1.0, 0.0]]),
+                                        np.array([0.5]), 5, 1.0)
+    assert oc[0] == 3 and list(oi[0, :3]) == [2, 0, 1] and oi[0, 3] == -1
+    assert list(osc[0, :3]) == [1.0, 0.0, 0.0]
+    # lambda 0.0 -> the reference's assert_ne! (count -1)
+    _, _, oc = O.search_lambda_aware(X, np.zeros(3), np.array([[1.0, 0.0]]), np.array([0.0]),
+                                     2, 0.5)
+    assert oc[0] == -1
+    rng = np.random.default_rng(3)
+    X = rng.uniform(-1, 1, (200, 9)).astype(np.float32).astype(np.float64)
+    X[17] = X[3]                        # duplicate rows -> exact score ties
+    lam = rng.uniform(0, 1, 200)
+    lam[17] = lam[3]
+    Q = rng.uniform(-1, 1, (4, 9))
+    lq = rng.uniform(0.01, 1, 4)
+    for alpha in (0.7, 0.1, 1.3):
+        oi, osc, oc = O.search_lambda_aware(X, lam, Q, lq, 25, alpha)
+        for t in range(4):
+            ref = _py_search(X.tolist(), lam.tolist(), Q[t].tolist(), lq[t], 25, alpha)
+            assert oc[t] == 25
+            assert [i for i, _ in ref] == oi[t].tolist()
+            assert [s for _, s in ref] == osc[t].tolist()

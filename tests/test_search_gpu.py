@@ -1,0 +1,111 @@
+"""§8(f) rank 2 parity on the GPU: batched search_lambda_aware (C ABI) vs the
+CPU oracle restatement of src_legacy/core.rs:1156-1193.
+
+Contract: bit-exact indices AND scores (same sequential non-contracted f64
+folds; order = stable sort by score descending, ties by ascending index).
+"""
+import numpy as np
+import pytest
+import torch
+
+import datagen
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+def hip_search(X, lam, Q, lq, k, alpha):
+    import surfface_hip as S
+    oi, osc = S.search_lambda_aware(torch.from_numpy(X).cuda(), torch.from_numpy(lam).cuda(),
+                                    torch.from_numpy(Q).cuda(), torch.from_numpy(lq).cuda(), k,
+                                    alpha)
+    return oi.cpu().numpy(), osc.cpu().numpy()
+
+
+def case(n, f, nq, seed, dup=False, zero=False):
+    rng = np.random.default_rng(seed)
+    X = rng.uniform(-1, 1, (n, f)).astype(np.float32)
+    lam = rng.uniform(0, 1, n)
+    if dup and n > 8:
+        X[n // 2] = X[1]
+        lam[n // 2] = lam[1]
+        lam[5] = lam[3]
+        X[5] = X[3]
+    if zero and n > 4:
+        X[2] = 0.0
+    Q = rng.uniform(-1, 1, (nq, f))
+    lq = rng.uniform(0.01, 1, nq)
+    return X, lam, Q, lq
+
+
+def check(X, lam, Q, lq, k, alpha):
+    oi, osc = hip_search(X, lam, Q, lq, k, alpha)
+    ri, rs, rc = O.search_lambda_aware(X.astype(np.float64), lam, Q, lq, k, alpha)
+    assert (rc == min(k, X.shape[0])).all()
+    np.testing.assert_array_equal(oi, ri)
+    np.testing.assert_array_equal(osc.view(np.uint64), rs.view(np.uint64))
+
+
+@pytest.mark.parametrize("n,f,nq,k", [(1, 3, 1, 1), (5, 7, 2, 10), (255, 33, 3, 8),
+                                      (256, 64, 16, 32), (257, 64, 17, 256),
+                                      (5000, 100, 20, 10), (70_001, 48, 5, 64)])
+@pytest.mark.parametrize("alpha", [0.7, 0.0, 1.3])
+def test_search_vs_oracle(n, f, nq, k, alpha):
+    check(*case(n, f, nq, n + nq, dup=True, zero=True), k, alpha)
+
+
+def test_search_f64_items():
+    X, lam, Q, lq = case(3000, 40, 4, 11, dup=True)
+    X64 = X.astype(np.float64) + 1e-9  # not representable in f32
+    import surfface_hip as S
+    oi, osc = S.search_lambda_aware(torch.from_numpy(X64).cuda(), torch.from_numpy(lam).cuda(),
+                                    torch.from_numpy(Q).cuda(), torch.from_numpy(lq).cuda(), 12,
+                                    0.6)
+    ri, rs, _ = O.search_lambda_aware(X64, lam, Q, lq, 12, 0.6)
+    np.testing.assert_array_equal(oi.cpu().numpy(), ri)
+    np.testing.assert_array_equal(osc.cpu().numpy().view(np.uint64), rs.view(np.uint64))
+
+
+def test_search_all_ties_index_order():
+    # identical items and lambdas: every score ties -> ascending index
+    X = np.ones((1000, 8), np.float32)
+    lam = np.full(1000, 0.25)
+    Q = np.ones((2, 8))
+    oi, osc = hip_search(X, lam, Q, np.array([0.5, 0.75]), 40, 0.5)
+    np.testing.assert_array_equal(oi, np.tile(np.arange(40), (2, 1)))
+
+
+def test_single_query_list_and_errors():
+    import surfface_hip as S
+    X, lam, Q, lq = case(100, 6, 1, 5)
+    res = S.search_lambda_aware(torch.from_numpy(X).cuda(), torch.from_numpy(lam).cuda(),
+                                torch.from_numpy(Q[0]).cuda(), float(lq[0]), 3, 0.7)
+    ri, rs, _ = O.search_lambda_aware(X.astype(np.float64), lam, Q, lq, 3, 0.7)
+    assert res == list(zip(ri[0].tolist(), rs[0].tolist()))
+    with pytest.raises(S.MnError) as e:   # core.rs:1169 assert_ne!(lambda, 0.0)
+        S.search_lambda_aware(torch.from_numpy(X).cuda(), torch.from_numpy(lam).cuda(),
+                              torch.from_numpy(Q).cuda(), 0.0, 3, 0.7)
+    assert e.value.code == S._lib.MN_EINVAL
+    Xn = X.copy()
+    Xn[7, 2] = np.nan   # norm NaN -> `denom > 0.0` false -> cos 0 (core.rs:234-241): no panic
+    check(Xn, lam, Q, lq, 10, 0.7)
+    Xn[7, 2] = np.inf   # inf/inf = NaN score: partial_cmp().unwrap() panics
+    with pytest.raises(S.MnError) as e:
+        S.search_lambda_aware(torch.from_numpy(Xn).cuda(), torch.from_numpy(lam).cuda(),
+                              torch.from_numpy(Q).cuda(), torch.from_numpy(lq).cuda(), 3, 0.7)
+    assert e.value.code == S._lib.MN_ENONFINITE
+    _, _, rc = O.search_lambda_aware(Xn.astype(np.float64), lam, Q, lq, 3, 0.7)
+    assert rc[0] == -3
+    with pytest.raises(S.MnError):
+        S.search_lambda_aware(torch.from_numpy(X).cuda(), torch.from_numpy(lam).cuda(),
+                              torch.from_numpy(Q).cuda(), torch.from_numpy(lq).cuda(), 257, 0.7)
+
+
+def test_search_large_c3_shape_sampled():
+    # 262144 x 768 items (C3 feature width): 3 queries checked against the oracle
+    X = datagen.uniform(262_144, 768, seed=42)
+    rng = np.random.default_rng(9)
+    lam = rng.uniform(0, 1, X.shape[0])
+    Q = X[[5, 100_000, 262_143]].astype(np.float64)
+    lq = lam[[5, 100_000, 262_143]]
+    check(X, lam, Q, lq, 32, 0.7)
