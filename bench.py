@@ -278,6 +278,22 @@ def c3_legs(S, X, idx, dist, k):
     ms, sl = _timed(lambda: S.SortedLambdas().build_from(lam_n))
     out["sorted_index"] = {"ms": round(ms, 3), "std_dev": sl.std_dev,
                            "GB_per_s": round(n * 16 / ms / 1e6, 1)}
+    # lambda-aware query path (§8(f) rank 2, core.rs:1156-1193): 64 queries
+    # (rows of X) against all N items with the normalised lambdas, k=32,
+    # alpha=0.7; work = 2 f64 flops per (query, item, feature) for the dots
+    # plus the item norm chains; bytes = X read once per 32-query group
+    nq = 64
+    qrows = torch.arange(0, n, max(n // nq, 1), device=X.device)[:nq]
+    Qs = X[qrows].double().contiguous()
+    lq = lam_n[qrows].clone().clamp_min(1e-6)
+    ms, _ = _timed(lambda: S.search_lambda_aware(X, lam_n, Qs, lq, 32, 0.7))
+    out["lambda_aware_search"] = {
+        "ms": round(ms, 3), "queries": nq, "k": 32, "queries_per_s": round(nq / (ms * 1e-3), 1),
+        "f64_gflops": round(2.0 * (nq + 4) * n * f / (ms * 1e6), 1),
+        # roofline: the reference's folds forbid FMA, so the ceiling is one f64
+        # mul or add per lane per cycle = FP64 vector peak 78.6 TFLOP/s / 2
+        "f64_valu_frac": round(2.0 * (nq + 4) * n * f / (ms * 1e-3) / 39.3e12, 3),
+        "GB_per_s": round(n * f * 4 * ((nq + 31) // 32) / ms / 1e6, 1)}
     return out
 
 

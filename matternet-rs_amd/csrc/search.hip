@@ -12,17 +12,20 @@
 //   sort_by is stable over ascending i => order = (score desc, i asc).
 //
 // GPU design (HBM stream of X, f64 VALU chains):
-//   k_lambda_scores: one block = 256 items x QB queries.  Items stream through
-//     LDS in 32-feature slabs (row-coalesced loads, padded stride), the query
-//     slab is an LDS broadcast; each thread runs the QB dot chains + its item's
-//     norm chain in the reference's order.  Scores go to LDS, one wave sorts a
-//     query's 256 (-score, i) keys (bitonic, key_less) and writes its top k.
+//   k_lambda_scores: one block = 256 items x 32 queries.  Items stream through
+//     LDS in 32-feature slabs (row-coalesced loads, stored transposed), the
+//     query slab beside them; each lane owns a 4-item x 8-query register
+//     micro-tile (one 16-B item read + 8 broadcast query reads per 32 f64
+//     mul/add) and one item-norm chain, all folded in the reference's order.
+//     Each wave then sorts its queries' 256 (-score, i) keys straight from
+//     registers (bitonic, key_less) and writes the top k.
 //   k_topk_reduce: waves sort 512-candidate chunks and keep the top k until one
 //     chunk is left (k <= 256 => each level at least halves the candidates).
 //   (score desc, i asc) is a total order, so per-tile selection + merges give
 //   exactly the reference's truncated stable sort.
 #include <climits>
 #include <cmath>
+#include <type_traits>
 
 #include "common.hpp"
 
@@ -31,7 +34,7 @@ namespace srch {
 
 constexpr int kTile = 256;  // items per block
 constexpr int kSlab = 32;   // features per LDS slab
-constexpr int kQB = 16;     // queries per block
+constexpr int kQB = 32;     // queries per block (8 per wave)
 constexpr int kChunk = 512; // candidates per reduce wave
 constexpr int kMaxK = 256;
 
@@ -55,90 +58,135 @@ __global__ __launch_bounds__(256) void k_lambda_scores(
     const double *__restrict__ Q, const double *__restrict__ qn, const double *__restrict__ lq,
     int64_t nq, double alpha, int32_t kk, int64_t ntiles, double *__restrict__ ck,
     int32_t *__restrict__ ci, int *__restrict__ flag) {
-    // xs (item slab) and the score matrix share one LDS buffer
-    constexpr int kXs = kTile * (kSlab + 1) * (int)sizeof(T);
-    constexpr int kSk = kQB * kTile * (int)sizeof(double);
-    __shared__ __attribute__((aligned(16))) char buf[kXs > kSk ? kXs : kSk];
-    __shared__ double qs[kQB][kSlab];
-    T(*xs)[kSlab + 1] = reinterpret_cast<T(*)[kSlab + 1]>(buf);
-    double(*sk)[kTile] = reinterpret_cast<double(*)[kTile]>(buf);
+    // xs: the item slab transposed, [feature][item] (+4 pad: 16-B aligned rows,
+    // two-way bank aliasing on the transposing stores); qs: [feature][query]
+    __shared__ __attribute__((aligned(16))) T xs[kSlab][kTile + 4];
+    __shared__ __attribute__((aligned(16))) double qs[kSlab][kQB];
+    __shared__ double xns[kTile];
 
     const int t = threadIdx.x;
+    const int w = t >> 6, lane = t & 63;
     const int64_t tile = blockIdx.x;
     const int64_t i0 = tile * kTile;
     const int64_t q0 = (int64_t)blockIdx.y * kQB;
     const int nqb = (int)min((int64_t)kQB, nq - q0);
+    // micro-tile: items 4*lane .. 4*lane+3 x queries kQW*w .. kQW*w+kQW-1
+    constexpr int kQW = kQB / 4;
 
-    double acc[kQB];
+    double acc[4][kQW];
 #pragma unroll
-    for (int q = 0; q < kQB; ++q) acc[q] = 0.0;
-    double nrm = 0.0;
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int q = 0; q < kQW; ++q) acc[a][q] = 0.0;
+    double nrm = 0.0;  // norm chain of item 4*lane + w
 
+    // slab element p of thread t: row 8p + t/32, feature t%32 (two 128-B row
+    // segments per wave load).  The next slab's loads are issued before the
+    // current slab's chains so their latency hides under the f64 VALU work.
+    const int lc = t & (kSlab - 1), lr = t >> 5;
+    // buffer descriptor over this tile's rows (wave-uniform inputs made
+    // provably uniform): rows >= n fall outside num_records and read as 0
+    const uint64_t tb = (uint64_t)(X + i0 * (int64_t)f);
+    const int32_t nbytes = __builtin_amdgcn_readfirstlane(
+        (int32_t)(min((int64_t)kTile, n - i0) * f * (int64_t)sizeof(T)));
+    const uint64_t tbu = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int32_t)(tb >> 32)) << 32) |
+                         (uint32_t)__builtin_amdgcn_readfirstlane((int32_t)(uint32_t)tb);
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc((void *)tbu, (short)0, nbytes, 0x00020000);
+    T v[kSlab];
+    auto load_slab = [&](int32_t f0) {
+        const int cc = min(lc, f - f0 - 1);
+        const int voff = (lr * f + cc) * (int)sizeof(T);
+#pragma unroll
+        for (int p = 0; p < kSlab; ++p) {
+            const int soff = (8 * p * f + f0) * (int)sizeof(T);
+            if constexpr (sizeof(T) == 4)
+                v[p] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, voff, soff, 0));
+            else
+                v[p] = __longlong_as_double(
+                    (long long)__builtin_amdgcn_raw_buffer_load_b64(rs, voff, soff, 0));
+        }
+    };
+    load_slab(0);
     for (int32_t f0 = 0; f0 < f; f0 += kSlab) {
         const int cn = min(kSlab, f - f0);
-        // item slab: element e -> (row e/32, col e%32): two 32-wide row
-        // segments per wave load
-#pragma unroll 8
+#pragma unroll
         for (int p = 0; p < kSlab; ++p) {
-            const int e = p * kTile + t;
-            const int r = e / kSlab, c = e % kSlab;
-            const int64_t i = i0 + r;
-            T v = T(0);
-            if (i < n && c < cn) v = X[i * f + f0 + c];
-            xs[r][c] = v;
+            const bool ok = (i0 + 8 * p + lr < n) && lc < cn;
+            xs[lc][8 * p + lr] = ok ? v[p] : T(0);
         }
-        for (int e = t; e < kQB * kSlab; e += kTile) {
-            const int q = e / kSlab, c = e % kSlab;
-            qs[q][c] = (q < nqb && c < cn) ? Q[(q0 + q) * f + f0 + c] : 0.0;
+        for (int e = t; e < kSlab * kQB; e += kTile) {
+            const int c = e / kQB, q = e % kQB;
+            qs[c][q] = (q < nqb && c < cn) ? Q[(q0 + q) * f + f0 + c] : 0.0;
         }
         __syncthreads();
+        if (f0 + kSlab < f) load_slab(f0 + kSlab);
         for (int c = 0; c < cn; ++c) {
-            const double x = (double)xs[t][c];
-            nrm = nrm + x * x;
+            T xv[4];
+            *reinterpret_cast<typename std::conditional<sizeof(T) == 4, float4, double4>::type *>(xv) =
+                *reinterpret_cast<const typename std::conditional<sizeof(T) == 4, float4,
+                                                                  double4>::type *>(&xs[c][4 * lane]);
+            double qv[kQW];
 #pragma unroll
-            for (int q = 0; q < kQB; ++q) acc[q] = acc[q] + qs[q][c] * x;
+            for (int q = 0; q < kQW; ++q) qv[q] = qs[c][kQW * w + q];
+            const double xw = (double)xv[w & 3];
+            nrm = nrm + xw * xw;
+#pragma unroll
+            for (int a = 0; a < 4; ++a) {
+                const double x = (double)xv[a];
+                double pr[kQW];  // products first, then the chain adds
+#pragma unroll
+                for (int q = 0; q < kQW; ++q) pr[q] = qv[q] * x;
+#pragma unroll
+                for (int q = 0; q < kQW; ++q) acc[a][q] = acc[a][q] + pr[q];
+            }
         }
         __syncthreads();
     }
-
-    const int64_t i = i0 + t;
-    const bool live = i < n;
-    const double xn = __builtin_sqrt(nrm);
-    const double li = live ? lambdas[i] : 0.0;
-    int nan = 0;
-#pragma unroll
-    for (int q = 0; q < kQB; ++q) {
-        double key = INFINITY;  // sorts after every live item
-        if (live && q < nqb) {
-            const double denom = qn[q0 + q] * xn;
-            const double cs = denom > 0.0 ? acc[q] / denom : 0.0;
-            const double ls = 1.0 - fmin(fabs(lq[q0 + q] - li), 1.0);
-            const double s = alpha * cs + (1.0 - alpha) * ls;
-            nan |= (s != s);
-            key = -s;
-        }
-        sk[q][t] = key;
-    }
-    if (nan) atomicOr(flag, kFlagNan);
+    xns[4 * lane + w] = __builtin_sqrt(nrm);
     __syncthreads();
 
-    const int w = t >> 6, lane = t & 63;
-    for (int q = w; q < nqb; q += kTile / 64) {
-        double d[4];
-        int ix[4];
+    int nan = 0;
+    double d[kQW][4];
+    int ix[4];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const int e = lane + 64 * r;
-            d[r] = sk[q][e];
-            ix[r] = (i0 + e < n) ? (int)(i0 + e) : INT_MAX;
+    for (int a = 0; a < 4; ++a) {
+        const int64_t i = i0 + 4 * lane + a;
+        const bool live = i < n;
+        ix[a] = live ? (int)i : INT_MAX;
+        const double xn = xns[4 * lane + a];
+        const double li = live ? lambdas[i] : 0.0;
+#pragma unroll
+        for (int q = 0; q < kQW; ++q) {
+            const int qq = kQW * w + q;
+            double key = INFINITY;  // sorts after every live item
+            if (live && qq < nqb) {
+                const double denom = qn[q0 + qq] * xn;
+                const double cs = denom > 0.0 ? acc[a][q] / denom : 0.0;
+                const double ls = 1.0 - fmin(fabs(lq[q0 + qq] - li), 1.0);
+                const double sc = alpha * cs + (1.0 - alpha) * ls;
+                nan |= (sc != sc);
+                key = -sc;
+            }
+            d[q][a] = key;
         }
-        wave_bitonic_sort<4>(d, ix);
-        double *okey = ck + ((q0 + q) * ntiles + tile) * kk;
-        int32_t *oidx = ci + ((q0 + q) * ntiles + tile) * kk;
+    }
+    if (nan) atomicOr(flag, kFlagNan);
+    // each wave holds its queries' 256 keys in registers (4 per lane): sort
+    // them in place (positions are irrelevant to the selection) and write the
+    // top kk
+#pragma unroll
+    for (int q = 0; q < kQW; ++q) {
+        const int qq = kQW * w + q;
+        if (qq >= nqb) break;  // wave-uniform
+        int jx[4] = {ix[0], ix[1], ix[2], ix[3]};
+        wave_bitonic_sort<4>(d[q], jx);
+        double *okey = ck + ((q0 + qq) * ntiles + tile) * kk;
+        int32_t *oidx = ci + ((q0 + qq) * ntiles + tile) * kk;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             const int e = lane + 64 * r;
-            if (e < kk) { okey[e] = d[r]; oidx[e] = ix[r]; }
+            if (e < kk) { okey[e] = d[q][r]; oidx[e] = jx[r]; }
         }
     }
 }
@@ -200,6 +248,8 @@ extern "C" int mn_search_lambda_aware(const void *X, int32_t x_is_f64, int64_t n
                "mn_search_lambda_aware: bad sizes");
     MN_REQUIRE(k <= kMaxK, MN_ENOTSUP, "mn_search_lambda_aware: k=%d > %d", k, kMaxK);
     MN_REQUIRE(n < INT_MAX, MN_ENOTSUP, "mn_search_lambda_aware: n >= 2^31");
+    MN_REQUIRE((int64_t)kTile * f * 8 < INT_MAX, MN_ENOTSUP,
+               "mn_search_lambda_aware: f too large for 32-bit tile offsets");
     MN_REQUIRE(nq == 0 || k == 0 || (Q && lambda_q && out_idx && out_score &&
                                      (n == 0 || (X && lambdas))),
                MN_EINVAL, "mn_search_lambda_aware: NULL pointer");
