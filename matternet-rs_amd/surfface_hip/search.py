@@ -8,6 +8,8 @@ rows: every query scores every item with ArrowItem::lambda_similarity
 """
 from __future__ import annotations
 
+import math
+
 import torch
 
 from . import _lib
@@ -56,3 +58,30 @@ def normalise_query_lambda(raw_lambda: float, min_lambdas: float, range_lambdas:
     """core.rs:1361-1372: (raw - min) / range clamped to [0, 1]."""
     v = (raw_lambda - min_lambdas) / range_lambdas
     return min(max(v, 0.0), 1.0)
+
+
+_UNDECIDABLE = ("Check your eps parameter for the builder, every dataset has an optimal eps. "
+                "Also, the query item may be out of context for the dataset (undecidable), "
+                "despite all safeguards its lambda is 0.0")
+
+
+def prepare_query_lambdas(queries: torch.Tensor, L_features, taumode=None, min_lambdas=None,
+                          range_lambdas=None):
+    """ArrowSpace::prepare_query_item, eigen mode without a projection
+    (core.rs:912-933), batched: the synthetic lambda of every query row
+    (TauMode::compute_synthetic_lambda, taumode.rs:261-320, tau =
+    select_tau(query)) on the GPU energy pass (mn_energy_rows, MN_G_TAUMODE),
+    then normalise_query_lambda when the index statistics are finite.
+    queries: [nq, f] f32 (the exactly widened values the reference's f64
+    query holds).  Raises ValueError where the reference panics (a raw lambda
+    within 1e-12 of 0, approx::relative_eq!)."""
+    from .energy import TauMode, energy_rows
+    tm = TauMode.Median if taumode is None else taumode
+    if not torch.isfinite(queries).all():
+        raise ValueError("query item has non-finite values")  # core.rs:865-868
+    _, _, lam = energy_rows(queries, L_features, _lib.MN_G_TAUMODE, tm)
+    if bool((lam.abs() <= 1e-12).any()):
+        raise ValueError(_UNDECIDABLE)
+    if range_lambdas is not None and math.isfinite(range_lambdas):
+        lam = ((lam - min_lambdas) / range_lambdas).clamp_(0.0, 1.0)
+    return lam

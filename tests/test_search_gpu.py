@@ -109,3 +109,30 @@ def test_search_large_c3_shape_sampled():
     Q = X[[5, 100_000, 262_143]].astype(np.float64)
     lq = lam[[5, 100_000, 262_143]]
     check(X, lam, Q, lq, 32, 0.7)
+
+
+def test_end_to_end_query_path_vs_oracle():
+    """build lambdas (taumode, normalised) -> prepare query lambdas -> search:
+    query lambdas within the energy pass tolerance (1e-9 rel), then the
+    search bit-exact given those lambdas (core.rs:864-933, 1156-1193)."""
+    import surfface_hip as S
+    from test_energy_gpu import csr_dev, feature_laplacian
+    ip, ix, iv = feature_laplacian(f=64, profile=800, topk=4, seed=3)
+    X = datagen.uniform(4000, 64, seed=5)
+    Lf = csr_dev(ip, ix, iv)
+    lam, st = S.compute_taumode_lambdas(torch.from_numpy(X).cuda(), Lf)
+    rng = np.random.default_rng(4)
+    Qf = (X[[0, 17, 3999]] + rng.uniform(-0.05, 0.05, (3, 64))).astype(np.float32)
+    lq = S.prepare_query_lambdas(torch.from_numpy(Qf).cuda(), Lf, min_lambdas=st["min"],
+                                 range_lambdas=st["range"])
+    _, _, rl = O.energy_rows(Qf, ip, ix, iv, O.G_TAUMODE, O.TAU_MEDIAN)
+    rq = np.clip((rl - st["min"]) / st["range"], 0.0, 1.0)
+    np.testing.assert_allclose(lq.cpu().numpy(), rq, rtol=1e-9, atol=1e-12)
+    oi, osc = S.search_lambda_aware(torch.from_numpy(X).cuda(), lam,
+                                    torch.from_numpy(Qf.astype(np.float64)).cuda(), lq, 10, 0.7)
+    ri, rs, rc = O.search_lambda_aware(X.astype(np.float64), lam.cpu().numpy(),
+                                       Qf.astype(np.float64), lq.cpu().numpy(), 10, 0.7)
+    np.testing.assert_array_equal(oi.cpu().numpy(), ri)
+    np.testing.assert_array_equal(osc.cpu().numpy().view(np.uint64), rs.view(np.uint64))
+    with pytest.raises(ValueError):    # zero query: raw lambda 0 -> the reference panics
+        S.prepare_query_lambdas(torch.zeros((1, 64), device="cuda"), Lf)
