@@ -294,6 +294,8 @@ def c3_legs(S, X, idx, dist, k):
         # mul or add per lane per cycle = FP64 vector peak 78.6 TFLOP/s / 2
         "f64_valu_frac": round(2.0 * (nq + 4) * n * f / (ms * 1e-3) / 39.3e12, 3),
         "GB_per_s": round(n * f * 4 * ((nq + 31) // 32) / ms / 1e6, 1)}
+    ms, _ = _timed(lambda: S.search_lambda_aware_hybrid(X, lam_n, Qs, lq, 32, 0.7))
+    out["lambda_aware_search"]["hybrid_ms"] = round(ms, 3)
     return out
 
 

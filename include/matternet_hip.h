@@ -339,6 +339,19 @@ int mn_search_lambda_aware(const void *X, int32_t x_is_f64, int64_t n, int32_t f
                            int64_t nq, int32_t k, double alpha, int64_t *out_idx,
                            double *out_score, void *stream);
 
+/* ArrowSpace::search_lambda_aware_hybrid (src_legacy/core.rs:1196-1318), same
+ * arguments: the union of the lambda-score top k, every item with cosine >
+ * 0.9999 (scored by its cosine) and the best-cosine item (first insertion
+ * wins: high-semantic, lambda top k, best cosine), sorted by score descending,
+ * first k (-1 / NaN padded).  The reference's parallel heap, reduce and
+ * sort_unstable leave tie order unspecified: here every tie goes to the
+ * smaller index.  No lambda != 0 check (the reference has none here).
+ * MN_ENOTSUP for k > 255. */
+int mn_search_lambda_aware_hybrid(const void *X, int32_t x_is_f64, int64_t n, int32_t f,
+                                  const double *lambdas, const double *Q,
+                                  const double *lambda_q, int64_t nq, int32_t k, double alpha,
+                                  int64_t *out_idx, double *out_score, void *stream);
+
 
 /* ---------------------------------------------------------------------- */
 /* K5 — sparsification of directed neighbour rows                         */

@@ -46,18 +46,24 @@ __global__ void k_query_norms(const double *__restrict__ Q, int64_t nq, int32_t 
     const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (q >= nq) return;
     const double *a = Q + q * f;
-    double s = 0.0;
+    double s = -0.0;  // Rust >= 1.83 float Sum starts at -0.0
     for (int32_t t = 0; t < f; ++t) s = s + a[t] * a[t];
     qn[q] = __builtin_sqrt(s);
     if (lq[q] == 0.0) atomicOr(flag, kFlagZeroLambda);  // core.rs:1169-1172 assert_ne!
 }
 
-template <typename T>
+// Per-tile candidate lists of up to three selections (NK = 1: the lambda
+// score; NK = 3, the hybrid search: + cosine > 0.9999, + best cosine).
+struct Cand {
+    double *k[3];
+    int32_t *i[3];
+};
+
+template <typename T, int NK>
 __global__ __launch_bounds__(256) void k_lambda_scores(
     const T *__restrict__ X, int64_t n, int32_t f, const double *__restrict__ lambdas,
     const double *__restrict__ Q, const double *__restrict__ qn, const double *__restrict__ lq,
-    int64_t nq, double alpha, int32_t kk, int64_t ntiles, double *__restrict__ ck,
-    int32_t *__restrict__ ci, int *__restrict__ flag) {
+    int64_t nq, double alpha, int32_t kk, int64_t ntiles, Cand cand, int *__restrict__ flag) {
     // xs: the item slab transposed, [feature][item] (+4 pad: 16-B aligned rows,
     // two-way bank aliasing on the transposing stores); qs: [feature][query]
     __shared__ __attribute__((aligned(16))) T xs[kSlab][kTile + 4];
@@ -77,8 +83,8 @@ __global__ __launch_bounds__(256) void k_lambda_scores(
 #pragma unroll
     for (int a = 0; a < 4; ++a)
 #pragma unroll
-        for (int q = 0; q < kQW; ++q) acc[a][q] = 0.0;
-    double nrm = 0.0;  // norm chain of item 4*lane + w
+        for (int q = 0; q < kQW; ++q) acc[a][q] = -0.0;  // Rust float Sum's start value
+    double nrm = -0.0;  // norm chain of item 4*lane + w
 
     // slab element p of thread t: row 8p + t/32, feature t%32 (two 128-B row
     // segments per wave load).  The next slab's loads are issued before the
@@ -147,48 +153,57 @@ __global__ __launch_bounds__(256) void k_lambda_scores(
     __syncthreads();
 
     int nan = 0;
-    double d[kQW][4];
-    int ix[4];
 #pragma unroll
-    for (int a = 0; a < 4; ++a) {
-        const int64_t i = i0 + 4 * lane + a;
-        const bool live = i < n;
-        ix[a] = live ? (int)i : INT_MAX;
-        const double xn = xns[4 * lane + a];
-        const double li = live ? lambdas[i] : 0.0;
+    for (int kind = 0; kind < NK; ++kind) {
+        double d[kQW][4];
+        int ix[4];
+#pragma unroll
+        for (int a = 0; a < 4; ++a) {
+            const int64_t i = i0 + 4 * lane + a;
+            const bool live = i < n;
+            ix[a] = live ? (int)i : INT_MAX;
+            const double xn = xns[4 * lane + a];
+            const double li = live ? lambdas[i] : 0.0;
+#pragma unroll
+            for (int q = 0; q < kQW; ++q) {
+                const int qq = kQW * w + q;
+                double key = INFINITY;  // sorts after every live item / absent
+                if (live && qq < nqb) {
+                    const double denom = qn[q0 + qq] * xn;
+                    const double cs = denom > 0.0 ? acc[a][q] / denom : 0.0;
+                    if (kind == 0) {
+                        const double ls = 1.0 - fmin(fabs(lq[q0 + qq] - li), 1.0);
+                        const double sc = alpha * cs + (1.0 - alpha) * ls;
+                        nan |= (sc != sc);
+                        key = -sc;
+                    } else if (kind == 1) {
+                        key = cs > 0.9999 ? -cs : INFINITY;  // core.rs:1198,1230-1232
+                    } else {
+                        key = -cs;
+                    }
+                }
+                d[q][a] = key;
+            }
+        }
+        // each wave holds its queries' 256 keys in registers (4 per lane):
+        // sort them in place (positions are irrelevant to the selection) and
+        // write the top kk
 #pragma unroll
         for (int q = 0; q < kQW; ++q) {
             const int qq = kQW * w + q;
-            double key = INFINITY;  // sorts after every live item
-            if (live && qq < nqb) {
-                const double denom = qn[q0 + qq] * xn;
-                const double cs = denom > 0.0 ? acc[a][q] / denom : 0.0;
-                const double ls = 1.0 - fmin(fabs(lq[q0 + qq] - li), 1.0);
-                const double sc = alpha * cs + (1.0 - alpha) * ls;
-                nan |= (sc != sc);
-                key = -sc;
+            if (qq >= nqb) break;  // wave-uniform
+            int jx[4] = {ix[0], ix[1], ix[2], ix[3]};
+            wave_bitonic_sort<4>(d[q], jx);
+            double *okey = cand.k[kind] + ((q0 + qq) * ntiles + tile) * kk;
+            int32_t *oidx = cand.i[kind] + ((q0 + qq) * ntiles + tile) * kk;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int e = lane + 64 * r;
+                if (e < kk) { okey[e] = d[q][r]; oidx[e] = jx[r]; }
             }
-            d[q][a] = key;
         }
     }
     if (nan) atomicOr(flag, kFlagNan);
-    // each wave holds its queries' 256 keys in registers (4 per lane): sort
-    // them in place (positions are irrelevant to the selection) and write the
-    // top kk
-#pragma unroll
-    for (int q = 0; q < kQW; ++q) {
-        const int qq = kQW * w + q;
-        if (qq >= nqb) break;  // wave-uniform
-        int jx[4] = {ix[0], ix[1], ix[2], ix[3]};
-        wave_bitonic_sort<4>(d[q], jx);
-        double *okey = ck + ((q0 + qq) * ntiles + tile) * kk;
-        int32_t *oidx = ci + ((q0 + qq) * ntiles + tile) * kk;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const int e = lane + 64 * r;
-            if (e < kk) { okey[e] = d[q][r]; oidx[e] = jx[r]; }
-        }
-    }
 }
 
 // One wave per 512-candidate chunk of one query.  Not final: keep the chunk's
@@ -228,7 +243,69 @@ __global__ __launch_bounds__(256) void k_topk_reduce(
     for (int r = 0; r < 8; ++r) {
         const int e = lane + 64 * r;
         if (e < k) {
-            const bool ok = e < c;
+            const bool ok = e < c && d[r] < INFINITY;  // INF: absent (hybrid lists)
+            out_idx[q * k + e] = ok ? (int64_t)ix[r] : -1;
+            out_score[q * k + e] = ok ? -d[r] : NAN;
+        }
+    }
+}
+
+// Hybrid union (core.rs:1282-1314), one wave per query: high-semantic
+// entries (score = cosine) first, then the lambda top-k (lambda score) where
+// the index is new, then the best-cosine item where new; the union sorted by
+// score descending (sort_unstable: ties here by ascending index), first k.
+// Inputs per query: B (cos > 0.9999 top k), A (lambda top k), C (best cos),
+// -1 padded.  Needs 2k + 1 <= 512.
+__global__ __launch_bounds__(64) void k_hybrid_union(
+    const int64_t *__restrict__ ai, const double *__restrict__ as, const int64_t *__restrict__ bi,
+    const double *__restrict__ bs, const int64_t *__restrict__ ci, const double *__restrict__ cs,
+    int64_t nq, int32_t k, int64_t *__restrict__ out_idx, double *__restrict__ out_score) {
+    __shared__ int64_t eidx[kChunk];
+    __shared__ double escore[kChunk];
+    __shared__ int keep[kChunk];
+    const int lane = threadIdx.x;
+    const int64_t q = blockIdx.x;
+    if (q >= nq) return;
+    double d[8];
+    int ix[8];
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+        const int e = lane + 64 * r;
+        int64_t id = -1;
+        double sc = 0.0;
+        int prio = 3;
+        if (e < k) { id = bi[q * k + e]; sc = bs[q * k + e]; prio = 0; }
+        else if (e < 2 * k) { id = ai[q * k + e - k]; sc = as[q * k + e - k]; prio = 1; }
+        else if (e == 2 * k) { id = ci[q]; sc = cs[q]; prio = 2; }
+        eidx[e] = id;
+        escore[e] = sc;
+        // first sort: by (index, priority); absent entries last
+        d[r] = id >= 0 ? (double)id * 4.0 + prio : INFINITY;
+        ix[r] = e;
+    }
+    wave_bitonic_sort<8>(d, ix);
+    // sorted position p = lane + 64 r holds entry ix[r]; keep the first of
+    // each index run (the highest-priority insertion, as HashMap::entry
+    // .or_insert keeps the first)
+#pragma unroll
+    for (int r = 0; r < 8; ++r) keep[lane + 64 * r] = ix[r];
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+        const int p = lane + 64 * r;
+        const int e = keep[p];
+        const bool present = d[r] < INFINITY;
+        const bool first = p == 0 || eidx[keep[p - 1]] != eidx[e];
+        const bool use = present && first;
+        d[r] = use ? -escore[e] : INFINITY;
+        ix[r] = use ? (int)eidx[e] : INT_MAX;
+    }
+    wave_bitonic_sort<8>(d, ix);
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+        const int e = lane + 64 * r;
+        if (e < k) {
+            const bool ok = d[r] < INFINITY;
             out_idx[q * k + e] = ok ? (int64_t)ix[r] : -1;
             out_score[q * k + e] = ok ? -d[r] : NAN;
         }
@@ -238,55 +315,13 @@ __global__ __launch_bounds__(256) void k_topk_reduce(
 }  // namespace srch
 }  // namespace mn
 
-extern "C" int mn_search_lambda_aware(const void *X, int32_t x_is_f64, int64_t n, int32_t f,
-                                      const double *lambdas, const double *Q,
-                                      const double *lambda_q, int64_t nq, int32_t k, double alpha,
-                                      int64_t *out_idx, double *out_score, void *stream) {
+namespace {
+
+// One selection's candidate lists -> final (idx, score) [nq][k] rows.
+int reduce_lists(double *ka, int32_t *ia, double *kb, int32_t *ib, int64_t m, int64_t nq,
+                 int32_t kk, int32_t k, int64_t n, int64_t *out_idx, double *out_score,
+                 hipStream_t s) {
     using namespace mn::srch;
-    mn::clear_error();
-    MN_REQUIRE(n >= 0 && f >= 0 && nq >= 0 && k >= 0, MN_EINVAL,
-               "mn_search_lambda_aware: bad sizes");
-    MN_REQUIRE(k <= kMaxK, MN_ENOTSUP, "mn_search_lambda_aware: k=%d > %d", k, kMaxK);
-    MN_REQUIRE(n < INT_MAX, MN_ENOTSUP, "mn_search_lambda_aware: n >= 2^31");
-    MN_REQUIRE((int64_t)kTile * f * 8 < INT_MAX, MN_ENOTSUP,
-               "mn_search_lambda_aware: f too large for 32-bit tile offsets");
-    MN_REQUIRE(nq == 0 || k == 0 || (Q && lambda_q && out_idx && out_score &&
-                                     (n == 0 || (X && lambdas))),
-               MN_EINVAL, "mn_search_lambda_aware: NULL pointer");
-    MN_REQUIRE(std::isfinite(alpha), MN_EINVAL, "mn_search_lambda_aware: alpha not finite");
-    if (nq == 0 || k == 0) return MN_OK;
-    hipStream_t s = (hipStream_t)stream;
-
-    const int64_t ntiles = (n + kTile - 1) / kTile;
-    const int32_t kk = (int32_t)std::min<int64_t>(k, kTile);
-    int *flag = (int *)mn::scratch(mn::kSlotFlags, sizeof(int));
-    double *qn = (double *)mn::scratch(mn::kSlotNorms, sizeof(double) * (size_t)nq);
-    MN_REQUIRE(flag && qn, MN_ENOMEM, "mn_search_lambda_aware: scratch");
-    MN_HIP_TRY(hipMemsetAsync(flag, 0, sizeof(int), s));
-    hipLaunchKernelGGL(k_query_norms, dim3((unsigned)((nq + 255) / 256)), dim3(256), 0, s, Q, nq,
-                       f, lambda_q, qn, flag);
-    MN_KCHECK(s, "k_query_norms");
-
-    int64_t m = ntiles * kk;  // candidates per query
-    const size_t cap = (size_t)nq * (size_t)std::max<int64_t>(m, 1);
-    double *ka = (double *)mn::scratch(mn::kSlotGeneric0, sizeof(double) * cap);
-    int32_t *ia = (int32_t *)mn::scratch(mn::kSlotGeneric1, sizeof(int32_t) * cap);
-    double *kb = (double *)mn::scratch(mn::kSlotGeneric2, sizeof(double) * cap);
-    int32_t *ib = (int32_t *)mn::scratch(mn::kSlotGeneric3, sizeof(int32_t) * cap);
-    MN_REQUIRE(ka && ia && kb && ib, MN_ENOMEM, "mn_search_lambda_aware: scratch");
-
-    if (n > 0) {
-        const dim3 g((unsigned)ntiles, (unsigned)((nq + kQB - 1) / kQB));
-        if (x_is_f64)
-            hipLaunchKernelGGL(k_lambda_scores<double>, g, dim3(kTile), 0, s, (const double *)X,
-                               n, f, lambdas, Q, qn, lambda_q, nq, alpha, kk, ntiles, ka, ia,
-                               flag);
-        else
-            hipLaunchKernelGGL(k_lambda_scores<float>, g, dim3(kTile), 0, s, (const float *)X, n,
-                               f, lambdas, Q, qn, lambda_q, nq, alpha, kk, ntiles, ka, ia, flag);
-        MN_KCHECK(s, "k_lambda_scores");
-    }
-    // reduce levels until one chunk per query is left, then the final pass
     while (true) {
         const int64_t nchunks = (m + kChunk - 1) / kChunk;
         const bool fin = nchunks <= 1;
@@ -295,17 +330,123 @@ extern "C" int mn_search_lambda_aware(const void *X, int32_t x_is_f64, int64_t n
                            std::max<int64_t>(nchunks, 1), kb, ib, fin ? 1 : 0, k, n, out_idx,
                            out_score);
         MN_KCHECK(s, "k_topk_reduce");
-        if (fin) break;
+        if (fin) return MN_OK;
         m = nchunks * kk;
         std::swap(ka, kb);
         std::swap(ia, ib);
     }
+}
+
+int search_impl(const void *X, int32_t x_is_f64, int64_t n, int32_t f, const double *lambdas,
+                const double *Q, const double *lambda_q, int64_t nq, int32_t k, double alpha,
+                int64_t *out_idx, double *out_score, void *stream, bool hybrid) {
+    using namespace mn::srch;
+    const char *fn = hybrid ? "mn_search_lambda_aware_hybrid" : "mn_search_lambda_aware";
+    MN_REQUIRE(n >= 0 && f >= 0 && nq >= 0 && k >= 0, MN_EINVAL, "%s: bad sizes", fn);
+    const int kmax = hybrid ? (kChunk - 1) / 2 : kMaxK;
+    MN_REQUIRE(k <= kmax, MN_ENOTSUP, "%s: k=%d > %d", fn, k, kmax);
+    MN_REQUIRE(n < INT_MAX, MN_ENOTSUP, "%s: n >= 2^31", fn);
+    MN_REQUIRE((int64_t)kTile * f * 8 < INT_MAX, MN_ENOTSUP,
+               "%s: f too large for 32-bit tile offsets", fn);
+    MN_REQUIRE(nq == 0 || k == 0 || (Q && lambda_q && out_idx && out_score &&
+                                     (n == 0 || (X && lambdas))),
+               MN_EINVAL, "%s: NULL pointer", fn);
+    MN_REQUIRE(std::isfinite(alpha), MN_EINVAL, "%s: alpha not finite", fn);
+    if (nq == 0 || k == 0) return MN_OK;
+    hipStream_t s = (hipStream_t)stream;
+
+    const int NK = hybrid ? 3 : 1;
+    const int64_t ntiles = (n + kTile - 1) / kTile;
+    const int32_t kk = (int32_t)std::min<int64_t>(k, kTile);
+    int *flag = (int *)mn::scratch(mn::kSlotFlags, sizeof(int));
+    double *qn = (double *)mn::scratch(mn::kSlotNorms, sizeof(double) * (size_t)nq);
+    MN_REQUIRE(flag && qn, MN_ENOMEM, "%s: scratch", fn);
+    MN_HIP_TRY(hipMemsetAsync(flag, 0, sizeof(int), s));
+    hipLaunchKernelGGL(k_query_norms, dim3((unsigned)((nq + 255) / 256)), dim3(256), 0, s, Q, nq,
+                       f, lambda_q, qn, flag);
+    MN_KCHECK(s, "k_query_norms");
+
+    // per selection: two ping-pong candidate buffers of nq * ntiles * kk
+    const int64_t m = ntiles * kk;
+    const size_t cap = (size_t)nq * (size_t)std::max<int64_t>(m, 1);
+    const size_t per = cap * (2 * sizeof(double) + 2 * sizeof(int32_t));
+    // hybrid: + the three selections' final rows, [nq][k] (idx, score) each
+    const size_t fin = hybrid ? (size_t)nq * (size_t)k * 3 * (sizeof(int64_t) + sizeof(double)) : 0;
+    char *base = (char *)mn::scratch(mn::kSlotGeneric0, per * (size_t)NK + fin);
+    MN_REQUIRE(base, MN_ENOMEM, "%s: scratch", fn);
+    Cand cand{};
+    double *kb[3];
+    int32_t *ib[3];
+    for (int c = 0; c < NK; ++c) {
+        char *p = base + per * (size_t)c;
+        cand.k[c] = (double *)p;
+        kb[c] = (double *)(p + cap * sizeof(double));
+        cand.i[c] = (int32_t *)(p + 2 * cap * sizeof(double));
+        ib[c] = (int32_t *)(p + 2 * cap * sizeof(double) + cap * sizeof(int32_t));
+    }
+    if (n > 0) {
+        const dim3 g((unsigned)ntiles, (unsigned)((nq + kQB - 1) / kQB));
+#define MN_SCORES(T, NKV)                                                                     \
+    hipLaunchKernelGGL((k_lambda_scores<T, NKV>), g, dim3(kTile), 0, s, (const T *)X, n, f,    \
+                       lambdas, Q, qn, lambda_q, nq, alpha, kk, ntiles, cand, flag)
+        if (x_is_f64) {
+            if (hybrid) MN_SCORES(double, 3); else MN_SCORES(double, 1);
+        } else {
+            if (hybrid) MN_SCORES(float, 3); else MN_SCORES(float, 1);
+        }
+#undef MN_SCORES
+        MN_KCHECK(s, "k_lambda_scores");
+    }
+    if (!hybrid) {
+        int rc = reduce_lists(cand.k[0], cand.i[0], kb[0], ib[0], m, nq, kk, k, n, out_idx,
+                              out_score, s);
+        if (rc != MN_OK) return rc;
+    } else {
+        char *fp = base + per * (size_t)NK;
+        int64_t *fi[3];
+        double *fs[3];
+        for (int c = 0; c < 3; ++c) {
+            fi[c] = (int64_t *)(fp + (size_t)c * nq * k * sizeof(int64_t));
+            fs[c] = (double *)(fp + 3 * (size_t)nq * k * sizeof(int64_t) +
+                               (size_t)c * nq * k * sizeof(double));
+        }
+        // A = lambda top k, B = cos > 0.9999 top k, C = best cosine (k = 1)
+        for (int c = 0; c < 3; ++c) {
+            int rc = reduce_lists(cand.k[c], cand.i[c], kb[c], ib[c], m, nq, kk, c == 2 ? 1 : k,
+                                  n, fi[c], fs[c], s);
+            if (rc != MN_OK) return rc;
+        }
+        hipLaunchKernelGGL(k_hybrid_union, dim3((unsigned)nq), dim3(64), 0, s, fi[0], fs[0], fi[1],
+                           fs[1], fi[2], fs[2], nq, k, out_idx, out_score);
+        MN_KCHECK(s, "k_hybrid_union");
+    }
     int hflag = 0;
     MN_HIP_TRY(hipMemcpyAsync(&hflag, flag, sizeof(int), hipMemcpyDeviceToHost, s));
     MN_HIP_TRY(hipStreamSynchronize(s));
-    MN_REQUIRE(!(hflag & kFlagZeroLambda), MN_EINVAL,
+    MN_REQUIRE(hybrid || !(hflag & kFlagZeroLambda), MN_EINVAL,
                "Lambda of the item is 0.0, prepare the item before searching (core.rs:1169)");
     MN_REQUIRE(!(hflag & kFlagNan), MN_ENONFINITE,
-               "mn_search_lambda_aware: NaN score (reference: partial_cmp().unwrap() panics)");
+               "%s: NaN score (reference: partial_cmp().unwrap() panics)", fn);
     return MN_OK;
+}
+
+}  // namespace
+
+extern "C" int mn_search_lambda_aware(const void *X, int32_t x_is_f64, int64_t n, int32_t f,
+                                      const double *lambdas, const double *Q,
+                                      const double *lambda_q, int64_t nq, int32_t k, double alpha,
+                                      int64_t *out_idx, double *out_score, void *stream) {
+    mn::clear_error();
+    return search_impl(X, x_is_f64, n, f, lambdas, Q, lambda_q, nq, k, alpha, out_idx, out_score,
+                       stream, false);
+}
+
+extern "C" int mn_search_lambda_aware_hybrid(const void *X, int32_t x_is_f64, int64_t n,
+                                             int32_t f, const double *lambdas, const double *Q,
+                                             const double *lambda_q, int64_t nq, int32_t k,
+                                             double alpha, int64_t *out_idx, double *out_score,
+                                             void *stream) {
+    mn::clear_error();
+    return search_impl(X, x_is_f64, n, f, lambdas, Q, lambda_q, nq, k, alpha, out_idx, out_score,
+                       stream, true);
 }

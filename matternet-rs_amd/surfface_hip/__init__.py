@@ -6,7 +6,8 @@ Every op runs on the GPU through the C ABI; there is no CPU fallback.
 from . import _lib
 from ._lib import MnError, lib
 from . import energy, laplacian, search, sorted_index, sparsification
-from .search import normalise_query_lambda, prepare_query_lambdas, search_lambda_aware
+from .search import (normalise_query_lambda, prepare_query_lambdas, search_lambda_aware,
+                     search_lambda_aware_hybrid)
 from .sparsification import SfGrassSparsifier, sparsify_rows
 from .sorted_index import SortedLambdas
 from .energy import (TauMode, compute_lambdas_gpu, compute_tau_mode_gpu, compute_taumode_lambdas,
@@ -29,4 +30,5 @@ __all__ = ["MnError", "lib", "knn_cos_columns", "knn_cos_bf16", "knn_cos_bf16_qc
            "laplacian_matvec_rows", "signal_energy_and_dispersion",
            "normalise_lambdas", "sorted_index", "SortedLambdas", "sparsification",
            "SfGrassSparsifier", "sparsify_rows", "search", "search_lambda_aware",
-           "normalise_query_lambda", "prepare_query_lambdas"]
+           "normalise_query_lambda", "prepare_query_lambdas",
+           "search_lambda_aware_hybrid"]

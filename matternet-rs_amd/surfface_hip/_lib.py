@@ -136,6 +136,8 @@ SIGNATURES = {
     "mn_bf16_last_stats": (C.c_int, [C.POINTER(KnnStats)]),
     "mn_search_lambda_aware": (C.c_int, [P, I32, I64, I32, P, P, P, I64, I32, C.c_double, P,
                                          P, P]),
+    "mn_search_lambda_aware_hybrid": (C.c_int, [P, I32, I64, I32, P, P, P, I64, I32,
+                                                C.c_double, P, P, P]),
 }
 MN_SPARSIFY_SFGRASS, MN_SPARSIFY_INLINE = 0, 1
 

@@ -17,13 +17,15 @@ from ._torch import ptr, require_cuda, stream_handle
 
 
 def search_lambda_aware(X: torch.Tensor, lambdas: torch.Tensor, queries: torch.Tensor,
-                        query_lambdas, k: int, alpha: float, stream=None):
+                        query_lambdas, k: int, alpha: float, stream=None, hybrid: bool = False):
     """X [n, f] (f32 — the exactly widened values of ArrowSpace.data — or f64),
     item lambdas [n] f64, queries [nq, f] (or [f]) f64, query_lambdas [nq] f64
     (or a float for one query).  Returns (idx int64 [nq, k], score f64 [nq, k]),
     (-1, NaN) padded when k > n; for a 1-D query, the reference's
     [(idx, score)] list.  Raises MnError(MN_EINVAL) where the reference's
-    assert_ne!(lambda, 0.0) fires and MnError(MN_ENONFINITE) on a NaN score."""
+    assert_ne!(lambda, 0.0) fires and MnError(MN_ENONFINITE) on a NaN score.
+    hybrid=True: search_lambda_aware_hybrid (core.rs:1196-1318; ties to the
+    smaller index where the reference leaves them unspecified)."""
     if X.dtype not in (torch.float32, torch.float64):
         raise TypeError("X must be float32 or float64")
     X = require_cuda(X, X.dtype, "X", 2)
@@ -44,13 +46,14 @@ def search_lambda_aware(X: torch.Tensor, lambdas: torch.Tensor, queries: torch.T
         raise ValueError("one lambda per query")
     oi = torch.empty((nq, max(k, 1)), dtype=torch.int64, device=X.device)
     osc = torch.empty((nq, max(k, 1)), dtype=torch.float64, device=X.device)
-    _lib.check(_lib.lib().mn_search_lambda_aware(
+    fn = _lib.lib().mn_search_lambda_aware_hybrid if hybrid else _lib.lib().mn_search_lambda_aware
+    _lib.check(fn(
         ptr(X), 1 if X.dtype == torch.float64 else 0, n, f, ptr(lam), ptr(Q), ptr(lq), nq, k,
         float(alpha), ptr(oi), ptr(osc), stream_handle(stream)))
     oi, osc = oi[:, :k], osc[:, :k]
     if single:
-        c = min(k, n)
-        return list(zip(oi[0, :c].cpu().tolist(), osc[0, :c].cpu().tolist()))
+        ids, scs = oi[0].cpu().tolist(), osc[0].cpu().tolist()
+        return [(i, v) for i, v in zip(ids, scs) if i >= 0]
     return oi, osc
 
 
@@ -85,3 +88,9 @@ def prepare_query_lambdas(queries: torch.Tensor, L_features, taumode=None, min_l
     if range_lambdas is not None and math.isfinite(range_lambdas):
         lam = ((lam - min_lambdas) / range_lambdas).clamp_(0.0, 1.0)
     return lam
+
+
+def search_lambda_aware_hybrid(X, lambdas, queries, query_lambdas, k: int, alpha: float,
+                               stream=None):
+    """ArrowSpace::search_lambda_aware_hybrid (core.rs:1196-1318), batched."""
+    return search_lambda_aware(X, lambdas, queries, query_lambdas, k, alpha, stream, hybrid=True)

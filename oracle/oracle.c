@@ -1007,7 +1007,7 @@ static int cmp_sscore(const void *pa, const void *pb) {
 
 /* ArrowItem::norm, core.rs:210-214: sequential f64 sum of x*x, sqrt */
 static double item_norm(const double *a, int32_t f) {
-    double s = 0.0;
+    double s = -0.0; /* Rust >= 1.83 float Sum starts at -0.0 */
     for (int32_t t = 0; t < f; ++t) s = s + a[t] * a[t];
     return sqrt(s);
 }
@@ -1039,7 +1039,7 @@ int or_search_lambda_aware(const double *X, int64_t n, int32_t f, const double *
             const double denom = qn * xn[i];
             double cs = 0.0;
             if (denom > 0.0) {
-                double dot = 0.0;
+                double dot = -0.0;
                 for (int32_t t = 0; t < f; ++t) dot = dot + qv[t] * x[t];
                 cs = dot / denom;
             }
@@ -1056,6 +1056,75 @@ int or_search_lambda_aware(const double *X, int64_t n, int32_t f, const double *
         for (int64_t r = 0; r < c; ++r) { oi[r] = sc[r].i; os[r] = sc[r].s; }
         out_count[q] = c;
         free(sc);
+    }
+    free(xn);
+    return rc;
+}
+
+/* ArrowSpace::search_lambda_aware_hybrid (core.rs:1196-1318), deterministic
+ * restatement: lambda top-k by (score desc, i asc) (the reference's parallel
+ * heap keeps an unspecified member of a tie class), every item with cosine >
+ * 0.9999 (score = cosine), the best-cosine item (smallest i on ties; the
+ * reference's rayon reduce picks an unspecified one); union with the first
+ * insertion winning (high-semantic, then lambda top-k, then best cosine);
+ * sorted by (score desc, i asc) (sort_unstable: ties unspecified), first k. */
+int or_search_lambda_aware_hybrid(const double *X, int64_t n, int32_t f, const double *lambdas,
+                                  const double *Q, const double *lambda_q, int64_t nq,
+                                  int64_t k, double alpha, int nthreads, int64_t *out_idx,
+                                  double *out_score, int64_t *out_count) {
+    if (n < 0 || f < 0 || nq < 0 || k < 0) return -1;
+    set_threads(nthreads);
+    double *xn = (double *)malloc(sizeof(double) * (size_t)(n > 0 ? n : 1));
+    if (!xn) return -2;
+#pragma omp parallel for schedule(static)
+    for (int64_t i = 0; i < n; ++i) xn[i] = item_norm(X + (size_t)i * f, f);
+    int rc = 0;
+#pragma omp parallel for schedule(dynamic, 1)
+    for (int64_t q = 0; q < nq; ++q) {
+        const double *qv = Q + (size_t)q * f;
+        int64_t *oi = out_idx + (size_t)q * k;
+        double *os = out_score + (size_t)q * k;
+        for (int64_t r = 0; r < k; ++r) { oi[r] = -1; os[r] = NAN; }
+        out_count[q] = 0;
+        if (k == 0) continue;
+        sscore *sc = (sscore *)malloc(sizeof(sscore) * (size_t)(n > 0 ? n : 1));
+        double *cosv = (double *)malloc(sizeof(double) * (size_t)(n > 0 ? n : 1));
+        sscore *u = (sscore *)malloc(sizeof(sscore) * (size_t)(n + k + 1));
+        char *in = (char *)calloc((size_t)(n > 0 ? n : 1), 1);
+        if (!sc || !cosv || !u || !in) { rc = -2; free(sc); free(cosv); free(u); free(in); continue; }
+        const double qn = item_norm(qv, f);
+        int nan = 0;
+        int64_t best = -1;
+        for (int64_t i = 0; i < n; ++i) {
+            const double *x = X + (size_t)i * f;
+            const double denom = qn * xn[i];
+            double cs = 0.0;
+            if (denom > 0.0) {
+                double dot = -0.0;
+                for (int32_t t = 0; t < f; ++t) dot = dot + qv[t] * x[t];
+                cs = dot / denom;
+            }
+            cosv[i] = cs;
+            const double ls = 1.0 - fmin(fabs(lambda_q[q] - lambdas[i]), 1.0);
+            const double s = alpha * cs + (1.0 - alpha) * ls;
+            if (isnan(s)) nan = 1;
+            sc[i].s = s;
+            sc[i].i = i;
+            if (best < 0 || cs > cosv[best]) best = i;
+        }
+        if (nan) { out_count[q] = -3; free(sc); free(cosv); free(u); free(in); continue; }
+        int64_t nu = 0;
+        for (int64_t i = 0; i < n; ++i)
+            if (cosv[i] > 0.9999) { u[nu].s = cosv[i]; u[nu].i = i; ++nu; in[i] = 1; }
+        qsort(sc, (size_t)n, sizeof(sscore), cmp_sscore);
+        for (int64_t r = 0; r < k && r < n; ++r)
+            if (!in[sc[r].i]) { u[nu++] = sc[r]; in[sc[r].i] = 1; }
+        if (best >= 0 && !in[best]) { u[nu].s = cosv[best]; u[nu].i = best; ++nu; }
+        qsort(u, (size_t)nu, sizeof(sscore), cmp_sscore);
+        const int64_t c = k < nu ? k : nu;
+        for (int64_t r = 0; r < c; ++r) { oi[r] = u[r].i; os[r] = u[r].s; }
+        out_count[q] = c;
+        free(sc); free(cosv); free(u); free(in);
     }
     free(xn);
     return rc;

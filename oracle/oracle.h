@@ -220,6 +220,14 @@ int or_search_lambda_aware(const double *X, int64_t n, int32_t f, const double *
                            double alpha, int nthreads, int64_t *out_idx, double *out_score,
                            int64_t *out_count);
 
+/* ArrowSpace::search_lambda_aware_hybrid (core.rs:1196-1318), deterministic
+ * restatement (tie policy in oracle.c); no lambda != 0 assert (the reference
+ * has none here). */
+int or_search_lambda_aware_hybrid(const double *X, int64_t n, int32_t f, const double *lambdas,
+                                  const double *Q, const double *lambda_q, int64_t nq,
+                                  int64_t k, double alpha, int nthreads, int64_t *out_idx,
+                                  double *out_score, int64_t *out_count);
+
 #ifdef __cplusplus
 }
 #endif

@@ -67,6 +67,8 @@ def _declare(L):
     L.or_k_nearest_by_lambda.restype = I64
     L.or_sfgrass.argtypes = [I64, P, P, P, D, P, P, P]
     L.or_search_lambda_aware.argtypes = [P, I64, I32, P, P, P, I64, I64, D, C.c_int, P, P, P]
+    L.or_search_lambda_aware_hybrid.argtypes = [P, I64, I32, P, P, P, I64, I64, D, C.c_int, P, P,
+                                                P]
 
 
 def _p(a):
@@ -273,7 +275,7 @@ def sfgrass(indptr, indices, w, ratio=0.5):
     return oi, oj[:nz].copy(), ow[:nz].copy()
 
 
-def search_lambda_aware(X, lambdas, Q, lambda_q, k, alpha, nthreads=0):
+def search_lambda_aware(X, lambdas, Q, lambda_q, k, alpha, nthreads=0, hybrid=False):
     """core.rs:1156-1193 for every query row of Q: (idx [nq,k], score [nq,k],
     count [nq]); count -1 where the reference asserts lambda != 0, -3 on NaN."""
     X = np.ascontiguousarray(X, dtype=np.float64)
@@ -285,7 +287,7 @@ def search_lambda_aware(X, lambdas, Q, lambda_q, k, alpha, nthreads=0):
     oi = np.empty((nq, max(k, 1)), np.int64)
     os_ = np.empty((nq, max(k, 1)), np.float64)
     oc = np.empty(nq, np.int64)
-    _check(lib().or_search_lambda_aware(_p(X), n, f, _p(lam), _p(Q), _p(lq), nq, k, alpha,
-                                        nthreads, _p(oi), _p(os_), _p(oc)),
-           "search_lambda_aware")
+    fn = lib().or_search_lambda_aware_hybrid if hybrid else lib().or_search_lambda_aware
+    _check(fn(_p(X), n, f, _p(lam), _p(Q), _p(lq), nq, k, alpha, nthreads, _p(oi), _p(os_),
+              _p(oc)), "search_lambda_aware")
     return oi[:, :k], os_[:, :k], oc

@@ -283,7 +283,7 @@ def test_lambda_lookups_known_answers():
 def _py_search(X, lam, q, lq, k, alpha):
     """Pure-Python restatement of core.rs:1156-1193 (sequential folds)."""
     def norm(a):
-        s = 0.0
+        s = -0.0
         for v in a:
             s = s + v * v
         return math.sqrt(s)
@@ -293,7 +293,7 @@ def _py_search(X, lam, q, lq, k, alpha):
         denom = qn * norm(x)
         cs = 0.0
         if denom > 0.0:
-            d = 0.0
+            d = -0.0
             for a, b in zip(q, x):
                 d = d + a * b
             cs = d / denom
@@ -335,3 +335,28 @@ def test_search_lambda_aware_known_answers_and_restatement():
             assert oc[t] == 25
             assert [i for i, _ in ref] == oi[t].tolist()
             assert [s for _, s in ref] == osc[t].tolist()
+
+
+def test_search_hybrid_oracle_vs_python():
+    # core.rs:1196-1318 restated with its tie policy (ties -> smaller index)
+    rng = np.random.default_rng(8)
+    X = rng.uniform(-1, 1, (150, 6)).astype(np.float32).astype(np.float64)
+    X[40] = X[7] * 2.0                       # cosine 1 with row 7 (high-semantic)
+    lam = rng.uniform(0, 1, 150)
+    Q = np.stack([X[7], rng.uniform(-1, 1, 6)])
+    lq = np.array([0.3, 0.6])
+    for alpha in (0.7, 0.0):
+        oi, osc, oc = O.search_lambda_aware(X, lam, Q, lq, 12, alpha, hybrid=True)
+        for t in range(2):
+            ref = _py_search(X.tolist(), lam.tolist(), Q[t].tolist(), lq[t], 12, alpha)
+            full = _py_search(X.tolist(), lam.tolist(), Q[t].tolist(), lq[t], 150, 1.0)
+            cosv = dict(full)
+            u = {i: c for i, c in cosv.items() if c > 0.9999}
+            for i, s in ref:
+                u.setdefault(i, s)
+            best = min(cosv, key=lambda i: (-cosv[i], i))
+            u.setdefault(best, cosv[best])
+            exp = sorted(u.items(), key=lambda p: (-p[1], p[0]))[:12]
+            assert oc[t] == len(exp)
+            assert [i for i, _ in exp] == oi[t, :oc[t]].tolist()
+            assert [s for _, s in exp] == osc[t, :oc[t]].tolist()

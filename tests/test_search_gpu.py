@@ -136,3 +136,40 @@ def test_end_to_end_query_path_vs_oracle():
     np.testing.assert_array_equal(osc.cpu().numpy().view(np.uint64), rs.view(np.uint64))
     with pytest.raises(ValueError):    # zero query: raw lambda 0 -> the reference panics
         S.prepare_query_lambdas(torch.zeros((1, 64), device="cuda"), Lf)
+
+
+def check_hybrid(X, lam, Q, lq, k, alpha):
+    import surfface_hip as S
+    oi, osc = S.search_lambda_aware_hybrid(torch.from_numpy(X).cuda(),
+                                           torch.from_numpy(lam).cuda(),
+                                           torch.from_numpy(Q).cuda(),
+                                           torch.from_numpy(lq).cuda(), k, alpha)
+    ri, rs, rc = O.search_lambda_aware(X.astype(np.float64), lam, Q, lq, k, alpha, hybrid=True)
+    np.testing.assert_array_equal(oi.cpu().numpy(), ri)
+    np.testing.assert_array_equal(osc.cpu().numpy().view(np.uint64), rs.view(np.uint64))
+    return ri, rc
+
+
+@pytest.mark.parametrize("n,f,k", [(1, 3, 1), (7, 5, 10), (300, 33, 8), (5000, 64, 32),
+                                   (70_001, 48, 255)])
+@pytest.mark.parametrize("alpha", [0.7, 0.0, 1.0])
+def test_hybrid_vs_oracle(n, f, k, alpha):
+    X, lam, Q, lq = case(n, f, 5, n + 3, dup=True, zero=True)
+    # high-semantic matches: queries that are (scaled) item rows, + scaled copies
+    if n > 20:
+        X[n - 1] = X[4] * 3.0
+        X[n - 2] = X[4] * 0.5
+        Q[0] = X[4]
+        Q[1] = X[n // 3]
+    ri, rc = check_hybrid(X, lam, Q, lq, k, alpha)
+    assert (rc >= 1).all()
+
+
+def test_hybrid_k_limit():
+    import surfface_hip as S
+    X, lam, Q, lq = case(100, 6, 1, 5)
+    with pytest.raises(S.MnError) as e:
+        S.search_lambda_aware_hybrid(torch.from_numpy(X).cuda(), torch.from_numpy(lam).cuda(),
+                                     torch.from_numpy(Q).cuda(), torch.from_numpy(lq).cuda(),
+                                     256, 0.7)
+    assert e.value.code == S._lib.MN_ENOTSUP
