@@ -40,7 +40,7 @@ namespace mn {
 namespace energy {
 
 constexpr int FMAX = 4096;             // row length limit (registers: FMAX/64 per lane)
-constexpr int ROWS = 2;                // item rows per wave per pass
+constexpr int ROWS = 2;                // item rows per wave per pass (interleaved in LDS)
 constexpr size_t LDS_BUDGET = 160 * 1024;
 constexpr size_t EDGE_LDS_MAX = 96 * 1024;  // entry lists kept in LDS up to this size
 
@@ -263,7 +263,7 @@ __global__ __launch_bounds__(NR <= 16 ? 1024 : 256) void k_energy_rows(
                 const int c = lane + 64 * r;
                 const float x = c < f ? xr[c] : 0.f;
                 if (c < f) {
-                    xs[t * fpad + c] = x;
+                    xs[c * ROWS + t] = x;
                     const double xd = (double)x;
                     dn += xd * xd;
                     ms += xd;
@@ -280,14 +280,20 @@ __global__ __launch_bounds__(NR <= 16 ? 1024 : 256) void k_energy_rows(
 #pragma unroll
         for (int t = 0; t < ROWS; ++t) nA[t] = nB[t] = S[t] = Q[t] = 0.0;
         // list A: num += v x_i x_j (v = -w), S += e, Q += e^2, e = w (x_i - x_j)^2
+        // the ROWS values of one feature are adjacent: one 8-B gather per
+        // endpoint serves both rows of the pass
+        static_assert(ROWS == 2, "gathers are float2");
 #pragma unroll 2
         for (int64_t p = lane; p < na; p += 64) {
             const uint32_t ij = EIJ[p];
             const double wv = EV[p];
             const int i = (int)(ij & 0xFFFFu), j = (int)(ij >> 16);
+            const float2 gi = *reinterpret_cast<const float2 *>(&xs[i * ROWS]);
+            const float2 gj = *reinterpret_cast<const float2 *>(&xs[j * ROWS]);
+            const float ai[2] = {gi.x, gi.y}, aj[2] = {gj.x, gj.y};
 #pragma unroll
             for (int t = 0; t < ROWS; ++t) {
-                const double xi = (double)xs[t * fpad + i], xj = (double)xs[t * fpad + j];
+                const double xi = (double)ai[t], xj = (double)aj[t];
                 nA[t] = __builtin_fma(-wv, xi * xj, nA[t]);
                 const double dd = xi - xj;
                 const double e = (dd * dd) * wv;
@@ -301,9 +307,12 @@ __global__ __launch_bounds__(NR <= 16 ? 1024 : 256) void k_energy_rows(
             const uint32_t ij = EIJ[p];
             const double v = EV[p];
             const int i = (int)(ij & 0xFFFFu), j = (int)(ij >> 16);
+            const float2 gi = *reinterpret_cast<const float2 *>(&xs[i * ROWS]);
+            const float2 gj = *reinterpret_cast<const float2 *>(&xs[j * ROWS]);
+            const float ai[2] = {gi.x, gi.y}, aj[2] = {gj.x, gj.y};
 #pragma unroll
             for (int t = 0; t < ROWS; ++t) {
-                const double xi = (double)xs[t * fpad + i], xj = (double)xs[t * fpad + j];
+                const double xi = (double)ai[t], xj = (double)aj[t];
                 nB[t] = __builtin_fma(v, xi * xj, nB[t]);
             }
         }
@@ -658,7 +667,7 @@ static int energy_impl(const mn_csr *L, const float *X, int64_t n, int32_t f,
     const int in_lds = ebytes <= EDGE_LDS_MAX ? 1 : 0;
     const size_t per_wave = (size_t)ROWS * fpad * 4 + 256 * 4;
     const size_t avail = LDS_BUDGET - (in_lds ? ebytes : 0);
-    const int wmax = nr <= 16 ? 16 : 4;
+    const int wmax = nr <= 16 ? 16 : 4;  // = launch bounds / 64
     const int nw = (int)std::min<size_t>((size_t)wmax, avail / per_wave);
     MN_REQUIRE(nw >= 1, MN_ENOTSUP, "mn_energy_rows: f=%d does not fit the LDS plan", f);
     const size_t shmem = (in_lds ? ebytes : 0) + (size_t)nw * per_wave;
