@@ -54,24 +54,46 @@ struct Vals {
     }
 };
 
-__global__ void k_check_sym(const int64_t *__restrict__ ip, const int32_t *__restrict__ ix,
-                            Vals v, int f, int *__restrict__ asym) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= f) return;
-    for (int64_t p = ip[i]; p < ip[i + 1]; ++p) {
-        const int j = ix[p];
-        if (j < 0 || j >= f) { atomicOr(asym, 2); return; }
-        if (j == i) continue;
-        // binary search (j, i) in row j
-        int64_t lo = ip[j], hi = ip[j + 1] - 1, hit = -1;
-        while (lo <= hi) {
-            const int64_t mid = (lo + hi) >> 1;
-            const int c = ix[mid];
-            if (c == i) { hit = mid; break; }
-            if (c < i) lo = mid + 1; else hi = mid - 1;
+// Symmetry / range check, one thread per stored entry (a row-per-thread walk
+// left the kNN item graph's hub rows, thousands of entries, on one thread).
+// The block finds the row of its first entry once (upper_bound on indptr);
+// each thread gallops forward from there to its own row, then binary-searches
+// the transposed entry (j, i) in row j.
+__global__ __launch_bounds__(256) void k_check_sym(const int64_t *__restrict__ ip,
+                                                   const int32_t *__restrict__ ix, Vals v, int f,
+                                                   int64_t nnz, int *__restrict__ asym) {
+    __shared__ int64_t r0s;
+    const int64_t p0 = (int64_t)blockIdx.x * blockDim.x;
+    if (threadIdx.x == 0) {
+        int64_t lo = 0, hi = f;  // last row r with ip[r] <= p0
+        while (lo < hi) {
+            const int64_t mid = (lo + hi + 1) >> 1;
+            if (ip[mid] <= p0) lo = mid; else hi = mid - 1;
         }
-        if (hit < 0 || v[hit] != v[p]) { atomicOr(asym, 1); return; }
+        r0s = lo;
     }
+    __syncthreads();
+    const int64_t p = p0 + threadIdx.x;
+    if (p >= nnz) return;
+    // row i: the r >= r0 with ip[r] <= p < ip[r + 1] (gallop, then bisect)
+    int64_t lo = r0s, step = 1, hi = lo;
+    while (hi < f && ip[hi + 1] <= p) { lo = hi + 1; hi = min<int64_t>(hi + step, f - 1); step <<= 1; }
+    while (lo < hi) {
+        const int64_t mid = (lo + hi) >> 1;
+        if (ip[mid + 1] <= p) lo = mid + 1; else hi = mid;
+    }
+    const int i = (int)lo;
+    const int j = ix[p];
+    if (j < 0 || j >= f) { atomicOr(asym, 2); return; }
+    if (j == i) return;
+    int64_t a = ip[j], b = ip[j + 1] - 1, hit = -1;
+    while (a <= b) {
+        const int64_t mid = (a + b) >> 1;
+        const int c = ix[mid];
+        if (c == i) { hit = mid; break; }
+        if (c < i) a = mid + 1; else b = mid - 1;
+    }
+    if (hit < 0 || v[hit] != v[p]) atomicOr(asym, 1);
 }
 
 // Every stored CSR entry (i, j, v) the reduction needs goes to one list,
@@ -626,8 +648,9 @@ static int energy_impl(const mn_csr *L, const float *X, int64_t n, int32_t f,
     tm.start(opts->timing != 0, s);
     MN_HIP_TRY(hipMemsetAsync(flag, 0, 8, s));
     const unsigned fb = (unsigned)((f + 255) / 256);
-    hipLaunchKernelGGL(k_check_sym, dim3(fb), dim3(256), 0, s, L->indptr, L->indices, vals, f,
-                       flag);
+    if (L->nnz > 0)
+        hipLaunchKernelGGL(k_check_sym, dim3((unsigned)((L->nnz + 255) / 256)), dim3(256), 0, s,
+                           L->indptr, L->indices, vals, f, L->nnz, flag);
     int hflag = 0;
     MN_HIP_TRY(hipMemcpyAsync(&hflag, flag, 4, hipMemcpyDeviceToHost, s));
     MN_HIP_TRY(hipStreamSynchronize(s));
@@ -724,8 +747,9 @@ static int energy_signals_impl(const mn_csr *L, const float *X, int64_t n, int32
     double *part = (double *)scratch(kSlotGeneric0, sizeof(double) * (size_t)nbu * 4 * f + 64);
     MN_REQUIRE(flag && part, MN_ENOMEM, "mn_energy_signals: scratch allocation failed");
     MN_HIP_TRY(hipMemsetAsync(flag, 0, 8, s));
-    hipLaunchKernelGGL(k_check_sym, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, L->indptr,
-                       L->indices, Vals{L->values, 0}, (int)n, flag);
+    if (L->nnz > 0)
+        hipLaunchKernelGGL(k_check_sym, dim3((unsigned)((L->nnz + 255) / 256)), dim3(256), 0, s,
+                           L->indptr, L->indices, Vals{L->values, 0}, (int)n, L->nnz, flag);
     int hflag = 0;
     MN_HIP_TRY(hipMemcpyAsync(&hflag, flag, 4, hipMemcpyDeviceToHost, s));
     MN_HIP_TRY(hipStreamSynchronize(s));
