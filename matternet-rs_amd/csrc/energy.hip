@@ -575,6 +575,32 @@ __global__ __launch_bounds__(256) void k_energy_signals(
     }
 }
 
+// First level of the fixed-order partial fold: segment y of the nb block
+// partials (contiguous, ascending b) summed per signal, so the finish reads
+// kSegs partials instead of nb (thousands) per signal on f threads.
+constexpr int kSegs = 64;
+__global__ __launch_bounds__(256) void k_energy_signals_fold(const double *__restrict__ part,
+                                                             int nb, int f,
+                                                             double *__restrict__ out) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= f) return;
+    const int seg = blockIdx.y;
+    const int b0 = (int)((int64_t)nb * seg / kSegs), b1 = (int)((int64_t)nb * (seg + 1) / kSegs);
+    double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+    for (int b = b0; b < b1; ++b) {
+        const double *pb = part + (size_t)b * 4 * f;
+        a0 += pb[c];
+        a1 += pb[f + c];
+        a2 += pb[2 * f + c];
+        a3 += pb[3 * f + c];
+    }
+    double *o = out + (size_t)seg * 4 * f;
+    o[c] = a0;
+    o[f + c] = a1;
+    o[2 * f + c] = a2;
+    o[3 * f + c] = a3;
+}
+
 __global__ __launch_bounds__(256) void k_energy_signals_finish(const double *__restrict__ part,
                                                                int nb, int f,
                                                                double *__restrict__ E,
@@ -763,8 +789,13 @@ static int energy_signals_impl(const mn_csr *L, const float *X, int64_t n, int32
     else if (fpt <= 4) MN_ES(4); else if (fpt <= 8) MN_ES(8); else MN_ES(16);
 #undef MN_ES
     MN_KCHECK(s, "k_energy_signals");
+    double *part2 = (double *)scratch(kSlotGeneric1, sizeof(double) * (size_t)kSegs * 4 * f);
+    MN_REQUIRE(part2, MN_ENOMEM, "mn_energy_signals: scratch allocation failed");
+    hipLaunchKernelGGL(k_energy_signals_fold, dim3((unsigned)((f + 255) / 256), kSegs), dim3(256),
+                       0, s, part, (int)nbu, f, part2);
+    MN_KCHECK(s, "k_energy_signals_fold");
     hipLaunchKernelGGL(k_energy_signals_finish, dim3((unsigned)((f + 255) / 256)), dim3(256), 0, s,
-                       part, (int)nbu, f, E, G);
+                       part2, kSegs, f, E, G);
     MN_KCHECK(s, "k_energy_signals_finish");
     MN_HIP_TRY(hipStreamSynchronize(s));
     return MN_OK;
