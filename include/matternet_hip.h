@@ -59,7 +59,8 @@ int mn_fill_uniform_f32(float *X, int64_t n, int32_t d, uint64_t seed,
 /* ---------------------------------------------------------------------- */
 enum mn_metric {
     MN_L2SQ = 0,     /* surfface-core/src/distance.rs:206-213 (f32 fold)     */
-    MN_COS_RECT = 1  /* src_legacy/tests/test_helpers.rs:77-126 (f64)        */
+    MN_COS_RECT = 1, /* src_legacy/tests/test_helpers.rs:77-126 (f64)        */
+    MN_L2 = 2        /* distance.rs:195-203: sqrt of the L2SQ fold (f32)     */
 };
 
 typedef struct mn_knn_opts {
@@ -74,10 +75,15 @@ typedef struct mn_knn_opts {
 } mn_knn_opts;
 
 enum mn_knn_algo {
-    MN_KNN_AUTO = 0,   /* bf16-split when k + margin <= 64, else f32                */
+    MN_KNN_AUTO = 0,   /* BF16X1 for large corpora (>= 2^17 rows), else BF16X3 when
+                          k + margin <= 64, else F32                                */
     MN_KNN_F32 = 1,    /* v_mfma_f32_16x16x4_f32 Gram (exact f32 products)          */
-    MN_KNN_BF16X3 = 2  /* f32 rows split into bf16 hi + lo; hi.hi + hi.lo + lo.hi on
+    MN_KNN_BF16X3 = 2, /* f32 rows split into bf16 hi + lo; hi.hi + hi.lo + lo.hi on
                           v_mfma_f32_32x32x16_bf16 (16x the rate per instruction)   */
+    MN_KNN_BF16X1 = 3  /* two-phase single-bf16 filter: a corpus sample sets each
+                          query's threshold, then one fixed-threshold bf16 Gram sweep
+                          (one MFMA per 16 features); certified by a residual-norm
+                          bound, uncertified rows rescanned exactly                  */
 };
 
 typedef struct mn_knn_stats {
@@ -87,6 +93,13 @@ typedef struct mn_knn_stats {
     int32_t list_len;       /* L = k + margin                                   */
     float ms_norms, ms_gram, ms_rerank, ms_fallback, ms_total; /* timing == 1   */
     int32_t algo;           /* candidate generator used (enum mn_knn_algo)      */
+    /* MN_KNN_BF16X1 only (else 0): ms_gram = ms_sample + ms_sweep             */
+    float ms_sample;        /* phase 1: sample Gram (thresholds)                */
+    float ms_sweep;         /* phase 2: fixed-threshold sweep (the hot kernel)  */
+    int64_t sample_rows;    /* corpus rows in the phase-1 sample                */
+    int64_t n_candidates;   /* buffered (query, row) pairs re-ranked            */
+    int32_t sweep_slices;
+    int32_t sweep_cap;      /* buffer entries per (query, slice, half)          */
 } mn_knn_stats;
 
 /* Self kNN over the rows of X [n][d] f32 (device, row-major): replaces

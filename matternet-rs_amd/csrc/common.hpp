@@ -33,6 +33,13 @@ enum ScratchSlot {
     kSlotGeneric1,
     kSlotGeneric2,
     kSlotGeneric3,
+    kSlotX1QR,     // MN_KNN_BF16X1: query rows, bf16 row-major (phase 1)
+    kSlotX1QK,     //                query rows, bf16 KB32 (phase 2)
+    kSlotX1CR,     //                corpus rows, bf16 row-major
+    kSlotX1CK,     //                corpus rows, bf16 KB32
+    kSlotX1Aux,    //                per-row norms / thresholds / bounds
+    kSlotX1Buf2,   //                phase-2 candidate buffer
+    kSlotX1Meta2,  //                phase-2 counts
     kNumSlots
 };
 

@@ -37,7 +37,10 @@ namespace kb16 {
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
-enum GramMode { GM_COS = 0, GM_L2 = 1 };
+// GM_L2H: L2 key on the single-bf16 rows (hi = bf16(x) only, one MFMA per 16
+// features, the GM_COS row layout) — the sample phase of the two-phase L2
+// generator (knn_f32.hip), certified with the residual-norm bound there.
+enum GramMode { GM_COS = 0, GM_L2 = 1, GM_L2H = 2 };
 
 constexpr int BM = 256;           // queries per block (8 waves x 32 rows)
 constexpr int BN = 128;           // corpus rows per tile (4 column blocks of 32)
@@ -62,8 +65,8 @@ struct alignas(16) Smem {
     uint16_t B[NSLOT][BN][BK];
     float lk[BM][LMAX];
     float qk[BM][QCAP];
-    float caux[2][BN];  // GM_COS: 1/|c|   GM_L2: |c|^2
-    float qaux[BM];     // GM_COS: 1/|q|   GM_L2: |q|^2
+    float caux[2][BN];  // GM_COS: 1/|c|   GM_L2/GM_L2H: |c|^2
+    float qaux[BM];     // GM_COS: 1/|q|   GM_L2/GM_L2H: |q|^2
     float tau[BM];
     int lsz[BM];
     int ovf[BM];
@@ -259,13 +262,13 @@ __global__ __launch_bounds__(NT) void k_gram_bf16(
     __syncthreads();
     const int nk = d / BK;  // a multiple of 4 (d is a multiple of DALIGN)
     // this lane's query row (clamped: rows past nq are masked in the epilogue).
-    // GM_COS: step j, lane half h covers elements 32h + 8j .. +7 of the stage
+    // GM_COS / GM_L2H: step j, lane half h covers elements 32h + 8j .. +7 of the stage
     // (the dot is order-free), so a lane's four fragments are one 64-B run.
     // GM_L2: stage = features 32s..32s+31 as [hi 32 | lo 32]; step j covers
     // features 16j + 8h .. +7: fragments hi(j=0), hi(j=1), lo(j=0), lo(j=1) =
     // 16-B chunks h, 2+h, 4+h, 6+h.
     const uint16_t *arow =
-        Q + min(q0 + WR * w + cl, nq - 1) * (int64_t)d + (MODE == GM_COS ? 32 * h : 8 * h);
+        Q + min(q0 + WR * w + cl, nq - 1) * (int64_t)d + (MODE != GM_L2 ? 32 * h : 8 * h);
     // Sweep = ntiles * nk stages; stage g: corpus tile g / nk, k-block g % nk.
     // Stage g's A fragments (4 loads into one of 4 register sets) are issued
     // three stages ahead, its B pieces (2 LDS-DMA into ring slot g % NSLOT) two
@@ -291,7 +294,7 @@ __global__ __launch_bounds__(NT) void k_gram_bf16(
     // cover them; `claim_a` then marks the registers as produced at that point.
     auto load_a = [&](bf16x8 (&av)[4], int kt) {
         const uint16_t *p = arow + kt * BK;
-        if constexpr (MODE == GM_COS)
+        if constexpr (MODE != GM_L2)
             asm volatile("global_load_dwordx4 %0, %4, off\n\t"
                          "global_load_dwordx4 %1, %4, off offset:16\n\t"
                          "global_load_dwordx4 %2, %4, off offset:32\n\t"
@@ -343,7 +346,7 @@ __global__ __launch_bounds__(NT) void k_gram_bf16(
             claim_a(ac);
             __builtin_amdgcn_s_barrier();  // stage landed for all; slot of g-1 free
             issue_b();      // B(g+2)
-            if constexpr (MODE == GM_COS) {
+            if constexpr (MODE != GM_L2) {
                 // B fragments one MFMA step ahead: 4 ds_read_b128 in flight
                 // behind each group of 4 MFMAs (the scheduler would otherwise
                 // serialise read -> wait -> MFMA and expose the LDS latency)

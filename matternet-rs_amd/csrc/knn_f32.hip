@@ -32,9 +32,11 @@
 #include <algorithm>
 #include <climits>
 #include <cstdlib>
+#include <cstring>
 
 #include "common.hpp"
 #include "gram_bf16.hpp"
+#include "gram_sweep.hpp"
 
 namespace mn {
 namespace knn {
@@ -572,6 +574,283 @@ __global__ __launch_bounds__(256) void k_rerank_buf(
     }
 }
 
+
+// ---------------------------------------------------------------------------
+// 2c. two-phase single-bf16 candidates (MN_KNN_BF16X1, the default at scale)
+//
+//   k_prep_x1    one wave per row: hi = bf16(x) (RNE, subnormals flushed) in
+//                two layouts (row-major for the phase-1 Gram, KB32 for the
+//                sweep), |x|^2 (f64 sum rounded to f32), and exact-residual
+//                bounds |hi| and |x - hi| (f64, rounded UP to f32).
+//   phase 1      gram_bf16.hpp GM_L2H on the first m0 corpus rows (a sample)
+//                with list length L1: tau0(q) = min over slices of the L1-th
+//                best key.
+//   k_tau_x1     tau0, tq = (tau0 - |q|^2)/2 and the certification bound
+//                delta(q) (below).
+//   phase 2      gram_sweep.hpp over rows m0..nc-1: every pair with
+//                key < tau0(q) is buffered.
+//   k_rerank_x1  exact re-rank + certification over both buffers.
+//
+// Certification: every pair never buffered (or dropped) has approximate key
+// >= T = tau0(q), and |key - d_ref| <= delta(q), so T - delta > D_k proves the
+// top k exact.  With q = qh + rq, c = ch + rc (exact residuals):
+//   |q.c - qh.ch| <= |qh||rc| + |rq||ch| + |rq||rc|        (Cauchy-Schwarz)
+// bounded over the corpus by max|ch|, max|rc|; plus the f32 accumulation of
+// dp products and the accumulator's start value (gamma (M + |qh| max|ch|),
+// gamma = (4 dp + 64) u), the roundings of the norms, tq, acc0 and the stored
+// key (4 u M), M = |T| + |q|^2 + max|c|^2; and the reference fold's own error
+// (d + 3) u (|T| + 2E).
+// ---------------------------------------------------------------------------
+
+// bounds must never round down: v >= 0
+__device__ __forceinline__ float f32_up(double v) {
+    float f = (float)v;
+    if ((double)f < v) f = __uint_as_float(__float_as_uint(f) + 1u);
+    return f;
+}
+
+// One wave per PAIR of rows (lanes 0-31: row r, 32-63: row r+1), so the
+// KB32 stores of the two rows fill whole 128-B lines.
+template <bool VEC4>
+__global__ __launch_bounds__(256) void k_prep_x1(const float *__restrict__ X, int64_t n, int d,
+                                                 int dp, uint16_t *__restrict__ XR,
+                                                 uint16_t *__restrict__ XK, float *__restrict__ nrm,
+                                                 float *__restrict__ hcv, float *__restrict__ hn,
+                                                 float *__restrict__ rn,
+                                                 unsigned *__restrict__ maxbits,
+                                                 int *__restrict__ flags, int corpus) {
+    const int lane = threadIdx.x & 63, hl = lane >> 5, ll = lane & 31;
+    const int64_t wave0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+    for (int64_t r2 = 2 * wave0; r2 < n; r2 += 2 * nwaves) {
+        const int64_t row = r2 + hl;
+        const bool live = row < n;
+        const float *p = X + min(row, n - 1) * (int64_t)d;
+        double s = 0.0, sh = 0.0, sr = 0.0;
+        bool bad = false;
+        for (int t0 = 8 * ll; t0 < dp; t0 += 256) {
+            uint32_t wv[4];
+            float xv[8];
+            if (VEC4 && t0 + 8 <= d) {
+                const float4 a = *reinterpret_cast<const float4 *>(p + t0);
+                const float4 b = *reinterpret_cast<const float4 *>(p + t0 + 4);
+                xv[0] = a.x; xv[1] = a.y; xv[2] = a.z; xv[3] = a.w;
+                xv[4] = b.x; xv[5] = b.y; xv[6] = b.z; xv[7] = b.w;
+            } else {
+#pragma unroll
+                for (int u = 0; u < 8; ++u) xv[u] = t0 + u < d ? p[t0 + u] : 0.f;
+            }
+#pragma unroll
+            for (int u = 0; u < 8; u += 2) {
+                uint32_t hb2[2];
+#pragma unroll
+                for (int v = 0; v < 2; ++v) {
+                    const float x = xv[u + v];
+                    bad |= !__builtin_isfinite(x);
+                    const uint32_t hb = __builtin_fabsf(x) >= 0x1p-126f ? bf16_rne(x) : 0u;
+                    const float hf = __uint_as_float(hb << 16);
+                    const float r = x - hf;  // exact
+                    s += (double)x * (double)x;
+                    sh += (double)hf * (double)hf;
+                    sr += (double)r * (double)r;
+                    hb2[v] = hb;
+                }
+                wv[u >> 1] = hb2[0] | (hb2[1] << 16);
+            }
+            if (live) {
+                const uint4 pk = make_uint4(wv[0], wv[1], wv[2], wv[3]);
+                *reinterpret_cast<uint4 *>(XR + row * (int64_t)dp + t0) = pk;
+                *reinterpret_cast<uint4 *>(XK + ((int64_t)(t0 >> 5) * n + row) * 32 + (t0 & 31)) =
+                    pk;
+            }
+        }
+#pragma unroll
+        for (int o = 16; o > 0; o >>= 1) {
+            s += __shfl_xor(s, o);
+            sh += __shfl_xor(sh, o);
+            sr += __shfl_xor(sr, o);
+        }
+        bad = bad && live;
+        const bool anybad = __any(bad);
+        if (ll == 0 && live) {
+            const float nf = (float)s;
+            nrm[row] = nf;
+            if (hcv) hcv[row] = 0.5f * nf;
+            const float hf = f32_up(__builtin_sqrt(sh) * (1.0 + 0x1p-50));
+            const float rf = f32_up(__builtin_sqrt(sr) * (1.0 + 0x1p-50));
+            hn[row] = hf;
+            rn[row] = rf;
+            if (anybad) atomicOr(flags, 1);
+            // keys stay far from f32 overflow (and bf16(x) finite) below 2^100
+            if (!(s <= 0x1p100)) atomicOr(flags + 1, 1);
+            if (corpus) {
+                atomicMax(maxbits + 0, __float_as_uint(nf));
+                atomicMax(maxbits + 1, __float_as_uint(hf));
+                atomicMax(maxbits + 2, __float_as_uint(rf));
+            }
+        }
+    }
+}
+
+// Per query: T = min over phase-1 slices of tau (-inf: forced), tq, delta.
+__global__ __launch_bounds__(256) void k_tau_x1(int64_t nq, int S1, const float *__restrict__ btau1,
+                                                const float *__restrict__ nq_f,
+                                                const float *__restrict__ hn_q,
+                                                const float *__restrict__ rn_q,
+                                                const unsigned *__restrict__ cmax, int d, int dp,
+                                                float *__restrict__ tq, float *__restrict__ tau0,
+                                                float *__restrict__ delta) {
+    const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= nq) return;
+    float T = __builtin_inff();
+    for (int s = 0; s < S1; ++s) T = fminf(T, btau1[q * S1 + s]);
+    const float qn = nq_f[q];
+    tau0[q] = T;
+    tq[q] = (T - qn) * 0.5f;
+    const double u = 0x1p-24;
+    const double Mn = __uint_as_float(cmax[0]), Mh = __uint_as_float(cmax[1]),
+                 Mr = __uint_as_float(cmax[2]);
+    const double qh = hn_q[q], qr = rn_q[q];
+    const double Tf = __builtin_isfinite(T) ? __builtin_fabs((double)T) : 0.0;
+    const double M = Tf + (double)qn + Mn;
+    const double Eprod = qh * Mr + qr * Mh + qr * Mr;
+    const double gam = (4.0 * dp + 64.0) * u;
+    const double E = Eprod + gam * (M + qh * Mh) + 4.0 * u * M;
+    const double dl = 2.0 * E + (d + 3.0) * u * (Tf + 2.0 * E) + 0x1p-100;
+    delta[q] = f32_up(dl * (1.0 + 0x1p-20));
+}
+
+// One wave per query: gather both phases' buffered candidates with key < T
+// (all of them when T = +inf: nothing was rejected), order by key, evaluate
+// the reference fold for the best kq and then for every other candidate whose
+// lower bound key - delta does not exceed the worst of those, sort by (dist,
+// idx), certify T - delta > D_k.  Overflowing buffers force the exact scan.
+// Rows with more than 64 NR candidates go to big_list (a second launch with a
+// wider NR re-ranks them; without a big_list they are rescanned exactly).
+template <int NR, int WPB, bool VEC4>
+__global__ __launch_bounds__(64 * WPB) void k_rerank_x1(
+    const float *__restrict__ Q, int64_t nq, const float *__restrict__ C, int d, int64_t c_off,
+    int S1, int cap1, const uint2 *__restrict__ buf1, const int *__restrict__ cnt1,
+    const float *__restrict__ tau0, int S2, int cap2, const uint2 *__restrict__ buf2,
+    const int *__restrict__ cnt2, const float *__restrict__ delta, int k, int64_t nvalid_max,
+    const int *__restrict__ qlist, const int *__restrict__ qlist_n, int *__restrict__ big_count,
+    int *__restrict__ big_list, int32_t *__restrict__ out_idx, float *__restrict__ out_dist,
+    int *__restrict__ fb_count, int *__restrict__ fb_list) {
+    __shared__ int cand[WPB][64 * NR];
+    __shared__ float candk[WPB][64 * NR];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int64_t wq = (int64_t)blockIdx.x * WPB + wid;
+    if (qlist ? wq >= *qlist_n : wq >= nq) return;
+    const int64_t q = qlist ? qlist[wq] : wq;
+    const float T = tau0[q];
+    bool forced = T == -__builtin_inff();
+    int M = 0;
+    auto gather = [&](const uint2 *bp, int cnt) {
+        for (int e0 = 0; e0 < cnt; e0 += 64) {
+            const int e = e0 + lane;
+            const uint2 v = e < cnt ? bp[e] : make_uint2(0x7f800000u, 0u);
+            const bool pass = e < cnt && __uint_as_float(v.x) < T;
+            const uint64_t pm = __ballot(pass);
+            const int pos = M + (int)__popcll(pm & ((1ull << lane) - 1ull));
+            if (pass && pos < 64 * NR) {
+                cand[wid][pos] = (int)v.y;
+                candk[wid][pos] = __uint_as_float(v.x);
+            }
+            M += (int)__popcll(pm);
+        }
+    };
+    for (int s = 0; s < S1; ++s) gather(buf1 + (q * S1 + s) * (int64_t)cap1, cnt1[q * S1 + s]);
+    for (int j = 0; j < S2; ++j) {
+        const int c = cnt2[q * S2 + j];
+        forced |= c < 0;
+        if (c > 0) gather(buf2 + (q * S2 + j) * (int64_t)cap2, c);
+    }
+    if (!forced && M > 64 * NR && big_list) {
+        if (lane == 0) big_list[atomicAdd(big_count, 1)] = (int)q;
+        return;
+    }
+    forced |= M > 64 * NR;
+    M = min(M, 64 * NR);
+    __builtin_amdgcn_wave_barrier();
+    float kk[NR];
+    int ix[NR];
+#pragma unroll
+    for (int r = 0; r < NR; ++r) {
+        const int e = lane + 64 * r;
+        kk[r] = e < M ? candk[wid][e] : __builtin_inff();
+        ix[r] = e < M ? cand[wid][e] : INT_MAX;
+    }
+    wave_bitonic_sort<NR>(kk, ix);
+    const float dlt = delta[q];
+    const float *qrow = Q + q * (int64_t)d;
+    const int kq = min(k, M);
+    float dd[NR];
+#pragma unroll
+    for (int r = 0; r < NR; ++r) {
+        const int e = lane + 64 * r;
+        dd[r] = __builtin_inff();
+        if (e < kq) dd[r] = exact_l2sq<VEC4>(qrow, C + ((int64_t)ix[r] - c_off) * d, d);
+    }
+    float Dp = -__builtin_inff();
+#pragma unroll
+    for (int r = 0; r < NR; ++r) Dp = fmaxf(Dp, (lane + 64 * r) < kq ? dd[r] : -__builtin_inff());
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) Dp = fmaxf(Dp, __shfl_xor(Dp, o));
+#pragma unroll
+    for (int r = 0; r < NR; ++r) {
+        const int e = lane + 64 * r;
+        if (e >= kq && e < M && !(kk[r] - dlt > Dp))
+            dd[r] = exact_l2sq<VEC4>(qrow, C + ((int64_t)ix[r] - c_off) * d, d);
+    }
+#pragma unroll
+    for (int r = 0; r < NR; ++r)
+        if (lane + 64 * r >= M) ix[r] = INT_MAX;
+    wave_bitonic_sort<NR>(dd, ix);
+    const int keff = (int)min((int64_t)min(k, M), nvalid_max);
+    bool cert = !forced;
+    if (cert && T < __builtin_inff() && keff > 0) {
+        const float Dk = wave_elem<NR>(dd, keff - 1);
+        cert = (T - dlt) > Dk;  // NaN/inf-safe: false => exact rescan
+    }
+    if (cert && T < __builtin_inff() && keff < (int)min((int64_t)k, nvalid_max)) cert = false;
+    if (!cert) {
+        if (lane == 0) fb_list[atomicAdd(fb_count, 1)] = (int)q;
+        return;
+    }
+    if (lane < k) {
+        const bool ok = lane < keff;
+        out_idx[q * k + lane] = ok ? ix[0] : -1;
+        out_dist[q * k + lane] = ok ? dd[0] : __builtin_inff();
+    }
+}
+
+// sum of buffered entries (statistics only; timing mode)
+__global__ __launch_bounds__(256) void k_count_cands(const int *__restrict__ c, int64_t n, int cap,
+                                                     unsigned long long *__restrict__ out) {
+    __shared__ unsigned long long part[4];
+    unsigned long long a = 0;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const int v = c[i];
+        a += (unsigned long long)(v < 0 ? cap : min(v, cap));
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) a += __shfl_xor(a, o);
+    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = a;
+    __syncthreads();
+    if (threadIdx.x == 0) atomicAdd(out, part[0] + part[1] + part[2] + part[3]);
+}
+
+// MN_L2: distances of the L2SQ result -> correctly rounded f32 sqrt
+// (Rust f32::sqrt; gfx950 sqrtf is not correctly rounded, common.hpp)
+__global__ __launch_bounds__(256) void k_sqrt_dist(float *__restrict__ dist, int64_t n) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) {
+        const float v = dist[i];
+        if (v < __builtin_inff()) dist[i] = sqrt_rn_f32(v);
+    }
+}
+
 // ---------------------------------------------------------------------------
 // 4. exact fallback scan for uncertified rows
 // ---------------------------------------------------------------------------
@@ -694,29 +973,18 @@ namespace {
 thread_local mn_knn_stats t_stats{};
 }
 
-// Host driver shared by mn_knn_f32 and mn_knn_f32_qc.
-static int knn_f32_impl(const float *Q, int64_t nq, const float *C, int64_t nc, int32_t d,
+// Host driver of the MN_KNN_F32 / MN_KNN_BF16X3 generators.
+static int knn_f32_core(const float *Q, int64_t nq, const float *C, int64_t nc, int32_t d,
                         int64_t q_off, int64_t c_off, const mn_knn_opts *opts,
-                        int32_t *out_idx, float *out_dist) {
+                        int32_t *out_idx, float *out_dist, int algo) {
     using namespace knn;
-    clear_error();
-    t_stats = mn_knn_stats{};
-    MN_REQUIRE(opts, MN_EINVAL, "mn_knn: opts is NULL");
-    MN_REQUIRE(Q && C && out_idx && out_dist, MN_EINVAL, "mn_knn: NULL pointer argument");
-    MN_REQUIRE(nq >= 0 && nc >= 0 && d >= 1, MN_EINVAL, "mn_knn: bad shape nq=%lld nc=%lld d=%d",
-               (long long)nq, (long long)nc, d);
-    MN_REQUIRE(opts->metric == MN_L2SQ, MN_ENOTSUP, "mn_knn_f32: metric %d not supported here",
-               opts->metric);
     const int k = opts->k;
     MN_REQUIRE(k >= 1 && k <= KMAX, MN_ENOTSUP, "mn_knn: k=%d outside [1,%d]", k, KMAX);
     const int margin = opts->margin > 0 ? opts->margin : 16;
     const int L = k + margin;
     MN_REQUIRE(L <= LMAX, MN_ENOTSUP, "mn_knn: k+margin=%d exceeds %d", L, LMAX);
-    // candidate generator: bf16-split MFMA (default) or f32 MFMA; both are
-    // followed by the same exact re-rank / certification / fallback contract
-    const int algo = opts->algo;
-    MN_REQUIRE(algo >= MN_KNN_AUTO && algo <= MN_KNN_BF16X3, MN_EINVAL, "mn_knn: bad algo %d",
-               algo);
+    // candidate generator: bf16-split MFMA or f32 MFMA; both are followed by
+    // the same exact re-rank / certification / fallback contract
     MN_REQUIRE(!(algo == MN_KNN_BF16X3 && L > kb16::LMAX), MN_ENOTSUP,
                "mn_knn: bf16-split candidates need k+margin <= %d", kb16::LMAX);
     const bool split = algo == MN_KNN_BF16X3 || (algo == MN_KNN_AUTO && L <= kb16::LMAX);
@@ -819,7 +1087,11 @@ static int knn_f32_impl(const float *Q, int64_t nq, const float *C, int64_t nc, 
         float *btau = (float *)(bmeta + (size_t)nq * pl.S * 4);
         if (nc > 0) {
             const int64_t bq = (nq + kb16::BM - 1) / kb16::BM;
-            hipLaunchKernelGGL((kb16::k_gram_bf16<kb16::GM_L2, 0>), dim3((unsigned)(bq * pl.S)),
+            // MN_L2_PROBE=noepi: timing probe (K loop only; results invalid)
+            const char *probe = getenv("MN_L2_PROBE");
+            auto kern = (probe && !strcmp(probe, "noepi")) ? kb16::k_gram_bf16<kb16::GM_L2, 1>
+                                                            : kb16::k_gram_bf16<kb16::GM_L2, 0>;
+            hipLaunchKernelGGL(kern, dim3((unsigned)(bq * pl.S)),
                                dim3(kb16::NT), 0, s, XSq, nq, XSc, nc, 2 * dp, q_off, c_off, excl, qn,
                                cn, L, (int)pl.S, pl.chunk, pl.cap, cbuf, bcnt, btau);
         } else {
@@ -904,6 +1176,248 @@ static int knn_f32_impl(const float *Q, int64_t nq, const float *C, int64_t nc, 
         t_stats.ms_rerank = tm.ms(3, 4);
         t_stats.ms_fallback = tm.ms(4, 5);
         t_stats.ms_total = tm.ms(0, 5);
+    }
+    return MN_OK;
+}
+
+
+// Host driver of MN_KNN_BF16X1 (section 2c).  Returns 1 (nothing written)
+// when some row is too large for the single-bf16 bound: the caller then runs
+// the split generator.
+static int knn_x1(const float *Q, int64_t nq, const float *C, int64_t nc, int32_t d,
+                  int64_t q_off, int64_t c_off, const mn_knn_opts *opts, int32_t *out_idx,
+                  float *out_dist) {
+    using namespace knn;
+    const int k = opts->k;
+    const int margin = opts->margin > 0 ? opts->margin : 16;
+    const int excl = opts->exclude_self ? 1 : 0;
+    hipStream_t s = (hipStream_t)opts->stream;
+    const bool vec4 = (d % 4 == 0) && (((uintptr_t)Q | (uintptr_t)C) % 16 == 0);
+    const bool same = (Q == C) && (nq == nc) && (q_off == c_off);
+    const int dp = (d + 255) / 256 * 256;  // kb16 DALIGN; KB32 stages: nkb = dp / 32 >= 8
+    const int nkb = dp / 32;
+    t_stats.algo = MN_KNN_BF16X1;
+
+    uint16_t *QR = (uint16_t *)scratch(kSlotX1QR, (size_t)nq * dp * 2 + 64);
+    uint16_t *QK = (uint16_t *)scratch(kSlotX1QK, (size_t)nq * dp * 2 + 64);
+    uint16_t *CR = same ? QR : (uint16_t *)scratch(kSlotX1CR, (size_t)nc * dp * 2 + 64);
+    uint16_t *CK = same ? QK : (uint16_t *)scratch(kSlotX1CK, (size_t)nc * dp * 2 + 64);
+    char *aux = (char *)scratch(kSlotX1Aux, (size_t)nq * 24 + (size_t)nc * 16 + 256);
+    int *flags = (int *)scratch(kSlotFlags, 64);
+    int *fb_list = (int *)scratch(kSlotFallback, sizeof(int) * (size_t)nq * 2 + 64);
+    MN_REQUIRE(QR && QK && CR && CK && aux && flags && fb_list, MN_ENOMEM,
+               "mn_knn: bf16x1 scratch allocation failed");
+    float *qn = (float *)aux, *qhn = qn + nq, *qrn = qhn + nq, *tq = qrn + nq, *tau0 = tq + nq,
+          *dlt = tau0 + nq;
+    float *cnv = dlt + nq, *chc = cnv + nc, *chn = chc + nc, *crn = chn + nc;
+    unsigned *cmax = (unsigned *)flags;  // [0..2]: max |c|^2, |ch|, |rc|
+    int *fb_count = flags + 5;  // [3]: non-finite input, [4]: too large for bf16x1
+    unsigned long long *ncand = (unsigned long long *)(flags + 8);
+
+    Timer tm;
+    tm.start(opts->timing != 0, s);
+    MN_HIP_TRY(hipMemsetAsync(flags, 0, 64, s));
+    auto prep = [&](const float *X, int64_t n, uint16_t *R, uint16_t *K, float *nv, float *hcv,
+                    float *hv, float *rv, int corpus) {
+        if (n == 0) return;
+        const int64_t blocks = std::min<int64_t>((n + 7) / 8, 16384);
+        if (vec4)
+            hipLaunchKernelGGL(k_prep_x1<true>, dim3((unsigned)blocks), dim3(256), 0, s, X, n, d,
+                               dp, R, K, nv, hcv, hv, rv, cmax, flags + 3, corpus);
+        else
+            hipLaunchKernelGGL(k_prep_x1<false>, dim3((unsigned)blocks), dim3(256), 0, s, X, n, d,
+                               dp, R, K, nv, hcv, hv, rv, cmax, flags + 3, corpus);
+    };
+    if (same) {
+        prep(C, nc, CR, CK, qn, chc, qhn, qrn, 1);
+    } else {
+        prep(Q, nq, QR, QK, qn, nullptr, qhn, qrn, 0);
+        prep(C, nc, CR, CK, cnv, chc, chn, crn, 1);
+    }
+    MN_KCHECK(s, "k_prep_x1");
+    if (same) cnv = qn;
+    int hflags[8] = {0};
+    MN_HIP_TRY(hipMemcpyAsync(hflags, flags, 32, hipMemcpyDeviceToHost, s));
+    MN_HIP_TRY(hipStreamSynchronize(s));
+    MN_REQUIRE(hflags[3] == 0, MN_ENONFINITE,
+               "mn_knn: input contains NaN/inf (the reference panics in partial_cmp().unwrap())");
+    if (hflags[4] != 0) return 1;
+    tm.mark();
+
+    // phase-1 sample: the first m0 corpus rows, list length L1 (tau0 ~ the
+    // (L1 nc / m0)-th best key); small corpora run phase 1 alone (m0 = nc)
+    int L1 = std::min(std::max((k + 1) / 2, 16), 48);
+    const char *fs = getenv("MN_X1_SAMPLE_DIV");  // experiments: sample = nc / div
+    const int64_t div = (fs && *fs) ? std::max(2, atoi(fs)) : 16;
+    int64_t m0 = std::max<int64_t>(nc / div, (int64_t)64 * L1);
+    m0 = (m0 + kb16::BN - 1) / kb16::BN * kb16::BN;
+    const bool two = m0 + 4 * ksw::BC <= nc;
+    if (!two) {
+        m0 = nc;
+        L1 = std::min(k + margin, kb16::LMAX);
+    }
+    t_stats.sample_rows = m0;
+    t_stats.list_len = L1;
+    const kb16::GramPlan pl = kb16::plan_gram(nq, m0, L1, 1);
+    t_stats.slices = (int)pl.S;
+    const size_t nbuf1 = (size_t)nq * pl.S * pl.cap;
+    uint2 *cbuf1 = (uint2 *)scratch(kSlotLists, nbuf1 * sizeof(uint2) + 64);
+    char *meta1 = (char *)scratch(kSlotListMeta, (size_t)nq * pl.S * 8 + 64);
+    MN_REQUIRE(cbuf1 && meta1, MN_ENOMEM, "mn_knn: phase-1 buffer allocation failed (%zu MB)",
+               (nbuf1 * sizeof(uint2)) >> 20);
+    int *bcnt1 = (int *)meta1;
+    float *btau1 = (float *)(meta1 + (size_t)nq * pl.S * 4);
+    {
+        const int64_t bq = (nq + kb16::BM - 1) / kb16::BM;
+        hipLaunchKernelGGL((kb16::k_gram_bf16<kb16::GM_L2H, 0>), dim3((unsigned)(bq * pl.S)),
+                           dim3(kb16::NT), 0, s, QR, nq, CR, m0, dp, q_off, c_off, excl, qn, cnv,
+                           L1, (int)pl.S, pl.chunk, pl.cap, cbuf1, bcnt1, btau1);
+        MN_KCHECK(s, "k_gram_bf16<L2H>");
+    }
+    hipLaunchKernelGGL(k_tau_x1, dim3((unsigned)((nq + 255) / 256)), dim3(256), 0, s, nq,
+                       (int)pl.S, btau1, qn, qhn, qrn, cmax, d, dp, tq, tau0, dlt);
+    MN_KCHECK(s, "k_tau_x1");
+    tm.mark();
+
+    int S2 = 0, cap2 = 0;
+    uint2 *cbuf2 = nullptr;
+    int *cnt2 = nullptr;
+    const char *probe = getenv("MN_X1_PROBE");  // noepi: sweep K loop only, no results
+    if (two) {
+        const double expect = (double)L1 * (double)(nc - m0) / (double)m0;
+        const ksw::SweepPlan p2 = ksw::plan_sweep(nq, nc - m0, expect);
+        S2 = (int)p2.S;
+        cap2 = p2.cap;
+        t_stats.sweep_slices = S2;
+        t_stats.sweep_cap = cap2;
+        const size_t nbuf2 = (size_t)nq * S2 * cap2;
+        cbuf2 = (uint2 *)scratch(kSlotX1Buf2, nbuf2 * sizeof(uint2) + 64);
+        cnt2 = (int *)scratch(kSlotX1Meta2, (size_t)nq * S2 * 4 + 64);
+        MN_REQUIRE(cbuf2 && cnt2, MN_ENOMEM, "mn_knn: sweep buffer allocation failed (%zu MB)",
+                   (nbuf2 * sizeof(uint2)) >> 20);
+        const int64_t nqb = (nq + ksw::BQ - 1) / ksw::BQ;
+        const int64_t grid = nqb * p2.S;
+        MN_REQUIRE(grid < INT_MAX && nq * 32 < INT_MAX && nc * 32 < INT_MAX, MN_ENOTSUP,
+                   "mn_knn: sweep grid too large (split the queries / corpus)");
+        auto kern = (probe && !strcmp(probe, "noepi")) ? ksw::k_gram_sweep<1> : ksw::k_gram_sweep<0>;
+        hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(ksw::NT), 0, s, QK, nq, CK, nc, nkb,
+                           q_off, c_off, excl, tq, tau0, chc, m0, S2, p2.chunk, cap2, cbuf2, cnt2);
+        MN_KCHECK(s, "k_gram_sweep");
+    }
+    tm.mark();
+    if (probe && *probe) {  // timing probe: outputs are not produced
+        MN_HIP_TRY(hipStreamSynchronize(s));
+        if (tm.on) {
+            t_stats.ms_norms = tm.ms(0, 1);
+            t_stats.ms_sample = tm.ms(1, 2);
+            t_stats.ms_sweep = tm.ms(2, 3);
+            t_stats.ms_gram = tm.ms(1, 3);
+        }
+        return MN_OK;
+    }
+
+    const int64_t nvalid = std::max<int64_t>(same ? nc - 1 : nc, 0);
+    int *big_count = flags + 6;
+    int *big_list = fb_list + nq;  // second half of the fallback-list slot
+    // pass 1: up to 512 candidates per row, 4 rows per block; pass 2 (the rare
+    // rows with more): up to 1024, one row per block
+#define MN_RRX(NRV, WPB, V, NB, QL, QN, BC, BL)                                                 \
+    hipLaunchKernelGGL((k_rerank_x1<NRV, WPB, V>), dim3((unsigned)(NB)), dim3(64 * WPB), 0, s, \
+                       Q, nq, C, d, c_off, (int)pl.S, pl.cap, cbuf1, bcnt1, tau0, S2, cap2,     \
+                       cbuf2, cnt2, dlt, k, nvalid, QL, QN, BC, BL, out_idx, out_dist,          \
+                       fb_count, fb_list)
+    const int64_t nb1 = (nq + 3) / 4;
+    if (vec4) MN_RRX(8, 4, true, nb1, (const int *)nullptr, (const int *)nullptr, big_count, big_list);
+    else MN_RRX(8, 4, false, nb1, (const int *)nullptr, (const int *)nullptr, big_count, big_list);
+    MN_KCHECK(s, "k_rerank_x1<8>");
+    int nbig = 0;
+    MN_HIP_TRY(hipMemcpyAsync(&nbig, big_count, 4, hipMemcpyDeviceToHost, s));
+    MN_HIP_TRY(hipStreamSynchronize(s));
+    if (nbig > 0) {
+        if (vec4) MN_RRX(16, 1, true, nbig, big_list, big_count, (int *)nullptr, (int *)nullptr);
+        else MN_RRX(16, 1, false, nbig, big_list, big_count, (int *)nullptr, (int *)nullptr);
+    }
+#undef MN_RRX
+    MN_KCHECK(s, "k_rerank_x1");
+    tm.mark();
+    const unsigned fgrid = (unsigned)std::min<int64_t>(nq, 1024);
+    if (vec4)
+        hipLaunchKernelGGL(k_fallback<true>, dim3(fgrid), dim3(FB_THREADS), 0, s, Q, C, nc, d,
+                           q_off, c_off, excl, k, fb_count, fb_list, out_idx, out_dist);
+    else
+        hipLaunchKernelGGL(k_fallback<false>, dim3(fgrid), dim3(FB_THREADS), 0, s, Q, C, nc, d,
+                           q_off, c_off, excl, k, fb_count, fb_list, out_idx, out_dist);
+    MN_KCHECK(s, "k_fallback");
+    tm.mark();
+    if (tm.on) {
+        hipLaunchKernelGGL(k_count_cands, dim3(1024), dim3(256), 0, s, bcnt1, nq * pl.S, pl.cap,
+                           ncand);
+        if (two)
+            hipLaunchKernelGGL(k_count_cands, dim3(1024), dim3(256), 0, s, cnt2, nq * S2, cap2,
+                               ncand);
+        MN_KCHECK(s, "k_count_cands");
+    }
+    int64_t hf[8] = {0};
+    MN_HIP_TRY(hipMemcpyAsync(hf, flags, 64, hipMemcpyDeviceToHost, s));
+    MN_HIP_TRY(hipStreamSynchronize(s));
+    t_stats.n_uncertified = ((const int *)hf)[5];
+    if (tm.on) {
+        t_stats.n_candidates = hf[4];
+        t_stats.ms_norms = tm.ms(0, 1);
+        t_stats.ms_sample = tm.ms(1, 2);
+        t_stats.ms_sweep = tm.ms(2, 3);
+        t_stats.ms_gram = tm.ms(1, 3);
+        t_stats.ms_rerank = tm.ms(3, 4);
+        t_stats.ms_fallback = tm.ms(4, 5);
+        t_stats.ms_total = tm.ms(0, 5);
+    }
+    return MN_OK;
+}
+
+// Host entry shared by mn_knn_f32 and mn_knn_f32_qc: argument checks, the
+// generator choice, and the Euclidean (MN_L2) root.
+static int knn_f32_impl(const float *Q, int64_t nq, const float *C, int64_t nc, int32_t d,
+                        int64_t q_off, int64_t c_off, const mn_knn_opts *opts,
+                        int32_t *out_idx, float *out_dist) {
+    using namespace knn;
+    clear_error();
+    t_stats = mn_knn_stats{};
+    MN_REQUIRE(opts, MN_EINVAL, "mn_knn: opts is NULL");
+    MN_REQUIRE(Q && C && out_idx && out_dist, MN_EINVAL, "mn_knn: NULL pointer argument");
+    MN_REQUIRE(nq >= 0 && nc >= 0 && d >= 1, MN_EINVAL, "mn_knn: bad shape nq=%lld nc=%lld d=%d",
+               (long long)nq, (long long)nc, d);
+    MN_REQUIRE(opts->metric == MN_L2SQ || opts->metric == MN_L2, MN_ENOTSUP,
+               "mn_knn_f32: metric %d not supported here", opts->metric);
+    const int k = opts->k;
+    MN_REQUIRE(k >= 1 && k <= KMAX, MN_ENOTSUP, "mn_knn: k=%d outside [1,%d]", k, KMAX);
+    const int algo = opts->algo;
+    MN_REQUIRE(algo >= MN_KNN_AUTO && algo <= MN_KNN_BF16X1, MN_EINVAL, "mn_knn: bad algo %d",
+               algo);
+    MN_REQUIRE(q_off >= 0 && c_off >= 0 && q_off + nq <= INT_MAX && c_off + nc <= INT_MAX,
+               MN_EINVAL, "mn_knn: global ids must fit int32");
+    t_stats.n_queries = nq;
+    int rc = 1;
+    const bool x1 = algo == MN_KNN_BF16X1 || (algo == MN_KNN_AUTO && nc >= (1 << 17));
+    if (x1 && nq > 0 && nc > 0) {
+        rc = knn_x1(Q, nq, C, nc, d, q_off, c_off, opts, out_idx, out_dist);
+        if (rc < 0) return rc;
+    }
+    if (rc == 1) {
+        int a = algo == MN_KNN_BF16X1 ? MN_KNN_AUTO : algo;
+        if (a == MN_KNN_AUTO) {
+            const int margin = opts->margin > 0 ? opts->margin : 16;
+            a = (k + margin <= kb16::LMAX) ? MN_KNN_BF16X3 : MN_KNN_F32;
+        }
+        rc = knn_f32_core(Q, nq, C, nc, d, q_off, c_off, opts, out_idx, out_dist, a);
+        if (rc != MN_OK) return rc;
+    }
+    if (opts->metric == MN_L2 && nq > 0) {
+        const int64_t n = nq * k;
+        hipStream_t s = (hipStream_t)opts->stream;
+        hipLaunchKernelGGL(k_sqrt_dist, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s,
+                           out_dist, n);
+        MN_KCHECK(s, "k_sqrt_dist");
+        MN_HIP_TRY(hipStreamSynchronize(s));
     }
     return MN_OK;
 }

@@ -16,7 +16,7 @@ MN_OK, MN_EINVAL, MN_ENOMEM, MN_ENONFINITE, MN_ECAP, MN_EHIP, MN_ENOTSUP = 0, -1
 _NAMES = {-1: "MN_EINVAL", -2: "MN_ENOMEM", -3: "MN_ENONFINITE", -4: "MN_ECAP", -5: "MN_EHIP",
           -6: "MN_ENOTSUP"}
 
-MN_L2SQ, MN_COS_RECT = 0, 1
+MN_L2SQ, MN_COS_RECT, MN_L2 = 0, 1, 2
 
 
 class MnError(RuntimeError):
@@ -32,14 +32,16 @@ class KnnOpts(C.Structure):
 
 
 # enum mn_knn_algo: candidate generator of mn_knn_f32 (outputs are identical)
-MN_KNN_AUTO, MN_KNN_F32, MN_KNN_BF16X3 = 0, 1, 2
+MN_KNN_AUTO, MN_KNN_F32, MN_KNN_BF16X3, MN_KNN_BF16X1 = 0, 1, 2, 3
 
 
 class KnnStats(C.Structure):
     _fields_ = [("n_queries", C.c_int64), ("n_uncertified", C.c_int64), ("slices", C.c_int32),
                 ("list_len", C.c_int32), ("ms_norms", C.c_float), ("ms_gram", C.c_float),
                 ("ms_rerank", C.c_float), ("ms_fallback", C.c_float), ("ms_total", C.c_float),
-                ("algo", C.c_int32)]
+                ("algo", C.c_int32), ("ms_sample", C.c_float), ("ms_sweep", C.c_float),
+                ("sample_rows", C.c_int64), ("n_candidates", C.c_int64),
+                ("sweep_slices", C.c_int32), ("sweep_cap", C.c_int32)]
 
     def as_dict(self):
         return {f: getattr(self, f) for f, _ in self._fields_}

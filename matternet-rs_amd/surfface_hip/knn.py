@@ -31,7 +31,8 @@ class KnnResult:
     stats: dict
 
 
-ALGOS = {"auto": _lib.MN_KNN_AUTO, "f32": _lib.MN_KNN_F32, "bf16x3": _lib.MN_KNN_BF16X3}
+ALGOS = {"auto": _lib.MN_KNN_AUTO, "f32": _lib.MN_KNN_F32, "bf16x3": _lib.MN_KNN_BF16X3,
+         "bf16x1": _lib.MN_KNN_BF16X1}
 
 
 def _opts(k, margin, timing, stream, exclude_self=True, metric=_lib.MN_L2SQ, algo="auto"):
@@ -47,15 +48,19 @@ def last_stats() -> dict:
 
 
 def knn_l2sq(X: torch.Tensor, k: int, margin: int = 16, timing: bool = False,
-             stream=None, out_idx=None, out_dist=None, algo: str = "auto") -> KnnResult:
-    """Exact kNN of every row of X [n, d] (f32, on device) by squared L2.
-    algo picks the candidate generator ("auto" = "bf16x3" when k + margin <= 64,
-    "f32"); the result is the same bit for bit."""
+             stream=None, out_idx=None, out_dist=None, algo: str = "auto",
+             euclidean: bool = False) -> KnnResult:
+    """Exact kNN of every row of X [n, d] (f32, on device) by squared L2
+    (euclidean=True: DistanceMetric::Euclidean, the correctly rounded sqrt of
+    the same fold, computed in the library).  algo picks the candidate
+    generator ("auto": "bf16x1" for corpora >= 2^17 rows, else "bf16x3" when
+    k + margin <= 64, else "f32"); the result is the same bit for bit."""
     X = require_cuda(X, torch.float32, "X", 2)
     n, d = X.shape
     idx = out_idx if out_idx is not None else torch.empty((n, k), dtype=torch.int32, device=X.device)
     dist = out_dist if out_dist is not None else torch.empty((n, k), dtype=torch.float32, device=X.device)
-    o = _opts(k, margin, timing, stream, algo=algo)
+    o = _opts(k, margin, timing, stream, algo=algo,
+              metric=_lib.MN_L2 if euclidean else _lib.MN_L2SQ)
     _lib.check(_lib.lib().mn_knn_f32(ptr(X), n, d, C.byref(o), ptr(idx), ptr(dist)))
     return KnnResult(idx, dist, last_stats())
 
@@ -103,13 +108,10 @@ def build_candidate_graph(means, k_neighbors: int,
     if k < 1:
         e = torch.empty(0, dtype=torch.int64, device=X.device)
         return e, e.clone(), torch.empty(0, dtype=torch.float32, device=X.device)
-    r = knn_l2sq(X, k)
+    r = knn_l2sq(X, k, euclidean=metric == DistanceMetric.Euclidean)
     u = torch.arange(c, device=X.device, dtype=torch.int64).repeat_interleave(k)
     v = r.idx.reshape(-1).to(torch.int64)
-    dist = r.dist.reshape(-1)
-    if metric == DistanceMetric.Euclidean:
-        dist = torch.sqrt(dist)
-    return u, v, dist
+    return u, v, r.dist.reshape(-1)
 
 
 def cos_last_stats() -> dict:

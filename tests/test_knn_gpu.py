@@ -18,7 +18,7 @@ GS = np.load(__import__("os").path.join(__import__("os").path.dirname(__file__),
                                         "golden_small.npz"))
 
 
-@pytest.fixture(params=["bf16x3", "f32"])
+@pytest.fixture(params=["bf16x1", "bf16x3", "f32"])
 def algo(request):
     return request.param
 
