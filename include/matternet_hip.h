@@ -130,6 +130,22 @@ int mn_knn_merge_f32(const int32_t *part_idx, const float *part_dist,
                      int32_t parts, int64_t nq, int32_t k, int32_t *out_idx,
                      float *out_dist, void *stream);
 
+/* f64 Euclidean kNN with the reference's exact f64 folds, for its three f64
+ * call sites: topk_by_l2 (src_legacy/energymaps.rs:875-892: d = sum
+ * (a-b)*(a-b), stable sort, use_sqrt = 0), prepare_query_item's energy-mode
+ * nearest sub-centroid (src_legacy/core.rs:872-909: sqrt'd distance, 1-NN
+ * with strict '<' = k 1, use_sqrt 1) and estimate_intrinsic_dimension's
+ * Two-NN distances (src_legacy/clustering.rs:132-195: k 2, use_sqrt 1).
+ * Q [nq][d], C [nc][d] (device; f64, or f32 widened exactly when
+ * x_is_f64 == 0); q_ids [nq] (device, may be NULL): the corpus index each
+ * query excludes (the reference's j != i).  out_idx [nq][k] int32 (-1 pad),
+ * out_dist [nq][k] f64 (+inf pad), in (dist, idx) order = the reference's
+ * stable sort truncated to k.  Bit-exact.  k <= 64, nq <= 2097120 per call.
+ * MN_ENONFINITE on a NaN distance (the reference's partial_cmp().unwrap()). */
+int mn_knn_l2_f64(const void *Q, int64_t nq, const void *C, int64_t nc, int32_t d,
+                  int32_t x_is_f64, const int64_t *q_ids, int32_t k, int32_t use_sqrt,
+                  int32_t *out_idx, double *out_dist, void *stream);
+
 /* Statistics of the calling thread's last mn_knn_* call. */
 int mn_knn_last_stats(mn_knn_stats *out);
 

@@ -5,7 +5,9 @@ Every op runs on the GPU through the C ABI; there is no CPU fallback.
 """
 from . import _lib
 from ._lib import MnError, lib
-from . import energy, laplacian, search, sorted_index, sparsification
+from . import energy, l2f64, laplacian, search, sorted_index, sparsification
+from .l2f64 import (estimate_intrinsic_dimension, knn_l2_f64, nearest_subcentroid,
+                    prepare_query_items_energy, topk_by_l2, topk_by_l2_rows)
 from .search import (normalise_query_lambda, prepare_query_lambdas, search_lambda_aware,
                      search_lambda_aware_hybrid)
 from .sparsification import SfGrassSparsifier, sparsify_rows
@@ -31,4 +33,5 @@ __all__ = ["MnError", "lib", "knn_cos_columns", "knn_cos_bf16", "knn_cos_bf16_qc
            "normalise_lambdas", "sorted_index", "SortedLambdas", "sparsification",
            "SfGrassSparsifier", "sparsify_rows", "search", "search_lambda_aware",
            "normalise_query_lambda", "prepare_query_lambdas",
-           "search_lambda_aware_hybrid"]
+           "search_lambda_aware_hybrid", "l2f64", "knn_l2_f64", "topk_by_l2", "topk_by_l2_rows",
+           "nearest_subcentroid", "prepare_query_items_energy", "estimate_intrinsic_dimension"]

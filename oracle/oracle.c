@@ -1129,3 +1129,62 @@ int or_search_lambda_aware_hybrid(const double *X, int64_t n, int32_t f, const d
     free(xn);
     return rc;
 }
+
+/* ------------------------------------------------------------------------ */
+/* K1 — f64 Euclidean call sites (topk_by_l2 / prepare_query_item / Two-NN) */
+/* ------------------------------------------------------------------------ */
+
+/* energymaps.rs:881-885 / core.rs:895-900 / clustering.rs:160-165:
+ * zip().map((a-b)*(a-b)).sum::<f64>() — sequential, from -0.0 */
+static inline double fold_l2sq_f64(const double *a, const double *b, int32_t d) {
+    double acc = -0.0;
+    for (int32_t t = 0; t < d; ++t) {
+        double diff = a[t] - b[t];
+        acc = acc + diff * diff;
+    }
+    return acc;
+}
+
+int or_knn_l2_f64(const double *Q, int64_t nq, const double *C, int64_t nc, int32_t d,
+                  const int64_t *q_ids, int32_t k, int use_sqrt, int nthreads,
+                  int32_t *out_idx, double *out_dist) {
+    if (!Q || !C || !out_idx || !out_dist || nq < 0 || nc < 0 || d < 1 || k < 1)
+        return OR_EINVAL;
+    set_threads(nthreads);
+    int err = 0;
+#pragma omp parallel for schedule(dynamic, 1)
+    for (int64_t q = 0; q < nq; ++q) {
+        /* sorted (d, j) list of the k best: insertion keeps the stable order */
+        double *bd = (double *)malloc(sizeof(double) * (size_t)k);
+        int32_t *bj = (int32_t *)malloc(sizeof(int32_t) * (size_t)k);
+        int32_t cnt = 0;
+        const double *qr = Q + q * (int64_t)d;
+        for (int64_t j = 0; j < nc; ++j) {
+            if (q_ids && q_ids[q] == j) continue;
+            double v = fold_l2sq_f64(qr, C + j * (int64_t)d, d);
+            if (use_sqrt) v = sqrt(v);
+            if (v != v) {
+#pragma omp atomic write
+                err = OR_ENONFINITE;
+                break;
+            }
+            if (cnt == k && !(v < bd[k - 1])) continue; /* later j loses ties */
+            int32_t p = cnt < k ? cnt : k - 1;
+            while (p > 0 && v < bd[p - 1]) {
+                bd[p] = bd[p - 1];
+                bj[p] = bj[p - 1];
+                --p;
+            }
+            bd[p] = v;
+            bj[p] = (int32_t)j;
+            if (cnt < k) ++cnt;
+        }
+        for (int32_t r = 0; r < k; ++r) {
+            out_idx[q * k + r] = r < cnt ? bj[r] : -1;
+            out_dist[q * k + r] = r < cnt ? bd[r] : INFINITY;
+        }
+        free(bd);
+        free(bj);
+    }
+    return err;
+}

@@ -74,6 +74,23 @@ int or_knn_cos_bf16_rows(const uint16_t *X, int64_t n, int32_t d, int32_t topk,
                          const int64_t *rows, int64_t nrows, int nthreads,
                          int32_t *out_idx, double *out_dist, double *out_w);
 
+/* f64 Euclidean kNN, the reference's three f64 call sites (exact folds):
+ *  - topk_by_l2 (src_legacy/energymaps.rs:875-892): d = sum (a-b)*(a-b),
+ *    f64 sequential fold, j != i, stable sort_by(partial_cmp), truncate k;
+ *  - prepare_query_item energy mode (src_legacy/core.rs:872-909): d =
+ *    sqrt(sum (a-b).powi(2)), 1-NN with strict '<' (lowest index among ties);
+ *  - estimate_intrinsic_dimension (src_legacy/clustering.rs:132-195): sqrt'd
+ *    distances of sampled rows to all j != i, stable sort, d1 and d2.
+ * Queries Q [nq][d], corpus C [nc][d] (f64, row-major); q_ids[q] (may be
+ * NULL) = the corpus index excluded for query q.  use_sqrt: order and report
+ * sqrt(d) (ties under the rounded root go to the smaller index, as the
+ * reference's stable sort / strict '<' on the rooted values).  out_idx
+ * [nq][k] (-1 padded), out_dist [nq][k] (+inf padded).  OR_ENONFINITE if a
+ * distance is NaN (the reference's partial_cmp().unwrap() panics). */
+int or_knn_l2_f64(const double *Q, int64_t nq, const double *C, int64_t nc, int32_t d,
+                  const int64_t *q_ids, int32_t k, int use_sqrt, int nthreads,
+                  int32_t *out_idx, double *out_dist);
+
 /* ---- K2: Laplacian assembly --------------------------------------------- */
 
 /* A.2 UNION / unnormalised (legacy).

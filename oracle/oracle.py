@@ -48,6 +48,7 @@ F = C.c_float
 def _declare(L):
     L.or_knn_l2sq_f32.argtypes = [P, I64, I32, I32, I64, I64, C.c_int, C.c_int, P, P]
     L.or_knn_l2sq_rows_f32.argtypes = [P, I64, I32, I32, P, I64, C.c_int, P, P]
+    L.or_knn_l2_f64.argtypes = [P, I64, P, I64, I32, P, I32, C.c_int, C.c_int, P, P]
     L.or_knn_cos_f64.argtypes = [P, I64, I32, I32, D, D, D, I64, I64, C.c_int, P, P, P]
     L.or_knn_cos_bf16_rows.argtypes = [P, I64, I32, I32, D, D, D, P, I64, C.c_int, P, P, P]
     L.or_laplacian_union.argtypes = [I64, I32, P, P, I64, P, P, P, P]
@@ -100,6 +101,19 @@ def knn_l2sq_rows(X, k, rows, nthreads=0):
     dist = np.empty((len(rows), k), np.float32)
     _check(lib().or_knn_l2sq_rows_f32(_p(X), n, d, k, _p(rows), len(rows), nthreads, _p(idx),
                                       _p(dist)), "knn_l2sq_rows")
+    return idx, dist
+
+
+def knn_l2_f64(Q, Cm, k, q_ids=None, use_sqrt=False, nthreads=0):
+    """f64 Euclidean kNN of the rows of Q against C (oracle.h or_knn_l2_f64)."""
+    Q = np.ascontiguousarray(Q, dtype=np.float64)
+    Cm = np.ascontiguousarray(Cm, dtype=np.float64)
+    nq, d = Q.shape
+    ids = None if q_ids is None else np.ascontiguousarray(q_ids, dtype=np.int64)
+    idx = np.empty((nq, k), np.int32)
+    dist = np.empty((nq, k), np.float64)
+    _check(lib().or_knn_l2_f64(_p(Q), nq, _p(Cm), Cm.shape[0], d, _p(ids), k,
+                               1 if use_sqrt else 0, nthreads, _p(idx), _p(dist)), "knn_l2_f64")
     return idx, dist
 
 

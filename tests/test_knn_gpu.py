@@ -168,3 +168,22 @@ def test_k64_uses_f32_generator_in_auto():
     assert_exact(idx, dist, ridx, rdist)
     with pytest.raises(S.MnError):
         hip_knn(X, 60, algo="bf16x3")
+
+
+@pytest.mark.parametrize("algo_e", ["bf16x1", "bf16x3", "f32"])
+def test_euclidean_metric_sqrt_is_correctly_rounded(algo_e):
+    """DistanceMetric::Euclidean (mst.rs:382-389, distance.rs:195-203): the
+    library returns Rust's correctly rounded f32::sqrt of the L2^2 fold (gfx950
+    sqrtf is not correctly rounded; numpy's float32 sqrt is IEEE)."""
+    import surfface_hip as S
+    X = datagen.clustered(4000, 40, seed=21, blobs=9, dup_frac=0.01, zero_frac=0.002)
+    r = S.knn_l2sq(torch.from_numpy(X).cuda(), 12, euclidean=True, algo=algo_e)
+    ridx, rdist = O.knn_l2sq(X, 12)
+    np.testing.assert_array_equal(r.idx.cpu().numpy(), ridx)
+    np.testing.assert_array_equal(r.dist.cpu().numpy().view(np.uint32),
+                                  np.sqrt(rdist).view(np.uint32))
+    # candidate-graph mirror (mst.rs:312-363) with the Euclidean metric
+    u, v, dist = S.build_candidate_graph(X, 12, S.DistanceMetric.Euclidean)
+    np.testing.assert_array_equal(v.cpu().numpy(), ridx.reshape(-1))
+    np.testing.assert_array_equal(dist.cpu().numpy().view(np.uint32),
+                                  np.sqrt(rdist).reshape(-1).view(np.uint32))
