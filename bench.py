@@ -32,6 +32,10 @@ import torch  # noqa: E402
 FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md chip-level table (dense f32 MFMA)
 HBM_PEAK_GBS = 8000.0
 BF16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X dense bf16 (MI355X_MICROARCH.md), no sparsity
+# scripts/probes/probe_mfma_peak.hip on the box (profiles/r02_mfma_peak.txt):
+# the sustained 32x32x16 bf16 rate on random operands under load (DVFS)
+MEASURED_BF16_32X32_TFLOPS = 1887.0
+FP64_VALU_PEAK_TFLOPS = 78.6
 
 
 def parse():
@@ -55,6 +59,11 @@ def parse():
                     help="skip the C3 legs (Laplacian assembly, energy pass, sorted index)")
     ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_gram_latest.json"),
                     help="PMC-derived HBM bytes per launch of the Gram kernel (optional)")
+    ap.add_argument("--time-budget-s", type=float, default=420.0,
+                    help="N>1: cap warmup+steps so the whole run fits this budget (the cap is "
+                         "reported in the line)")
+    ap.add_argument("--query-chunk", type=int, default=2_097_152,
+                    help="N>1: queries per per-shard kNN call (bounds candidate buffers)")
     return ap.parse_args()
 
 
@@ -92,23 +101,52 @@ def main():
     last = {}
 
     def knn_fn(Q, C, kk, c_off):
-        r = S.knn_l2sq_qc(Q, C, kk, q_offset=0, c_offset=c_off, timing=True)
-        gram_ms.append(r.stats["ms_gram"])
-        last["stats"] = r.stats
-        return r.idx, r.dist
+        # per-shard exact top-k of all queries, in query chunks (the candidate
+        # buffers scale with the queries of one call)
+        nq_all = Q.shape[0]
+        idx = torch.empty((nq_all, kk), dtype=torch.int32, device=Q.device)
+        dd = torch.empty((nq_all, kk), dtype=torch.float32, device=Q.device)
+        g = 0.0
+        for a0 in range(0, nq_all, a.query_chunk):
+            b0 = min(nq_all, a0 + a.query_chunk)
+            r = S.knn_l2sq_qc(Q[a0:b0], C, kk, q_offset=a0, c_offset=c_off, timing=True)
+            idx[a0:b0].copy_(r.idx)
+            dd[a0:b0].copy_(r.dist)
+            g += r.stats.get("ms_sweep") or r.stats["ms_gram"]
+            last["stats"] = r.stats
+        gram_ms.append(g)
+        return idx, dd
 
     def step():
         if world == 1:
             r = S.knn_l2sq(X, k, timing=True)
-            gram_ms.append(r.stats["ms_gram"])
+            # the dominant kernel: the bf16x1 sweep (phase 2), else the Gram
+            gram_ms.append(r.stats.get("ms_sweep") or r.stats["ms_gram"])
+            last["stats"] = r.stats
             return r.idx, r.dist, r.stats
         # all-gather queries, exact per-shard top-k vs the resident shard,
         # all-to-all of the lists, merge on the owner (surfface_hip/dist.py)
         idx, dd = sharded_knn(X, k, knn_fn=knn_fn, merge_fn=S.merge_parts)
         return idx, dd, last["stats"]
 
-    for _ in range(a.warmup):
+    steps_req, warm_req = a.steps, a.warmup
+    t_w = time.perf_counter()
+    for i in range(a.warmup):
         step()
+        if world > 1 and i == 0:
+            # time budget (N>1: every rank does N x the C2 work per step): one
+            # warmup step measured, then warmup + steps capped to fit
+            torch.cuda.synchronize()
+            tw = torch.tensor([time.perf_counter() - t_w], dtype=torch.float64, device=dev)
+            dist.all_reduce(tw, op=dist.ReduceOp.MAX)
+            per = float(tw.item())
+            left = max(a.time_budget_s - per, 0.0)
+            a.warmup = 1
+            a.steps = max(1, min(a.steps, int(left / max(per, 1e-3))))
+            break
+    if world > 1 and warm_req == 0:
+        # no warmup step to measure: budget on the estimate of N x ~2 s per step
+        a.steps = max(1, min(a.steps, int(a.time_budget_s / (2.0 * world))))
     gram_ms.clear()
     if dist:
         dist.barrier()
@@ -129,43 +167,68 @@ def main():
     pairs = float(n_tot) * float(n_tot)
     value = pairs * a.steps / el
 
-    # roofline of the dominant kernel: algorithmic flops per launch
-    # = 2 * nq * nc_shard * d (full Gram); duration from HIP
-    # events recorded on the launch stream inside the library.
-    nq = n_tot
-    flops_launch = 2.0 * nq * n_loc * d
-    gms = float(np.mean(gram_ms)) if gram_ms else float("nan")
-    achieved = flops_launch / (gms * 1e-3) / 1e12
+    # roofline of the dominant kernel: algorithmic flops per launch =
+    # 2 * nq * nc * d over the rows that launch sweeps; its
+    # duration from HIP events recorded on the launch stream inside the library
     st0 = out[2]
-    split = st0.get("algo") == 2
-    kname = "k_gram_bf16<GM_L2>" if split else "k_gram_topk"
-    traffic = None
-    if os.path.exists(a.pmc_json):
-        try:
-            pm = json.load(open(a.pmc_json))
-            if (pm.get("rows_per_gpu") == n_loc and pm.get("dim") == d and world == 1
-                    and pm.get("kernel", "").startswith(kname.split("<")[0])):
-                traffic = pm.get("hbm_bytes_per_launch")
-        except (OSError, ValueError):
-            traffic = None
-    if split:
-        # bf16-split candidates: every f32 product is hi*hi + hi*lo + lo*hi, three
-        # bf16 MFMA products, so the ceiling for this algorithm's Gram flops is the
-        # dense bf16 MFMA peak / 3
+    nq = n_tot
+    gms = float(np.mean(gram_ms)) if gram_ms else float("nan")
+    algo = st0.get("algo")
+    if algo == 3:
+        # two-phase single-bf16 generator: phase 2 (k_gram_sweep) sweeps the
+        # rows outside the phase-1 sample, one bf16 product per f32 product
+        m0 = int(st0.get("sample_rows") or 0)
+        nc_sw = n_loc - m0
+        kname = "k_gram_sweep"
+        flops_launch = 2.0 * nq * nc_sw * d
+        achieved = flops_launch / (gms * 1e-3) / 1e12
+        ms_all = float(st0["ms_gram"])
+        roof = {"bound": "mfma", "kernel": kname, "achieved": round(achieved, 3),
+                "peak": BF16_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                "frac": round(achieved / BF16_MFMA_PEAK_TFLOPS, 4),
+                "traffic": None, "ms_per_launch": round(gms, 3), "flop_per_launch": flops_launch,
+                "peak_basis": "dense bf16 MFMA 2500 TFLOP/s (one v_mfma_f32_32x32x16_bf16 product "
+                              "per f32 product: x ~ bf16(x), certified by the residual-norm bound)",
+                "measured_mfma_ceiling": {"tflops": MEASURED_BF16_32X32_TFLOPS,
+                                          "frac": round(achieved / MEASURED_BF16_32X32_TFLOPS, 4),
+                                          "basis": "probe_mfma_peak.hip: back-to-back "
+                                                   "v_mfma_f32_32x32x16_bf16 on random register "
+                                                   "operands, every CU (DVFS-limited clock)"},
+                "whole_gram": {"ms": round(ms_all, 3), "sample_ms": round(st0["ms_sample"], 3),
+                               "sample_rows": m0,
+                               "effective_tflops": round(2.0 * nq * n_loc * d / (ms_all * 1e-3) / 1e12, 1),
+                               "vs_f32_mfma_peak": round(2.0 * nq * n_loc * d / (ms_all * 1e-3) / 1e12
+                                                         / FP32_MFMA_PEAK_TFLOPS, 3)}}
+    elif algo == 2:
+        kname = "k_gram_bf16<GM_L2>"
+        flops_launch = 2.0 * nq * n_loc * d
+        achieved = flops_launch / (gms * 1e-3) / 1e12
         peak = BF16_MFMA_PEAK_TFLOPS / 3.0
         roof = {"bound": "mfma", "kernel": kname, "achieved": round(achieved, 3),
                 "peak": round(peak, 1), "unit": "TFLOP/s", "frac": round(achieved / peak, 4),
-                "traffic": traffic, "ms_per_launch": round(gms, 3),
-                "flop_per_launch": flops_launch,
+                "traffic": None, "ms_per_launch": round(gms, 3), "flop_per_launch": flops_launch,
                 "peak_basis": ("dense bf16 MFMA 2500 TFLOP/s / 3 bf16 products per f32 product "
-                               "(x = hi + lo; hi.hi + hi.lo + lo.hi)"),
-                "mfma_issued_tflops": round(3.0 * achieved, 1),
-                "vs_f32_mfma_peak": round(achieved / FP32_MFMA_PEAK_TFLOPS, 3)}
+                               "(x = hi + lo; hi.hi + hi.lo + lo.hi)")}
     else:
+        kname = "k_gram_topk"
+        flops_launch = 2.0 * nq * n_loc * d
+        achieved = flops_launch / (gms * 1e-3) / 1e12
         roof = {"bound": "mfma", "kernel": kname, "achieved": round(achieved, 3),
                 "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
-                "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": traffic,
+                "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": None,
                 "ms_per_launch": round(gms, 3), "flop_per_launch": flops_launch}
+    if os.path.exists(a.pmc_json) and world == 1:
+        # HBM bytes per launch from separate FETCH_SIZE / WRITE_SIZE rocprofv3
+        # passes of an earlier run (FETCH x2 per the gfx950 note); labelled
+        # with the run it came from
+        try:
+            pm = json.load(open(a.pmc_json))
+            if (pm.get("rows_per_gpu") == n_loc and pm.get("dim") == d
+                    and pm.get("kernel", "").startswith(kname.split("<")[0])):
+                roof["traffic"] = pm.get("hbm_bytes_per_launch")
+                roof["traffic_source"] = pm.get("source", os.path.relpath(a.pmc_json, ROOT))
+        except (OSError, ValueError):
+            pass
 
     # C3 legs (configs[2]): Laplacian assembly + energymaps/taumode pass + index,
     # on this rank's rows (timed individually after the headline step)
@@ -179,35 +242,54 @@ def main():
 
     cpu = None
     parity = None
+    energy_cpu = None
     if rank == 0 and world == 1 and a.cpu_seconds > 0:
         cpu, parity = cpu_baseline(X, out[0], out[1], k, a.cpu_seconds)
+        if c3 is not None:
+            energy_cpu = energy_cpu_baseline(X, c3.pop("_Lf"), a.cpu_seconds)
+    elif c3 is not None:
+        c3.pop("_Lf", None)
 
     if rank == 0:
         st = out[2]
+        gen = {3: "bf16x1 two-phase MFMA (sample thresholds + fixed-threshold sweep)",
+               2: "bf16x3 split MFMA", 1: "f32 MFMA"}.get(st.get("algo"), "f32 MFMA")
+        energy = None
+        if c3 is not None:
+            er = c3["energy_rows"]
+            energy = {"rows_per_sec": c3["energy_rows_per_sec"],
+                      "workload": "C3: 1M items x 768 features vs the 768 x 768 feature "
+                                  "Laplacian (taumode, Median tau)",
+                      "roofline": er["roofline"], "cpu_baseline": energy_cpu}
         line = {
             "metric": "vector-pairs/sec for k-NN graph build (N=1M, d=768) + Laplacian energy rows/sec",
             "value": value, "unit": "pairs/s", "n_gpus": world, "steps": a.steps,
             "warmup": a.warmup, "ms_per_step": round(ms_step, 3), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "f32",
-            "candidate_generator": "bf16x3 split MFMA" if split else "f32 MFMA",
+            "candidate_generator": gen,
             "data": "synthetic U[-1,1) f32 (splitmix64 counter stream, seed 42), generated on device",
             "config": {"workload": ("C2: 1M x 768 f32 exact kNN k=32" if world == 1 else
                                     f"C4-style: {n_tot} x {d} f32 exact kNN k={k}, row-sharded"),
                        "n_rows": n_tot, "dim": d, "k": k, "rows_per_gpu": n_loc,
                        "metric_space": "squared L2 (reference sequential f32 fold)",
-                       "parallelism": (f"corpus row-shard x{world}: RCCL all-gather of queries, "
+                       "parallelism": ("single GPU (no collective)" if world == 1 else
+                                       f"corpus row-shard x{world}: RCCL all-gather of queries, "
                                        "exact per-shard top-k, all-to-all + merge")},
             "roofline": roof,
             "cpu_baseline": cpu,
             "parity_sample": parity,
             "energy_rows_per_sec": (c3 or {}).get("energy_rows_per_sec"),
+            "energy": energy,
             "c3_legs": c3,
             "c5_leg": c5,
-            "knn_stats": {"uncertified_rows": st["n_uncertified"], "slices": st["slices"],
-                          "list_len": st["list_len"], "ms_norms": st["ms_norms"],
-                          "ms_gram": st["ms_gram"], "ms_rerank": st["ms_rerank"],
-                          "ms_fallback": st["ms_fallback"], "algo": st.get("algo")},
+            "knn_stats": {kk: (round(v, 3) if isinstance(v, float) else v)
+                          for kk, v in st.items() if kk != "reserved1"},
         }
+        if world > 1:
+            line["time_budget"] = {"budget_s": a.time_budget_s, "steps_requested": steps_req,
+                                   "warmup_requested": warm_req, "steps_timed": a.steps,
+                                   "warmup_run": a.warmup,
+                                   "query_chunk": a.query_chunk}
         print(json.dumps(line), flush=True)
     if dist:
         dist.barrier()
@@ -252,9 +334,23 @@ def c3_legs(S, X, idx, dist, k):
     out["feature_laplacian"] = {"ms": round(ms, 3), "nnz": Lf.nnz}
     ms, (E, G, lam) = _timed(lambda: S.energy_rows(X, Lf))
     ebytes = n * f * 4 + Lf.nnz * 12 + (f + 1) * 8 + n * 3 * 8
-    out["energy_rows"] = {"ms": round(ms, 3), "GB_per_s": round(ebytes / ms / 1e6, 1),
-                          "entries_per_row": S.energy.last_stats()["entries"]}
+    ent = S.energy.last_stats()["entries"]
+    gbs = ebytes / ms / 1e6
+    # bound: HBM (X streamed once, L resident); the f64 work per
+    # row (7 f64 ops per stored entry and row + the tau radix-select) is
+    # reported beside it
+    f64_ops = 7.0 * ent * n
+    out["energy_rows"] = {"ms": round(ms, 3), "GB_per_s": round(gbs, 1), "entries_per_row": ent,
+                          "roofline": {"bound": "hbm", "kernel": "k_energy_rows",
+                                       "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS,
+                                       "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4),
+                                       "traffic": None, "bytes_per_launch": ebytes,
+                                       "ms_per_launch": round(ms, 3),
+                                       "f64_tflops": round(f64_ops / (ms * 1e-3) / 1e12, 2),
+                                       "f64_frac_of_78.6": round(f64_ops / (ms * 1e-3) / 1e12
+                                                                 / FP64_VALU_PEAK_TFLOPS, 4)}}
     out["energy_rows_per_sec"] = n / (ms * 1e-3)
+    out["_Lf"] = Lf
     # energymaps diffusion pre-pass (eta 0.1, 4 steps; energymaps.rs:518-546) on
     # the same rows: f32 in, f64 out; bytes = N F (4 + 8)
     Xd = torch.empty((n, f), dtype=torch.float64, device=X.device)
@@ -351,21 +447,57 @@ def c5_leg(S, _lib, L, a, dev, stream):
     return out
 
 
+def host_info():
+    """Core count and model of the host the CPU baselines run on."""
+    info = {"nproc": os.cpu_count()}
+    try:
+        info["affinity_cpus"] = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        pass
+    try:
+        import subprocess
+        lines = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
+        for ln in lines.splitlines():
+            if ln.startswith("Model name:"):
+                info["cpu_model"] = ln.split(":", 1)[1].strip()
+            if ln.startswith("Socket(s):") or ln.startswith("Core(s) per socket:") \
+                    or ln.startswith("Thread(s) per core:"):
+                info[ln.split(":")[0].strip().lower().replace("(s)", "s").replace(" ", "_")] = \
+                    ln.split(":", 1)[1].strip()
+    except Exception:  # noqa: BLE001 — informational only
+        pass
+    return info
+
+
+def cpu_threads():
+    """All cores this run may use: OMP_NUM_THREADS when the environment sets
+    it (the GPU box sets the job's CPU share), else the affinity mask."""
+    env = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    if env > 0:
+        return env
+    try:
+        return len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        return os.cpu_count() or 1
+
+
 def cpu_baseline(X, idx, dd, k, target_s):
-    """Oracle (C restatement, OpenMP) timed on the host on a bounded sample of
-    query rows against the full corpus; also a free bit-exact parity check of
-    those rows against the GPU result."""
+    """The oracle (C restatement, OpenMP on all allowed host cores) timed on
+    bounded samples of query rows against the full corpus:
+    efficient = bounded-heap top-k (the restated-efficient form), faithful =
+    collect all n-1 distances and sort them (mst.rs:330-360 as written).  The
+    sampled rows double as a bit-exact parity check of the GPU result."""
     from oracle import oracle as O
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+    threads = cpu_threads()
     Xh = X.cpu().numpy()
     n = Xh.shape[0]
     rng = np.random.default_rng(1)
     cal = np.sort(rng.choice(n, threads, replace=False))  # warms pages + threads
     i0, d0 = O.knn_l2sq_rows(Xh, k, cal, nthreads=threads)
     perm = rng.permutation(n)
-    batch = threads * 4
+    batch = threads * 4  # schedule(dynamic, 1): every thread busy
     done, el = 0, 0.0
-    ri_l, rd_l = [], []
+    ri_l = []
     while el < target_s and done + batch <= min(n, 65536):
         rows_b = np.sort(perm[done:done + batch])
         t0 = time.perf_counter()
@@ -381,12 +513,55 @@ def cpu_baseline(X, idx, dd, k, target_s):
     gd = dd.cpu().numpy()[rows]
     ok = int(np.sum(np.all(gi == ri, axis=1) & np.all(gd.view(np.uint32) == rd.view(np.uint32),
                                                        axis=1)))
+    # faithful: the first rows (full sort per row), a smaller bounded sample
+    fr = max(threads, int(m * 0.5) // threads * threads)
+    t0 = time.perf_counter()
+    f_i, f_d = O.knn_l2sq(Xh, k, q_begin=0, q_end=fr, mode=0, nthreads=threads)
+    fel = time.perf_counter() - t0
+    f_ok = bool(np.array_equal(f_i, idx[:fr].cpu().numpy()))
     cpu = {"value": m * (n - 1) / el, "unit": "pairs/s", "cores": threads, "kind": "port",
            "sample": f"{m} random query rows x {n} corpus rows, d={Xh.shape[1]}, k={k} "
-                     f"(oracle/or_knn_l2sq_rows_f32, OpenMP), {el:.1f}s"}
+                     f"(oracle/or_knn_l2sq_rows_f32, bounded heap, OpenMP {threads} threads), "
+                     f"{el:.1f}s",
+           "form": "restated-efficient",
+           "faithful": {"value": fr * (n - 1) / fel, "unit": "pairs/s", "cores": threads,
+                        "sample": f"rows 0..{fr - 1} x {n} (mode 0: all n-1 distances collected "
+                                  f"and sorted per row), {fel:.1f}s",
+                        "rows_bit_exact": f_ok},
+           "host": host_info()}
     parity = {"rows_checked": m, "rows_bit_exact": ok, "plus_calibration_rows": threads,
               "calibration_bit_exact": bool(np.array_equal(i0, idx.cpu().numpy()[cal]))}
     return cpu, parity
+
+
+def energy_cpu_baseline(X, Lf, target_s):
+    """K3 CPU baseline: the taumode energy rows of the first
+    65,536 items against the same feature Laplacian, restated-efficient (CSR
+    iteration) and faithful (compute_item_dispersion's F^2 CsMat::get pairs,
+    taumode.rs:366-408) on all allowed host cores; rows/s."""
+    from oracle import oracle as O
+    threads = cpu_threads()
+    ip, ix, iv = (Lf.indptr.cpu().numpy(), Lf.indices.cpu().numpy(), Lf.values.cpu().numpy())
+    Xh = X[:65536].cpu().numpy()
+    t0 = time.perf_counter()
+    O.energy_rows(Xh, ip, ix, iv, O.G_TAUMODE, O.TAU_MEDIAN, nthreads=threads)
+    el = time.perf_counter() - t0
+    # faithful: F^2 binary-search lookups per row, a bounded sample
+    nf = threads * 8
+    t0 = time.perf_counter()
+    O.energy_rows_faithful(Xh[:nf], ip, ix, iv, O.TAU_MEDIAN, nthreads=threads)
+    fel = time.perf_counter() - t0
+    while fel < target_s * 0.5 and nf < 65536:
+        nf = min(65536, nf * 4)
+        t0 = time.perf_counter()
+        O.energy_rows_faithful(Xh[:nf], ip, ix, iv, O.TAU_MEDIAN, nthreads=threads)
+        fel = time.perf_counter() - t0
+    return {"value": 65536 / el, "unit": "rows/s", "cores": threads, "kind": "port",
+            "sample": f"first 65536 items x {X.shape[1]} features vs the feature Laplacian "
+                      f"(nnz {Lf.nnz}), oracle/or_energy_rows TAUMODE Median, {el:.2f}s",
+            "form": "restated-efficient",
+            "faithful": {"value": nf / fel, "unit": "rows/s", "cores": threads,
+                         "sample": f"first {nf} items, F^2 CsMat::get dispersion, {fel:.1f}s"}}
 
 
 if __name__ == "__main__":

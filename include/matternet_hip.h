@@ -99,7 +99,11 @@ typedef struct mn_knn_stats {
     int64_t sample_rows;    /* corpus rows in the phase-1 sample                */
     int64_t n_candidates;   /* buffered (query, row) pairs re-ranked            */
     int32_t sweep_slices;
-    int32_t sweep_cap;      /* buffer entries per (query, slice, half)          */
+    int32_t sweep_cap;      /* buffer entries per (query, slice)                */
+    int64_t n_escalated;    /* rows the bf16x1 bound could not certify, re-run
+                               on the split (bf16x3) generator                 */
+    float ms_escalate;
+    int32_t reserved1;
 } mn_knn_stats;
 
 /* Self kNN over the rows of X [n][d] f32 (device, row-major): replaces
@@ -145,6 +149,27 @@ int mn_knn_merge_f32(const int32_t *part_idx, const float *part_dist,
 int mn_knn_l2_f64(const void *Q, int64_t nq, const void *C, int64_t nc, int32_t d,
                   int32_t x_is_f64, const int64_t *q_ids, int32_t k, int32_t use_sqrt,
                   int32_t *out_idx, double *out_dist, void *stream);
+
+/* Row-sharded multi-GPU build (SURVEY.md §8(b) mn_knn_sharded_f32, §8(e)
+ * strategy A) on a caller-owned RCCL communicator (an ncclComm_t, passed as
+ * void*; one rank per GPU, rank r holding rows [r n_local, (r+1) n_local) of X).
+ * The shards are all-gathered, every rank computes the exact per-shard top-k
+ * of all N queries against its resident shard (mn_knn_f32_qc, queries in
+ * chunks of query_chunk rows; <= 0: 2^21), the lists are exchanged so each
+ * query's owner receives its R lists (grouped ncclSend/ncclRecv) and merged
+ * (mn_knn_merge_f32).  out_idx / out_dist [n_local][k]: the rank's rows of the
+ * global graph, global ids, bit-identical to a single-GPU mn_knn_f32 of X.
+ * opts as mn_knn_f32 (opts->stream is used for every operation).  Collective:
+ * every rank calls it with the same n_local, d and opts->k.  <= 16 ranks. */
+int mn_knn_sharded_f32(const float *X_shard, int64_t n_local, int32_t d, void *rccl_comm,
+                       const mn_knn_opts *opts, int64_t query_chunk, int32_t *out_idx,
+                       float *out_dist);
+/* RCCL communicator helpers for callers without an RCCL binding of their own:
+ * rank 0 creates the 128-byte id and distributes it; each rank then inits. */
+int mn_rccl_unique_id(void *out_128_bytes);
+int mn_rccl_comm_init(const void *unique_id_128_bytes, int32_t world, int32_t rank,
+                      void **comm_out);
+int mn_rccl_comm_destroy(void *comm);
 
 /* Statistics of the calling thread's last mn_knn_* call. */
 int mn_knn_last_stats(mn_knn_stats *out);

@@ -40,6 +40,8 @@ enum ScratchSlot {
     kSlotX1Aux,    //                per-row norms / thresholds / bounds
     kSlotX1Buf2,   //                phase-2 candidate buffer
     kSlotX1Meta2,  //                phase-2 counts
+    kSlotX1Esc,    //                escalated rows (gathered queries, lists)
+    kSlotPerm,     // corpus visiting order (+ permuted norms / sample rows)
     kNumSlots
 };
 

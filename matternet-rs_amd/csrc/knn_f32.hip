@@ -429,6 +429,27 @@ __global__ __launch_bounds__(256) void k_rerank(
 //     rate per instruction, three instructions per 16 features.
 // ---------------------------------------------------------------------------
 
+// Corpus visiting order of the running-threshold generators: a fixed
+// pseudo-random bijection perm(i) = (A i + B) mod n (A ~ 0.618 n, coprime
+// with n).  Corpora stored in a sorted order (rows sorted along a coordinate)
+// would otherwise make nearly every pair beat the running L-th best and
+// overflow the candidate buffers; in a golden-ratio order the threshold
+// updates behave as for random order (about L (1 + ln(m / L)) writes).
+__global__ __launch_bounds__(256) void k_perm_init(int *__restrict__ perm, int *__restrict__ ipos,
+                                                   int64_t n, uint64_t a, uint64_t b) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int r = (int)((a * (uint64_t)i + b) % (uint64_t)n);  // a, b < n < 2^31
+    perm[i] = r;
+    if (ipos) ipos[r] = (int)i;
+}
+__global__ __launch_bounds__(256) void k_gather_f32(const float *__restrict__ src,
+                                                    const int *__restrict__ perm, int64_t n,
+                                                    float *__restrict__ dst) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) dst[i] = src[perm[i]];
+}
+
 // f32 -> bf16, round to nearest even (finite inputs; values beyond the bf16
 // range round to +-inf, which the Gram epilogue flags as unusable).
 __device__ __forceinline__ uint32_t bf16_rne(float x) {
@@ -442,12 +463,14 @@ __device__ __forceinline__ uint32_t bf16_rne(float x) {
 // MFMA may flush them anyway), which adds at most 2^-126 per term: covered by
 // the absolute slack of the certification bound.  Features d..dp-1 are 0.
 __global__ __launch_bounds__(256) void k_split_bf16(const float *__restrict__ X, int64_t n, int d,
-                                                    int dp, uint16_t *__restrict__ XS) {
+                                                    int dp, uint16_t *__restrict__ XS,
+                                                    const int *__restrict__ perm) {
     const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int per = dp >> 3;
     if (e >= n * per) return;
-    const int64_t row = e / per;
-    const int f0 = (int)(e - row * per) * 8;
+    const int64_t orow = e / per;
+    const int64_t row = perm ? (int64_t)perm[orow] : orow;  // source row
+    const int f0 = (int)(e - orow * per) * 8;
     uint32_t hw[4], lw[4];
 #pragma unroll
     for (int u = 0; u < 8; u += 2) {
@@ -468,7 +491,7 @@ __global__ __launch_bounds__(256) void k_split_bf16(const float *__restrict__ X,
         hw[u >> 1] = hp[0] | (hp[1] << 16);
         lw[u >> 1] = lp[0] | (lp[1] << 16);
     }
-    uint16_t *o = XS + row * (int64_t)(2 * dp) + 64 * (f0 >> 5) + (f0 & 31);
+    uint16_t *o = XS + orow * (int64_t)(2 * dp) + 64 * (f0 >> 5) + (f0 & 31);
     *reinterpret_cast<uint4 *>(o) = make_uint4(hw[0], hw[1], hw[2], hw[3]);
     *reinterpret_cast<uint4 *>(o + 32) = make_uint4(lw[0], lw[1], lw[2], lw[3]);
 }
@@ -483,13 +506,35 @@ __global__ __launch_bounds__(256) void k_split_bf16(const float *__restrict__ X,
 //   residuals and the dropped lo.lo term <= 3 2^-16 sum|q_t c_t|, f32
 //   accumulation of 3 dp exact products, the two norms, the final fma; sum
 //   |q_t c_t| <= (|q|^2 + |c|^2)/2; 2^-100 covers flushed subnormal parts).
+// |d~ - d_ref| bound of the split generator for query q (bf16x3):
+//   dot error  <= (3 2^-16 + gamma) sum|q_t c_t| (1 + 2^-6),  gamma = 6 dp u
+//   (3 dp exact products accumulated in f32; 2x the round-to-nearest bound,
+//   so any internal rounding of the MFMA adder is covered), sum|q_t c_t| <=
+//   |q| max|c| (Cauchy-Schwarz); key = |q|^2 + |c|^2 - 2 dot~: x2, plus the
+//   norms' lane-parallel f32 folds and the final fma (24 u (|q|^2 + max|c|^2));
+//   plus the reference fold's own error (d + 3) u (Mkey + base) where Mkey
+//   bounds the keys the bound is applied to.  Evaluated in f64, rounded up.
+__device__ __forceinline__ float delta_x3(float qn, float cmax, int dp, int d, float mkey) {
+    const double u = 0x1p-24;
+    const double qa = __builtin_sqrt((double)qn) * (1.0 + 0x1p-40);
+    const double ca = __builtin_sqrt((double)cmax) * (1.0 + 0x1p-40);
+    const double base = 2.0 * (3.0 * 0x1p-16 + 6.0 * dp * u) * (1.0 + 0x1p-6) * qa * ca +
+                        24.0 * u * ((double)qn + (double)cmax);
+    const double dl = base + (d + 3.0) * u * ((double)mkey + base) + 0x1p-100;
+    const double v = dl * (1.0 + 0x1p-20);
+    float f = (float)v;
+    if ((double)f < v) f = __uint_as_float(__float_as_uint(f) + 1u);
+    return f;
+}
+
 template <int NR, bool VEC4>
 __global__ __launch_bounds__(256) void k_rerank_buf(
     const float *__restrict__ Q, int64_t nq, const float *__restrict__ C, int d, int64_t c_off,
     const float *__restrict__ qnrm, const unsigned *__restrict__ cmax_bits, int S, int cap,
     const uint2 *__restrict__ buf, const int *__restrict__ bcnt, const float *__restrict__ btau,
-    int k, int64_t nvalid_max, float cert_c, int32_t *__restrict__ out_idx,
-    float *__restrict__ out_dist, int *__restrict__ fb_count, int *__restrict__ fb_list) {
+    int k, int64_t nvalid_max, int dp, const int *__restrict__ perm, int64_t q_off, int excl,
+    int32_t *__restrict__ out_idx, float *__restrict__ out_dist, int *__restrict__ fb_count,
+    int *__restrict__ fb_list) {
     __shared__ int cand[4][64 * NR];
     __shared__ float candk[4][64 * NR];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -507,11 +552,15 @@ __global__ __launch_bounds__(256) void k_rerank_buf(
         for (int e0 = 0; e0 < cnt; e0 += 64) {
             const int e = e0 + lane;
             const uint2 v = e < cnt ? bp[e] : make_uint2(0x7f800000u, 0u);
-            const bool pass = e < cnt && __uint_as_float(v.x) <= ts;
+            // ids are positions in the permuted corpus copy: map them back,
+            // and drop the query's own row (the kernel ran without exclusion)
+            int64_t gid = (int64_t)v.y;
+            if (perm && e < cnt) gid = c_off + perm[gid - c_off];
+            const bool pass = e < cnt && __uint_as_float(v.x) <= ts && !(excl && gid == q_off + q);
             const uint64_t pm = __ballot(pass);
             const int pos = M + (int)__popcll(pm & ((1ull << lane) - 1ull));
             if (pass && pos < 64 * NR) {
-                cand[wid][pos] = (int)v.y;
+                cand[wid][pos] = (int)gid;
                 candk[wid][pos] = __uint_as_float(v.x);
             }
             M += (int)__popcll(pm);
@@ -529,7 +578,13 @@ __global__ __launch_bounds__(256) void k_rerank_buf(
         ix[r] = e < M ? cand[wid][e] : INT_MAX;
     }
     wave_bitonic_sort<NR>(kk, ix);
-    const float delta = cert_c * (qnrm[q] + __uint_as_float(*cmax_bits)) + 0x1p-100f;
+    float mkey = T < __builtin_inff() ? __builtin_fabsf(T) : 0.f;
+#pragma unroll
+    for (int r = 0; r < NR; ++r)
+        if (lane + 64 * r < M && __builtin_isfinite(kk[r])) mkey = fmaxf(mkey, __builtin_fabsf(kk[r]));
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) mkey = fmaxf(mkey, __shfl_xor(mkey, o));
+    const float delta = delta_x3(qnrm[q], __uint_as_float(*cmax_bits), dp, d, mkey);
     const float *qrow = Q + q * (int64_t)d;
     const int kq = min(k, M);
     float dd[NR];
@@ -611,9 +666,12 @@ __device__ __forceinline__ float f32_up(double v) {
 
 // One wave per PAIR of rows (lanes 0-31: row r, 32-63: row r+1), so the
 // KB32 stores of the two rows fill whole 128-B lines.
+// Output position `row` holds source row perm[row] (perm == NULL: row): the
+// corpus copies are written in the visiting order, the query copies in place.
 template <bool VEC4>
 __global__ __launch_bounds__(256) void k_prep_x1(const float *__restrict__ X, int64_t n, int d,
-                                                 int dp, uint16_t *__restrict__ XR,
+                                                 int dp, const int *__restrict__ perm,
+                                                 uint16_t *__restrict__ XR,
                                                  uint16_t *__restrict__ XK, float *__restrict__ nrm,
                                                  float *__restrict__ hcv, float *__restrict__ hn,
                                                  float *__restrict__ rn,
@@ -625,7 +683,8 @@ __global__ __launch_bounds__(256) void k_prep_x1(const float *__restrict__ X, in
     for (int64_t r2 = 2 * wave0; r2 < n; r2 += 2 * nwaves) {
         const int64_t row = r2 + hl;
         const bool live = row < n;
-        const float *p = X + min(row, n - 1) * (int64_t)d;
+        const int64_t srow = perm ? (int64_t)perm[min(row, n - 1)] : min(row, n - 1);
+        const float *p = X + srow * (int64_t)d;
         double s = 0.0, sh = 0.0, sr = 0.0;
         bool bad = false;
         for (int t0 = 8 * ll; t0 < dp; t0 += 256) {
@@ -674,12 +733,12 @@ __global__ __launch_bounds__(256) void k_prep_x1(const float *__restrict__ X, in
         const bool anybad = __any(bad);
         if (ll == 0 && live) {
             const float nf = (float)s;
-            nrm[row] = nf;
+            if (nrm) nrm[row] = nf;
             if (hcv) hcv[row] = 0.5f * nf;
             const float hf = f32_up(__builtin_sqrt(sh) * (1.0 + 0x1p-50));
             const float rf = f32_up(__builtin_sqrt(sr) * (1.0 + 0x1p-50));
-            hn[row] = hf;
-            rn[row] = rf;
+            if (hn) hn[row] = hf;
+            if (rn) rn[row] = rf;
             if (anybad) atomicOr(flags, 1);
             // keys stay far from f32 overflow (and bf16(x) finite) below 2^100
             if (!(s <= 0x1p100)) atomicOr(flags + 1, 1);
@@ -734,8 +793,9 @@ __global__ __launch_bounds__(64 * WPB) void k_rerank_x1(
     const float *__restrict__ tau0, int S2, int cap2, const uint2 *__restrict__ buf2,
     const int *__restrict__ cnt2, const float *__restrict__ delta, int k, int64_t nvalid_max,
     const int *__restrict__ qlist, const int *__restrict__ qlist_n, int *__restrict__ big_count,
-    int *__restrict__ big_list, int32_t *__restrict__ out_idx, float *__restrict__ out_dist,
-    int *__restrict__ fb_count, int *__restrict__ fb_list) {
+    int *__restrict__ big_list, const int *__restrict__ perm, int64_t q_off, int excl,
+    int32_t *__restrict__ out_idx, float *__restrict__ out_dist, int *__restrict__ fb_count,
+    int *__restrict__ fb_list) {
     __shared__ int cand[WPB][64 * NR];
     __shared__ float candk[WPB][64 * NR];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -745,25 +805,31 @@ __global__ __launch_bounds__(64 * WPB) void k_rerank_x1(
     const float T = tau0[q];
     bool forced = T == -__builtin_inff();
     int M = 0;
-    auto gather = [&](const uint2 *bp, int cnt) {
+    // ids are positions in the visiting order: map them back (c_off +
+    // perm[p]); the generators ran without exclusion, so the query's own row
+    // is dropped here
+    auto gather = [&](const uint2 *bp, int cnt, bool) {
         for (int e0 = 0; e0 < cnt; e0 += 64) {
             const int e = e0 + lane;
             const uint2 v = e < cnt ? bp[e] : make_uint2(0x7f800000u, 0u);
-            const bool pass = e < cnt && __uint_as_float(v.x) < T;
+            int64_t gid = (int64_t)v.y;
+            if (e < cnt) gid = c_off + perm[gid];
+            const bool pass = e < cnt && __uint_as_float(v.x) < T && !(excl && gid == q_off + q);
             const uint64_t pm = __ballot(pass);
             const int pos = M + (int)__popcll(pm & ((1ull << lane) - 1ull));
             if (pass && pos < 64 * NR) {
-                cand[wid][pos] = (int)v.y;
+                cand[wid][pos] = (int)gid;
                 candk[wid][pos] = __uint_as_float(v.x);
             }
             M += (int)__popcll(pm);
         }
     };
-    for (int s = 0; s < S1; ++s) gather(buf1 + (q * S1 + s) * (int64_t)cap1, cnt1[q * S1 + s]);
+    for (int s = 0; s < S1; ++s)
+        gather(buf1 + (q * S1 + s) * (int64_t)cap1, cnt1[q * S1 + s], true);
     for (int j = 0; j < S2; ++j) {
         const int c = cnt2[q * S2 + j];
         forced |= c < 0;
-        if (c > 0) gather(buf2 + (q * S2 + j) * (int64_t)cap2, c);
+        if (c > 0) gather(buf2 + (q * S2 + j) * (int64_t)cap2, c, false);
     }
     if (!forced && M > 64 * NR && big_list) {
         if (lane == 0) big_list[atomicAdd(big_count, 1)] = (int)q;
@@ -848,6 +914,43 @@ __global__ __launch_bounds__(256) void k_sqrt_dist(float *__restrict__ dist, int
     if (i < n) {
         const float v = dist[i];
         if (v < __builtin_inff()) dist[i] = sqrt_rn_f32(v);
+    }
+}
+
+// Escalation of rows the bf16x1 bound could not certify (dense clusters: the
+// bound scales with |q||c|, not with the neighbour distances): gather them,
+// run the split generator on them with k + 1 neighbours and self included,
+// then drop the query's own id (d = +0: it is in the k + 1 list unless > k
+// exact duplicates precede it, in which case the last entry goes).
+__global__ __launch_bounds__(256) void k_gather_rows(const float *__restrict__ X, int d,
+                                                     const int *__restrict__ rows, int64_t n,
+                                                     float *__restrict__ out) {
+    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= n * d) return;
+    const int64_t i = e / d;
+    out[e] = X[(int64_t)rows[i] * d + (e - i * d)];
+}
+
+__global__ __launch_bounds__(256) void k_scatter_escalated(
+    const int *__restrict__ rows, int64_t n, int64_t q_off, int excl, int k,
+    const int32_t *__restrict__ eidx, const float *__restrict__ edist,
+    int32_t *__restrict__ out_idx, float *__restrict__ out_dist) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int64_t q = rows[i], gid = q_off + q;
+    int wpos = 0;
+    for (int r = 0; r <= k; ++r) {
+        const int id = eidx[i * (k + 1) + r];
+        if (excl && id >= 0 && id == gid) continue;
+        if (wpos < k) {
+            out_idx[q * k + wpos] = id;
+            out_dist[q * k + wpos] = id >= 0 ? edist[i * (k + 1) + r] : __builtin_inff();
+            ++wpos;
+        }
+    }
+    for (; wpos < k; ++wpos) {
+        out_idx[q * k + wpos] = -1;
+        out_dist[q * k + wpos] = __builtin_inff();
     }
 }
 
@@ -973,7 +1076,25 @@ namespace {
 thread_local mn_knn_stats t_stats{};
 }
 
-// Host driver of the MN_KNN_F32 / MN_KNN_BF16X3 generators.
+// perm = the golden-ratio bijection of k_perm_init over n rows, in scratch slot
+// `slot`; with_inverse: ipos = perm + n (position of row r in the order);
+// then `extra` bytes for the caller.
+static int *make_perm(int64_t n, int slot, size_t extra, hipStream_t s, bool with_inverse = false) {
+    const size_t words = (size_t)n * (with_inverse ? 2 : 1);
+    int *perm = (int *)scratch(slot, sizeof(int) * words + extra + 256);
+    if (!perm || n == 0) return perm;
+    uint64_t a = (uint64_t)((double)n * 0.6180339887498949);
+    if (a == 0) a = 1;
+    auto gcd = [](uint64_t x, uint64_t y) { while (y) { const uint64_t t = x % y; x = y; y = t; } return x; };
+    while (gcd(a, (uint64_t)n) != 1) ++a;
+    a %= (uint64_t)n;
+    if (a == 0) a = 1;
+    const uint64_t b = (uint64_t)n / 3;
+    hipLaunchKernelGGL(knn::k_perm_init, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, perm,
+                       with_inverse ? perm + n : (int *)nullptr, n, a, b);
+    return perm;
+}
+
 static int knn_f32_core(const float *Q, int64_t nq, const float *C, int64_t nc, int32_t d,
                         int64_t q_off, int64_t c_off, const mn_knn_opts *opts,
                         int32_t *out_idx, float *out_dist, int algo) {
@@ -1063,16 +1184,23 @@ static int knn_f32_core(const float *Q, int64_t nq, const float *C, int64_t nc, 
         // ---- bf16-split candidates (gram_bf16.hpp GM_L2) + buffer re-rank ----
         const int dp = (d + 127) / 128 * 128;  // 2 dp bf16 per row: a multiple of DALIGN
         uint16_t *XSq = (uint16_t *)scratch(kSlotGeneric0, (size_t)nq * dp * 4 + 64);
-        uint16_t *XSc = same ? XSq : (uint16_t *)scratch(kSlotGeneric1, (size_t)nc * dp * 4 + 64);
-        MN_REQUIRE(XSq && XSc, MN_ENOMEM, "mn_knn: split copy allocation failed");
-        auto split_rows = [&](const float *X, int64_t n, uint16_t *XS) {
+        uint16_t *XSc = (uint16_t *)scratch(kSlotGeneric1, (size_t)nc * dp * 4 + 64);
+        // the corpus copy is stored in the golden-ratio visiting order (see
+        // k_perm_init), with its norms; ids are mapped back in the re-rank
+        int *perm = make_perm(nc, kSlotPerm, sizeof(float) * (size_t)nc, s);
+        MN_REQUIRE(XSq && XSc && perm, MN_ENOMEM, "mn_knn: split copy allocation failed");
+        float *cnp = (float *)(perm + nc);
+        auto split_rows = [&](const float *X, int64_t n, uint16_t *XS, const int *pm) {
             const int64_t th = n * (dp / 8);
             if (th > 0)
                 hipLaunchKernelGGL(k_split_bf16, dim3((unsigned)((th + 255) / 256)), dim3(256), 0, s,
-                                   X, n, d, dp, XS);
+                                   X, n, d, dp, XS, pm);
         };
-        split_rows(Q, nq, XSq);
-        if (!same) split_rows(C, nc, XSc);
+        split_rows(Q, nq, XSq, nullptr);
+        split_rows(C, nc, XSc, perm);
+        if (nc > 0)
+            hipLaunchKernelGGL(k_gather_f32, dim3((unsigned)((nc + 255) / 256)), dim3(256), 0, s, cn,
+                               perm, nc, cnp);
         MN_KCHECK(s, "k_split_bf16");
         tm.mark();
         const char *ms = getenv("MN_L2_MIN_SLICES");
@@ -1092,22 +1220,20 @@ static int knn_f32_core(const float *Q, int64_t nq, const float *C, int64_t nc, 
             auto kern = (probe && !strcmp(probe, "noepi")) ? kb16::k_gram_bf16<kb16::GM_L2, 1>
                                                             : kb16::k_gram_bf16<kb16::GM_L2, 0>;
             hipLaunchKernelGGL(kern, dim3((unsigned)(bq * pl.S)),
-                               dim3(kb16::NT), 0, s, XSq, nq, XSc, nc, 2 * dp, q_off, c_off, excl, qn,
-                               cn, L, (int)pl.S, pl.chunk, pl.cap, cbuf, bcnt, btau);
+                               dim3(kb16::NT), 0, s, XSq, nq, XSc, nc, 2 * dp, q_off, c_off, 0, qn,
+                               cnp, L, (int)pl.S, pl.chunk, pl.cap, cbuf, bcnt, btau);
         } else {
             MN_HIP_TRY(hipMemsetAsync(bcnt, 0, sizeof(int) * (size_t)nq * pl.S, s));
         }
         MN_KCHECK(s, "k_gram_bf16<L2>");
         tm.mark();
-        // |d~ - d| bound per unit of (|q|^2 + max|c|^2); generous constants
-        const float cert_c =
-            2.0f * (3.0f * 0x1p-16f + (4.0f * (float)dp + 32.0f) * 0x1p-24f);
         const int64_t nvalid = same ? nc - 1 : nc;
         const dim3 rgrid((unsigned)((nq + 3) / 4));
 #define MN_RRB(NRV, V)                                                                          \
     hipLaunchKernelGGL((k_rerank_buf<NRV, V>), rgrid, dim3(256), 0, s, Q, nq, C, d, c_off, qn,   \
                        maxbits, (int)pl.S, pl.cap, cbuf, bcnt, btau, k,                         \
-                       std::max<int64_t>(nvalid, 0), cert_c, out_idx, out_dist, fb_count, fb_list)
+                       std::max<int64_t>(nvalid, 0), dp, perm, q_off, excl, out_idx, out_dist,  \
+                       fb_count, fb_list)
         if (vec4) {
             if (pl.NR == 1) MN_RRB(1, true);
             else if (pl.NR == 2) MN_RRB(2, true);
@@ -1181,6 +1307,10 @@ static int knn_f32_core(const float *Q, int64_t nq, const float *C, int64_t nc, 
 }
 
 
+static int knn_f32_core(const float *Q, int64_t nq, const float *C, int64_t nc, int32_t d,
+                        int64_t q_off, int64_t c_off, const mn_knn_opts *opts,
+                        int32_t *out_idx, float *out_dist, int algo);
+
 // Host driver of MN_KNN_BF16X1 (section 2c).  Returns 1 (nothing written)
 // when some row is too large for the single-bf16 bound: the caller then runs
 // the split generator.
@@ -1198,18 +1328,23 @@ static int knn_x1(const float *Q, int64_t nq, const float *C, int64_t nc, int32_
     const int nkb = dp / 32;
     t_stats.algo = MN_KNN_BF16X1;
 
+    // queries in place (QR row-major for phase 1, QK KB32 for the sweep); the
+    // corpus in the golden-ratio visiting order (CR, CK; position p holds row
+    // perm[p]), so the phase-1 sample is the contiguous prefix [0, m0) and the
+    // sweep covers [m0, nc); ids are mapped back through perm in the re-rank
     uint16_t *QR = (uint16_t *)scratch(kSlotX1QR, (size_t)nq * dp * 2 + 64);
     uint16_t *QK = (uint16_t *)scratch(kSlotX1QK, (size_t)nq * dp * 2 + 64);
-    uint16_t *CR = same ? QR : (uint16_t *)scratch(kSlotX1CR, (size_t)nc * dp * 2 + 64);
-    uint16_t *CK = same ? QK : (uint16_t *)scratch(kSlotX1CK, (size_t)nc * dp * 2 + 64);
-    char *aux = (char *)scratch(kSlotX1Aux, (size_t)nq * 24 + (size_t)nc * 16 + 256);
+    uint16_t *CR = (uint16_t *)scratch(kSlotX1CR, (size_t)nc * dp * 2 + 64);
+    uint16_t *CK = (uint16_t *)scratch(kSlotX1CK, (size_t)nc * dp * 2 + 64);
+    char *aux = (char *)scratch(kSlotX1Aux, (size_t)nq * 24 + (size_t)nc * 8 + 256);
     int *flags = (int *)scratch(kSlotFlags, 64);
     int *fb_list = (int *)scratch(kSlotFallback, sizeof(int) * (size_t)nq * 2 + 64);
-    MN_REQUIRE(QR && QK && CR && CK && aux && flags && fb_list, MN_ENOMEM,
+    int *perm = make_perm(nc, kSlotPerm, 0, s);
+    MN_REQUIRE(QR && QK && CR && CK && aux && flags && fb_list && perm, MN_ENOMEM,
                "mn_knn: bf16x1 scratch allocation failed");
     float *qn = (float *)aux, *qhn = qn + nq, *qrn = qhn + nq, *tq = qrn + nq, *tau0 = tq + nq,
           *dlt = tau0 + nq;
-    float *cnv = dlt + nq, *chc = cnv + nc, *chn = chc + nc, *crn = chn + nc;
+    float *cnv = dlt + nq, *chc = cnv + nc;  // corpus norms / half norms, visiting order
     unsigned *cmax = (unsigned *)flags;  // [0..2]: max |c|^2, |ch|, |rc|
     int *fb_count = flags + 5;  // [3]: non-finite input, [4]: too large for bf16x1
     unsigned long long *ncand = (unsigned long long *)(flags + 8);
@@ -1217,25 +1352,20 @@ static int knn_x1(const float *Q, int64_t nq, const float *C, int64_t nc, int32_
     Timer tm;
     tm.start(opts->timing != 0, s);
     MN_HIP_TRY(hipMemsetAsync(flags, 0, 64, s));
-    auto prep = [&](const float *X, int64_t n, uint16_t *R, uint16_t *K, float *nv, float *hcv,
-                    float *hv, float *rv, int corpus) {
+    auto prep = [&](const float *X, int64_t n, const int *pm, uint16_t *R, uint16_t *K, float *nv,
+                    float *hcv, float *hv, float *rv, int corpus) {
         if (n == 0) return;
         const int64_t blocks = std::min<int64_t>((n + 7) / 8, 16384);
         if (vec4)
             hipLaunchKernelGGL(k_prep_x1<true>, dim3((unsigned)blocks), dim3(256), 0, s, X, n, d,
-                               dp, R, K, nv, hcv, hv, rv, cmax, flags + 3, corpus);
+                               dp, pm, R, K, nv, hcv, hv, rv, cmax, flags + 3, corpus);
         else
             hipLaunchKernelGGL(k_prep_x1<false>, dim3((unsigned)blocks), dim3(256), 0, s, X, n, d,
-                               dp, R, K, nv, hcv, hv, rv, cmax, flags + 3, corpus);
+                               dp, pm, R, K, nv, hcv, hv, rv, cmax, flags + 3, corpus);
     };
-    if (same) {
-        prep(C, nc, CR, CK, qn, chc, qhn, qrn, 1);
-    } else {
-        prep(Q, nq, QR, QK, qn, nullptr, qhn, qrn, 0);
-        prep(C, nc, CR, CK, cnv, chc, chn, crn, 1);
-    }
+    prep(Q, nq, nullptr, QR, QK, qn, nullptr, qhn, qrn, 0);
+    prep(C, nc, perm, CR, CK, cnv, chc, nullptr, nullptr, 1);
     MN_KCHECK(s, "k_prep_x1");
-    if (same) cnv = qn;
     int hflags[8] = {0};
     MN_HIP_TRY(hipMemcpyAsync(hflags, flags, 32, hipMemcpyDeviceToHost, s));
     MN_HIP_TRY(hipStreamSynchronize(s));
@@ -1270,7 +1400,7 @@ static int knn_x1(const float *Q, int64_t nq, const float *C, int64_t nc, int32_
     {
         const int64_t bq = (nq + kb16::BM - 1) / kb16::BM;
         hipLaunchKernelGGL((kb16::k_gram_bf16<kb16::GM_L2H, 0>), dim3((unsigned)(bq * pl.S)),
-                           dim3(kb16::NT), 0, s, QR, nq, CR, m0, dp, q_off, c_off, excl, qn, cnv,
+                           dim3(kb16::NT), 0, s, QR, nq, CR, m0, dp, q_off, (int64_t)0, 0, qn, cnv,
                            L1, (int)pl.S, pl.chunk, pl.cap, cbuf1, bcnt1, btau1);
         MN_KCHECK(s, "k_gram_bf16<L2H>");
     }
@@ -1301,7 +1431,8 @@ static int knn_x1(const float *Q, int64_t nq, const float *C, int64_t nc, int32_
                    "mn_knn: sweep grid too large (split the queries / corpus)");
         auto kern = (probe && !strcmp(probe, "noepi")) ? ksw::k_gram_sweep<1> : ksw::k_gram_sweep<0>;
         hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(ksw::NT), 0, s, QK, nq, CK, nc, nkb,
-                           q_off, c_off, excl, tq, tau0, chc, m0, S2, p2.chunk, cap2, cbuf2, cnt2);
+                           q_off, (int64_t)0, 0, tq, tau0, chc, m0, S2, p2.chunk, cap2, cbuf2,
+                           cnt2);
         MN_KCHECK(s, "k_gram_sweep");
     }
     tm.mark();
@@ -1324,8 +1455,8 @@ static int knn_x1(const float *Q, int64_t nq, const float *C, int64_t nc, int32_
 #define MN_RRX(NRV, WPB, V, NB, QL, QN, BC, BL)                                                 \
     hipLaunchKernelGGL((k_rerank_x1<NRV, WPB, V>), dim3((unsigned)(NB)), dim3(64 * WPB), 0, s, \
                        Q, nq, C, d, c_off, (int)pl.S, pl.cap, cbuf1, bcnt1, tau0, S2, cap2,     \
-                       cbuf2, cnt2, dlt, k, nvalid, QL, QN, BC, BL, out_idx, out_dist,          \
-                       fb_count, fb_list)
+                       cbuf2, cnt2, dlt, k, nvalid, QL, QN, BC, BL, perm, q_off, excl,          \
+                       out_idx, out_dist, fb_count, fb_list)
     const int64_t nb1 = (nq + 3) / 4;
     if (vec4) MN_RRX(8, 4, true, nb1, (const int *)nullptr, (const int *)nullptr, big_count, big_list);
     else MN_RRX(8, 4, false, nb1, (const int *)nullptr, (const int *)nullptr, big_count, big_list);
@@ -1340,6 +1471,51 @@ static int knn_x1(const float *Q, int64_t nq, const float *C, int64_t nc, int32_
 #undef MN_RRX
     MN_KCHECK(s, "k_rerank_x1");
     tm.mark();
+    // many uncertified rows: escalate them to the split generator instead of
+    // the exact scan (whose cost is O(nc d) per row)
+    int nfb = 0;
+    MN_HIP_TRY(hipMemcpyAsync(&nfb, fb_count, 4, hipMemcpyDeviceToHost, s));
+    MN_HIP_TRY(hipStreamSynchronize(s));
+    float ms_esc = 0.f;
+    int64_t esc_uncert = 0;
+    if (nfb > 256) {
+        const int k1 = k + 1;
+        const int m1 = opts->margin > 0 ? opts->margin : 16;
+        const int ealgo = k1 + m1 <= kb16::LMAX ? MN_KNN_BF16X3 : MN_KNN_F32;
+        MN_REQUIRE(k1 <= KMAX && k1 + m1 <= LMAX, MN_ENOTSUP,
+                   "mn_knn: escalation needs k + 1 + margin <= %d", LMAX);
+        char *eb = (char *)scratch(kSlotX1Esc, (size_t)nfb * (4 + 4 * (size_t)d + 8 * k1) + 256);
+        MN_REQUIRE(eb, MN_ENOMEM, "mn_knn: escalation scratch allocation failed");
+        int *erows = (int *)eb;
+        float *EQ = (float *)(eb + (((size_t)nfb * 4 + 15) & ~(size_t)15));
+        int32_t *eidx = (int32_t *)(EQ + (size_t)nfb * d);
+        float *edist = (float *)(eidx + (size_t)nfb * k1);
+        MN_HIP_TRY(hipMemcpyAsync(erows, fb_list, sizeof(int) * (size_t)nfb, hipMemcpyDeviceToDevice, s));
+        const int64_t ne = (int64_t)nfb * d;
+        hipLaunchKernelGGL(k_gather_rows, dim3((unsigned)((ne + 255) / 256)), dim3(256), 0, s, Q, d,
+                           erows, (int64_t)nfb, EQ);
+        MN_KCHECK(s, "k_gather_rows");
+        const mn_knn_stats keep = t_stats;
+        Timer te;
+        te.start(true, s);
+        mn_knn_opts eo = *opts;
+        eo.k = k1;
+        eo.exclude_self = 0;
+        eo.timing = 0;
+        const int rc = knn_f32_core(EQ, nfb, C, nc, d, 0, c_off, &eo, eidx, edist, ealgo);
+        if (rc != MN_OK) return rc;
+        hipLaunchKernelGGL(k_scatter_escalated, dim3((unsigned)((nfb + 255) / 256)), dim3(256), 0,
+                           s, erows, (int64_t)nfb, q_off, excl, k, eidx, edist, out_idx, out_dist);
+        MN_KCHECK(s, "k_scatter_escalated");
+        te.mark();
+        ms_esc = te.ms(0, 1);
+        esc_uncert = t_stats.n_uncertified;
+        t_stats = keep;
+        t_stats.n_escalated = nfb;
+        t_stats.ms_escalate = ms_esc;
+        // the split generator's own uncertified rows were rescanned inside it
+        MN_HIP_TRY(hipMemsetAsync(fb_count, 0, 4, s));
+    }
     const unsigned fgrid = (unsigned)std::min<int64_t>(nq, 1024);
     if (vec4)
         hipLaunchKernelGGL(k_fallback<true>, dim3(fgrid), dim3(FB_THREADS), 0, s, Q, C, nc, d,
@@ -1360,7 +1536,7 @@ static int knn_x1(const float *Q, int64_t nq, const float *C, int64_t nc, int32_
     int64_t hf[8] = {0};
     MN_HIP_TRY(hipMemcpyAsync(hf, flags, 64, hipMemcpyDeviceToHost, s));
     MN_HIP_TRY(hipStreamSynchronize(s));
-    t_stats.n_uncertified = ((const int *)hf)[5];
+    t_stats.n_uncertified = ((const int *)hf)[5] + esc_uncert;
     if (tm.on) {
         t_stats.n_candidates = hf[4];
         t_stats.ms_norms = tm.ms(0, 1);

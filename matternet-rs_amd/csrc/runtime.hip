@@ -108,6 +108,7 @@ void Timer::mark() {
 }
 float Timer::ms(int a, int b) {
     if (!on || a >= n || b >= n) return 0.f;
+    (void)hipEventSynchronize(ev[b]);
     float t = 0.f;
     (void)hipEventElapsedTime(&t, ev[a], ev[b]);
     return t;

@@ -256,6 +256,34 @@ __global__ __launch_bounds__(256) void k_topk_reduce(
 // score descending (sort_unstable: ties here by ascending index), first k.
 // Inputs per query: B (cos > 0.9999 top k), A (lambda top k), C (best cos),
 // -1 padded.  Needs 2k + 1 <= 512.
+// Hybrid, lambda top k (list A): an item whose cosine is > 0.9999 was inserted
+// with its COSINE first (high_semantic_vec, core.rs:1289-1293; or_insert keeps
+// it, :1296-1299), even when it falls outside list B's top k.  Re-evaluate
+// each A entry's cosine with the score kernel's exact folds (sequential f64
+// norm and dot, same order) and substitute it.  One thread per (query, entry).
+template <typename T>
+__global__ __launch_bounds__(256) void k_hybrid_cos_fix(const T *__restrict__ X, int32_t f,
+                                                        const double *__restrict__ Q,
+                                                        const double *__restrict__ qn, int64_t nq,
+                                                        int32_t k, const int64_t *__restrict__ ai,
+                                                        double *__restrict__ as) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= nq * k) return;
+    const int64_t q = t / k, i = ai[t];
+    if (i < 0) return;
+    const T *x = X + i * f;
+    const double *a = Q + q * f;
+    double dot = -0.0, nrm = -0.0;
+    for (int32_t c = 0; c < f; ++c) {
+        const double xv = (double)x[c];
+        nrm = nrm + xv * xv;
+        dot = dot + a[c] * xv;
+    }
+    const double denom = qn[q] * __builtin_sqrt(nrm);
+    const double cs = denom > 0.0 ? dot / denom : 0.0;
+    if (cs > 0.9999) as[t] = cs;
+}
+
 __global__ __launch_bounds__(64) void k_hybrid_union(
     const int64_t *__restrict__ ai, const double *__restrict__ as, const int64_t *__restrict__ bi,
     const double *__restrict__ bs, const int64_t *__restrict__ ci, const double *__restrict__ cs,
@@ -337,9 +365,37 @@ int reduce_lists(double *ka, int32_t *ia, double *kb, int32_t *ib, int64_t m, in
     }
 }
 
+int search_batch(const void *X, int32_t x_is_f64, int64_t n, int32_t f, const double *lambdas,
+                 const double *Q, const double *lambda_q, int64_t nq, int32_t k, double alpha,
+                 int64_t *out_idx, double *out_score, void *stream, bool hybrid);
+
+// Queries run in batches that keep the reduce grid (one row of blocks per
+// query, gridDim.y <= 65535) and the candidate scratch (nq x tiles x k
+// entries per selection) bounded.
 int search_impl(const void *X, int32_t x_is_f64, int64_t n, int32_t f, const double *lambdas,
                 const double *Q, const double *lambda_q, int64_t nq, int32_t k, double alpha,
                 int64_t *out_idx, double *out_score, void *stream, bool hybrid) {
+    using namespace mn::srch;
+    const int64_t ntiles = std::max<int64_t>((n + kTile - 1) / kTile, 1);
+    const int64_t kk = std::max<int64_t>(std::min<int64_t>(k, kTile), 1);
+    const int64_t per_q = ntiles * kk * 24 * (hybrid ? 3 : 1);
+    const int64_t budget = (int64_t)4 << 30;
+    const int64_t qb = std::max<int64_t>(kQB, std::min<int64_t>(65535, budget / per_q) / kQB * kQB);
+    if (nq <= qb)
+        return search_batch(X, x_is_f64, n, f, lambdas, Q, lambda_q, nq, k, alpha, out_idx,
+                            out_score, stream, hybrid);
+    for (int64_t a = 0; a < nq; a += qb) {
+        const int64_t b = std::min(nq, a + qb);
+        const int rc = search_batch(X, x_is_f64, n, f, lambdas, Q + a * f, lambda_q + a, b - a, k,
+                                    alpha, out_idx + a * k, out_score + a * k, stream, hybrid);
+        if (rc != MN_OK) return rc;
+    }
+    return MN_OK;
+}
+
+int search_batch(const void *X, int32_t x_is_f64, int64_t n, int32_t f, const double *lambdas,
+                 const double *Q, const double *lambda_q, int64_t nq, int32_t k, double alpha,
+                 int64_t *out_idx, double *out_score, void *stream, bool hybrid) {
     using namespace mn::srch;
     const char *fn = hybrid ? "mn_search_lambda_aware_hybrid" : "mn_search_lambda_aware";
     MN_REQUIRE(n >= 0 && f >= 0 && nq >= 0 && k >= 0, MN_EINVAL, "%s: bad sizes", fn);
@@ -415,6 +471,16 @@ int search_impl(const void *X, int32_t x_is_f64, int64_t n, int32_t f, const dou
             int rc = reduce_lists(cand.k[c], cand.i[c], kb[c], ib[c], m, nq, kk, c == 2 ? 1 : k,
                                   n, fi[c], fs[c], s);
             if (rc != MN_OK) return rc;
+        }
+        if (n > 0) {
+            const unsigned gb = (unsigned)((nq * k + 255) / 256);
+            if (x_is_f64)
+                hipLaunchKernelGGL(k_hybrid_cos_fix<double>, dim3(gb), dim3(256), 0, s,
+                                   (const double *)X, f, Q, qn, nq, k, fi[0], fs[0]);
+            else
+                hipLaunchKernelGGL(k_hybrid_cos_fix<float>, dim3(gb), dim3(256), 0, s,
+                                   (const float *)X, f, Q, qn, nq, k, fi[0], fs[0]);
+            MN_KCHECK(s, "k_hybrid_cos_fix");
         }
         hipLaunchKernelGGL(k_hybrid_union, dim3((unsigned)nq), dim3(64), 0, s, fi[0], fs[0], fi[1],
                            fs[1], fi[2], fs[2], nq, k, out_idx, out_score);

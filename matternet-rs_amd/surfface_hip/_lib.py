@@ -41,7 +41,8 @@ class KnnStats(C.Structure):
                 ("ms_rerank", C.c_float), ("ms_fallback", C.c_float), ("ms_total", C.c_float),
                 ("algo", C.c_int32), ("ms_sample", C.c_float), ("ms_sweep", C.c_float),
                 ("sample_rows", C.c_int64), ("n_candidates", C.c_int64),
-                ("sweep_slices", C.c_int32), ("sweep_cap", C.c_int32)]
+                ("sweep_slices", C.c_int32), ("sweep_cap", C.c_int32),
+                ("n_escalated", C.c_int64), ("ms_escalate", C.c_float), ("reserved1", C.c_int32)]
 
     def as_dict(self):
         return {f: getattr(self, f) for f, _ in self._fields_}
@@ -113,6 +114,11 @@ SIGNATURES = {
     "mn_knn_f32": (C.c_int, [P, I64, I32, C.POINTER(KnnOpts), P, P]),
     "mn_knn_f32_qc": (C.c_int, [P, I64, P, I64, I32, I64, I64, C.POINTER(KnnOpts), P, P]),
     "mn_knn_merge_f32": (C.c_int, [P, P, I32, I64, I32, P, P, P]),
+    "mn_knn_l2_f64": (C.c_int, [P, I64, P, I64, I32, I32, P, I32, I32, P, P, P]),
+    "mn_knn_sharded_f32": (C.c_int, [P, I64, I32, P, C.POINTER(KnnOpts), I64, P, P]),
+    "mn_rccl_unique_id": (C.c_int, [P]),
+    "mn_rccl_comm_init": (C.c_int, [P, I32, I32, C.POINTER(C.c_void_p)]),
+    "mn_rccl_comm_destroy": (C.c_int, [P]),
     "mn_knn_last_stats": (C.c_int, [C.POINTER(KnnStats)]),
     "mn_laplacian_from_knn": (C.c_int, [P, P, I32, I64, I32, C.POINTER(LapOpts), C.POINTER(Csr), P]),
     "mn_csr_free": (C.c_int, [C.POINTER(Csr)]),

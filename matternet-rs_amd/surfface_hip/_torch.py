@@ -30,3 +30,29 @@ def to_device(a, device="cuda") -> torch.Tensor:
     if isinstance(a, torch.Tensor):
         return a.to(device).contiguous()
     return torch.from_numpy(np.ascontiguousarray(a)).to(device)
+
+
+def _first_cuda(args, kwargs):
+    for a in list(args) + list(kwargs.values()):
+        if isinstance(a, torch.Tensor) and a.device.type == "cuda":
+            return a.device
+        for v in (getattr(a, "indptr", None), getattr(a, "keys", None)):
+            if isinstance(v, torch.Tensor) and v.device.type == "cuda":
+                return v.device
+    return None
+
+
+def on_device(fn):
+    """Run a wrapper with its first device tensor's GPU current, so the
+    library's launches, scratch and the default stream (the current stream of
+    that device) all land on the device that holds the data."""
+    import functools
+
+    @functools.wraps(fn)
+    def wrapped(*args, **kwargs):
+        dev = _first_cuda(args, kwargs)
+        if dev is None or dev.index is None or dev.index == torch.cuda.current_device():
+            return fn(*args, **kwargs)
+        with torch.cuda.device(dev):
+            return fn(*args, **kwargs)
+    return wrapped

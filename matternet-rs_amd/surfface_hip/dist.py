@@ -41,3 +41,51 @@ def sharded_knn(X_shard: torch.Tensor, k: int, knn_fn=None, merge_fn=None, group
     dist.all_to_all_single(recv_i.view(world, -1), part_i.contiguous().view(world, -1), group=group)
     dist.all_to_all_single(recv_d.view(world, -1), part_d.contiguous().view(world, -1), group=group)
     return merge_fn(recv_i, recv_d)
+
+
+# ---- the same build behind the library's C entry (caller-owned RCCL comm) ----
+
+class RcclComm:
+    """An RCCL communicator created through the library (mn_rccl_comm_init):
+    rank 0 makes the 128-byte id (`unique_id()`), every rank passes it here."""
+
+    def __init__(self, uid: bytes, world: int, rank: int):
+        import ctypes as C
+        from . import _lib
+        self._lib = _lib
+        buf = C.create_string_buffer(bytes(uid), 128)
+        h = C.c_void_p()
+        _lib.check(_lib.lib().mn_rccl_comm_init(buf, world, rank, C.byref(h)))
+        self.handle = h
+
+    @staticmethod
+    def unique_id() -> bytes:
+        import ctypes as C
+        from . import _lib
+        buf = C.create_string_buffer(128)
+        _lib.check(_lib.lib().mn_rccl_unique_id(buf))
+        return buf.raw
+
+    def close(self):
+        if self.handle:
+            self._lib.check(self._lib.lib().mn_rccl_comm_destroy(self.handle))
+            self.handle = None
+
+
+def knn_sharded_capi(X_shard: torch.Tensor, k: int, comm: RcclComm, query_chunk: int = 0,
+                     margin: int = 16, timing: bool = False, stream=None):
+    """mn_knn_sharded_f32: this rank's rows of the global exact kNN graph
+    (idx [n_loc, k] int32 global ids, dist [n_loc, k] f32)."""
+    import ctypes as C
+    from . import _lib
+    from ._torch import ptr, require_cuda, stream_handle
+    X_shard = require_cuda(X_shard, torch.float32, "X_shard", 2)
+    n, d = X_shard.shape
+    idx = torch.empty((n, k), dtype=torch.int32, device=X_shard.device)
+    dd = torch.empty((n, k), dtype=torch.float32, device=X_shard.device)
+    o = _lib.KnnOpts(k=k, metric=_lib.MN_L2SQ, exclude_self=1, margin=margin,
+                     timing=1 if timing else 0, algo=_lib.MN_KNN_AUTO,
+                     stream=stream_handle(stream))
+    _lib.check(_lib.lib().mn_knn_sharded_f32(ptr(X_shard), n, d, comm.handle, C.byref(o),
+                                             query_chunk, ptr(idx), ptr(dd)))
+    return idx, dd

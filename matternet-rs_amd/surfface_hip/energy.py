@@ -26,7 +26,7 @@ from dataclasses import dataclass
 import torch
 
 from . import _lib
-from ._torch import ptr, require_cuda, stream_handle
+from ._torch import ptr, require_cuda, stream_handle, on_device
 from .laplacian import CsrMatrix
 
 
@@ -70,6 +70,9 @@ def last_stats() -> dict:
     return st.as_dict()
 
 
+@on_device
+
+
 def energy_rows(X: torch.Tensor, L: CsrMatrix, g_mode: int = _lib.MN_G_TAUMODE,
                 taumode: TauMode = TauMode.Median, timing: bool = False, stream=None):
     """Raw per-row (E, G, lambda) as f64 device tensors."""
@@ -84,6 +87,9 @@ def energy_rows(X: torch.Tensor, L: CsrMatrix, g_mode: int = _lib.MN_G_TAUMODE,
     _lib.check(_lib.lib().mn_energy_rows(C.byref(csr), ptr(X), n, f, C.byref(o), ptr(E), ptr(G),
                                          ptr(lam)))
     return E, G, lam
+
+
+@on_device
 
 
 def normalise_lambdas(lam: torch.Tensor, stream=None):
@@ -137,6 +143,9 @@ def _rows_in(X: torch.Tensor):
     return X, 1 if X.dtype == torch.float64 else 0
 
 
+@on_device
+
+
 def diffuse_rows(X: torch.Tensor, L: CsrMatrix, eta: float = 0.1, steps: int = 4,
                  out: torch.Tensor = None, stream=None) -> torch.Tensor:
     """`steps` x [x <- x - eta * L x] per row (EnergyParams defaults eta 0.1,
@@ -150,6 +159,9 @@ def diffuse_rows(X: torch.Tensor, L: CsrMatrix, eta: float = 0.1, steps: int = 4
     return out
 
 
+@on_device
+
+
 def laplacian_matvec_rows(X: torch.Tensor, L: CsrMatrix, stream=None) -> torch.Tensor:
     """Y = L x per row (GraphLaplacian::multiply_vector); f64 result."""
     X, xf64 = _rows_in(X)
@@ -159,6 +171,9 @@ def laplacian_matvec_rows(X: torch.Tensor, L: CsrMatrix, stream=None) -> torch.T
     _lib.check(_lib.lib().mn_laplacian_matvec_rows(C.byref(csr), ptr(X), xf64, n, f, ptr(Y),
                                                    stream_handle(stream)))
     return Y
+
+
+@on_device
 
 
 def signal_energy_and_dispersion(X: torch.Tensor, L_items: CsrMatrix,

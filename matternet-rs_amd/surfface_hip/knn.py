@@ -15,7 +15,7 @@ from enum import IntEnum
 import torch
 
 from . import _lib
-from ._torch import ptr, require_cuda, stream_handle, to_device
+from ._torch import ptr, require_cuda, stream_handle, to_device, on_device
 
 
 class DistanceMetric(IntEnum):
@@ -47,6 +47,9 @@ def last_stats() -> dict:
     return st.as_dict()
 
 
+@on_device
+
+
 def knn_l2sq(X: torch.Tensor, k: int, margin: int = 16, timing: bool = False,
              stream=None, out_idx=None, out_dist=None, algo: str = "auto",
              euclidean: bool = False) -> KnnResult:
@@ -65,6 +68,9 @@ def knn_l2sq(X: torch.Tensor, k: int, margin: int = 16, timing: bool = False,
     return KnnResult(idx, dist, last_stats())
 
 
+@on_device
+
+
 def knn_l2sq_qc(Qm: torch.Tensor, Cm: torch.Tensor, k: int, q_offset: int = 0, c_offset: int = 0,
                 exclude_self: bool = True, margin: int = 16, timing: bool = False,
                 stream=None, algo: str = "auto") -> KnnResult:
@@ -81,6 +87,9 @@ def knn_l2sq_qc(Qm: torch.Tensor, Cm: torch.Tensor, k: int, q_offset: int = 0, c
     _lib.check(_lib.lib().mn_knn_f32_qc(ptr(Qm), nq, ptr(Cm), nc, d, q_offset, c_offset,
                                         C.byref(o), ptr(idx), ptr(dist)))
     return KnnResult(idx, dist, last_stats())
+
+
+@on_device
 
 
 def merge_parts(part_idx: torch.Tensor, part_dist: torch.Tensor, stream=None):
@@ -120,6 +129,9 @@ def cos_last_stats() -> dict:
     return st.as_dict()
 
 
+@on_device
+
+
 def knn_cos_columns(X: torch.Tensor, topk: int, eps: float = 1.0, sigma: float = 1.0,
                     p: float = 2.0, margin: int = 16, timing: bool = False, stream=None):
     """Rectified-cosine kNN of the FEATURE columns of X [n, f] (each column is a
@@ -144,6 +156,9 @@ def bf16_last_stats() -> dict:
     return st.as_dict()
 
 
+@on_device
+
+
 def knn_cos_bf16(X: torch.Tensor, topk: int, eps: float = 1.0, sigma: float = 1.0,
                  p: float = 2.0, margin: int = 16, timing: bool = False, stream=None):
     """Item graph of config 5: rectified-cosine kNN over the ROWS of a bf16
@@ -160,6 +175,9 @@ def knn_cos_bf16(X: torch.Tensor, topk: int, eps: float = 1.0, sigma: float = 1.
                      timing=1 if timing else 0, reserved0=0, stream=stream_handle(stream))
     _lib.check(_lib.lib().mn_knn_cos_bf16(ptr(X), n, d, C.byref(o), ptr(idx), ptr(dist), ptr(w)))
     return idx, dist, w, bf16_last_stats()
+
+
+@on_device
 
 
 def knn_cos_bf16_qc(Q: torch.Tensor, C_: torch.Tensor, topk: int, q_offset: int = 0,

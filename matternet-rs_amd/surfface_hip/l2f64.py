@@ -16,9 +16,12 @@ import numpy as np
 import torch
 
 from . import _lib
-from ._torch import ptr, stream_handle, to_device
+from ._torch import ptr, stream_handle, to_device, on_device
 
 _MAX_NQ = 65535 * 32  # queries per library call
+
+
+@on_device
 
 
 def knn_l2_f64(Q, Cm, k: int, q_ids=None, use_sqrt: bool = False, stream=None):

@@ -22,7 +22,7 @@ import numpy as np
 import torch
 
 from . import _lib
-from ._torch import ptr, require_cuda, stream_handle
+from ._torch import ptr, require_cuda, stream_handle, on_device
 
 
 @dataclass
@@ -104,6 +104,9 @@ def _adopt(csr: _lib.Csr, device) -> CsrMatrix:
     return CsrMatrix(indptr, indices, values, (n, n))
 
 
+@on_device
+
+
 def build_laplacian_from_knn(nbr_idx: torch.Tensor, nbr_val: torch.Tensor, *,
                              weight_kernel: str = "rational", symmetrise: str = "union",
                              normalize: bool = False, eps: float = 1.0, sigma: float = 1.0,
@@ -149,6 +152,9 @@ def laplacian_stage_from_edges(nbr_idx: torch.Tensor, weights: torch.Tensor,
     f = nbr_idx.shape[0]
     return LaplacianOutput(matrix=m, n_features=f, nnz=m.nnz, degrees=deg,
                            sparsity=1.0 - m.nnz / float(f * f))
+
+
+@on_device
 
 
 def compute_bhattacharyya_weights(means: torch.Tensor, variances: torch.Tensor,

@@ -13,7 +13,10 @@ import math
 import torch
 
 from . import _lib
-from ._torch import ptr, require_cuda, stream_handle
+from ._torch import ptr, require_cuda, stream_handle, on_device
+
+
+@on_device
 
 
 def search_lambda_aware(X: torch.Tensor, lambdas: torch.Tensor, queries: torch.Tensor,
@@ -88,6 +91,9 @@ def prepare_query_lambdas(queries: torch.Tensor, L_features, taumode=None, min_l
     if range_lambdas is not None and math.isfinite(range_lambdas):
         lam = ((lam - min_lambdas) / range_lambdas).clamp_(0.0, 1.0)
     return lam
+
+
+@on_device
 
 
 def search_lambda_aware_hybrid(X, lambdas, queries, query_lambdas, k: int, alpha: float,

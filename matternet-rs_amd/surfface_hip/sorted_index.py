@@ -11,7 +11,7 @@ import ctypes as C
 import torch
 
 from . import _lib
-from ._torch import ptr, require_cuda, stream_handle
+from ._torch import ptr, require_cuda, stream_handle, on_device
 
 
 class SortedLambdas:
@@ -19,6 +19,8 @@ class SortedLambdas:
         self.order = None   # int64 [n] item index at each rank (device)
         self.keys = None    # f64 [n] bucket key at each rank (device)
         self.std_dev = 0.0
+
+    @on_device
 
     def build_from(self, lambdas: torch.Tensor, stream=None) -> "SortedLambdas":
         lam = require_cuda(lambdas, torch.float64, "lambdas", 1)
@@ -53,6 +55,8 @@ class SortedLambdas:
                 torch.empty((nq, max(k, 1)), dtype=torch.float64, device=dev),
                 torch.empty(nq, dtype=torch.int32, device=dev))
 
+    @on_device
+
     def range_bylambda(self, lambda_q, k: int, p: float):
         """Items with key in [lq - std/2^p, lq + std/2^p], index order, first k.
         Scalar query -> [(idx, lambda)]; tensor [nq] -> (idx [nq,k], lambda
@@ -63,6 +67,8 @@ class SortedLambdas:
             ptr(self.keys), ptr(self.order), self.order.numel(), self.std_dev, ptr(q), q.numel(),
             k, p, ptr(oi), ptr(ol), ptr(oc), stream_handle()))
         return self._result(scalar, oi, ol, oc, k, with_id=False)
+
+    @on_device
 
     def k_nearest_by_lambda(self, lambda_q, k: int, lambda_p: float, base_delta=None,
                             growth: float = 1.7, max_multiplier: float = 10.0):

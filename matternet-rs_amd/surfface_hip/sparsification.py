@@ -13,7 +13,10 @@ import ctypes as C
 import torch
 
 from . import _lib
-from ._torch import ptr, require_cuda, stream_handle
+from ._torch import ptr, require_cuda, stream_handle, on_device
+
+
+@on_device
 
 
 def sparsify_rows(nbr_idx: torch.Tensor, nbr_w: torch.Tensor, ratio: float = 0.5,

@@ -111,7 +111,7 @@ static int knn_l2sq_core(const float *X, int64_t n, int32_t d, int32_t k,
 #pragma omp atomic write
             err = OR_ENOMEM;
         }
-#pragma omp for schedule(dynamic, 16)
+#pragma omp for schedule(dynamic, 1) /* rows cost ~n d each: one per chunk */
         for (int64_t qq = q_begin; qq < q_end; ++qq) {
             if (!buf) continue;
             const int64_t i = rows ? rows[qq] : qq;
@@ -1185,6 +1185,91 @@ int or_knn_l2_f64(const double *Q, int64_t nq, const double *C, int64_t nc, int3
         }
         free(bd);
         free(bj);
+    }
+    return err;
+}
+
+/* ------------------------------------------------------------------------ */
+/* K3 faithful cost model (taumode.rs:366-408 with CsMat::get)               */
+/* ------------------------------------------------------------------------ */
+
+/* sprs CsMat::get(i, j) on a CSR matrix with sorted indices: binary search */
+static inline double csr_get(const int64_t *indptr, const int32_t *indices, const double *values,
+                             int32_t i, int32_t j) {
+    int64_t lo = indptr[i], hi = indptr[i + 1];
+    while (lo < hi) {
+        int64_t mid = lo + (hi - lo) / 2;
+        if (indices[mid] < j) lo = mid + 1;
+        else hi = mid;
+    }
+    return (lo < indptr[i + 1] && indices[lo] == j) ? values[lo] : 0.0;
+}
+
+int or_energy_rows_faithful(const float *X, int64_t n_rows, int32_t f,
+                            const int64_t *indptr, const int32_t *indices,
+                            const double *values, int tau_mode, double tau_param,
+                            int nthreads, double *E, double *G, double *lambda) {
+    if (!X || n_rows < 0 || f < 1 || !indptr || !indices || !values) return OR_EINVAL;
+    set_threads(nthreads);
+    int err = 0;
+#pragma omp parallel
+    {
+        double *x = (double *)malloc(sizeof(double) * (size_t)f);
+        if (!x) {
+#pragma omp atomic write
+            err = OR_ENOMEM;
+        }
+#pragma omp for schedule(dynamic, 4)
+        for (int64_t r = 0; r < n_rows; ++r) {
+            if (!x) continue;
+            const float *xr = X + r * (int64_t)f;
+            for (int32_t t = 0; t < f; ++t) x[t] = (double)xr[t];
+            double e_raw = 0.0, g_raw = 0.0, lam = 0.0;
+            int zero = 1;
+            for (int32_t t = 0; t < f; ++t) if (!(fabs(x[t]) <= 1e-10)) { zero = 0; break; }
+            if (!zero) {
+                double num = 0.0;
+                for (int32_t i = 0; i < f; ++i) {
+                    double xi = x[i], rs = -0.0;
+                    for (int64_t p = indptr[i]; p < indptr[i + 1]; ++p)
+                        rs = rs + (xi * values[p]) * x[indices[p]];
+                    num = num + rs;
+                }
+                double den = -0.0;
+                for (int32_t t = 0; t < f; ++t) den = den + x[t] * x[t];
+                e_raw = den > 1e-12 ? fmax0(num / den) : 0.0;
+                double s = 0.0;
+                for (int32_t i = 0; i < f; ++i)
+                    for (int32_t j = 0; j < f; ++j) {
+                        if (i == j) continue;
+                        double wv = fmax0(-csr_get(indptr, indices, values, i, j));
+                        if (wv > 0.0) { double dd = x[i] - x[j]; s += wv * dd * dd; }
+                    }
+                if (s <= 1e-12) g_raw = 0.0;
+                else {
+                    double g = 0.0;
+                    for (int32_t i = 0; i < f; ++i)
+                        for (int32_t j = 0; j < f; ++j) {
+                            if (i == j) continue;
+                            double wv = fmax0(-csr_get(indptr, indices, values, i, j));
+                            if (wv > 0.0) {
+                                double dd = x[i] - x[j];
+                                double c = wv * dd * dd;
+                                double sh = c / s;
+                                g += sh * sh;
+                            }
+                        }
+                    g_raw = clamp01(g);
+                }
+                double tau = or_select_tau(x, f, tau_mode, tau_param);
+                double eb = e_raw / (e_raw + tau);
+                lam = tau * eb + (1.0 - tau) * clamp01(g_raw);
+            }
+            if (E) E[r] = e_raw;
+            if (G) G[r] = g_raw;
+            if (lambda) lambda[r] = lam;
+        }
+        free(x);
     }
     return err;
 }

@@ -154,6 +154,17 @@ int or_energy_rows(const float *X, int64_t n_rows, int32_t f,
                    double tau_param, int nthreads, double *E, double *G,
                    double *lambda);
 
+/* The same TAUMODE rows computed as the reference writes them (the FAITHFUL
+ * CPU baseline of BASELINE.md): compute_item_dispersion's two passes over all
+ * F^2 ordered pairs with a CsMat::get (binary search of row i) per pair
+ * (src_legacy/taumode.rs:366-408); Rayleigh by CSR rows (:340-354).  Values
+ * equal or_energy_rows(G_TAUMODE) (zero pairs add +0.0); only the cost
+ * differs. */
+int or_energy_rows_faithful(const float *X, int64_t n_rows, int32_t f,
+                            const int64_t *indptr, const int32_t *indices,
+                            const double *values, int tau_mode, double tau_param,
+                            int nthreads, double *E, double *G, double *lambda);
+
 /* src_legacy/core.rs:1341-1354 normalise_lambdas: min = fold(+inf,min),
  * max = fold(0.0,max), range = max(max-min,1e-9), x' = (x-min)/range. */
 int or_normalise_lambdas(double *lam, int64_t n, double *min_out,

@@ -56,6 +56,7 @@ def _declare(L):
     L.or_select_tau.argtypes = [P, I64, C.c_int, D]
     L.or_select_tau.restype = D
     L.or_energy_rows.argtypes = [P, I64, I32, P, P, P, C.c_int, C.c_int, D, C.c_int, P, P, P]
+    L.or_energy_rows_faithful.argtypes = [P, I64, I32, P, P, P, C.c_int, D, C.c_int, P, P, P]
     L.or_normalise_lambdas.argtypes = [P, I64, P, P, P]
     L.or_spectral_lambdas_f32.argtypes = [P, I64, I32, P, P, P, P]
     L.or_sorted_index.argtypes = [P, I64, P, P, P]
@@ -196,6 +197,22 @@ def energy_rows(X, indptr, indices, values, g_mode=G_TAUMODE, tau_mode=TAU_MEDIA
     _check(lib().or_energy_rows(_p(X), n, f, _p(indptr), _p(indices), _p(values), g_mode,
                                 tau_mode, tau_param, nthreads, _p(E), _p(G), _p(lam)),
            "energy_rows")
+    return E, G, lam
+
+
+def energy_rows_faithful(X, indptr, indices, values, tau_mode=TAU_MEDIAN, tau_param=0.0,
+                         nthreads=0):
+    """TAUMODE rows with the reference's F^2 CsMat::get dispersion (cost model
+    of the faithful CPU baseline); values equal energy_rows(G_TAUMODE)."""
+    X = np.ascontiguousarray(X, dtype=np.float32)
+    n, f = X.shape
+    indptr = np.ascontiguousarray(indptr, dtype=np.int64)
+    indices = np.ascontiguousarray(indices, dtype=np.int32)
+    values = np.ascontiguousarray(values, dtype=np.float64)
+    E = np.empty(n); G = np.empty(n); lam = np.empty(n)
+    _check(lib().or_energy_rows_faithful(_p(X), n, f, _p(indptr), _p(indices), _p(values),
+                                         tau_mode, tau_param, nthreads, _p(E), _p(G), _p(lam)),
+           "energy_rows_faithful")
     return E, G, lam
 
 

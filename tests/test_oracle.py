@@ -360,3 +360,18 @@ def test_search_hybrid_oracle_vs_python():
             assert oc[t] == len(exp)
             assert [i for i, _ in exp] == oi[t, :oc[t]].tolist()
             assert [s for _, s in exp] == osc[t, :oc[t]].tolist()
+
+
+def test_energy_rows_faithful_equals_csr_restatement():
+    """The faithful (F^2 CsMat::get) TAUMODE rows equal the CSR-iterating
+    restatement bit for bit (absent pairs add +0.0)."""
+    rng = np.random.default_rng(3)
+    f = 40
+    X = rng.standard_normal((300, f)).astype(np.float32)
+    X[7] = 0.0
+    idx, _, w = O.knn_cos(X.T.copy(), 4, eps=1.0, sigma=1.0, p=2.0)
+    ip, ix, iv = O.laplacian_union(idx, np.where(idx >= 0, w, 0.0))
+    e1, g1, l1 = O.energy_rows(X, ip, ix, iv, O.G_TAUMODE, O.TAU_MEDIAN)
+    e2, g2, l2 = O.energy_rows_faithful(X, ip, ix, iv, O.TAU_MEDIAN)
+    for a, b in ((e1, e2), (g1, g2), (l1, l2)):
+        np.testing.assert_array_equal(a.view(np.uint64), b.view(np.uint64))

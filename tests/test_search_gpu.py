@@ -173,3 +173,21 @@ def test_hybrid_k_limit():
                                      torch.from_numpy(Q).cuda(), torch.from_numpy(lq).cuda(),
                                      256, 0.7)
     assert e.value.code == S._lib.MN_ENOTSUP
+
+
+@pytest.mark.parametrize("k", [1, 2, 3, 8])
+def test_hybrid_many_high_semantic_items_small_k(k):
+    """More than k items with cosine > 0.9999 (scaled copies of the query):
+    every such item keeps its COSINE as score (core.rs:1289-1299), including
+    one that reaches the union only through the lambda top k (advisor r1)."""
+    rng = np.random.default_rng(40 + k)
+    n, f = 2000, 16
+    X, lam, Q, lq = case(n, f, 3, 77)
+    scales = rng.uniform(0.2, 5.0, size=40).astype(np.float32)
+    rows = rng.choice(n, 40, replace=False)
+    X[rows] = (Q[0].astype(np.float32)[None, :] * scales[:, None]).astype(np.float32)
+    Q[0] = X[rows[0]].astype(np.float64)
+    # lambdas: the copies' lambdas near lq[0] beat every other item's lambda score
+    lam[rows] = lq[0] + rng.uniform(-1e-3, 1e-3, size=40)
+    for alpha in (0.7, 0.2):
+        check_hybrid(X, lam, Q, lq, k, alpha)
