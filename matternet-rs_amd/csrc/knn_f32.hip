@@ -1471,11 +1471,24 @@ static int knn_x1(const float *Q, int64_t nq, const float *C, int64_t nc, int32_
 #undef MN_RRX
     MN_KCHECK(s, "k_rerank_x1");
     tm.mark();
-    // many uncertified rows: escalate them to the split generator instead of
-    // the exact scan (whose cost is O(nc d) per row)
-    int nfb = 0;
-    MN_HIP_TRY(hipMemcpyAsync(&nfb, fb_count, 4, hipMemcpyDeviceToHost, s));
+    // statistics of the buffers now: an escalation below reuses (and may
+    // reallocate) the scratch slots that hold them
+    if (tm.on) {
+        hipLaunchKernelGGL(k_count_cands, dim3(1024), dim3(256), 0, s, bcnt1, nq * pl.S, pl.cap,
+                           ncand);
+        if (two)
+            hipLaunchKernelGGL(k_count_cands, dim3(1024), dim3(256), 0, s, cnt2, nq * S2, cap2,
+                               ncand);
+        MN_KCHECK(s, "k_count_cands");
+    }
+    int64_t hpre[8] = {0};
+    MN_HIP_TRY(hipMemcpyAsync(hpre, flags, 64, hipMemcpyDeviceToHost, s));
     MN_HIP_TRY(hipStreamSynchronize(s));
+    const int nfb = ((const int *)hpre)[5];
+    const int64_t n_cand = hpre[4];
+    // many uncertified rows: escalate them to the split generator instead of
+    // the exact scan (whose cost is O(nc d) per row).  No x1 buffer (phase-1 /
+    // sweep lists, perm, sample) is touched after this point.
     float ms_esc = 0.f;
     int64_t esc_uncert = 0;
     if (nfb > 256) {
@@ -1525,20 +1538,12 @@ static int knn_x1(const float *Q, int64_t nq, const float *C, int64_t nc, int32_
                            q_off, c_off, excl, k, fb_count, fb_list, out_idx, out_dist);
     MN_KCHECK(s, "k_fallback");
     tm.mark();
-    if (tm.on) {
-        hipLaunchKernelGGL(k_count_cands, dim3(1024), dim3(256), 0, s, bcnt1, nq * pl.S, pl.cap,
-                           ncand);
-        if (two)
-            hipLaunchKernelGGL(k_count_cands, dim3(1024), dim3(256), 0, s, cnt2, nq * S2, cap2,
-                               ncand);
-        MN_KCHECK(s, "k_count_cands");
-    }
     int64_t hf[8] = {0};
     MN_HIP_TRY(hipMemcpyAsync(hf, flags, 64, hipMemcpyDeviceToHost, s));
     MN_HIP_TRY(hipStreamSynchronize(s));
     t_stats.n_uncertified = ((const int *)hf)[5] + esc_uncert;
     if (tm.on) {
-        t_stats.n_candidates = hf[4];
+        t_stats.n_candidates = n_cand;
         t_stats.ms_norms = tm.ms(0, 1);
         t_stats.ms_sample = tm.ms(1, 2);
         t_stats.ms_sweep = tm.ms(2, 3);

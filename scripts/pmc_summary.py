@@ -33,7 +33,9 @@ def main():
     dom = max(stats, key=lambda k: float(stats[k]["TotalDurationNs"]))
     dshort = dom.split("(")[0].replace("void ", "")
     out = {"tag": tag, "rows_per_gpu": n, "dim": d, "kernel": dshort.split("::")[-1],
-           "kernel_full": dshort, "kernels": {}}
+           "kernel_full": dshort, "kernels": {},
+           "source": f"profiles/{tag}_summary.json (rocprofv3 passes of run '{tag}': "
+                     f"kernel trace + separate FETCH_SIZE / WRITE_SIZE --pmc passes)"}
     for name, r in stats.items():
         short = name.split("(")[0].replace("void ", "")
         out["kernels"][short] = {"calls": int(r["Calls"]), "avg_ms": float(r["AverageNs"]) / 1e6,
@@ -58,7 +60,9 @@ def main():
         out["dominant_pmc"] = {"FETCH_SIZE_KiB": pm["FETCH_SIZE"], "WRITE_SIZE_KiB": pm["WRITE_SIZE"],
                            "fetch_bytes_corrected": fetch_b, "write_bytes": write_b}
         out["hbm_bytes_per_launch"] = fetch_b + write_b
-        out["algorithmic_bytes_per_launch"] = 2 * n * d * 4
+        # operands read once: bf16 query and corpus copies (the sweep) or the
+        # f32 rows (older generators)
+        out["algorithmic_bytes_per_launch"] = (2 * n * d * 2 if "sweep" in dshort else 2 * n * d * 4)
     with open(os.path.join(dst, f"{tag}_summary.json"), "w") as fh:
         json.dump(out, fh, indent=1)
     with open(os.path.join(dst, "pmc_gram_latest.json"), "w") as fh:

@@ -1,0 +1,180 @@
+"""Every single-GPU BASELINE config at full size through the C ABI.
+
+  C2  1M x 768 f32, k=32 (uniform, seed 42): oracle-sampled rows bit-exact,
+      sortedness / self-exclusion on every row, no uncertified row;
+  C2c the same shape on the SURVEY §8(d) clustered stress distribution (64
+      blobs sigma 0.1, 1% duplicates, 0.1% zero rows, seed 7): sampled rows
+      bit-exact, with the certification / escalation / fallback cost recorded
+      and bounded;
+  C3  the chain at 1M: item Laplacian (legacy UNION, rational weights) rows
+      vs the oracle on the sampled rows' full incident subgraph, the 768-node
+      feature graph + Laplacian, taumode energy rows on sampled items vs the
+      oracle (1e-9), the sorted index of all 1M lambdas vs the oracle;
+  C5  1M x 3072 bf16 rectified cosine, k=32: sampled rows bit-exact,
+      SF-GRASS (ratio 0.5) applied.
+Reference: mst.rs:312-363, test_helpers.rs:73-138, laplacian.rs:297-419,
+taumode.rs:117-408, sorted_index.rs:22-54, sparsification.rs:32-113.
+"""
+import json
+import os
+import time
+
+import numpy as np
+import pytest
+import torch
+
+import datagen
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+N, D, K = 1_000_000, 768, 32
+THREADS = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+
+
+def _uniform_dev(n, d, seed):
+    import surfface_hip as S
+    X = torch.empty((n, d), dtype=torch.float32, device="cuda")
+    S._lib.check(S.lib().mn_fill_uniform_f32(X.data_ptr(), n, d, seed, 0,
+                                             torch.cuda.current_stream().cuda_stream))
+    torch.cuda.synchronize()
+    return X
+
+
+def _check_graph(Xh, idx, dist, rows):
+    ridx, rdist = O.knn_l2sq_rows(Xh, K, rows, nthreads=THREADS)
+    np.testing.assert_array_equal(idx[rows], ridx)
+    np.testing.assert_array_equal(dist[rows].view(np.uint32), rdist.view(np.uint32))
+    assert (np.diff(dist, axis=1) >= 0).all()
+    assert (idx != np.arange(idx.shape[0])[:, None]).all()
+
+
+@pytest.fixture(scope="module")
+def c2():
+    import surfface_hip as S
+    X = _uniform_dev(N, D, 42)
+    r = S.knn_l2sq(X, K, timing=True)
+    return X, r
+
+
+def test_c2_1m_uniform_sampled_rows_bit_exact(c2):
+    X, r = c2
+    rows = np.random.default_rng(0).choice(N, 128, replace=False)
+    _check_graph(X.cpu().numpy(), r.idx.cpu().numpy(), r.dist.cpu().numpy(), rows)
+    st = r.stats
+    print("C2 stats", json.dumps({k: v for k, v in st.items() if k != "reserved1"}))
+    assert st["n_uncertified"] == 0 and st["n_escalated"] == 0
+
+
+def test_c2_1m_clustered_stress_bounded():
+    import surfface_hip as S
+    t0 = time.time()
+    Xh = datagen.clustered(N, D, seed=7)
+    X = torch.from_numpy(Xh).cuda()
+    t1 = time.time()
+    r = S.knn_l2sq(X, K, timing=True)
+    torch.cuda.synchronize()
+    t2 = time.time()
+    rows = np.random.default_rng(1).choice(N, 128, replace=False)
+    zero = np.flatnonzero(~Xh.any(axis=1))[:4]  # all-zero rows: exact ties far beyond k
+    rows = np.unique(np.concatenate([rows, zero]))
+    _check_graph(Xh, r.idx.cpu().numpy(), r.dist.cpu().numpy(), rows)
+    st = r.stats
+    rec = {"gen_s": round(t1 - t0, 1), "knn_wall_s": round(t2 - t1, 2),
+           **{k: (round(v, 2) if isinstance(v, float) else v) for k, v in st.items()
+              if k != "reserved1"}}
+    print("C2-clustered stats", json.dumps(rec))
+    # bounded: the escalation / exact-scan cost stays within a small multiple
+    # of the uniform build (2 s)
+    assert t2 - t1 < 60.0, rec
+
+
+def _union_rows_oracle(idx, dist, rows, sigma=1.0):
+    """Expected legacy UNION Laplacian rows of `rows` (laplacian.rs:297-419)
+    from their full incident edge set: the oracle on the induced subgraph
+    (every edge touching a sampled row, ids kept in ascending order)."""
+    n, k = idx.shape
+    inc = np.isin(idx, rows)                       # rows j with an edge j -> sampled
+    src = np.unique(np.concatenate([rows, np.flatnonzero(inc.any(axis=1))]))
+    nodes = np.unique(np.concatenate([src, idx[src].ravel()]))
+    nodes = nodes[nodes >= 0]
+    pos = {int(v): i for i, v in enumerate(nodes)}
+    sub_idx = -np.ones((len(nodes), k), np.int32)
+    sub_w = np.zeros((len(nodes), k), np.float64)
+    d64 = dist.astype(np.float64)
+    for j in src:
+        p = pos[int(j)]
+        for t in range(k):
+            c = int(idx[j, t])
+            if c >= 0:
+                sub_idx[p, t] = pos[c]
+                sub_w[p, t] = 1.0 / (1.0 + (d64[j, t] / sigma) ** 2)
+    ip, ix, iv = O.laplacian_union(sub_idx, sub_w)
+    out = {}
+    for i in rows:
+        p = pos[int(i)]
+        out[int(i)] = (nodes[ix[ip[p]:ip[p + 1]]], iv[ip[p]:ip[p + 1]])
+    return out
+
+
+def test_c3_chain_1m(c2):
+    import surfface_hip as S
+    X, r = c2
+    idx = r.idx.cpu().numpy()
+    dist = r.dist.cpu().numpy()
+    # 1. item Laplacian (legacy UNION, rational weights sigma 1, p 2)
+    L, deg = S.build_laplacian_from_knn(r.idx, r.dist, weight_kernel="rational",
+                                        symmetrise="union", eps=float("inf"), sigma=1.0, p=2.0)
+    ip, ix, iv = L.to_numpy()
+    rows = np.random.default_rng(2).choice(N, 48, replace=False)
+    exp = _union_rows_oracle(idx, dist, rows)
+    for i in rows:
+        cols, vals = exp[int(i)]
+        np.testing.assert_array_equal(ix[ip[i]:ip[i + 1]], cols)
+        np.testing.assert_array_equal(iv[ip[i]:ip[i + 1]].view(np.uint64), vals.view(np.uint64))
+    # 2. feature graph (768 column nodes, topk 4) + its Laplacian
+    fi, fd, fw, fst = S.knn_cos_columns(X, 4, eps=1.0, sigma=1.0, p=2.0)
+    assert fst["n_uncertified"] == 0
+    Lf, _ = S.build_laplacian_from_knn(fi, fw, weight_kernel="given", symmetrise="union")
+    fip, fix, fiv = Lf.to_numpy()
+    # 3. taumode energy rows of all 1M items; sampled rows vs the oracle
+    E, G, lam = S.energy_rows(X, Lf)
+    Xh = X.cpu().numpy()
+    srows = np.random.default_rng(3).choice(N, 4096, replace=False)
+    rE, rG, rl = O.energy_rows(Xh[srows], fip, fix, fiv, O.G_TAUMODE, O.TAU_MEDIAN)
+    for got, ref in ((E, rE), (G, rG), (lam, rl)):
+        np.testing.assert_allclose(got.cpu().numpy()[srows], ref, rtol=1e-9, atol=1e-12)
+    # 4. normalise + sorted index of all 1M lambdas vs the oracle (bit-exact
+    #    given identical lambdas)
+    lam_n = lam.clone()
+    S.normalise_lambdas(lam_n)
+    sl = S.SortedLambdas().build_from(lam_n)
+    lh = lam_n.cpu().numpy()
+    order, keys, std = O.sorted_index(lh)
+    np.testing.assert_array_equal(sl.order.cpu().numpy(), order)
+    np.testing.assert_array_equal(sl.keys.cpu().numpy().view(np.uint64), keys.view(np.uint64))
+
+
+def test_c5_1m_3072_bf16_cosine_sampled_rows():
+    import surfface_hip as S
+    n, d = 1_048_576, 3072
+    Xb = torch.empty((n, d), dtype=torch.bfloat16, device="cuda")
+    tmp = torch.empty((1 << 17, d), dtype=torch.float32, device="cuda")
+    for r0 in range(0, n, 1 << 17):
+        S._lib.check(S.lib().mn_fill_uniform_f32(tmp.data_ptr(), 1 << 17, d, 47, r0,
+                                                 torch.cuda.current_stream().cuda_stream))
+        Xb[r0:r0 + (1 << 17)].copy_(tmp)
+    del tmp
+    idx, dist, w, st = S.knn_cos_bf16(Xb, K, eps=1.0, sigma=1.0, p=2.0, timing=True)
+    print("C5 stats", json.dumps({k: v for k, v in st.items() if k != "reserved1"}))
+    rows = np.array([0, 77_777, 524_287, n - 1])
+    bits = Xb.view(torch.int16).cpu().numpy().view(np.uint16)
+    ri, rd, rw = O.knn_cos_bf16_rows(bits, K, rows, nthreads=THREADS)
+    sel = torch.from_numpy(rows).cuda()
+    np.testing.assert_array_equal(idx[sel].cpu().numpy(), ri)
+    np.testing.assert_array_equal(dist[sel].cpu().numpy().view(np.uint64), rd.view(np.uint64))
+    np.testing.assert_array_equal(w[sel].cpu().numpy().view(np.uint64), rw.view(np.uint64))
+    sidx, sw, applied = S.sparsify_rows(idx, w, 0.5)
+    assert applied
+    kept = (sidx >= 0).sum(dim=1)
+    assert int(kept.min()) == 16 and int(kept.max()) == 16  # ceil(32 * 0.5) per full row
