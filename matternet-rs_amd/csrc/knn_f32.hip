@@ -751,6 +751,162 @@ __global__ __launch_bounds__(256) void k_prep_x1(const float *__restrict__ X, in
     }
 }
 
+// ---------------------------------------------------------------------------
+// 2d. refill of the rows the bf16x1 bound could not certify (dense clusters:
+// the bound scales with |q||c|, not with the neighbour distances)
+//
+// The bf16x3 product q.c ~ qh.ch + qh.cl + ql.ch is ONE dot product of length
+// 3 dp: [qh | qh | ql] . [ch | cl | ch].  So the same sweep kernel, given KB32
+// copies of those concatenated rows, evaluates the split Gram with a
+// per-query fixed threshold and NO list-length limit.  Each uncertified row
+// already holds an upper bound ub >= D_k (the k-th exact distance among its
+// re-ranked candidates); the refill buffers every pair with key < T = ub +
+// 1.125 delta3(ub), so every pair with d <= ub is buffered and the re-rank
+// certifies T - delta3(T) > D_k by construction (buffer overflow aside).
+//
+// delta3: with x = h + l + r2 (hi = bf16(x), lo = bf16(x - hi), r2 exact),
+//   omitted products  <= |ql| max|cl| + (|qh|+|ql|+|q2|) max|c2| + |q2|(max|ch|+max|cl|)
+//   f32 accumulation of the 3 dp exact products on top of acc0:
+//                        (6 dp + 64) u (M + (|qh|+|ql|)(max|ch|+max|cl|))
+//                        (2x the round-to-nearest bound, acc0 <= M / 2)
+//   norms, tq, acc0, stored key: 4 u M, M = |T| + |q|^2 + max|c|^2
+//   and the reference fold's own error (d + 3) u (|T| + 2E), as in k_tau_x1.
+// ---------------------------------------------------------------------------
+
+// KB32 rows of width 3 dp (nkb3 = 3 dp / 32 blocks): queries [hi | hi | lo],
+// corpus [hi | lo | hi].  Output position `row` holds source row rows[row]
+// (queries gathered by the fallback list) or perm[row] (corpus, visiting
+// order).  One wave per pair of rows, like k_prep_x1.
+template <bool VEC4>
+__global__ __launch_bounds__(256) void k_prep_x3(const float *__restrict__ X, int64_t n, int d,
+                                                 int dp, const int *__restrict__ src,
+                                                 uint16_t *__restrict__ XK, int corpus,
+                                                 float *__restrict__ nrm, float *__restrict__ hn,
+                                                 float *__restrict__ ln, float *__restrict__ r2n,
+                                                 unsigned *__restrict__ cmax3) {
+    const int lane = threadIdx.x & 63, hl = lane >> 5, ll = lane & 31;
+    const int64_t wave0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+    const int nkb = dp >> 5;
+    for (int64_t r2 = 2 * wave0; r2 < n; r2 += 2 * nwaves) {
+        const int64_t row = r2 + hl;
+        const bool live = row < n;
+        const int64_t srow = src ? (int64_t)src[min(row, n - 1)] : min(row, n - 1);
+        const float *p = X + srow * (int64_t)d;
+        double s = 0.0, sh = 0.0, sl = 0.0, s2 = 0.0;
+        for (int t0 = 8 * ll; t0 < dp; t0 += 256) {
+            float xv[8];
+            if (VEC4 && t0 + 8 <= d) {
+                const float4 a = *reinterpret_cast<const float4 *>(p + t0);
+                const float4 b = *reinterpret_cast<const float4 *>(p + t0 + 4);
+                xv[0] = a.x; xv[1] = a.y; xv[2] = a.z; xv[3] = a.w;
+                xv[4] = b.x; xv[5] = b.y; xv[6] = b.z; xv[7] = b.w;
+            } else {
+#pragma unroll
+                for (int u = 0; u < 8; ++u) xv[u] = t0 + u < d ? p[t0 + u] : 0.f;
+            }
+            uint32_t hw[4], lw[4];
+#pragma unroll
+            for (int u = 0; u < 8; u += 2) {
+                uint32_t hb2[2], lb2[2];
+#pragma unroll
+                for (int v = 0; v < 2; ++v) {
+                    const float x = xv[u + v];
+                    uint32_t hb = 0, lb = 0;
+                    if (__builtin_fabsf(x) >= 0x1p-126f) hb = bf16_rne(x);
+                    const float hf = __uint_as_float(hb << 16);
+                    const float r = x - hf;  // exact
+                    if (__builtin_fabsf(r) >= 0x1p-126f) lb = bf16_rne(r);
+                    const float lf = __uint_as_float(lb << 16);
+                    const float rr = r - lf;  // exact
+                    s += (double)x * (double)x;
+                    sh += (double)hf * (double)hf;
+                    sl += (double)lf * (double)lf;
+                    s2 += (double)rr * (double)rr;
+                    hb2[v] = hb;
+                    lb2[v] = lb;
+                }
+                hw[u >> 1] = hb2[0] | (hb2[1] << 16);
+                lw[u >> 1] = lb2[0] | (lb2[1] << 16);
+            }
+            if (live) {
+                const uint4 H = make_uint4(hw[0], hw[1], hw[2], hw[3]);
+                const uint4 Lo = make_uint4(lw[0], lw[1], lw[2], lw[3]);
+                const int64_t kb = t0 >> 5, off = row * 32 + (t0 & 31);
+                *reinterpret_cast<uint4 *>(XK + (kb * n) * 32 + off) = H;
+                *reinterpret_cast<uint4 *>(XK + ((kb + nkb) * n) * 32 + off) = corpus ? Lo : H;
+                *reinterpret_cast<uint4 *>(XK + ((kb + 2 * nkb) * n) * 32 + off) = corpus ? H : Lo;
+            }
+        }
+#pragma unroll
+        for (int o = 16; o > 0; o >>= 1) {
+            s += __shfl_xor(s, o);
+            sh += __shfl_xor(sh, o);
+            sl += __shfl_xor(sl, o);
+            s2 += __shfl_xor(s2, o);
+        }
+        if (ll == 0 && live) {
+            const float nf = (float)s;
+            const float hf = f32_up(__builtin_sqrt(sh) * (1.0 + 0x1p-50));
+            const float lf = f32_up(__builtin_sqrt(sl) * (1.0 + 0x1p-50));
+            const float rf = f32_up(__builtin_sqrt(s2) * (1.0 + 0x1p-50));
+            if (nrm) nrm[row] = nf;
+            if (hn) hn[row] = hf;
+            if (ln) ln[row] = lf;
+            if (r2n) r2n[row] = rf;
+            if (corpus) {
+                atomicMax(cmax3 + 0, __float_as_uint(nf));
+                atomicMax(cmax3 + 1, __float_as_uint(hf));
+                atomicMax(cmax3 + 2, __float_as_uint(lf));
+                atomicMax(cmax3 + 3, __float_as_uint(rf));
+            }
+        }
+    }
+}
+
+__device__ __forceinline__ double delta3_at(double Tf, double qn, double qh, double ql, double q2,
+                                            double Mn, double Mh, double Ml, double M2, int d,
+                                            int dp) {
+    const double u = 0x1p-24;
+    const double M = Tf + qn + Mn;
+    const double Eprod = ql * Ml + (qh + ql + q2) * M2 + q2 * (Mh + Ml);
+    const double gam = (6.0 * dp + 64.0) * u;
+    const double E = Eprod + gam * (M + (qh + ql) * (Mh + Ml)) + 4.0 * u * M;
+    return (2.0 * E + (d + 3.0) * u * (Tf + 2.0 * E) + 0x1p-100) * (1.0 + 0x1p-20);
+}
+
+// Per refilled row i (query rows[i]): T = ub + 1.125 delta3(|ub|), tq, and
+// the certification bound delta3(|T|).  ub = +inf (no k candidates) forces
+// the exact scan (T = -inf).
+__global__ __launch_bounds__(256) void k_tau_x3(int64_t n, const int *__restrict__ rows,
+                                                const float *__restrict__ ub,
+                                                const float *__restrict__ qn3,
+                                                const float *__restrict__ qh3,
+                                                const float *__restrict__ ql3,
+                                                const float *__restrict__ q23,
+                                                const unsigned *__restrict__ cmax3, int d, int dp,
+                                                float *__restrict__ tq, float *__restrict__ tau,
+                                                float *__restrict__ delta) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const float b = ub[rows[i]];
+    if (!(b < __builtin_inff())) {
+        tq[i] = -__builtin_inff();
+        tau[i] = -__builtin_inff();
+        delta[i] = 0.f;
+        return;
+    }
+    const double Mn = __uint_as_float(cmax3[0]), Mh = __uint_as_float(cmax3[1]),
+                 Ml = __uint_as_float(cmax3[2]), M2 = __uint_as_float(cmax3[3]);
+    const float qnf = qn3[i];
+    const double qn = qnf, qh = qh3[i], ql = ql3[i], q2 = q23[i];
+    const double d0 = delta3_at(__builtin_fabs((double)b), qn, qh, ql, q2, Mn, Mh, Ml, M2, d, dp);
+    const float T = f32_up((double)b + 1.125 * d0);
+    tau[i] = T;
+    tq[i] = (T - qnf) * 0.5f;
+    delta[i] = f32_up(delta3_at(__builtin_fabs((double)T), qn, qh, ql, q2, Mn, Mh, Ml, M2, d, dp));
+}
+
 // Per query: T = min over phase-1 slices of tau (-inf: forced), tq, delta.
 __global__ __launch_bounds__(256) void k_tau_x1(int64_t nq, int S1, const float *__restrict__ btau1,
                                                 const float *__restrict__ nq_f,
@@ -794,14 +950,16 @@ __global__ __launch_bounds__(64 * WPB) void k_rerank_x1(
     const int *__restrict__ cnt2, const float *__restrict__ delta, int k, int64_t nvalid_max,
     const int *__restrict__ qlist, const int *__restrict__ qlist_n, int *__restrict__ big_count,
     int *__restrict__ big_list, const int *__restrict__ perm, int64_t q_off, int excl,
-    int32_t *__restrict__ out_idx, float *__restrict__ out_dist, int *__restrict__ fb_count,
-    int *__restrict__ fb_list) {
+    const int *__restrict__ qmap, float *__restrict__ ub, int32_t *__restrict__ out_idx,
+    float *__restrict__ out_dist, int *__restrict__ fb_count, int *__restrict__ fb_list) {
     __shared__ int cand[WPB][64 * NR];
     __shared__ float candk[WPB][64 * NR];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const int64_t wq = (int64_t)blockIdx.x * WPB + wid;
     if (qlist ? wq >= *qlist_n : wq >= nq) return;
     const int64_t q = qlist ? qlist[wq] : wq;
+    // qo: the row of Q / the output (refill: the buffers are per refilled row)
+    const int64_t qo = qmap ? (int64_t)qmap[q] : q;
     const float T = tau0[q];
     bool forced = T == -__builtin_inff();
     int M = 0;
@@ -814,7 +972,7 @@ __global__ __launch_bounds__(64 * WPB) void k_rerank_x1(
             const uint2 v = e < cnt ? bp[e] : make_uint2(0x7f800000u, 0u);
             int64_t gid = (int64_t)v.y;
             if (e < cnt) gid = c_off + perm[gid];
-            const bool pass = e < cnt && __uint_as_float(v.x) < T && !(excl && gid == q_off + q);
+            const bool pass = e < cnt && __uint_as_float(v.x) < T && !(excl && gid == q_off + qo);
             const uint64_t pm = __ballot(pass);
             const int pos = M + (int)__popcll(pm & ((1ull << lane) - 1ull));
             if (pass && pos < 64 * NR) {
@@ -848,7 +1006,7 @@ __global__ __launch_bounds__(64 * WPB) void k_rerank_x1(
     }
     wave_bitonic_sort<NR>(kk, ix);
     const float dlt = delta[q];
-    const float *qrow = Q + q * (int64_t)d;
+    const float *qrow = Q + qo * (int64_t)d;
     const int kq = min(k, M);
     float dd[NR];
 #pragma unroll
@@ -878,15 +1036,22 @@ __global__ __launch_bounds__(64 * WPB) void k_rerank_x1(
         const float Dk = wave_elem<NR>(dd, keff - 1);
         cert = (T - dlt) > Dk;  // NaN/inf-safe: false => exact rescan
     }
-    if (cert && T < __builtin_inff() && keff < (int)min((int64_t)k, nvalid_max)) cert = false;
+    const int kneed = (int)min((int64_t)k, nvalid_max);
+    if (cert && T < __builtin_inff() && keff < kneed) cert = false;
     if (!cert) {
-        if (lane == 0) fb_list[atomicAdd(fb_count, 1)] = (int)q;
+        if (ub) {
+            // any k exact candidate distances bound D_k from above (the refill)
+            const float b = (kneed > 0 && keff >= kneed) ? wave_elem<NR>(dd, kneed - 1)
+                                                         : __builtin_inff();
+            if (lane == 0) ub[qo] = b;
+        }
+        if (lane == 0) fb_list[atomicAdd(fb_count, 1)] = (int)qo;
         return;
     }
     if (lane < k) {
         const bool ok = lane < keff;
-        out_idx[q * k + lane] = ok ? ix[0] : -1;
-        out_dist[q * k + lane] = ok ? dd[0] : __builtin_inff();
+        out_idx[qo * k + lane] = ok ? ix[0] : -1;
+        out_dist[qo * k + lane] = ok ? dd[0] : __builtin_inff();
     }
 }
 
@@ -1336,7 +1501,7 @@ static int knn_x1(const float *Q, int64_t nq, const float *C, int64_t nc, int32_
     uint16_t *QK = (uint16_t *)scratch(kSlotX1QK, (size_t)nq * dp * 2 + 64);
     uint16_t *CR = (uint16_t *)scratch(kSlotX1CR, (size_t)nc * dp * 2 + 64);
     uint16_t *CK = (uint16_t *)scratch(kSlotX1CK, (size_t)nc * dp * 2 + 64);
-    char *aux = (char *)scratch(kSlotX1Aux, (size_t)nq * 24 + (size_t)nc * 8 + 256);
+    char *aux = (char *)scratch(kSlotX1Aux, (size_t)nq * 28 + (size_t)nc * 8 + 256);
     int *flags = (int *)scratch(kSlotFlags, 64);
     int *fb_list = (int *)scratch(kSlotFallback, sizeof(int) * (size_t)nq * 2 + 64);
     int *perm = make_perm(nc, kSlotPerm, 0, s);
@@ -1345,6 +1510,7 @@ static int knn_x1(const float *Q, int64_t nq, const float *C, int64_t nc, int32_
     float *qn = (float *)aux, *qhn = qn + nq, *qrn = qhn + nq, *tq = qrn + nq, *tau0 = tq + nq,
           *dlt = tau0 + nq;
     float *cnv = dlt + nq, *chc = cnv + nc;  // corpus norms / half norms, visiting order
+    float *ubv = chc + nc;                   // upper bounds of D_k of uncertified rows
     unsigned *cmax = (unsigned *)flags;  // [0..2]: max |c|^2, |ch|, |rc|
     int *fb_count = flags + 5;  // [3]: non-finite input, [4]: too large for bf16x1
     unsigned long long *ncand = (unsigned long long *)(flags + 8);
@@ -1456,7 +1622,7 @@ static int knn_x1(const float *Q, int64_t nq, const float *C, int64_t nc, int32_
     hipLaunchKernelGGL((k_rerank_x1<NRV, WPB, V>), dim3((unsigned)(NB)), dim3(64 * WPB), 0, s, \
                        Q, nq, C, d, c_off, (int)pl.S, pl.cap, cbuf1, bcnt1, tau0, S2, cap2,     \
                        cbuf2, cnt2, dlt, k, nvalid, QL, QN, BC, BL, perm, q_off, excl,          \
-                       out_idx, out_dist, fb_count, fb_list)
+                       (const int *)nullptr, ubv, out_idx, out_dist, fb_count, fb_list)
     const int64_t nb1 = (nq + 3) / 4;
     if (vec4) MN_RRX(8, 4, true, nb1, (const int *)nullptr, (const int *)nullptr, big_count, big_list);
     else MN_RRX(8, 4, false, nb1, (const int *)nullptr, (const int *)nullptr, big_count, big_list);
@@ -1486,48 +1652,82 @@ static int knn_x1(const float *Q, int64_t nq, const float *C, int64_t nc, int32_
     MN_HIP_TRY(hipStreamSynchronize(s));
     const int nfb = ((const int *)hpre)[5];
     const int64_t n_cand = hpre[4];
-    // many uncertified rows: escalate them to the split generator instead of
-    // the exact scan (whose cost is O(nc d) per row).  No x1 buffer (phase-1 /
-    // sweep lists, perm, sample) is touched after this point.
-    float ms_esc = 0.f;
-    int64_t esc_uncert = 0;
+    // many uncertified rows: refill them with the bf16x3 sweep (section 2d)
+    // instead of the exact scan, whose cost is O(nc d) per row.  No x1 buffer
+    // (phase-1 / sweep lists, sample) is read after this point; perm, chc and
+    // ubv stay live.
     if (nfb > 256) {
-        const int k1 = k + 1;
-        const int m1 = opts->margin > 0 ? opts->margin : 16;
-        const int ealgo = k1 + m1 <= kb16::LMAX ? MN_KNN_BF16X3 : MN_KNN_F32;
-        MN_REQUIRE(k1 <= KMAX && k1 + m1 <= LMAX, MN_ENOTSUP,
-                   "mn_knn: escalation needs k + 1 + margin <= %d", LMAX);
-        char *eb = (char *)scratch(kSlotX1Esc, (size_t)nfb * (4 + 4 * (size_t)d + 8 * k1) + 256);
-        MN_REQUIRE(eb, MN_ENOMEM, "mn_knn: escalation scratch allocation failed");
-        int *erows = (int *)eb;
-        float *EQ = (float *)(eb + (((size_t)nfb * 4 + 15) & ~(size_t)15));
-        int32_t *eidx = (int32_t *)(EQ + (size_t)nfb * d);
-        float *edist = (float *)(eidx + (size_t)nfb * k1);
-        MN_HIP_TRY(hipMemcpyAsync(erows, fb_list, sizeof(int) * (size_t)nfb, hipMemcpyDeviceToDevice, s));
-        const int64_t ne = (int64_t)nfb * d;
-        hipLaunchKernelGGL(k_gather_rows, dim3((unsigned)((ne + 255) / 256)), dim3(256), 0, s, Q, d,
-                           erows, (int64_t)nfb, EQ);
-        MN_KCHECK(s, "k_gather_rows");
-        const mn_knn_stats keep = t_stats;
         Timer te;
         te.start(true, s);
-        mn_knn_opts eo = *opts;
-        eo.k = k1;
-        eo.exclude_self = 0;
-        eo.timing = 0;
-        const int rc = knn_f32_core(EQ, nfb, C, nc, d, 0, c_off, &eo, eidx, edist, ealgo);
-        if (rc != MN_OK) return rc;
-        hipLaunchKernelGGL(k_scatter_escalated, dim3((unsigned)((nfb + 255) / 256)), dim3(256), 0,
-                           s, erows, (int64_t)nfb, q_off, excl, k, eidx, edist, out_idx, out_dist);
-        MN_KCHECK(s, "k_scatter_escalated");
+        const int nkb3 = 3 * nkb;
+        char *eb = (char *)scratch(kSlotX1Esc, (size_t)nfb * 32 + 256);
+        // the row-major phase-1 copies are dead: their slots hold the 3 dp copies
+        uint16_t *CK3 = (uint16_t *)scratch(kSlotX1CR, (size_t)nc * dp * 6 + 64);
+        uint16_t *QK3 = (uint16_t *)scratch(kSlotX1QR, (size_t)nfb * dp * 6 + 64);
+        MN_REQUIRE(eb && CK3 && QK3, MN_ENOMEM, "mn_knn: refill scratch allocation failed");
+        int *erows = (int *)eb;
+        float *qn3 = (float *)(eb + (((size_t)nfb * 4 + 15) & ~(size_t)15));
+        float *qh3 = qn3 + nfb, *ql3 = qh3 + nfb, *q23 = ql3 + nfb, *tq3 = q23 + nfb,
+              *tau3 = tq3 + nfb, *dlt3 = tau3 + nfb;
+        unsigned *cmax3 = (unsigned *)(flags + 10);  // [10..13]: max |c|^2, |ch|, |cl|, |c2|
+        MN_HIP_TRY(hipMemcpyAsync(erows, fb_list, sizeof(int) * (size_t)nfb, hipMemcpyDeviceToDevice, s));
+        MN_HIP_TRY(hipMemsetAsync(cmax3, 0, 16, s));
+        MN_HIP_TRY(hipMemsetAsync(fb_count, 0, 8, s));  // fb_count, big_count
+        auto prep3 = [&](const float *X, int64_t n, const int *src, uint16_t *K, int corpus,
+                         float *nv, float *hv, float *lv, float *rv) {
+            const int64_t blocks = std::min<int64_t>((n + 7) / 8, 16384);
+            if (vec4)
+                hipLaunchKernelGGL(k_prep_x3<true>, dim3((unsigned)blocks), dim3(256), 0, s, X, n,
+                                   d, dp, src, K, corpus, nv, hv, lv, rv, cmax3);
+            else
+                hipLaunchKernelGGL(k_prep_x3<false>, dim3((unsigned)blocks), dim3(256), 0, s, X, n,
+                                   d, dp, src, K, corpus, nv, hv, lv, rv, cmax3);
+        };
+        prep3(C, nc, perm, CK3, 1, nullptr, nullptr, nullptr, nullptr);
+        prep3(Q, nfb, erows, QK3, 0, qn3, qh3, ql3, q23);
+        MN_KCHECK(s, "k_prep_x3");
+        hipLaunchKernelGGL(k_tau_x3, dim3((unsigned)((nfb + 255) / 256)), dim3(256), 0, s,
+                           (int64_t)nfb, erows, ubv, qn3, qh3, ql3, q23, cmax3, d, dp, tq3, tau3,
+                           dlt3);
+        MN_KCHECK(s, "k_tau_x3");
+        // expected candidates per row: those within ~2 delta3 of D_k; a
+        // generous plan (an overflowing slice only costs that row's exact scan)
+        const ksw::SweepPlan p3 = ksw::plan_sweep(nfb, nc, 8.0 * (k + 16));
+        const size_t nbuf3 = (size_t)nfb * p3.S * p3.cap;
+        uint2 *cbuf3 = (uint2 *)scratch(kSlotX1Buf2, nbuf3 * sizeof(uint2) + 64);
+        int *cnt3 = (int *)scratch(kSlotX1Meta2, (size_t)nfb * p3.S * 4 + 64);
+        MN_REQUIRE(cbuf3 && cnt3, MN_ENOMEM, "mn_knn: refill buffer allocation failed (%zu MB)",
+                   (nbuf3 * sizeof(uint2)) >> 20);
+        const int64_t grid3 = ((nfb + ksw::BQ - 1) / ksw::BQ) * p3.S;
+        MN_REQUIRE(grid3 < INT_MAX, MN_ENOTSUP, "mn_knn: refill grid too large");
+        hipLaunchKernelGGL(ksw::k_gram_sweep<0>, dim3((unsigned)grid3), dim3(ksw::NT), 0, s, QK3,
+                           (int64_t)nfb, CK3, nc, nkb3, (int64_t)0, (int64_t)0, 0, tq3, tau3, chc,
+                           (int64_t)0, (int)p3.S, p3.chunk, p3.cap, cbuf3, cnt3);
+        MN_KCHECK(s, "k_gram_sweep<x3>");
+        int *big_count3 = flags + 6;
+        int *big_list3 = fb_list + nq;
+#define MN_RR3(NRV, WPB, V, NB, QL, QN, BC, BL)                                                 \
+    hipLaunchKernelGGL((k_rerank_x1<NRV, WPB, V>), dim3((unsigned)(NB)), dim3(64 * WPB), 0, s, \
+                       Q, (int64_t)nfb, C, d, c_off, 0, 0, (const uint2 *)nullptr,            \
+                       (const int *)nullptr, tau3, (int)p3.S, p3.cap, cbuf3, cnt3, dlt3, k,    \
+                       nvalid, QL, QN, BC, BL, perm, q_off, excl, erows, (float *)nullptr,     \
+                       out_idx, out_dist, fb_count, fb_list)
+        const int64_t nb3 = (nfb + 3) / 4;
+        if (vec4) MN_RR3(8, 4, true, nb3, (const int *)nullptr, (const int *)nullptr, big_count3, big_list3);
+        else MN_RR3(8, 4, false, nb3, (const int *)nullptr, (const int *)nullptr, big_count3, big_list3);
+        MN_KCHECK(s, "k_rerank_x1<refill>");
+        int nbig3 = 0;
+        MN_HIP_TRY(hipMemcpyAsync(&nbig3, big_count3, 4, hipMemcpyDeviceToHost, s));
+        MN_HIP_TRY(hipStreamSynchronize(s));
+        if (nbig3 > 0) {
+            if (vec4) MN_RR3(16, 1, true, nbig3, big_list3, big_count3, (int *)nullptr, (int *)nullptr);
+            else MN_RR3(16, 1, false, nbig3, big_list3, big_count3, (int *)nullptr, (int *)nullptr);
+            MN_KCHECK(s, "k_rerank_x1<refill, wide>");
+        }
+#undef MN_RR3
         te.mark();
-        ms_esc = te.ms(0, 1);
-        esc_uncert = t_stats.n_uncertified;
-        t_stats = keep;
         t_stats.n_escalated = nfb;
-        t_stats.ms_escalate = ms_esc;
-        // the split generator's own uncertified rows were rescanned inside it
-        MN_HIP_TRY(hipMemsetAsync(fb_count, 0, 4, s));
+        t_stats.ms_escalate = te.ms(0, 1);
     }
     const unsigned fgrid = (unsigned)std::min<int64_t>(nq, 1024);
     if (vec4)
@@ -1541,7 +1741,7 @@ static int knn_x1(const float *Q, int64_t nq, const float *C, int64_t nc, int32_
     int64_t hf[8] = {0};
     MN_HIP_TRY(hipMemcpyAsync(hf, flags, 64, hipMemcpyDeviceToHost, s));
     MN_HIP_TRY(hipStreamSynchronize(s));
-    t_stats.n_uncertified = ((const int *)hf)[5] + esc_uncert;
+    t_stats.n_uncertified = ((const int *)hf)[5];
     if (tm.on) {
         t_stats.n_candidates = n_cand;
         t_stats.ms_norms = tm.ms(0, 1);
