@@ -100,20 +100,21 @@ typedef struct mn_knn_stats {
     int64_t n_candidates;   /* buffered (query, row) pairs re-ranked            */
     int32_t sweep_slices;
     int32_t sweep_cap;      /* buffer entries per (query, slice)                */
-    int64_t n_escalated;    /* rows the bf16x1 bound could not certify, re-run
-                               on the split (bf16x3) generator                 */
+    int64_t n_escalated;    /* rows the bf16x1 bound could not certify, refilled
+                               by the bf16x3 sweep at their own threshold      */
     float ms_escalate;
     int32_t reserved1;
 } mn_knn_stats;
 
 /* Self kNN over the rows of X [n][d] f32 (device, row-major): replaces
  * MSTStage::build_candidate_graph's kNN (surfface-core/src/mst.rs:312-363,
- * DistanceMetric::SquaredEuclidean) and the brute-force kNN inside
- * build_laplacian_matrix / topk_by_l2 (src_legacy/laplacian.rs:205-294,
- * energymaps.rs:875-892).  Output row i: out_idx[i*k + r], out_dist[i*k + r]
- * in (dist asc, idx asc) order — bit-identical to the reference's sequential
- * f32 fold and stable sort.  Slots beyond min(k, n-1): idx -1, dist +inf.
- * metric must be MN_L2SQ (cosine: mn_knn_cos_f32 / mn_knn_cos_bf16). */
+ * DistanceMetric::SquaredEuclidean, or Euclidean with metric MN_L2: the
+ * correctly rounded f32 sqrt of the same fold, distance.rs:195-203).  The f64
+ * topk_by_l2 (energymaps.rs:875-892) is mn_knn_l2_f64 below; the cosine
+ * graphs are mn_knn_cos_columns_f32 / mn_knn_cos_bf16.  Output row i:
+ * out_idx[i*k + r], out_dist[i*k + r] in (dist asc, idx asc) order —
+ * bit-identical to the reference's sequential f32 fold and stable sort.
+ * Slots beyond min(k, n-1): idx -1, dist +inf.  metric MN_L2SQ or MN_L2. */
 int mn_knn_f32(const float *X, int64_t n, int32_t d, const mn_knn_opts *opts,
                int32_t *out_idx, float *out_dist);
 

@@ -25,8 +25,9 @@
 //                       row's degree: a sequential ascending-column fold (the
 //                       reference's order on the legacy path) over the kept
 //                       entries, lane values read in order by v_readlane; one
-//                       1024-thread block per row <= 8192 (bitonic in LDS); a
-//                       dense column map for hub rows
+//                       1024-thread block per row <= 8192 (bitonic in LDS); hub
+//                       rows: a block-wide bitonic network in HBM + LDS chunks
+//                       (no host round trip: nnz is the call's one read-back)
 //   5. (MAX) kept count per row (needs every degree), one wave per row
 //   6. scan + CSR write, one wave per row, diagonal at its sorted position.
 #include <algorithm>
@@ -351,52 +352,28 @@ __global__ __launch_bounds__(1024) void k_row_sort_block(const int64_t *__restri
     }
 }
 
-// hub rows (m > BLOCK_CAP): dense column map, one row at a time
-__global__ void k_dense_fill(double *__restrict__ dense, int64_t n) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) dense[i] = -__builtin_inf();
+// hub rows (m > BLOCK_CAP): one 1024-thread block per row, sorted in place in
+// HBM by a bitonic network that keeps every sequence ascending (the first
+// step of each merge compares e with e ^ (kk - 1)), so positions >= m act as
+// +inf and are never touched; every step with partner distance < CH runs on
+// LDS-resident chunks of CH entries.  Between steps that exchange data through
+// HBM the block waits for its stores and invalidates its L1 (agent acquire).
+constexpr int CH = BLOCK_CAP;
+
+__device__ __forceinline__ void hub_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    __syncthreads();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
 }
-__global__ void k_dense_scatter(const int32_t *__restrict__ col, const double *__restrict__ wt,
-                                int64_t o, int m, double *__restrict__ dense) {
-    const int e = blockIdx.x * blockDim.x + threadIdx.x;
-    if (e >= m) return;
-    const int c = col[o + e];
-    if (c == EMPTY) return;
-    const double w = wt[o + e];
-    unsigned long long *p = (unsigned long long *)&dense[c];
-    unsigned long long old = *p, assumed;
-    do {  // atomic max on doubles (any sign)
-        assumed = old;
-        if (!(w > __longlong_as_double((long long)assumed))) break;
-        old = atomicCAS(p, assumed, (unsigned long long)__double_as_longlong(w));
-    } while (old != assumed);
-}
-__global__ __launch_bounds__(256) void k_dense_flag(const double *__restrict__ dense, int64_t n,
-                                                    int32_t *__restrict__ flag) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) flag[i] = dense[i] != -__builtin_inf() ? 1 : 0;
-}
-__global__ void k_dense_compact(const double *__restrict__ dense, const int32_t *__restrict__ flag,
-                                const int64_t *__restrict__ pos, int64_t n, int64_t o,
-                                int32_t *__restrict__ col, double *__restrict__ wt) {
-    const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= n || !flag[c]) return;
-    col[o + pos[c]] = (int32_t)c;
-    wt[o + pos[c]] = dense[c];
-}
-// the hub row's count and degree: one wave, coalesced 64-entry chunks, the
-// ascending-column fold reads the lanes in order (v_readlane)
-__global__ __launch_bounds__(64) void k_hub_finish(int64_t i, int64_t o,
-                                                   const int64_t *__restrict__ total, int sym,
-                                                   const double *__restrict__ wt,
-                                                   int32_t *__restrict__ uniq,
-                                                   int32_t *__restrict__ kept,
-                                                   double *__restrict__ deg64,
-                                                   float *__restrict__ deg32) {
+
+// the kept entries' count and degree: one wave, coalesced 64-entry chunks;
+// the ascending-column fold reads the lanes in order
+__device__ __forceinline__ void hub_fold(int64_t i, int64_t o, int u, int sym,
+                                         const double *__restrict__ wt, double (&cb)[2][64],
+                                         int32_t *__restrict__ uniq, int32_t *__restrict__ kept,
+                                         double *__restrict__ deg64, float *__restrict__ deg32) {
     constexpr int PF = 8;  // 64-entry chunks in flight ahead of the fold
-    __shared__ double cb[2][64];
-    const int lane = threadIdx.x;
-    const int u = (int)*total;
+    const int lane = threadIdx.x & 63;
     const int nch = (u + 63) / 64;
     double ring[PF];
 #pragma unroll
@@ -434,6 +411,130 @@ __global__ __launch_bounds__(64) void k_hub_finish(int64_t i, int64_t o,
         } else {
             deg32[i] = s32;
         }
+    }
+}
+
+struct alignas(16) HubSmem {
+    double w[CH];
+    int c[CH];
+    int wsum[16];
+    int carry;
+    double cb[2][64];
+};
+
+__global__ __launch_bounds__(1024) void k_row_sort_hub(const int64_t *__restrict__ offs,
+                                                       const int32_t *__restrict__ huge_list,
+                                                       const int *__restrict__ huge_count,
+                                                       int sym, int32_t *__restrict__ col,
+                                                       double *__restrict__ wt,
+                                                       int32_t *__restrict__ uniq,
+                                                       int32_t *__restrict__ kept,
+                                                       double *__restrict__ deg64,
+                                                       float *__restrict__ deg32) {
+    __shared__ HubSmem sm;
+    const int t = threadIdx.x;
+    const int nh = *huge_count;
+    for (int h = blockIdx.x; h < nh; h += gridDim.x) {
+        const int64_t i = huge_list[h];
+        const int64_t o = offs[i];
+        const int m = (int)(offs[i + 1] - o);
+        int32_t *C = col + o;
+        double *W = wt + o;
+        int P = CH;
+        while (P < m) P <<= 1;
+        // one chunk through LDS: steps kk (or the half-cleaners below jmax when
+        // full == false) of the network
+        auto chunk_pass = [&](int base, bool full, int jmax) {
+            for (int e = t; e < CH; e += blockDim.x) {
+                const int g = base + e;
+                sm.c[e] = g < m ? C[g] : EMPTY;
+                sm.w[e] = g < m ? W[g] : 0.0;
+            }
+            __syncthreads();
+            for (int kk = full ? 2 : 2 * CH; kk <= (full ? CH : 2 * CH); kk <<= 1) {
+                const int j0 = full ? kk >> 1 : jmax;
+                for (int j = j0; j > 0; j >>= 1) {
+                    const bool flip = full && j == (kk >> 1);
+                    for (int q = t; q < CH / 2; q += blockDim.x) {
+                        const int e = ((q & ~(j - 1)) << 1) | (q & (j - 1));  // bit j clear
+                        const int pe = flip ? (e ^ (2 * j - 1)) : (e | j);
+                        if (base + pe < m && cw_less(sm.c[pe], sm.w[pe], sm.c[e], sm.w[e])) {
+                            int tc = sm.c[e]; sm.c[e] = sm.c[pe]; sm.c[pe] = tc;
+                            double tw = sm.w[e]; sm.w[e] = sm.w[pe]; sm.w[pe] = tw;
+                        }
+                    }
+                    __syncthreads();
+                }
+            }
+            for (int e = t; e < CH; e += blockDim.x) {
+                const int g = base + e;
+                if (g < m) {
+                    C[g] = sm.c[e];
+                    W[g] = sm.w[e];
+                }
+            }
+        };
+        for (int base = 0; base < m; base += CH) {  // sorted CH-runs
+            chunk_pass(base, true, 0);
+            __syncthreads();
+        }
+        hub_sync();
+        for (int kk = 2 * CH; kk <= P; kk <<= 1) {
+            for (int j = kk >> 1; j >= CH; j >>= 1) {  // steps across chunks, in HBM
+                const bool flip = j == (kk >> 1);
+                for (int q = t; q < P / 2; q += blockDim.x) {
+                    const int e = ((q & ~(j - 1)) << 1) | (q & (j - 1));
+                    const int pe = flip ? (e ^ (2 * j - 1)) : (e | j);
+                    if (pe < m) {
+                        const int ce = C[e], cp = C[pe];
+                        const double we = W[e], wp = W[pe];
+                        if (cw_less(cp, wp, ce, we)) {
+                            C[e] = cp; W[e] = wp;
+                            C[pe] = ce; W[pe] = we;
+                        }
+                    }
+                }
+                hub_sync();
+            }
+            for (int base = 0; base < m; base += CH) {  // the remaining steps per chunk
+                chunk_pass(base, false, CH >> 1);
+                __syncthreads();
+            }
+            hub_sync();
+        }
+        // dedupe (the first of each column run carries the max weight) and
+        // compact in place: every chunk is read before any of it is written,
+        // and a write lands at or before its source
+        int nk = 0;
+        if (t == 0) sm.carry = INT_MIN;
+        __syncthreads();
+        for (int c0 = 0; c0 < m; c0 += 1024) {
+            const int e = c0 + t;
+            const int ce = e < m ? C[e] : EMPTY;
+            const double we = e < m ? W[e] : 0.0;
+            const int prev = t == 0 ? sm.carry : (e - 1 < m ? C[e - 1] : EMPTY);
+            const bool keep = e < m && ce != EMPTY && ce != prev;
+            const uint64_t mk = __ballot(keep);
+            const int lane = t & 63, wv = t >> 6;
+            if (lane == 0) sm.wsum[wv] = (int)__popcll(mk);
+            __syncthreads();
+            int before = 0, tot = 0;
+            for (int q = 0; q < 16; ++q) {
+                if (q < wv) before += sm.wsum[q];
+                tot += sm.wsum[q];
+            }
+            if (t == 1023) sm.carry = ce;
+            hub_sync();  // every load of this chunk precedes its writes
+            if (keep) {
+                const int pos = nk + before + (int)__popcll(mk & ((1ull << lane) - 1ull));
+                C[pos] = ce;
+                W[pos] = we;
+            }
+            nk += tot;
+            hub_sync();
+        }
+        if (t < 64) hub_fold(i, o, nk, sym, wt, sm.cb, uniq, kept, deg64, deg32);
+        __syncthreads();
     }
 }
 
@@ -486,12 +587,14 @@ __global__ __launch_bounds__(256) void k_write_csr(const int64_t *__restrict__ o
                                                    Params P, const double *__restrict__ deg64,
                                                    const float *__restrict__ deg32,
                                                    const int64_t *__restrict__ indptr,
-                                                   int32_t *__restrict__ out_col,
+                                                   int64_t cap, int32_t *__restrict__ out_col,
                                                    double *__restrict__ out_v64,
                                                    float *__restrict__ out_v32) {
     const int lane = threadIdx.x & 63;
     const int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     if (i >= n) return;
+    // a caller-owned output that is too small gets nothing (MN_ECAP on return)
+    if (indptr[n] > cap) return;
     const int64_t o = offs[i];
     const int u = uniq[i];
     const int64_t q0 = indptr[i];
@@ -626,75 +729,51 @@ static int laplacian_impl(const int32_t *nbr, const void *val, int32_t val_f64, 
                        col, wt, uniq, kept, deg64, deg32, big_list, flags + 1);
     hipLaunchKernelGGL(k_row_sort_block, dim3(256), dim3(1024), 0, s, offs, big_list, flags + 1,
                        P.sym, col, wt, uniq, kept, deg64, deg32, huge_list, flags + 2);
+    hipLaunchKernelGGL(k_row_sort_hub, dim3(64), dim3(1024), 0, s, offs, huge_list, flags + 2,
+                       P.sym, col, wt, uniq, kept, deg64, deg32);
     MN_KCHECK(s, "k_row_sort");
-    int hf[4] = {0, 0, 0, 0};
-    MN_HIP_TRY(hipMemcpyAsync(hf, flags, 16, hipMemcpyDeviceToHost, s));
-    MN_HIP_TRY(hipStreamSynchronize(s));
-    MN_REQUIRE(hf[0] == 0, MN_EINVAL, "mn_laplacian_from_knn: neighbour index >= n");
-    t_lap_stats.big_rows = hf[1];
-    t_lap_stats.hub_rows = hf[2];
-    if (hf[2] > 0) {  // hub rows: dense column map, one at a time (rare)
-        std::vector<int32_t> hubs(hf[2]);
-        MN_HIP_TRY(hipMemcpyAsync(hubs.data(), huge_list, sizeof(int32_t) * hf[2],
-                                  hipMemcpyDeviceToHost, s));
-        MN_HIP_TRY(hipStreamSynchronize(s));
-        // persistent scratch (no per-call hipMalloc/hipFree: hipFree synchronises)
-        char *hb = (char *)scratch(kSlotLists, (size_t)n * 8 + 64);
-        char *hm = (char *)scratch(kSlotListMeta, (size_t)n * 4 + (size_t)(n + 1) * 8 +
-                                                      ((size_t)n / scan::SB + 2) * 8 + 64);
-        MN_REQUIRE(hb && hm, MN_ENOMEM, "mn_laplacian_from_knn: hub scratch allocation failed");
-        double *dense = (double *)hb;
-        int32_t *dflag = (int32_t *)hm;
-        int64_t *dpos = (int64_t *)(((uintptr_t)(dflag + n) + 15) & ~(uintptr_t)15);
-        int64_t *dpart = dpos + (n + 1);
-        for (int h = 0; h < hf[2]; ++h) {
-            const int64_t i = hubs[h];
-            int64_t oo[2];
-            MN_HIP_TRY(hipMemcpyAsync(oo, offs + i, 16, hipMemcpyDeviceToHost, s));
-            MN_HIP_TRY(hipStreamSynchronize(s));
-            const int64_t o = oo[0];
-            const int m = (int)(oo[1] - o);
-            hipLaunchKernelGGL(k_dense_fill, dim3(grid_for(n)), dim3(256), 0, s, dense, n);
-            hipLaunchKernelGGL(k_dense_scatter, dim3(grid_for(m)), dim3(256), 0, s, col, wt, o, m,
-                               dense);
-            hipLaunchKernelGGL(k_dense_flag, dim3(grid_for(n)), dim3(256), 0, s, dense, n, dflag);
-            MN_HIP_TRY(scan::exclusive_scan(dflag, n, dpos, dpart, s));
-            hipLaunchKernelGGL(k_dense_compact, dim3(grid_for(n)), dim3(256), 0, s, dense, dflag,
-                               dpos, n, o, col, wt);
-            hipLaunchKernelGGL(k_hub_finish, dim3(1), dim3(64), 0, s, i, o, dpos + n, P.sym, wt,
-                               uniq, kept, deg64, deg32);
-        }
-        MN_KCHECK(s, "k_hub_finish");
-    }
     if (P.sym == MN_SYM_MAX)
         hipLaunchKernelGGL(k_kept_max, dim3(grid_for(n * 64)), dim3(256), 0, s, offs, col, wt,
                            uniq, n, P, deg32, kept);
+    // outputs sized on the device side: a library-owned CSR gets the bound
+    // n + 2 n k (every row: its diagonal + at most k forward and all reverse
+    // slots), a caller-owned one is checked against its capacity inside
+    // k_write_csr, so nnz is read back once, with the final synchronisation
+    const size_t vsz = P.sym == MN_SYM_UNION ? 8 : 4;
+    const int64_t cap = caller ? given.nnz : n + 2 * nk;
     int64_t *indptr = caller ? given.indptr : nullptr;
-    if (!caller) MN_HIP_TRY(hipMalloc(&indptr, sizeof(int64_t) * (n + 1)));
-    MN_HIP_TRY(scan::exclusive_scan(kept, n, indptr, part, s));
-    int64_t nnz = 0;
-    MN_HIP_TRY(hipMemcpyAsync(&nnz, indptr + n, 8, hipMemcpyDeviceToHost, s));
-    MN_HIP_TRY(hipStreamSynchronize(s));
     int32_t *ocol = caller ? given.indices : nullptr;
     void *oval = caller ? given.values : nullptr;
-    const size_t vsz = P.sym == MN_SYM_UNION ? 8 : 4;
-    if (caller && nnz > given.nnz) {
+    if (!caller && (hipMalloc(&indptr, sizeof(int64_t) * (n + 1)) != hipSuccess ||
+                    hipMalloc(&ocol, sizeof(int32_t) * std::max<int64_t>(cap, 1)) != hipSuccess ||
+                    hipMalloc(&oval, vsz * std::max<int64_t>(cap, 1)) != hipSuccess)) {
+        (void)hipFree(indptr); (void)hipFree(ocol); (void)hipFree(oval);
+        set_error("mn_laplacian_from_knn: output allocation (%lld entries) failed", (long long)cap);
+        return MN_ENOMEM;
+    }
+    MN_HIP_TRY(scan::exclusive_scan(kept, n, indptr, part, s));
+    hipLaunchKernelGGL(k_write_csr, dim3(grid_for(n * 64)), dim3(256), 0, s, offs, col, wt, uniq,
+                       n, P, deg64, deg32, indptr, cap, ocol, (double *)oval, (float *)oval);
+    MN_HIP_TRY(hipGetLastError());
+    tm.mark();
+    int64_t nnz = 0;
+    int hf[4] = {0, 0, 0, 0};
+    MN_HIP_TRY(hipMemcpyAsync(&nnz, indptr + n, 8, hipMemcpyDeviceToHost, s));
+    MN_HIP_TRY(hipMemcpyAsync(hf, flags, 16, hipMemcpyDeviceToHost, s));
+    MN_HIP_TRY(hipStreamSynchronize(s));
+    t_lap_stats.big_rows = hf[1];
+    t_lap_stats.hub_rows = hf[2];
+    if (hf[0] != 0) {  // out-of-range neighbour ids were skipped everywhere; outputs void
+        if (!caller) { (void)hipFree(indptr); (void)hipFree(ocol); (void)hipFree(oval); }
+        set_error("mn_laplacian_from_knn: neighbour index >= n");
+        return MN_EINVAL;
+    }
+    if (nnz > cap) {  // caller-owned only (the library bound always holds)
         out->nnz = nnz;
-        set_error("mn_laplacian_from_knn: output capacity %lld < nnz %lld", (long long)given.nnz,
+        set_error("mn_laplacian_from_knn: output capacity %lld < nnz %lld", (long long)cap,
                   (long long)nnz);
         return MN_ECAP;
     }
-    if (!caller && (hipMalloc(&ocol, sizeof(int32_t) * std::max<int64_t>(nnz, 1)) != hipSuccess ||
-                    hipMalloc(&oval, vsz * std::max<int64_t>(nnz, 1)) != hipSuccess)) {
-        (void)hipFree(indptr); (void)hipFree(ocol);
-        set_error("mn_laplacian_from_knn: output allocation (nnz=%lld) failed", (long long)nnz);
-        return MN_ENOMEM;
-    }
-    hipLaunchKernelGGL(k_write_csr, dim3(grid_for(n * 64)), dim3(256), 0, s, offs, col, wt, uniq,
-                       n, P, deg64, deg32, indptr, ocol, (double *)oval, (float *)oval);
-    MN_HIP_TRY(hipGetLastError());
-    tm.mark();
-    MN_HIP_TRY(hipStreamSynchronize(s));
     t_lap_stats.ms_total = tm.ms(0, 1);
     t_lap_stats.nnz = nnz;
     out->n_rows = n;

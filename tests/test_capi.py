@@ -40,7 +40,7 @@ def test_version_and_error_paths_without_gpu():
     # NULL opts / pointers are rejected before any HIP call
     assert L.mn_knn_f32(None, 10, 4, None, None, None) == _lib.MN_EINVAL
     assert b"opts" in L.mn_last_error()
-    o = _lib.KnnOpts(k=0, metric=0, exclude_self=1, margin=0, timing=0, reserved0=0, stream=None)
+    o = _lib.KnnOpts(k=0, metric=0, exclude_self=1, margin=0, timing=0, algo=0, stream=None)
     assert L.mn_knn_f32(C.c_void_p(16), 10, 4, C.byref(o), C.c_void_p(16), C.c_void_p(16)) \
         == _lib.MN_ENOTSUP
     o.k, o.metric = 5, 7

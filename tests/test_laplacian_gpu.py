@@ -79,6 +79,36 @@ def test_union_eps_filter_and_hub_rows():
     np.testing.assert_allclose(iv, riv, rtol=1e-15, atol=0)
 
 
+@pytest.mark.parametrize("sym", ["union", "max"])
+def test_large_hub_rows_device_sort(sym):
+    """Hub rows far beyond one LDS chunk (P = 65536: global flip + half-cleaner
+    steps and chunk passes) with duplicate columns (max weight kept)."""
+    import surfface_hip as S
+    n, k = 50000, 4
+    rng = np.random.default_rng(11)
+    idx = rng.integers(0, n, size=(n, k)).astype(np.int32)
+    idx[:, 0] = 0                       # node 0: in-degree n -> m ~ 50k
+    idx[: n // 2, 1] = 3                # node 3: ~25k
+    idx[::3, 2] = idx[::3, 3]           # duplicate columns within rows
+    w = rng.uniform(0.01, 1.0, size=(n, k)).astype(np.float64 if sym == "union" else np.float32)
+    if sym == "union":
+        ip, ix, iv, deg = lap(idx, w, weight_kernel="given")
+        rip, rix, riv = O.laplacian_union(idx, w.astype(np.float64))
+        np.testing.assert_array_equal(ip, rip)
+        np.testing.assert_array_equal(ix, rix)
+        np.testing.assert_array_equal(iv.view(np.uint64), riv.view(np.uint64))
+    else:
+        ip, ix, iv, deg = lap(idx, w, weight_kernel="given", symmetrise="max",
+                              weight_threshold=1e-9)
+        src = np.repeat(np.arange(n), k)
+        rip, rix, riv, rdeg, _ = O.laplacian_max(n, src, idx.ravel(), w.ravel(), thr=1e-9,
+                                                 normalize=False)
+        np.testing.assert_array_equal(ip, rip)
+        np.testing.assert_array_equal(ix, rix)
+        np.testing.assert_allclose(iv, riv, rtol=1e-5, atol=1e-7)
+    assert S.laplacian.last_stats()["hub_rows"] >= 2
+
+
 @pytest.mark.parametrize("normalize", [True, False])
 def test_max_variant_vs_oracle(normalize):
     X = datagen.clustered(3000, 24, seed=7, blobs=6)
