@@ -191,6 +191,40 @@ int mn_knn_last_stats(mn_knn_stats *out);
 int mn_bc_knn_f32(const float *means, const float *vars, int64_t c, int32_t f, int32_t k,
                   float var_reg, float weight_thr, int32_t *out_idx, float *out_w, void *stream);
 
+/* MST stage candidate graph (surfface-core/src/mst.rs:312-363
+ * MSTStage::build_candidate_graph + compute_distance :366-397 +
+ * compute_edge_cost :400-412).  Nodes are the C centroid ROWS of means /
+ * vars [C][F] (device, f32).  Per node i, the k = min(k_neighbors, C-1)
+ * nearest j != i by (distance asc, j asc) — the reference's stable sort —
+ * as edges out_v / out_dist / out_cost [C][k] (u = i implicit), cost =
+ * distance * phi(t_i, t_j) (MN_TW_NONE: cost = distance).  thickness [C]
+ * (device) or NULL = the mean variance per row (centroid.rs:107-109;
+ * sequential f32 sum / F — Burn's summation order is backend-defined, so
+ * that default is parity-unpinned); out_thickness [C] optional.
+ * MN_MST_BHATTACHARYYA (the default metric, mst.rs:77-84) folds
+ * bhattacharyya_distance_diagonal (distance.rs:78-108) in feature order with
+ * the reference's f32 operations (sqrt correctly rounded; ln = f64 log
+ * rounded to f32 where the reference calls libm logf: bit-exact but for rare
+ * ulp-level terms); C <= 65536, k <= 512.  MN_MST_EUCLIDEAN /
+ * MN_MST_SQEUCLIDEAN run mn_knn_f32 (bit-exact).  MN_ENONFINITE on a NaN
+ * distance (the reference's partial_cmp().unwrap()). */
+enum mn_mst_metric {
+    MN_MST_BHATTACHARYYA = 0,
+    MN_MST_EUCLIDEAN = 1,
+    MN_MST_SQEUCLIDEAN = 2
+};
+enum mn_thickness_weight { /* mst.rs:58-74 ThicknessWeight */
+    MN_TW_MEAN = 0,    /* (t_i + t_j) / 2 */
+    MN_TW_MIN = 1,
+    MN_TW_MAX = 2,
+    MN_TW_GEOMEAN = 3, /* sqrt(t_i * t_j) */
+    MN_TW_NONE = 4
+};
+int mn_mst_candidate_graph_f32(const float *means, const float *vars, int64_t c, int32_t f,
+                               int32_t k_neighbors, int32_t metric, int32_t thickness_weight,
+                               const float *thickness, float *out_thickness, int32_t *out_v,
+                               float *out_dist, float *out_cost, void *stream);
+
 
 /* ---------------------------------------------------------------------- */
 /* K2 — Laplacian assembly from kNN rows (CSR)                            */
@@ -452,6 +486,20 @@ typedef struct mn_cos_opts {
  * NULL).  Bit-exact.  2 <= f <= 4096, topk <= 64. */
 int mn_knn_cos_columns_f32(const float *X, int64_t n_rows, int32_t f, const mn_cos_opts *opts,
                            int32_t *out_idx, double *out_dist, double *out_w);
+/* Same over an f64 X [n_rows][f] (the legacy DenseMatrix<f64> path:
+ * build_laplacian_matrix on arbitrary f64 items, src_legacy/laplacian.rs:
+ * 122-201, and the "Laplacian of Laplacian" signals graph built on the
+ * densified F x F Laplacian, graph.rs:257-313).  Products are the reference's
+ * rounded f64 products, folded in the same order: bit-exact. */
+int mn_knn_cos_columns_f64(const double *X, int64_t n_rows, int32_t f, const mn_cos_opts *opts,
+                           int32_t *out_idx, double *out_dist, double *out_w);
+/* GraphParams.normalise pre-pass of build_laplacian_matrix
+ * (src_legacy/laplacian.rs:143-150: smartcore StandardScaler over the columns
+ * of the items matrix).  smartcore is not in the reference tree, so this is
+ * parity-unpinned: mean and population std by sequential f64 folds, out =
+ * (x - mean) / std, std == 0 -> x - mean.  X, out [n_rows][n_cols] f64. */
+int mn_standardize_columns_f64(const double *X, int64_t n_rows, int32_t n_cols, double *out,
+                               void *stream);
 int mn_cos_last_stats(mn_knn_stats *out);
 
 /* C5 item graph (config 5): rectified-cosine kNN over the ROWS of a bf16

@@ -1,0 +1,342 @@
+// gram_sweep2.hpp — phase 2 of the two-phase L2 candidate generator
+// (MN_KNN_BF16X1), second generation: the same contract as gram_sweep.hpp
+// (fixed per-query threshold folded into the accumulator, a pair is a
+// candidate iff acc = tq(q) - hc(c) + qh.ch > 0, buffered per (query, slice)),
+// re-scheduled for gfx950's MFMA pipe:
+//
+//  * v_mfma_f32_16x16x32_bf16 (the chip holds a higher clock on this shape
+//    than on 32x32x16 for the same FLOPs: MI355X_MICROARCH.md 'DVFS give-back'
+//    item 7), 256-query x 256-row block tile, each wave 64 queries x 128 rows
+//    = 4 x 8 fragments, 128 accumulator VGPRs.
+//  * Ping-pong: the two waves that share a SIMD (w and w+4) run one barrier
+//    window apart.  In every window one of them issues its 32 MFMAs (one
+//    32-deep k-step) while the other reads the next k-step's 12 fragments
+//    from LDS and issues its LDS-DMA pieces, so the MFMA pipe never waits on
+//    LDS latency or on the barrier itself.
+//  * 4-slot LDS ring of 32-deep k-steps (both operands, 32 KB per slot), each
+//    k-step issued 3 ahead by LDS-DMA (`global_load_lds_dwordx4`): a k-step
+//    is read 6 windows after its DMA was issued; counted `vmcnt(8)` (never 0
+//    in the loop), raw `s_barrier`.
+//  * One KB32 row is 64 B (4 chunks of 16 B); a 16x16x32 fragment read is 16
+//    rows x 4 chunks.  Chunk c of row r sits at c ^ (((r >> 3) & 1) << 1):
+//    every ds_read_b128 lane group covers all 16 slots of a 256-B bank row
+//    (conflict-free); the DMA writes lane-linear and the swizzle is applied to
+//    its source address.
+//  * The next tile's |c|^2/2 values come in by waves 0-3's dword loads issued
+//    4 k-steps before the tile ends (older than the counted window, so the
+//    regular waits retire it) and are written to LDS 2 k-steps before use.
+//  * The per-tile epilogue (max3 tree + ballot over the 128 accumulators, the
+//    rare candidate staging, the next tile's accumulator init) runs in the
+//    wave's READ window, beside its partner's MFMAs.
+#pragma once
+#include <climits>
+
+#include "common.hpp"
+
+namespace mn {
+namespace ksw2 {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+constexpr int BQ = 256;      // queries per block
+constexpr int BC = 256;      // corpus rows per tile
+constexpr int KB = 32;       // bf16 per k-step (one KB32 block)
+constexpr int NWAVES = 8;
+constexpr int NT = 64 * NWAVES;
+constexpr int NSLOT = 4;     // LDS ring of k-steps
+constexpr int WQF = 4;       // 16-query fragments per wave
+constexpr int WCF = 8;       // 16-row corpus fragments per wave
+constexpr int SCAP = 256;    // staged candidates per wave
+
+struct alignas(16) Smem {
+    uint16_t C[NSLOT][BC][KB];   // corpus k-step, 16 KB per slot
+    uint16_t Q[NSLOT][BQ][KB];   // query k-step, 16 KB per slot
+    float hc[2][BC];             // |c|^2 / 2 of a tile (+inf past the slice end)
+    int qcnt[BQ];                // candidates written per query of the block
+    float t0[BQ];                // tau0 of the block's queries
+    float tq[BQ];                // (tau0 - |q|^2) / 2 of the block's queries
+    int scnt[NWAVES];            // staged entries per wave
+    uint2 stk[NWAVES][SCAP];     // staged candidates per wave: (key bits, global id)
+    uint32_t stp[NWAVES][SCAP];  //   and (query in block | buffer position << 8)
+};
+static_assert(sizeof(Smem) <= 163840, "LDS budget");
+
+__device__ __forceinline__ int swz(int r, int c) { return c ^ (((r >> 3) & 1) << 1); }
+
+__device__ __forceinline__ int xcd_remap(int orig, int nwg) {
+    const int q = nwg / 8, r = nwg % 8, xcd = orig % 8;
+    return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + orig / 8;
+}
+
+// vmcnt waits with an immediate count
+#define MN_VMCNT(N) asm volatile("s_waitcnt vmcnt(" #N ")" ::: "memory")
+
+// Qk [nkb][nq][32], Ck [nkb][nc][32] (KB32 bf16).  Corpus rows [c_begin, nc)
+// in S slices of `chunk` rows (a multiple of BC).  tq / tau0 [nq], hc [nc].
+// Per (query, slice): buf[(q*S + s)*cap + i] = (key bits, global corpus id),
+// cnt[q*S + s] = entries (-1: overflow).  PROBE = 1: K loop only (timing).
+template <int PROBE>
+__global__ __launch_bounds__(NT) void k_gram_sweep2(
+    const uint16_t *__restrict__ Qk, int64_t nq, const uint16_t *__restrict__ Ck, int64_t nc,
+    int nkb, int64_t q_off, int64_t c_off, int excl, const float *__restrict__ tq,
+    const float *__restrict__ tau0, const float *__restrict__ hc, int64_t c_begin, int S,
+    int64_t chunk, int cap, uint2 *__restrict__ buf, int *__restrict__ cnt) {
+    __shared__ Smem sm;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wq = w & 3, wc = w >> 2;  // wc: ping-pong group (0 leads by one window)
+    const int fr = lane & 15, fk = lane >> 4;
+    const int v = xcd_remap((int)blockIdx.x, (int)gridDim.x);
+    // (32-bit row / step counters: nq * 32, nc * 32 < 2^31 is checked by the driver)
+    const int q0 = (v / S) * BQ;
+    const int sl = v % S;
+    const int cbeg = (int)(c_begin + (int64_t)sl * chunk);
+    const int cend = (int)min(nc, (int64_t)cbeg + chunk);
+    const int ntile = cend > cbeg ? (cend - cbeg + BC - 1) / BC : 0;
+    const int gtot = ntile * nkb;
+
+    if (tid < NWAVES) sm.scnt[tid] = 0;
+    if (tid < BQ) {
+        sm.tq[tid] = q0 + tid < nq ? tq[q0 + tid] : -__builtin_inff();
+        sm.qcnt[tid] = 0;
+        sm.t0[tid] = q0 + tid < nq ? tau0[q0 + tid] : 0.f;
+    }
+    if (ntile > 0 && tid < BC) {
+        const int c = cbeg + tid;
+        sm.hc[0][tid] = (c < cend) ? hc[c] : __builtin_inff();
+    }
+
+    // ---- LDS-DMA issue state: the next k-step gi to stage (tile row bt0,
+    // k-block bkb).  Each wave stages rows [32w, 32w+32) of both operands:
+    // two 16-row pieces each, lane l -> row +(l>>2), physical chunk l&3.
+    int bt0 = cbeg;
+    int bkb = 0, bslot = 0;
+    const int prow0 = 32 * w + (lane >> 2), prow1 = prow0 + 16;
+    const int pch = 8 * ((lane & 3) ^ (((lane >> 5) & 1) << 1));  // source chunk (swizzle)
+    const int qo0 = min(q0 + prow0, (int)nq - 1) * KB + pch;
+    const int qo1 = min(q0 + prow1, (int)nq - 1) * KB + pch;
+    int co0 = min(bt0 + prow0, cend - 1) * KB + pch;
+    int co1 = min(bt0 + prow1, cend - 1) * KB + pch;
+    const uint16_t *cbk = Ck, *qbk = Qk;
+    const int cstep = (int)nc * KB, qstep = (int)nq * KB;
+    auto dma = [&](const uint16_t *src, uint16_t *lds) {
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)src,
+                                         (__attribute__((address_space(3))) void *)lds, 16, 0, 0);
+    };
+    auto issue = [&]() {
+        if (bt0 < cend) {
+            dma(cbk + co0, &sm.C[bslot][32 * w][0]);
+            dma(cbk + co1, &sm.C[bslot][32 * w + 16][0]);
+            dma(qbk + qo0, &sm.Q[bslot][32 * w][0]);
+            dma(qbk + qo1, &sm.Q[bslot][32 * w + 16][0]);
+            bslot = (bslot + 1) & (NSLOT - 1);
+            cbk += cstep;
+            qbk += qstep;
+            if (++bkb == nkb) {
+                bkb = 0;
+                bt0 += BC;
+                cbk = Ck;
+                qbk = Qk;
+                co0 = min(bt0 + prow0, cend - 1) * KB + pch;
+                co1 = min(bt0 + prow1, cend - 1) * KB + pch;
+            }
+        }
+    };
+
+    f32x4 acc[WQF][WCF];
+    bf16x8 fq[WQF], fc[WCF];
+    auto init_acc = [&](int par) {
+        float tql[WQF];  // this lane's queries, one per 16-query fragment
+#pragma unroll
+        for (int f = 0; f < WQF; ++f) tql[f] = sm.tq[64 * wq + 16 * f + fr];
+#pragma unroll
+        for (int g = 0; g < WCF; ++g) {
+            const float4 x =
+                *reinterpret_cast<const float4 *>(&sm.hc[par][128 * wc + 16 * g + 4 * fk]);
+#pragma unroll
+            for (int f = 0; f < WQF; ++f) {
+                acc[f][g][0] = tql[f] - x.x;
+                acc[f][g][1] = tql[f] - x.y;
+                acc[f][g][2] = tql[f] - x.z;
+                acc[f][g][3] = tql[f] - x.w;
+            }
+        }
+    };
+    auto read_frags = [&](int slot) {
+        const int chs = 8 * swz(fr, fk);
+#pragma unroll
+        for (int f = 0; f < WQF; ++f)
+            fq[f] = *reinterpret_cast<const bf16x8 *>(&sm.Q[slot][64 * wq + 16 * f + fr][chs]);
+#pragma unroll
+        for (int g = 0; g < WCF; ++g)
+            fc[g] = *reinterpret_cast<const bf16x8 *>(&sm.C[slot][128 * wc + 16 * g + fr][chs]);
+    };
+    auto mfmas = [&]() {
+#pragma unroll
+        for (int f = 0; f < WQF; ++f)
+#pragma unroll
+            for (int g = 0; g < WCF; ++g)
+                acc[f][g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fc[g], fq[f], acc[f][g], 0, 0, 0);
+    };
+
+    bool dirty = false;  // candidate stores issued since the last counted wait
+    // Stores complete out of order with the DMA loads on the VM counter, so a
+    // counted wait after a store is not trusted: candidates are staged in LDS
+    // (a per-wave area, slots from an LDS counter) and written out in batches
+    // when the area fills; only then is the next wait a full drain.
+    auto flush = [&]() {
+        const int n = min(sm.scnt[w], SCAP);
+        for (int e = lane; e < n; e += 64) {
+            const uint32_t pq = sm.stp[w][e];
+            const int ql = (int)(pq & 255u), pos = (int)(pq >> 8);
+            buf[((int64_t)(q0 + ql) * S + sl) * cap + pos] = sm.stk[w][e];
+        }
+        sm.scnt[w] = 0;
+        dirty = true;
+    };
+    // candidates of the tile starting at corpus row ct0: positive accumulators.
+    // Per 16 x 16 fragment one max and one ballot (wave-uniform branch); the
+    // staging body runs only for fragments where some lane has a candidate
+    // (a few per wave and tile at the C2 threshold).
+    auto check = [&](int ct0) {
+        if constexpr (PROBE == 0) {
+            // (global ids fit int32: the outputs are int32 ids)
+            const int cg0 = (int)c_off + ct0 + 128 * wc + 4 * fk;
+#pragma unroll
+            for (int f = 0; f < WQF; ++f) {
+                const int ql = 64 * wq + 16 * f + fr;
+                const int qgl = (int)q_off + q0 + ql;
+#pragma unroll
+                for (int g = 0; g < WCF; ++g) {
+                    const f32x4 a = acc[f][g];
+                    const float m4 = fmaxf(fmaxf(a[0], a[1]), fmaxf(a[2], a[3]));
+                    if (__builtin_expect(__ballot(m4 > 0.f) == 0, 1)) continue;
+                    unsigned pm = 0;
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) pm |= a[r] > 0.f ? (1u << r) : 0u;
+                    const int c = cg0 + 16 * g;  // corpus id of register 0
+                    if (excl && (unsigned)(qgl - c) < 4u) pm &= ~(1u << (qgl - c));
+                    if (pm != 0) {
+                        const int mine = __popc(pm);
+                        int pos = atomicAdd(&sm.qcnt[ql], mine);
+                        int e = atomicAdd(&sm.scnt[w], mine);
+                        const float t0l = sm.t0[ql];
+                        while (pm) {
+                            const int r = __builtin_ctz(pm);
+                            pm &= pm - 1;
+                            const uint2 kv = make_uint2(__float_as_uint(t0l - 2.f * a[r]),
+                                                        (uint32_t)(c + r));
+                            if (pos < cap) {
+                                if (e < SCAP) {
+                                    sm.stk[w][e] = kv;
+                                    sm.stp[w][e] = (uint32_t)ql | ((uint32_t)pos << 8);
+                                } else {  // area full: straight out (rare)
+                                    buf[((int64_t)(q0 + ql) * S + sl) * cap + pos] = kv;
+                                    dirty = true;
+                                }
+                            }
+                            ++e;
+                            ++pos;
+                        }
+                    }
+                }
+            }
+            // wave-uniform: spill the area once it is 3/4 full (or overran)
+            if (sm.scnt[w] >= SCAP * 3 / 4) flush();
+        } else {
+            float sum = 0.f;
+#pragma unroll
+            for (int f = 0; f < WQF; ++f)
+#pragma unroll
+                for (int g = 0; g < WCF; ++g) sum += acc[f][g][0];
+            if (sum == 12345.678f) sm.qcnt[0] = 1;
+        }
+    };
+
+    // ---- prologue: k-steps 0, 1, 2 in flight; k-step 0 landed everywhere
+    issue();
+    issue();
+    issue();
+    if (gtot > 2) MN_VMCNT(8);
+    else if (gtot == 2) MN_VMCNT(4);
+    else MN_VMCNT(0);
+    __syncthreads();  // also publishes sm.hc[0], qcnt, t0
+    if (gtot > 0) init_acc(0);
+    if (wc == 1) __builtin_amdgcn_s_barrier();  // the trailing group starts one window late
+
+    int c0 = cbeg;  // first corpus row of the current tile
+    int kb = 0, par = 0;
+    float hcn = 0.f;  // next tile's hc (waves 0-3, one value per lane)
+    for (int g = 0; g < gtot; ++g) {
+        // ================= READ window of k-step g =================
+        const bool more = c0 + BC < cend;
+        if (wc == 0 && kb == nkb - 4 && more) {
+            // the next tile's |c|^2 / 2: waves 0-3 load one value per lane
+            // (asm loads: the compiler's own waits would drain the DMA queue);
+            // older than the DMA issued just below, so the counted waits
+            // retire them
+            const float *p = hc + min(c0 + BC + 64 * wq + lane, (int)nc - 1);
+            asm volatile("global_load_dword %0, %1, off" : "=v"(hcn) : "v"(p) : "memory");
+        }
+        issue();  // k-step g + 3
+        if (kb == 0 && g > 0) {
+            // the previous tile's candidates, then this tile's accumulator
+            // init (before the fragment reads: the fragments are dead here)
+            check(c0 - BC);
+            init_acc(par);
+        }
+        read_frags((int)(g & (NSLOT - 1)));
+        if (kb == nkb - 2 && more && wc == 0) {
+            // written 2 k-steps (>= 2 barriers) before init_acc reads it
+            const int cb = c0 + BC + 64 * wq + lane;
+            sm.hc[par ^ 1][64 * wq + lane] = cb < cend ? hcn : __builtin_inff();
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (wc == 1) {
+            // trailing group: k-step g+1 landed for the window after this one
+            const int rem = gtot - 1 - g;
+            if (dirty) MN_VMCNT(0);
+            else if (rem >= 3) MN_VMCNT(8);
+            else if (rem == 2) MN_VMCNT(4);
+            else MN_VMCNT(0);
+            dirty = false;
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+        // ================= MFMA window of k-step g =================
+        __builtin_amdgcn_s_setprio(1);
+        mfmas();
+        __builtin_amdgcn_s_setprio(0);
+        __builtin_amdgcn_sched_barrier(0);
+        if (wc == 0) {
+            const int rem = gtot - 1 - g;
+            if (dirty) MN_VMCNT(0);
+            else if (rem >= 3) MN_VMCNT(8);
+            else if (rem == 2) MN_VMCNT(4);
+            else MN_VMCNT(0);
+            dirty = false;
+        }
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+        if (++kb == nkb) {
+            kb = 0;
+            c0 += BC;
+            par ^= 1;
+        }
+    }
+    if (wc == 0) __builtin_amdgcn_s_barrier();  // match the trailing group's extra window
+    if (gtot > 0) check(c0 - BC);
+    if (sm.scnt[w] > 0) flush();
+    __syncthreads();
+    if (tid < BQ && q0 + tid < nq) {
+        const int c = sm.qcnt[tid];
+        cnt[(int64_t)(q0 + tid) * S + sl] = c > cap ? -1 : c;
+    }
+}
+
+#undef MN_VMCNT
+
+}  // namespace ksw2
+}  // namespace mn

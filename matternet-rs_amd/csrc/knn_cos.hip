@@ -46,16 +46,17 @@ constexpr int FMAXC = 4096;  // features (nodes) limit
 constexpr int LMAXC = 64;    // candidate list length limit
 
 // ---- 1. transpose -------------------------------------------------------
-__global__ __launch_bounds__(256) void k_transpose(const float *__restrict__ X, int64_t n, int f,
-                                                   float *__restrict__ XT) {
-    __shared__ float tile[64][65];
+template <typename T>
+__global__ __launch_bounds__(256) void k_transpose(const T *__restrict__ X, int64_t n, int f,
+                                                   T *__restrict__ XT) {
+    __shared__ T tile[64][65];
     const int64_t r0 = (int64_t)blockIdx.x * 64;
     const int c0 = blockIdx.y * 64;
     const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
     for (int r = ty; r < 64; r += 4) {
         const int64_t row = r0 + r;
         const int col = c0 + tx;
-        tile[r][tx] = (row < n && col < f) ? X[row * f + col] : 0.f;
+        tile[r][tx] = (row < n && col < f) ? X[row * f + col] : (T)0;
     }
     __syncthreads();
     for (int c = ty; c < 64; c += 4) {
@@ -123,26 +124,39 @@ __device__ __forceinline__ double ordered_dot(const float *__restrict__ a,
 // redundant-lane issue cost of a single-chain wave is cut by four.
 constexpr int CHP = CH + 2;  // buffer stride (16 B pad: the 4 groups hit different banks)
 
-__device__ __forceinline__ double ordered_dot4(const float *__restrict__ a,
-                                               const float *__restrict__ b, int64_t n,
+// 16 consecutive values per lane (f32: 4 x float4, f64: 8 x double2)
+__device__ __forceinline__ void load16(const float *p, bool vec, float (&o)[16]) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        float4 x;
+        if (vec) x = *reinterpret_cast<const float4 *>(p + 4 * u);
+        else x = make_float4(p[4 * u], p[4 * u + 1], p[4 * u + 2], p[4 * u + 3]);
+        o[4 * u] = x.x; o[4 * u + 1] = x.y; o[4 * u + 2] = x.z; o[4 * u + 3] = x.w;
+    }
+}
+__device__ __forceinline__ void load16(const double *p, bool vec, double (&o)[16]) {
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+        double2 x;
+        if (vec) x = *reinterpret_cast<const double2 *>(p + 2 * u);
+        else x = make_double2(p[2 * u], p[2 * u + 1]);
+        o[2 * u] = x.x; o[2 * u + 1] = x.y;
+    }
+}
+
+// The products are the reference's fl(a*b) in f64 (exact for f32 inputs).
+template <typename T>
+__device__ __forceinline__ double ordered_dot4(const T *__restrict__ a,
+                                               const T *__restrict__ b, int64_t n,
                                                double (*buf)[4][CHP]) {
     const int lane = threadIdx.x & 63, g = lane >> 4, gl = lane & 15;
     const int64_t nfull = n / CH;
     const bool vec = ((((uintptr_t)a) | ((uintptr_t)b)) & 15) == 0;
-    float4 ra[2][4], rb[2][4];
-    auto fetch = [&](int64_t c, float4 (&pa)[4], float4 (&pb)[4]) {
+    T ra[2][16], rb[2][16];
+    auto fetch = [&](int64_t c, T (&pa)[16], T (&pb)[16]) {
         const int64_t o = c * CH + 16 * gl;
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            if (vec) {
-                pa[u] = *reinterpret_cast<const float4 *>(a + o + 4 * u);
-                pb[u] = *reinterpret_cast<const float4 *>(b + o + 4 * u);
-            } else {
-                const float *x = a + o + 4 * u, *y = b + o + 4 * u;
-                pa[u] = make_float4(x[0], x[1], x[2], x[3]);
-                pb[u] = make_float4(y[0], y[1], y[2], y[3]);
-            }
-        }
+        load16(a + o, vec, pa);
+        load16(b + o, vec, pb);
     };
     if (nfull > 0) fetch(0, ra[0], rb[0]);
     if (nfull > 1) fetch(1, ra[1], rb[1]);
@@ -154,12 +168,7 @@ __device__ __forceinline__ double ordered_dot4(const float *__restrict__ a,
             if (c >= nfull) break;
             double *bb = buf[h][g];
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                bb[16 * gl + 4 * u + 0] = (double)ra[h][u].x * (double)rb[h][u].x;
-                bb[16 * gl + 4 * u + 1] = (double)ra[h][u].y * (double)rb[h][u].y;
-                bb[16 * gl + 4 * u + 2] = (double)ra[h][u].z * (double)rb[h][u].z;
-                bb[16 * gl + 4 * u + 3] = (double)ra[h][u].w * (double)rb[h][u].w;
-            }
+            for (int u = 0; u < 16; ++u) bb[16 * gl + u] = (double)ra[h][u] * (double)rb[h][u];
             if (c + 2 < nfull) fetch(c + 2, ra[h], rb[h]);
             __builtin_amdgcn_wave_barrier();
             acc = lds_chain_f64<CH>(acc, bb);
@@ -171,12 +180,13 @@ __device__ __forceinline__ double ordered_dot4(const float *__restrict__ a,
 }
 
 // four columns per wave
-__global__ __launch_bounds__(64) void k_col_norms(const float *__restrict__ XT, int64_t n, int f,
+template <typename T>
+__global__ __launch_bounds__(64) void k_col_norms(const T *__restrict__ XT, int64_t n, int f,
                                                   double *__restrict__ nrm) {
     __shared__ double buf[2][4][CHP];
     const int g = threadIdx.x >> 4;
     const int i = blockIdx.x * 4 + g;
-    const float *p = XT + (int64_t)min(i, f - 1) * n;
+    const T *p = XT + (int64_t)min(i, f - 1) * n;
     const double acc = ordered_dot4(p, p, n, buf);
     if ((threadIdx.x & 15) == 0 && i < f) nrm[i] = __builtin_sqrt(acc);
 }
@@ -185,11 +195,12 @@ __global__ __launch_bounds__(64) void k_col_norms(const float *__restrict__ XT, 
 constexpr int GT = 64;  // output tile
 constexpr int GK = 16;  // rows per LDS stage
 
-__global__ __launch_bounds__(256) void k_gram_f64(const float *__restrict__ X, int64_t n, int f,
+template <typename T>
+__global__ __launch_bounds__(256) void k_gram_f64(const T *__restrict__ X, int64_t n, int f,
                                                   int ntile, int64_t kchunk, int nchunk,
                                                   double *__restrict__ G) {
-    __shared__ float As[GK][GT + 4];
-    __shared__ float Bs[GK][GT + 4];
+    __shared__ T As[GK][GT + 4];
+    __shared__ T Bs[GK][GT + 4];
     // blockIdx.x = chunk-major over upper-triangle tiles (concurrent blocks share rows)
     const int ntri = ntile * (ntile + 1) / 2;
     const int chunk = blockIdx.x / ntri;
@@ -205,27 +216,25 @@ __global__ __launch_bounds__(256) void k_gram_f64(const float *__restrict__ X, i
     for (int a = 0; a < 2; ++a)
 #pragma unroll
         for (int b = 0; b < 2; ++b) acc[a][b] = f64x4{0.0, 0.0, 0.0, 0.0};
-    const int lr = threadIdx.x >> 4, lc4 = (threadIdx.x & 15) * 4;  // 16 rows x 16 float4
+    const int lr = threadIdx.x >> 4, lc4 = (threadIdx.x & 15) * 4;  // 16 rows x 16 x 4 values
     for (int64_t kb = k0; kb < k1; kb += GK) {
         const int64_t row = kb + lr;
-        float4 va = make_float4(0.f, 0.f, 0.f, 0.f), vb = va;
+        T va[4] = {0, 0, 0, 0}, vb[4] = {0, 0, 0, 0};
         if (row < k1) {
-            const float *pr = X + row * f;
+            const T *pr = X + row * f;
             const int ca = bi * GT + lc4, cb = bj * GT + lc4;
-            if (ca + 3 < f && (f & 3) == 0) va = *reinterpret_cast<const float4 *>(pr + ca);
-            else {
-                va.x = ca < f ? pr[ca] : 0.f; va.y = ca + 1 < f ? pr[ca + 1] : 0.f;
-                va.z = ca + 2 < f ? pr[ca + 2] : 0.f; va.w = ca + 3 < f ? pr[ca + 3] : 0.f;
-            }
-            if (cb + 3 < f && (f & 3) == 0) vb = *reinterpret_cast<const float4 *>(pr + cb);
-            else {
-                vb.x = cb < f ? pr[cb] : 0.f; vb.y = cb + 1 < f ? pr[cb + 1] : 0.f;
-                vb.z = cb + 2 < f ? pr[cb + 2] : 0.f; vb.w = cb + 3 < f ? pr[cb + 3] : 0.f;
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                va[u] = ca + u < f ? pr[ca + u] : (T)0;
+                vb[u] = cb + u < f ? pr[cb + u] : (T)0;
             }
         }
         __syncthreads();
-        *reinterpret_cast<float4 *>(&As[lr][lc4]) = va;
-        *reinterpret_cast<float4 *>(&Bs[lr][lc4]) = vb;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            As[lr][lc4 + u] = va[u];
+            Bs[lr][lc4 + u] = vb[u];
+        }
         __syncthreads();
 #pragma unroll
         for (int s = 0; s < GK / 4; ++s) {
@@ -309,7 +318,8 @@ __global__ __launch_bounds__(256) void k_cos_select(const double *__restrict__ G
 }
 
 // ---- 5. exact sequential dot for (node, candidate) ---------------------------
-__global__ __launch_bounds__(256) void k_cos_exact(const float *__restrict__ XT, int64_t n,
+template <typename T>
+__global__ __launch_bounds__(256) void k_cos_exact(const T *__restrict__ XT, int64_t n,
                                                    const int32_t *__restrict__ pi,
                                                    const int32_t *__restrict__ pj, int64_t npairs,
                                                    const double *__restrict__ nrm,
@@ -320,12 +330,12 @@ __global__ __launch_bounds__(256) void k_cos_exact(const float *__restrict__ XT,
     if (i < 0 || j < 0) { dist[q] = __builtin_inf(); return; }
     const double denom = nrm[i] * nrm[j];
     if (!(denom > 1e-12)) { dist[q] = 1.0; return; }  // cos = 0 without a dot
-    const float *a = XT + (int64_t)i * n;
-    const float *b = XT + (int64_t)j * n;
+    const T *a = XT + (int64_t)i * n;
+    const T *b = XT + (int64_t)j * n;
     double acc = -0.0;
     int64_t t = 0;
     for (; t + 8 <= n; t += 8) {
-        float va[8], vb[8];
+        T va[8], vb[8];
 #pragma unroll
         for (int u = 0; u < 8; ++u) { va[u] = a[t + u]; vb[u] = b[t + u]; }
 #pragma unroll
@@ -337,7 +347,8 @@ __global__ __launch_bounds__(256) void k_cos_exact(const float *__restrict__ XT,
 
 // one wave per listed pair q: (node i = pi[q], candidate slot) -> dist[slot]
 // four listed pairs per wave, pair q = (node i, candidate slot) -> dist[slot]
-__global__ __launch_bounds__(256) void k_cos_exact_wave(const float *__restrict__ XT, int64_t n,
+template <typename T>
+__global__ __launch_bounds__(256) void k_cos_exact_wave(const T *__restrict__ XT, int64_t n,
                                                         const int32_t *__restrict__ plist,
                                                         const int *__restrict__ pcount,
                                                         int64_t pmax, const int32_t *__restrict__ cand,
@@ -362,7 +373,7 @@ __global__ __launch_bounds__(256) void k_cos_exact_wave(const float *__restrict_
         }
     }
     const bool dot = act && denom > 1e-12;  // else cos = 0 without a dot
-    const float *pa = XT + (int64_t)(dot ? i : 0) * n, *pb = XT + (int64_t)(dot ? j : 0) * n;
+    const T *pa = XT + (int64_t)(dot ? i : 0) * n, *pb = XT + (int64_t)(dot ? j : 0) * n;
     const double acc = ordered_dot4(pa, pb, n, buf[w]);
     if ((threadIdx.x & 15) == 0 && act) dist[slot] = dot ? cos_dist(acc, nrm[i], nrm[j]) : 1.0;
 }
@@ -503,6 +514,32 @@ __global__ __launch_bounds__(256) void k_fb_finish(const int32_t *__restrict__ f
     }
 }
 
+// StandardScaler on the columns of X [n][m] (f64): smartcore's
+// StandardScaler::fit/transform as build_laplacian_matrix applies it when
+// GraphParams.normalise is set (src_legacy/laplacian.rs:143-150).  smartcore
+// is not in the reference tree, so its exact arithmetic is parity-unpinned;
+// restated as mean = sequential sum / n, std = sqrt(sequential sum of
+// (x - mean)^2 / n), out = (x - mean) / std (std == 0: x - mean).  One thread
+// per column, rows streamed (adjacent threads read adjacent columns).
+__global__ void k_standardize_cols(const double *__restrict__ X, int64_t n, int m,
+                                   double *__restrict__ out) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= m) return;
+    double s = 0.0;
+    for (int64_t r = 0; r < n; ++r) s = s + X[r * m + c];
+    const double mean = s / (double)n;
+    double v = 0.0;
+    for (int64_t r = 0; r < n; ++r) {
+        const double t = X[r * m + c] - mean;
+        v = v + t * t;
+    }
+    const double sd = __builtin_sqrt(v / (double)n);
+    for (int64_t r = 0; r < n; ++r) {
+        const double t = X[r * m + c] - mean;
+        out[r * m + c] = sd > 0.0 ? t / sd : t;
+    }
+}
+
 inline unsigned grid(int64_t n, int t = 256) {
     return (unsigned)std::max<int64_t>(1, (n + t - 1) / t);
 }
@@ -511,12 +548,13 @@ inline unsigned grid(int64_t n, int t = 256) {
 
 static thread_local mn_knn_stats t_cos_stats{};
 
-static int knn_cos_columns_impl(const float *X, int64_t n, int32_t f, const mn_cos_opts *o,
+template <typename T>
+static int knn_cos_columns_impl(const T *X, int64_t n, int32_t f, const mn_cos_opts *o,
                                 int32_t *out_idx, double *out_dist, double *out_w) {
     using namespace kcos;
     clear_error();
     t_cos_stats = mn_knn_stats{};
-    MN_REQUIRE(o && X && out_idx && out_dist, MN_EINVAL, "mn_knn_cos_columns_f32: NULL argument");
+    MN_REQUIRE(o && X && out_idx && out_dist, MN_EINVAL, "mn_knn_cos_columns: NULL argument");
     MN_REQUIRE(n >= 1 && f >= 2 && f <= FMAXC, MN_EINVAL,
                "mn_knn_cos_columns_f32: need n >= 1 and 2 <= f <= %d", FMAXC);
     MN_REQUIRE(o->topk >= 1 && o->topk <= 64, MN_ENOTSUP, "mn_knn_cos_columns_f32: topk in [1,64]");
@@ -531,7 +569,7 @@ static int knn_cos_columns_impl(const float *X, int64_t n, int32_t f, const mn_c
     kchunk = ((kchunk + GK - 1) / GK) * GK;
     nchunk = (int)((n + kchunk - 1) / kchunk);
 
-    float *XT = (float *)scratch(kSlotGeneric0, sizeof(float) * (size_t)n * f);
+    T *XT = (T *)scratch(kSlotGeneric0, sizeof(T) * (size_t)n * f);
     char *g = (char *)scratch(kSlotGeneric1, sizeof(double) * ((size_t)f * f + f * 2 + 64) +
                                                 (size_t)f * L * 24 + (size_t)f * 8 + 64);
     MN_REQUIRE(XT && g, MN_ENOMEM, "mn_knn_cos_columns_f32: scratch allocation failed");
@@ -550,16 +588,16 @@ static int knn_cos_columns_impl(const float *X, int64_t n, int32_t f, const mn_c
     tm.start(o->timing != 0, s);
     MN_HIP_TRY(hipMemsetAsync(G, 0, sizeof(double) * (size_t)f * f, s));
     MN_HIP_TRY(hipMemsetAsync(flags, 0, 64, s));
-    hipLaunchKernelGGL(k_transpose, dim3(grid(n, 64), (unsigned)((f + 63) / 64)), dim3(256), 0, s,
+    hipLaunchKernelGGL(k_transpose<T>, dim3(grid(n, 64), (unsigned)((f + 63) / 64)), dim3(256), 0, s,
                        X, n, f, XT);
     // the exact norms (768 latency-bound chains) run on the side stream while
     // the Gram occupies the MFMAs
     hipStream_t side = side_stream();
     MN_REQUIRE(side, MN_EHIP, "mn_knn_cos_columns_f32: side stream creation failed");
     MN_HIP_TRY(stream_wait(side, s));
-    hipLaunchKernelGGL(k_col_norms, dim3((unsigned)((f + 3) / 4)), dim3(64), 0, side, XT, n, f, nrm);
+    hipLaunchKernelGGL(k_col_norms<T>, dim3((unsigned)((f + 3) / 4)), dim3(64), 0, side, XT, n, f, nrm);
     MN_KCHECK(side, "k_col_norms");
-    hipLaunchKernelGGL(k_gram_f64, dim3((unsigned)(ntri * nchunk)), dim3(256), 0, s, X, n, f, ntile,
+    hipLaunchKernelGGL(k_gram_f64<T>, dim3((unsigned)(ntri * nchunk)), dim3(256), 0, s, X, n, f, ntile,
                        kchunk, nchunk, G);
     MN_HIP_TRY(hipGetLastError());
     MN_HIP_TRY(stream_wait(s, side));
@@ -572,7 +610,9 @@ static int knn_cos_columns_impl(const float *X, int64_t n, int32_t f, const mn_c
 #undef MN_SEL
     // exact distances: the first kq candidates of every node, then the ones
     // whose lower bound can still reach the top k (the rest stay +inf)
-    const double delta = 2.0 * ((double)n + 16.0) * 0x1p-53 + 1e-300;
+    // |d~ - d| bound: f64 accumulation of n products (f64 inputs: each product
+    // rounded once more), norms and the quotient, with a factor-2 margin
+    const double delta = 2.0 * ((double)n + (sizeof(T) == 8 ? 17.0 : 16.0)) * 0x1p-53 + 1e-300;
     const int kq = std::min(o->topk, L);
     const int fkq = f * kq;
     hipLaunchKernelGGL(k_fill_f64, dim3(grid((int64_t)f * L)), dim3(256), 0, s, cdist,
@@ -584,7 +624,7 @@ static int knn_cos_columns_impl(const float *X, int64_t n, int32_t f, const mn_c
     if (L > kq)
         hipLaunchKernelGGL(k_extra_pairs, dim3(grid(f)), dim3(256), 0, s, cand, capx, f, L, kq,
                            delta, pi, flags + 1);
-    hipLaunchKernelGGL(k_cos_exact_wave, dim3(grid((int64_t)f * L, 16)), dim3(256), 0, s, XT, n, pi,
+    hipLaunchKernelGGL(k_cos_exact_wave<T>, dim3(grid((int64_t)f * L, 16)), dim3(256), 0, s, XT, n, pi,
                        flags + 1, (int64_t)f * L, cand, L, nrm, cdist);
     hipLaunchKernelGGL(k_cos_finish, dim3(grid(f, 4)), dim3(256), 0, s, cand, cdist, gnext, f, L,
                        o->topk, o->eps, o->sigma, o->p, delta, out_idx, out_dist, out_w, flags,
@@ -602,7 +642,7 @@ static int knn_cos_columns_impl(const float *X, int64_t n, int32_t f, const mn_c
         MN_HIP_TRY(hipMalloc(&fpj, 4 * np));
         MN_HIP_TRY(hipMalloc(&fd, 8 * np));
         hipLaunchKernelGGL(k_fb_pairs, dim3(grid(np)), dim3(256), 0, s, fb_list, flags, f, fpi, fpj);
-        hipLaunchKernelGGL(k_cos_exact, dim3(grid(np)), dim3(256), 0, s, XT, n, fpi, fpj, np, nrm, fd);
+        hipLaunchKernelGGL(k_cos_exact<T>, dim3(grid(np)), dim3(256), 0, s, XT, n, fpi, fpj, np, nrm, fd);
 #define MN_FB(NRV) hipLaunchKernelGGL(k_fb_finish<NRV>, dim3(grid(nfb, 4)), dim3(256), 0, s, fb_list, flags, fd, f, o->topk, o->eps, o->sigma, o->p, out_idx, out_dist, out_w)
         if (nr <= 1) MN_FB(1); else if (nr <= 2) MN_FB(2); else if (nr <= 4) MN_FB(4);
         else if (nr <= 8) MN_FB(8); else if (nr <= 16) MN_FB(16); else if (nr <= 32) MN_FB(32);
@@ -633,7 +673,25 @@ extern "C" {
 
 int mn_knn_cos_columns_f32(const float *X, int64_t n_rows, int32_t f, const mn_cos_opts *opts,
                            int32_t *out_idx, double *out_dist, double *out_w) {
-    return mn::knn_cos_columns_impl(X, n_rows, f, opts, out_idx, out_dist, out_w);
+    return mn::knn_cos_columns_impl<float>(X, n_rows, f, opts, out_idx, out_dist, out_w);
+}
+
+int mn_knn_cos_columns_f64(const double *X, int64_t n_rows, int32_t f, const mn_cos_opts *opts,
+                           int32_t *out_idx, double *out_dist, double *out_w) {
+    return mn::knn_cos_columns_impl<double>(X, n_rows, f, opts, out_idx, out_dist, out_w);
+}
+
+int mn_standardize_columns_f64(const double *X, int64_t n_rows, int32_t n_cols, double *out,
+                               void *stream) {
+    mn::clear_error();
+    MN_REQUIRE(X && out && n_rows >= 1 && n_cols >= 1, MN_EINVAL,
+               "mn_standardize_columns_f64: bad arguments");
+    hipStream_t s = (hipStream_t)stream;
+    hipLaunchKernelGGL(mn::kcos::k_standardize_cols, dim3(mn::kcos::grid(n_cols)), dim3(256), 0,
+                       s, X, n_rows, n_cols, out);
+    MN_KCHECK(s, "k_standardize_cols");
+    MN_HIP_TRY(hipStreamSynchronize(s));
+    return MN_OK;
 }
 
 int mn_cos_last_stats(mn_knn_stats *out) {

@@ -37,6 +37,7 @@
 #include "common.hpp"
 #include "gram_bf16.hpp"
 #include "gram_sweep.hpp"
+#include "gram_sweep2.hpp"
 
 namespace mn {
 namespace knn {
@@ -1476,6 +1477,13 @@ static int knn_f32_core(const float *Q, int64_t nq, const float *C, int64_t nc, 
                         int64_t q_off, int64_t c_off, const mn_knn_opts *opts,
                         int32_t *out_idx, float *out_dist, int algo);
 
+// Phase-2 sweep kernel: 2 = gram_sweep2.hpp (ping-pong, 16x16x32 MFMA; the
+// default), 1 = gram_sweep.hpp (MN_X1_SWEEP=1, kept for A/B measurements).
+static int sweep_version() {
+    const char *e = getenv("MN_X1_SWEEP");
+    return (e && *e == '1') ? 1 : 2;
+}
+
 // Host driver of MN_KNN_BF16X1 (section 2c).  Returns 1 (nothing written)
 // when some row is too large for the single-bf16 bound: the caller then runs
 // the split generator.
@@ -1595,10 +1603,18 @@ static int knn_x1(const float *Q, int64_t nq, const float *C, int64_t nc, int32_
         const int64_t grid = nqb * p2.S;
         MN_REQUIRE(grid < INT_MAX && nq * 32 < INT_MAX && nc * 32 < INT_MAX, MN_ENOTSUP,
                    "mn_knn: sweep grid too large (split the queries / corpus)");
-        auto kern = (probe && !strcmp(probe, "noepi")) ? ksw::k_gram_sweep<1> : ksw::k_gram_sweep<0>;
-        hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(ksw::NT), 0, s, QK, nq, CK, nc, nkb,
-                           q_off, (int64_t)0, 0, tq, tau0, chc, m0, S2, p2.chunk, cap2, cbuf2,
-                           cnt2);
+        const bool noepi = probe && !strcmp(probe, "noepi");
+        if (sweep_version() == 1) {
+            auto kern = noepi ? ksw::k_gram_sweep<1> : ksw::k_gram_sweep<0>;
+            hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(ksw::NT), 0, s, QK, nq, CK, nc,
+                               nkb, q_off, (int64_t)0, 0, tq, tau0, chc, m0, S2, p2.chunk, cap2,
+                               cbuf2, cnt2);
+        } else {
+            auto kern = noepi ? ksw2::k_gram_sweep2<1> : ksw2::k_gram_sweep2<0>;
+            hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(ksw2::NT), 0, s, QK, nq, CK, nc,
+                               nkb, q_off, (int64_t)0, 0, tq, tau0, chc, m0, S2, p2.chunk, cap2,
+                               cbuf2, cnt2);
+        }
         MN_KCHECK(s, "k_gram_sweep");
     }
     tm.mark();
@@ -1700,9 +1716,14 @@ static int knn_x1(const float *Q, int64_t nq, const float *C, int64_t nc, int32_
                    (nbuf3 * sizeof(uint2)) >> 20);
         const int64_t grid3 = ((nfb + ksw::BQ - 1) / ksw::BQ) * p3.S;
         MN_REQUIRE(grid3 < INT_MAX, MN_ENOTSUP, "mn_knn: refill grid too large");
-        hipLaunchKernelGGL(ksw::k_gram_sweep<0>, dim3((unsigned)grid3), dim3(ksw::NT), 0, s, QK3,
-                           (int64_t)nfb, CK3, nc, nkb3, (int64_t)0, (int64_t)0, 0, tq3, tau3, chc,
-                           (int64_t)0, (int)p3.S, p3.chunk, p3.cap, cbuf3, cnt3);
+        if (sweep_version() == 1)
+            hipLaunchKernelGGL(ksw::k_gram_sweep<0>, dim3((unsigned)grid3), dim3(ksw::NT), 0, s,
+                               QK3, (int64_t)nfb, CK3, nc, nkb3, (int64_t)0, (int64_t)0, 0, tq3,
+                               tau3, chc, (int64_t)0, (int)p3.S, p3.chunk, p3.cap, cbuf3, cnt3);
+        else
+            hipLaunchKernelGGL(ksw2::k_gram_sweep2<0>, dim3((unsigned)grid3), dim3(ksw2::NT), 0, s,
+                               QK3, (int64_t)nfb, CK3, nc, nkb3, (int64_t)0, (int64_t)0, 0, tq3,
+                               tau3, chc, (int64_t)0, (int)p3.S, p3.chunk, p3.cap, cbuf3, cnt3);
         MN_KCHECK(s, "k_gram_sweep<x3>");
         int *big_count3 = flags + 6;
         int *big_list3 = fb_list + nq;

@@ -5,7 +5,9 @@ Every op runs on the GPU through the C ABI; there is no CPU fallback.
 """
 from . import _lib
 from ._lib import MnError, lib
-from . import energy, l2f64, laplacian, search, sorted_index, sparsification
+from . import energy, graph, l2f64, laplacian, search, sorted_index, sparsification
+from .graph import (BuilderParams, EigenMaps, GraphFactory, GraphLaplacian, SparsityError,
+                    build_laplacian_matrix, standardize_columns)
 from .l2f64 import (estimate_intrinsic_dimension, knn_l2_f64, nearest_subcentroid,
                     prepare_query_items_energy, topk_by_l2, topk_by_l2_rows)
 from .search import (normalise_query_lambda, prepare_query_lambdas, search_lambda_aware,
@@ -19,11 +21,12 @@ from .energy import (TauMode, compute_lambdas_gpu, compute_tau_mode_gpu, compute
 from .laplacian import (CsrMatrix, GraphParams, LaplacianConfig, LaplacianOutput, LaplacianStage,
                         build_laplacian_from_knn, compute_bhattacharyya_weights,
                         laplacian_stage_from_edges)
-from .knn import (DistanceMetric, KnnResult, bf16_last_stats, build_candidate_graph, knn_cos_bf16,
+from .knn import (CandidateEdges, DistanceMetric, MSTConfig, ThicknessWeight, KnnResult, bf16_last_stats, build_candidate_graph, knn_cos_bf16,
                   knn_cos_bf16_qc, knn_cos_columns, knn_l2sq,
                   knn_l2sq_qc, last_stats, merge_parts)
 
-__all__ = ["MnError", "lib", "knn_cos_columns", "knn_cos_bf16", "knn_cos_bf16_qc", "bf16_last_stats", "DistanceMetric", "KnnResult", "build_candidate_graph", "knn_l2sq",
+__all__ = ["MnError", "lib", "graph", "BuilderParams", "EigenMaps", "GraphFactory",
+           "GraphLaplacian", "SparsityError", "build_laplacian_matrix", "standardize_columns", "knn_cos_columns", "knn_cos_bf16", "knn_cos_bf16_qc", "bf16_last_stats", "DistanceMetric", "MSTConfig", "ThicknessWeight", "CandidateEdges", "KnnResult", "build_candidate_graph", "knn_l2sq",
            "knn_l2sq_qc", "last_stats", "merge_parts", "CsrMatrix", "GraphParams",
            "LaplacianConfig", "LaplacianOutput", "build_laplacian_from_knn",
            "laplacian_stage_from_edges", "LaplacianStage", "compute_bhattacharyya_weights", "laplacian", "energy", "TauMode",

@@ -1,10 +1,14 @@
 """K1 — brute-force kNN through the HIP C ABI (mn_knn_f32 / _qc / merge).
 
 Host-side mirror of the reference's kNN entry points:
-  * surfface-core/src/mst.rs:312-363  MSTStage::build_candidate_graph
-    (DistanceMetric::SquaredEuclidean / Euclidean)  -> build_candidate_graph()
-  * surfface-core/src/distance.rs:195-213 squared/euclidean distance
-Results are bit-identical to the reference's sequential f32 fold + stable sort.
+  * surfface-core/src/mst.rs:312-412  MSTStage::build_candidate_graph with
+    compute_distance / compute_edge_cost (every DistanceMetric, every
+    ThicknessWeight)  -> build_candidate_graph()
+  * surfface-core/src/distance.rs:78-108 bhattacharyya_distance_diagonal,
+    :195-213 squared/euclidean distance
+L2 results are bit-identical to the reference's sequential f32 fold + stable
+sort; Bhattacharyya distances are bit-identical but for rare ulp-level log
+terms (mst.hip header).
 """
 from __future__ import annotations
 
@@ -19,9 +23,50 @@ from ._torch import ptr, require_cuda, stream_handle, to_device, on_device
 
 
 class DistanceMetric(IntEnum):
-    """surfface-core/src/mst.rs:45-54 (Bhattacharyya is not on this path)."""
-    SquaredEuclidean = 0
-    Euclidean = 100  # same ordering as SquaredEuclidean; distances are sqrt'd
+    """surfface-core/src/mst.rs:45-54 (values = enum mn_mst_metric)."""
+    Bhattacharyya = 0
+    Euclidean = 1
+    SquaredEuclidean = 2
+
+
+class ThicknessWeight(IntEnum):
+    """surfface-core/src/mst.rs:58-74 (values = enum mn_thickness_weight)."""
+    Mean = 0
+    Min = 1
+    Max = 2
+    GeometricMean = 3
+    NoWeight = 4  # ThicknessWeight::None
+
+
+@dataclass
+class MSTConfig:
+    """surfface-core/src/mst.rs:26-40, defaults :77-84 (the candidate-graph
+    fields; compute_trunk belongs to the out-of-scope MST/trunk stage)."""
+    k_neighbors: int = 8
+    distance_metric: DistanceMetric = DistanceMetric.Bhattacharyya
+    thickness_weight: ThicknessWeight = ThicknessWeight.Mean
+    compute_trunk: bool = True
+
+    @staticmethod
+    def high_dimensional() -> "MSTConfig":
+        return MSTConfig(k_neighbors=16)
+
+    @staticmethod
+    def prototype() -> "MSTConfig":
+        return MSTConfig(4, DistanceMetric.SquaredEuclidean, ThicknessWeight.NoWeight, False)
+
+
+@dataclass
+class CandidateEdges:
+    """The reference's Vec<Edge> (mst.rs:110-119) as device columns, edge
+    e = i * k + r for node i's r-th nearest (u ascending, then distance, then v)."""
+    u: torch.Tensor            # [E] int64
+    v: torch.Tensor            # [E] int64
+    distance: torch.Tensor     # [E] f32
+    thickness_u: torch.Tensor  # [E] f32
+    thickness_v: torch.Tensor  # [E] f32
+    cost: torch.Tensor         # [E] f32
+    thickness: torch.Tensor    # [C] f32 per-node thickness used
 
 
 @dataclass
@@ -104,23 +149,42 @@ def merge_parts(part_idx: torch.Tensor, part_dist: torch.Tensor, stream=None):
     return idx, dist
 
 
-def build_candidate_graph(means, k_neighbors: int,
-                          metric: DistanceMetric = DistanceMetric.SquaredEuclidean):
-    """Mirror of MSTStage::build_candidate_graph (mst.rs:312-363), kNN part.
-
-    Returns directed edges (u, v, distance) as device tensors, k = min(k, C-1)
-    per node, in the reference's order (u ascending, then distance, then v).
-    """
-    X = to_device(means).float()
-    c = X.shape[0]
-    k = min(k_neighbors, c - 1)
-    if k < 1:
-        e = torch.empty(0, dtype=torch.int64, device=X.device)
-        return e, e.clone(), torch.empty(0, dtype=torch.float32, device=X.device)
-    r = knn_l2sq(X, k, euclidean=metric == DistanceMetric.Euclidean)
-    u = torch.arange(c, device=X.device, dtype=torch.int64).repeat_interleave(k)
-    v = r.idx.reshape(-1).to(torch.int64)
-    return u, v, r.dist.reshape(-1)
+@on_device
+def build_candidate_graph(means, variances=None, k_neighbors: int = 8,
+                          metric: DistanceMetric = DistanceMetric.Bhattacharyya,
+                          thickness_weight: ThicknessWeight = ThicknessWeight.Mean,
+                          thickness=None, stream=None) -> CandidateEdges:
+    """Mirror of MSTStage::build_candidate_graph (mst.rs:312-363) with
+    compute_distance (:366-397) and compute_edge_cost (:400-412), through
+    mn_mst_candidate_graph_f32.  means / variances [C, F] (the CentroidState
+    rows); thickness [C] or None = the mean variance per centroid
+    (centroid.rs:107-109).  k = min(k_neighbors, C - 1) edges per node."""
+    X = to_device(means).float().contiguous()
+    require_cuda(X, torch.float32, "means", 2)
+    c, f = X.shape
+    V = None
+    if variances is not None:
+        V = to_device(variances).float().contiguous().to(X.device)
+        if tuple(V.shape) != (c, f):
+            raise ValueError("variances must have the shape of means")
+    if c < 2:
+        raise ValueError("build_candidate_graph needs at least 2 centroids (the reference "
+                         "computes k = min(k, C - 1) and indexes thickness)")
+    T = None
+    if thickness is not None:
+        T = to_device(thickness).float().contiguous().to(X.device)
+    kk = min(k_neighbors, c - 1)
+    v = torch.empty((c, kk), dtype=torch.int32, device=X.device)
+    dist = torch.empty((c, kk), dtype=torch.float32, device=X.device)
+    cost = torch.empty((c, kk), dtype=torch.float32, device=X.device)
+    th = torch.empty(c, dtype=torch.float32, device=X.device)
+    _lib.check(_lib.lib().mn_mst_candidate_graph_f32(
+        ptr(X), ptr(V) if V is not None else None, c, f, k_neighbors, int(metric),
+        int(thickness_weight), ptr(T) if T is not None else None, ptr(th), ptr(v), ptr(dist),
+        ptr(cost), stream_handle(stream)))
+    u = torch.arange(c, device=X.device, dtype=torch.int64).repeat_interleave(kk)
+    vv = v.reshape(-1).to(torch.int64)
+    return CandidateEdges(u, vv, dist.reshape(-1), th[u], th[vv], cost.reshape(-1), th)
 
 
 def cos_last_stats() -> dict:

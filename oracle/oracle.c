@@ -266,6 +266,89 @@ int or_knn_cos_f64(const float *X, int64_t n, int32_t d, int32_t topk,
     return err;
 }
 
+/* A.1c on f64 rows (the legacy DenseMatrix<f64> items): the same arithmetic
+ * with the reference's rounded f64 products (test_helpers.rs:77-126). */
+static double norm_f64d(const double *x, int32_t d) {
+    double s = -0.0;
+    for (int32_t t = 0; t < d; ++t) s = s + x[t] * x[t];
+    return sqrt(s);
+}
+
+int or_knn_cos_f64d(const double *X, int64_t n, int32_t d, int32_t topk,
+                   double eps, double sigma, double p,
+                   int64_t q_begin, int64_t q_end, int nthreads,
+                   int32_t *out_idx, double *out_dist, double *out_w) {
+    if (!X || !out_idx || !out_dist || n < 1 || d < 1 || topk < 1 || q_begin < 0 ||
+        q_end > n || q_begin > q_end)
+        return OR_EINVAL;
+    double *norms = (double *)malloc(sizeof(double) * (size_t)n);
+    if (!norms) return OR_ENOMEM;
+    set_threads(nthreads);
+    int err = 0;
+#pragma omp parallel for schedule(static)
+    for (int64_t i = 0; i < n; ++i) norms[i] = norm_f64d(X + i * (int64_t)d, d);
+
+#pragma omp parallel
+    {
+        cand_f64 *buf = (cand_f64 *)malloc(sizeof(cand_f64) * (size_t)topk);
+        if (!buf) {
+#pragma omp atomic write
+            err = OR_ENOMEM;
+        }
+#pragma omp for schedule(dynamic, 16)
+        for (int64_t i = q_begin; i < q_end; ++i) {
+            if (!buf) continue;
+            const double *xi = X + i * (int64_t)d;
+            int32_t cnt = 0;
+            int bad = 0;
+            for (int64_t j = 0; j < n; ++j) {
+                if (j == i) continue;
+                double denom = norms[i] * norms[j];
+                double cs;
+                if (denom > 1e-12) {
+                    const double *xj = X + j * (int64_t)d;
+                    double dot = -0.0;
+                    for (int32_t t = 0; t < d; ++t) dot = dot + (double)xi[t] * (double)xj[t];
+                    cs = dot / denom;
+                    if (cs != cs) { bad = 1; break; }
+                    cs = cs < -1.0 ? -1.0 : (cs > 1.0 ? 1.0 : cs);
+                } else {
+                    cs = 0.0;
+                }
+                double dist = 1.0 - (cs > 0.0 ? cs : 0.0);
+                if (!(dist <= eps)) continue;
+                double nd = dist / sigma;
+                double wgt = 1.0 / (1.0 + (p == 2.0 ? nd * nd : pow(nd, p)));
+                if (!(wgt > 1e-12)) continue;
+                if (cnt < topk) {
+                    buf[cnt].d = dist; buf[cnt].w = wgt; buf[cnt].j = (int32_t)j;
+                    heap64_up(buf, cnt); ++cnt;
+                } else if (lt_f64(dist, (int32_t)j, buf[0].d, buf[0].j)) {
+                    buf[0].d = dist; buf[0].w = wgt; buf[0].j = (int32_t)j;
+                    heap64_down(buf, cnt, 0);
+                }
+            }
+            if (bad) {
+#pragma omp atomic write
+                err = OR_ENONFINITE;
+                continue;
+            }
+            qsort(buf, (size_t)cnt, sizeof(cand_f64), cmp_cand_f64);
+            int32_t *oi = out_idx + (i - q_begin) * (int64_t)topk;
+            double *od = out_dist + (i - q_begin) * (int64_t)topk;
+            double *ow = out_w ? out_w + (i - q_begin) * (int64_t)topk : NULL;
+            for (int32_t r = 0; r < topk; ++r) {
+                if (r < cnt) { oi[r] = buf[r].j; od[r] = buf[r].d; if (ow) ow[r] = buf[r].w; }
+                else { oi[r] = -1; od[r] = INFINITY; if (ow) ow[r] = 0.0; }
+            }
+        }
+        free(buf);
+    }
+    free(norms);
+    return err;
+}
+
+
 /* A.1c on bf16 rows (config 5), explicit query rows: the same arithmetic as
  * or_knn_cos_f64 on the exactly widened values (bf16 -> f32 is a 16-bit
  * shift).  Used for full-size parity samples without a 4x host copy. */
@@ -881,6 +964,104 @@ int or_diffuse_rows(const double *X, int64_t n, int32_t f, const int64_t *indptr
         free(x);
         free(lx);
     }
+    return err;
+}
+
+/* ---- MST candidate graph (mst.rs:312-412, distance.rs:78-108) ---------- */
+
+float or_bhattacharyya_distance(const float *mean_i, const float *var_i, const float *mean_j,
+                                const float *var_j, int64_t f) {
+    const float eps = 1e-10f; /* distance.rs:87 */
+    float distance = 0.0f;
+    for (int64_t k = 0; k < f; ++k) {
+        float sigma_i = fmaxf(var_i[k], eps); /* f32::max: NaN -> the other */
+        float sigma_j = fmaxf(var_j[k], eps);
+        float sigma_sum = sigma_i + sigma_j;
+        float sigma_prod = sigma_i * sigma_j;
+        float mean_diff = mean_i[k] - mean_j[k];
+        float mahalanobis = 0.25f * (mean_diff * mean_diff) / sigma_sum;
+        float log_term = 0.25f * logf(fmaxf(sigma_sum / (2.0f * sqrtf(sigma_prod)), eps));
+        distance += mahalanobis + log_term;
+    }
+    return distance;
+}
+
+typedef struct { float d; int32_t j; } mstc;
+static int cmp_mstc(const void *pa, const void *pb) { /* stable sort_by on ascending j */
+    const mstc *a = (const mstc *)pa, *b = (const mstc *)pb;
+    if (a->d < b->d) return -1;
+    if (a->d > b->d) return 1;
+    return a->j < b->j ? -1 : (a->j > b->j ? 1 : 0);
+}
+
+int or_mst_candidates(const float *means, const float *vars, int64_t c, int32_t f, int32_t k,
+                      int metric, int tw, const float *thickness, int32_t *out_v,
+                      float *out_dist, float *out_cost) {
+    if (!means || !out_v || !out_dist || !out_cost || c < 2 || f < 1 || k < 1) return OR_EINVAL;
+    if (metric < 0 || metric > 2 || tw < 0 || tw > 4) return OR_EINVAL;
+    if ((metric == 0 || !thickness) && !vars) return OR_EINVAL;
+    const int64_t kk = k < c - 1 ? k : c - 1; /* mst.rs:317 */
+    float *th = (float *)malloc(sizeof(float) * (size_t)c);
+    if (!th) return OR_ENOMEM;
+    for (int64_t i = 0; i < c; ++i) {
+        if (thickness) { th[i] = thickness[i]; continue; }
+        float s = 0.0f; /* centroid.rs:107-109 (Burn's order unspecified) */
+        for (int32_t t = 0; t < f; ++t) s += vars[i * f + t];
+        th[i] = s / (float)f;
+    }
+    int err = 0;
+#pragma omp parallel
+    {
+        mstc *sc = (mstc *)malloc(sizeof(mstc) * (size_t)c);
+        if (!sc) {
+#pragma omp atomic write
+            err = OR_ENOMEM;
+        }
+#pragma omp for schedule(dynamic, 4)
+        for (int64_t i = 0; i < c; ++i) {
+            if (!sc) continue;
+            int64_t m = 0;
+            for (int64_t j = 0; j < c; ++j) {
+                if (j == i) continue;
+                float d;
+                if (metric == 0) {
+                    d = or_bhattacharyya_distance(means + i * f, vars + i * f, means + j * f,
+                                                  vars + j * f, f);
+                } else {
+                    float s = 0.0f; /* mst.rs:383-397 */
+                    for (int32_t t = 0; t < f; ++t) {
+                        float diff = means[i * f + t] - means[j * f + t];
+                        s += diff * diff;
+                    }
+                    d = metric == 1 ? sqrtf(s) : s;
+                }
+                if (d != d) {
+#pragma omp atomic write
+                    err = OR_ENONFINITE;
+                }
+                sc[m].d = d;
+                sc[m].j = (int32_t)j;
+                ++m;
+            }
+            qsort(sc, (size_t)m, sizeof(mstc), cmp_mstc);
+            for (int64_t r = 0; r < kk; ++r) {
+                const float d = sc[r].d, ti = th[i], tj = th[sc[r].j];
+                float cost;
+                switch (tw) { /* mst.rs:400-412 */
+                case 0: cost = d * ((ti + tj) / 2.0f); break;
+                case 1: cost = d * fminf(ti, tj); break;
+                case 2: cost = d * fmaxf(ti, tj); break;
+                case 3: cost = d * sqrtf(ti * tj); break;
+                default: cost = d; break;
+                }
+                out_v[i * kk + r] = sc[r].j;
+                out_dist[i * kk + r] = d;
+                out_cost[i * kk + r] = cost;
+            }
+        }
+        free(sc);
+    }
+    free(th);
     return err;
 }
 

@@ -66,6 +66,11 @@ int or_knn_cos_f64(const float *X, int64_t n, int32_t d, int32_t topk,
                    double eps, double sigma, double p,
                    int64_t q_begin, int64_t q_end, int nthreads,
                    int32_t *out_idx, double *out_dist, double *out_w);
+/* The same over f64 rows (products rounded in f64 like the reference's). */
+int or_knn_cos_f64d(const double *X, int64_t n, int32_t d, int32_t topk,
+                    double eps, double sigma, double p,
+                    int64_t q_begin, int64_t q_end, int nthreads,
+                    int32_t *out_idx, double *out_dist, double *out_w);
 
 /* A.1c on bf16 rows (bf16 bits, row-major [n][d]) for explicit query rows
  * (config 5 parity samples); outputs [nrows][topk]. */
@@ -218,6 +223,23 @@ int or_diffuse_rows(const double *X, int64_t n, int32_t f, const int64_t *indptr
  * (BC desc, j asc).  out_idx/out_w [f][k] (-1 / 0 padded). */
 int or_bc_knn(const float *means, const float *vars, int64_t c, int32_t f, int32_t k,
               float reg, float thr, int32_t *out_idx, float *out_w);
+
+/* surfface-core/src/distance.rs:78-108 bhattacharyya_distance_diagonal (f32,
+ * sequential fold, host libm logf / IEEE sqrtf as the Rust reference links). */
+float or_bhattacharyya_distance(const float *mean_i, const float *var_i, const float *mean_j,
+                                const float *var_j, int64_t f);
+
+/* surfface-core/src/mst.rs:312-412 build_candidate_graph + compute_distance +
+ * compute_edge_cost: nodes = the c rows of means/vars [c][f]; metric 0 =
+ * Bhattacharyya, 1 = Euclidean (sqrtf of the f32 fold), 2 = SquaredEuclidean;
+ * per node i every j != i, stable sort by distance (j ascending on ties),
+ * truncated to k' = min(k, c-1); cost = distance * phi(t_i, t_j) with tw
+ * 0 Mean, 1 Min, 2 Max, 3 GeometricMean, 4 None (cost = distance);
+ * thickness [c] (host) or NULL = sequential f32 mean of the variance row.
+ * out_v / out_dist / out_cost [c][k'].  OR_ENONFINITE on a NaN distance. */
+int or_mst_candidates(const float *means, const float *vars, int64_t c, int32_t f, int32_t k,
+                      int metric, int tw, const float *thickness, int32_t *out_v,
+                      float *out_dist, float *out_cost);
 
 /* ---- K5: SF-GRASS ------------------------------------------------------- */
 

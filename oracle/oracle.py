@@ -50,6 +50,7 @@ def _declare(L):
     L.or_knn_l2sq_rows_f32.argtypes = [P, I64, I32, I32, P, I64, C.c_int, P, P]
     L.or_knn_l2_f64.argtypes = [P, I64, P, I64, I32, P, I32, C.c_int, C.c_int, P, P]
     L.or_knn_cos_f64.argtypes = [P, I64, I32, I32, D, D, D, I64, I64, C.c_int, P, P, P]
+    L.or_knn_cos_f64d.argtypes = [P, I64, I32, I32, D, D, D, I64, I64, C.c_int, P, P, P]
     L.or_knn_cos_bf16_rows.argtypes = [P, I64, I32, I32, D, D, D, P, I64, C.c_int, P, P, P]
     L.or_laplacian_union.argtypes = [I64, I32, P, P, I64, P, P, P, P]
     L.or_laplacian_max.argtypes = [I64, I64, P, P, P, F, C.c_int, I64, P, P, P, P, P, P]
@@ -61,6 +62,9 @@ def _declare(L):
     L.or_spectral_lambdas_f32.argtypes = [P, I64, I32, P, P, P, P]
     L.or_sorted_index.argtypes = [P, I64, P, P, P]
     L.or_bc_knn.argtypes = [P, P, I64, I32, I32, C.c_float, C.c_float, P, P]
+    L.or_bhattacharyya_distance.argtypes = [P, P, P, P, I64]
+    L.or_bhattacharyya_distance.restype = C.c_float
+    L.or_mst_candidates.argtypes = [P, P, I64, I32, I32, C.c_int, C.c_int, P, P, P, P]
     L.or_diffuse_rows.argtypes = [P, I64, I32, P, P, P, C.c_double, I32, C.c_int, P]
     L.or_range_bylambda.argtypes = [P, P, I64, C.c_double, C.c_double, I64, C.c_double, P, P]
     L.or_range_bylambda.restype = I64
@@ -128,6 +132,18 @@ def knn_cos(X, topk, eps=1.0, sigma=1.0, p=2.0, q_begin=0, q_end=None, nthreads=
     w = np.empty((m, topk), np.float64)
     _check(lib().or_knn_cos_f64(_p(X), n, d, topk, eps, sigma, p, q_begin, q_end, nthreads,
                                 _p(idx), _p(dist), _p(w)), "knn_cos")
+    return idx, dist, w
+
+
+def knn_cos_f64(X, topk, eps=1.0, sigma=1.0, p=2.0, nthreads=0):
+    """A.1c over f64 rows (nodes = rows)."""
+    X = np.ascontiguousarray(X, dtype=np.float64)
+    n, d = X.shape
+    idx = np.empty((n, topk), np.int32)
+    dist = np.empty((n, topk), np.float64)
+    w = np.empty((n, topk), np.float64)
+    _check(lib().or_knn_cos_f64d(_p(X), n, d, topk, eps, sigma, p, 0, n, nthreads,
+                                 _p(idx), _p(dist), _p(w)), "knn_cos_f64")
     return idx, dist, w
 
 
@@ -254,6 +270,32 @@ def bc_knn(means, variances, k, reg=1e-6, thr=1e-9):
     w = np.empty((f, k), np.float32)
     _check(lib().or_bc_knn(_p(means), _p(variances), c, f, k, reg, thr, _p(idx), _p(w)), "bc_knn")
     return idx, w
+
+
+def bhattacharyya_distance(mean_i, var_i, mean_j, var_j):
+    """distance.rs:78-108 bhattacharyya_distance_diagonal (f32)."""
+    a = [np.ascontiguousarray(v, np.float32) for v in (mean_i, var_i, mean_j, var_j)]
+    return np.float32(lib().or_bhattacharyya_distance(*[_p(v) for v in a], a[0].shape[0]))
+
+
+MST_BHATTACHARYYA, MST_EUCLIDEAN, MST_SQEUCLIDEAN = 0, 1, 2
+TW_MEAN, TW_MIN, TW_MAX, TW_GEOMEAN, TW_NONE = 0, 1, 2, 3, 4
+
+
+def mst_candidates(means, variances, k, metric=MST_BHATTACHARYYA, tw=TW_MEAN, thickness=None):
+    """MSTStage::build_candidate_graph (mst.rs:312-412): (v, dist, cost) [c, k']."""
+    means = np.ascontiguousarray(means, np.float32)
+    c, f = means.shape
+    variances = None if variances is None else np.ascontiguousarray(variances, np.float32)
+    th = None if thickness is None else np.ascontiguousarray(thickness, np.float32)
+    kk = min(k, c - 1)
+    v = np.empty((c, kk), np.int32)
+    d = np.empty((c, kk), np.float32)
+    cost = np.empty((c, kk), np.float32)
+    _check(lib().or_mst_candidates(_p(means), None if variances is None else _p(variances), c, f,
+                                   k, metric, tw, None if th is None else _p(th), _p(v), _p(d),
+                                   _p(cost)), "mst_candidates")
+    return v, d, cost
 
 
 def diffuse_rows(X, indptr, indices, values, eta=0.1, steps=4, matvec=False):

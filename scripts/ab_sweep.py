@@ -1,0 +1,52 @@
+"""A/B of the two phase-2 sweep kernels (MN_X1_SWEEP=1 gram_sweep.hpp vs 2
+gram_sweep2.hpp) in ONE process on the same device and data (guide rule 24):
+C2 shape by default, interleaved rounds, outputs compared bit for bit.
+  python scripts/ab_sweep.py [n] [d] [rounds]"""
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "matternet-rs_amd")]
+import torch  # noqa: E402
+
+import surfface_hip as S  # noqa: E402
+from surfface_hip import _lib  # noqa: E402
+
+n = int(sys.argv[1]) if len(sys.argv) > 1 else 1_000_000
+d = int(sys.argv[2]) if len(sys.argv) > 2 else 768
+rounds = int(sys.argv[3]) if len(sys.argv) > 3 else 2
+X = torch.empty((n, d), dtype=torch.float32, device="cuda")
+_lib.check(_lib.lib().mn_fill_uniform_f32(X.data_ptr(), n, d, 42, 0, None))
+torch.cuda.synchronize()
+ref = None
+res = {1: [], 2: []}
+probe = {1: [], 2: []}
+for r in range(rounds):
+    for v in (1, 2):
+        os.environ["MN_X1_SWEEP"] = str(v)
+        os.environ.pop("MN_X1_PROBE", None)
+        t = time.time()
+        out = S.knn_l2sq(X, 32, timing=True, algo="bf16x1")
+        torch.cuda.synchronize()
+        st = out.stats
+        res[v].append({"ms_sweep": round(st["ms_sweep"], 2), "ms_total": round(st["ms_total"], 2),
+                       "n_cand": st["n_candidates"], "unc": st["n_uncertified"],
+                       "esc": st["n_escalated"], "wall": round(time.time() - t, 3)})
+        if ref is None:
+            ref = (out.idx.clone(), out.dist.clone())
+        else:
+            same = torch.equal(ref[0], out.idx) and torch.equal(ref[1].view(torch.int32),
+                                                                 out.dist.view(torch.int32))
+            res[v][-1]["same_as_first"] = bool(same)
+        del out
+        os.environ["MN_X1_PROBE"] = "noepi"
+        S.knn_l2sq(X, 32, timing=True, algo="bf16x1")
+        st = S.knn.last_stats()
+        probe[v].append(round(st["ms_sweep"], 2))
+        os.environ.pop("MN_X1_PROBE", None)
+        print(json.dumps({"round": r, "v": v, **res[v][-1], "probe_ms": probe[v][-1]}), flush=True)
+flop = 2.0 * n * (n - res[2][-1].get("sample_rows", 0)) * d
+print(json.dumps({"summary": {v: min(x["ms_sweep"] for x in res[v]) for v in (1, 2)},
+                  "probe": {v: min(probe[v]) for v in (1, 2)}}))

@@ -183,7 +183,10 @@ def test_euclidean_metric_sqrt_is_correctly_rounded(algo_e):
     np.testing.assert_array_equal(r.dist.cpu().numpy().view(np.uint32),
                                   np.sqrt(rdist).view(np.uint32))
     # candidate-graph mirror (mst.rs:312-363) with the Euclidean metric
-    u, v, dist = S.build_candidate_graph(X, 12, S.DistanceMetric.Euclidean)
-    np.testing.assert_array_equal(v.cpu().numpy(), ridx.reshape(-1))
-    np.testing.assert_array_equal(dist.cpu().numpy().view(np.uint32),
+    e = S.build_candidate_graph(X, None, 12, S.DistanceMetric.Euclidean,
+                                S.ThicknessWeight.NoWeight, thickness=np.ones(len(X), np.float32))
+    np.testing.assert_array_equal(e.v.cpu().numpy(), ridx.reshape(-1))
+    np.testing.assert_array_equal(e.distance.cpu().numpy().view(np.uint32),
                                   np.sqrt(rdist).reshape(-1).view(np.uint32))
+    np.testing.assert_array_equal(e.cost.cpu().numpy().view(np.uint32),
+                                  e.distance.cpu().numpy().view(np.uint32))

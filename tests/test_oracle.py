@@ -375,3 +375,97 @@ def test_energy_rows_faithful_equals_csr_restatement():
     e2, g2, l2 = O.energy_rows_faithful(X, ip, ix, iv, O.TAU_MEDIAN)
     for a, b in ((e1, e2), (g1, g2), (l1, l2)):
         np.testing.assert_array_equal(a.view(np.uint64), b.view(np.uint64))
+
+
+# ---- MST candidate graph (mst.rs:312-412, distance.rs:78-108) -------------
+
+def _bd_python(mi, vi, mj, vj):
+    """Independent scalar restatement of bhattacharyya_distance_diagonal
+    (distance.rs:78-108) in numpy float32 (math.log of the f32 value, rounded
+    to f32: correctly rounded ln)."""
+    f32 = np.float32
+    eps = f32(1e-10)
+    dist = f32(0.0)
+    for k in range(len(mi)):
+        si = max(f32(vi[k]), eps)
+        sj = max(f32(vj[k]), eps)
+        ss = f32(si + sj)
+        sp = f32(si * sj)
+        md = f32(f32(mi[k]) - f32(mj[k]))
+        mahal = f32(f32(f32(0.25) * f32(md * md)) / ss)
+        r = max(f32(ss / f32(f32(2.0) * np.sqrt(sp))), eps)
+        lt = f32(f32(0.25) * f32(math.log(float(r))))
+        dist = f32(dist + f32(mahal + lt))
+    return dist
+
+
+def test_bhattacharyya_distance_known_answers():
+    """test_distance.rs:9-60: identical distributions -> 0 (asserted < 1e-5),
+    different means / variances -> > 0; the exact values follow from the
+    formula: means 0 vs 1 at var 1 -> 2 x 0.125; var 0.5 vs 2 -> 2 x ln(1.25)/4."""
+    z = O.bhattacharyya_distance([1, 2, 3], [0.5] * 3, [1, 2, 3], [0.5] * 3)
+    assert z == np.float32(0.0)
+    assert O.bhattacharyya_distance([0, 0], [1, 1], [1, 1], [1, 1]) == np.float32(0.25)
+    dv = O.bhattacharyya_distance([0, 0], [0.5, 0.5], [0, 0], [2.0, 2.0])
+    t = np.float32(np.float32(0.25) * np.float32(math.log(1.25)))
+    assert dv == np.float32(t + t) and dv > 0
+    # test_bhattacharyya_slice_vs_tensor (test_distance.rs:62-88): the slice
+    # value agrees with the tensor formula (f64 here) within 1e-4
+    mi, mj, vi, vj = [1.0, 2.0, 3.0], [1.5, 2.5, 3.5], [0.5] * 3, [0.6] * 3
+    # tensor form (distance.rs:28-61): 0.25 md^2/ss + 0.25 ln(ss / (2 sqrt(sp)))
+    ref = sum(0.25 * (a - b) ** 2 / (x + y) + 0.25 * math.log((x + y) / (2 * math.sqrt(x * y)))
+              for a, b, x, y in zip(mi, mj, vi, vj))
+    s = O.bhattacharyya_distance(mi, vi, mj, vj)
+    assert abs(float(s) - ref) < 1e-4
+
+
+def test_bhattacharyya_oracle_vs_python_restatement():
+    rng = np.random.default_rng(5)
+    for f in (1, 7, 33):
+        for _ in range(40):
+            mi, mj = rng.normal(size=f).astype(np.float32), rng.normal(size=f).astype(np.float32)
+            vi = np.abs(rng.normal(size=f)).astype(np.float32)
+            vj = np.abs(rng.normal(size=f)).astype(np.float32)
+            vi[rng.random(f) < 0.1] = 0.0  # floored to 1e-10
+            a = O.bhattacharyya_distance(mi, vi, mj, vj)
+            b = _bd_python(mi, vi, mj, vj)
+            # glibc logf vs correctly rounded ln: equal but for rare ulp terms
+            assert abs(float(a) - float(b)) <= 4e-6 * max(1.0, abs(float(b)))
+
+
+def test_mst_candidates_oracle_semantics():
+    """mst.rs:312-412 on a small case: stable (dist, j) order, k = min(k, C-1),
+    thickness = mean variance (test_thickness_weight_functions' centroids:
+    equal means, per-row constant variances), every ThicknessWeight."""
+    means = np.ones((4, 3), np.float32)
+    var = np.repeat(np.array([[0.5], [1.0], [0.2], [0.8]], np.float32), 3, axis=1)
+    th = var.mean(axis=1).astype(np.float32)
+    for tw in range(5):
+        v, d, cost = O.mst_candidates(means, var, 3, O.MST_BHATTACHARYYA, tw)
+        assert v.shape == (4, 3)
+        for i in range(4):
+            dd = [(_bd_python(means[i], var[i], means[j], var[j]), j) for j in range(4) if j != i]
+            dd.sort(key=lambda t: (t[0], t[1]))
+            assert list(v[i]) == [j for _, j in dd]
+            for r, (dv, j) in enumerate(dd):
+                assert abs(float(d[i, r]) - float(dv)) <= 1e-6
+                ti, tj = th[i], th[j]
+                phi = [np.float32((ti + tj) / np.float32(2)), min(ti, tj), max(ti, tj),
+                       np.sqrt(np.float32(ti * tj)), None][tw]
+                want = d[i, r] if phi is None else np.float32(d[i, r] * phi)
+                assert cost[i, r] == want
+    # duplicates tie at distance 0 -> j ascending; k > C-1 truncates
+    m2 = np.zeros((5, 2), np.float32)
+    v2, d2, _ = O.mst_candidates(m2, np.ones((5, 2), np.float32), 10, O.MST_BHATTACHARYYA, 4)
+    assert v2.shape == (5, 4) and (d2 == 0).all()
+    assert [list(r) for r in v2] == [[j for j in range(5) if j != i] for i in range(5)]
+    # L2 metrics agree with the kNN oracle
+    X = datagen.uniform(300, 12, seed=3)
+    v3, d3, c3 = O.mst_candidates(X, None, 7, O.MST_SQEUCLIDEAN, 4,
+                                  thickness=np.ones(300, np.float32))
+    ridx, rdist = O.knn_l2sq(X, 7)
+    assert np.array_equal(v3, ridx) and np.array_equal(d3.view(np.uint32), rdist.view(np.uint32))
+    v4, d4, _ = O.mst_candidates(X, None, 7, O.MST_EUCLIDEAN, 4,
+                                 thickness=np.ones(300, np.float32))
+    assert np.array_equal(v4, ridx)
+    assert np.array_equal(d4.view(np.uint32), np.sqrt(rdist).view(np.uint32))
