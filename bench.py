@@ -35,6 +35,7 @@ BF16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X dense bf16 (MI355X_MICROARCH.md), no sp
 # scripts/probes/probe_mfma_peak.hip on the box (profiles/r02_mfma_peak.txt):
 # the sustained 32x32x16 bf16 rate on random operands under load (DVFS)
 MEASURED_BF16_32X32_TFLOPS = 1887.0
+MEASURED_BF16_16X16X32_TFLOPS = 2113.0  # same probe, v_mfma_f32_16x16x32_bf16 (the sweep's shape)
 FP64_VALU_PEAK_TFLOPS = 78.6
 
 
@@ -175,11 +176,11 @@ def main():
     gms = float(np.mean(gram_ms)) if gram_ms else float("nan")
     algo = st0.get("algo")
     if algo == 3:
-        # two-phase single-bf16 generator: phase 2 (k_gram_sweep) sweeps the
+        # two-phase single-bf16 generator: phase 2 (k_gram_sweep2) sweeps the
         # rows outside the phase-1 sample, one bf16 product per f32 product
         m0 = int(st0.get("sample_rows") or 0)
         nc_sw = n_loc - m0
-        kname = "k_gram_sweep"
+        kname = "k_gram_sweep2" if os.environ.get("MN_X1_SWEEP", "2") != "1" else "k_gram_sweep"
         flops_launch = 2.0 * nq * nc_sw * d
         achieved = flops_launch / (gms * 1e-3) / 1e12
         ms_all = float(st0["ms_gram"])
@@ -187,12 +188,13 @@ def main():
                 "peak": BF16_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                 "frac": round(achieved / BF16_MFMA_PEAK_TFLOPS, 4),
                 "traffic": None, "ms_per_launch": round(gms, 3), "flop_per_launch": flops_launch,
-                "peak_basis": "dense bf16 MFMA 2500 TFLOP/s (one v_mfma_f32_32x32x16_bf16 product "
+                "peak_basis": "dense bf16 MFMA 2500 TFLOP/s (one v_mfma_f32_16x16x32_bf16 product "
                               "per f32 product: x ~ bf16(x), certified by the residual-norm bound)",
-                "measured_mfma_ceiling": {"tflops": MEASURED_BF16_32X32_TFLOPS,
-                                          "frac": round(achieved / MEASURED_BF16_32X32_TFLOPS, 4),
-                                          "basis": "probe_mfma_peak.hip: back-to-back "
-                                                   "v_mfma_f32_32x32x16_bf16 on random register "
+                "measured_mfma_ceiling": {"tflops": MEASURED_BF16_16X16X32_TFLOPS,
+                                          "frac": round(achieved / MEASURED_BF16_16X16X32_TFLOPS, 4),
+                                          "basis": "scripts/probes/probe_mfma_peak.hip "
+                                                   "(profiles/r02_mfma_peak.txt): back-to-back "
+                                                   "v_mfma_f32_16x16x32_bf16 on random register "
                                                    "operands, every CU (DVFS-limited clock)"},
                 "whole_gram": {"ms": round(ms_all, 3), "sample_ms": round(st0["ms_sample"], 3),
                                "sample_rows": m0,

@@ -208,6 +208,17 @@ int mn_bc_knn_f32(const float *means, const float *vars, int64_t c, int32_t f, i
  * ulp-level terms); C <= 65536, k <= 512.  MN_MST_EUCLIDEAN /
  * MN_MST_SQEUCLIDEAN run mn_knn_f32 (bit-exact).  MN_ENONFINITE on a NaN
  * distance (the reference's partial_cmp().unwrap()). */
+/* Clustering stage, batch nearest centroid (surfface-pipeline/src/stages/
+ * clustering.rs:42-63): per item of batch [b][f] the nearest of the c
+ * centroids [c][f] (device, f32) by sqrt((|x|^2 + |c|^2) - 2 x.c), out_idx /
+ * out_dist [b] (first index of the minimum; NaN distances never win).  The
+ * reference's Burn reductions have a backend-defined order (parity-unpinned):
+ * here sequential f32 folds over the features, correctly rounded sqrt —
+ * bit-exact against the oracle's restatement of that order.  The incremental
+ * centroid creation (:65-88) stays on the host, as in the reference. */
+int mn_nearest_centroid_f32(const float *batch, int64_t b, const float *centroids, int64_t c,
+                            int32_t f, int32_t *out_idx, float *out_dist, void *stream);
+
 enum mn_mst_metric {
     MN_MST_BHATTACHARYYA = 0,
     MN_MST_EUCLIDEAN = 1,

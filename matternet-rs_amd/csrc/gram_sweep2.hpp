@@ -76,6 +76,9 @@ __device__ __forceinline__ int xcd_remap(int orig, int nwg) {
 // in S slices of `chunk` rows (a multiple of BC).  tq / tau0 [nq], hc [nc].
 // Per (query, slice): buf[(q*S + s)*cap + i] = (key bits, global corpus id),
 // cnt[q*S + s] = entries (-1: overflow).  PROBE = 1: K loop only (timing).
+// A tile's epilogue (candidate check + next accumulator init) runs in the
+// wave's read window (fusing the init into the first MFMA window measured
+// equal within noise: 1240-1274 vs 1271 ms at C2).
 template <int PROBE>
 __global__ __launch_bounds__(NT) void k_gram_sweep2(
     const uint16_t *__restrict__ Qk, int64_t nq, const uint16_t *__restrict__ Ck, int64_t nc,
@@ -199,49 +202,49 @@ __global__ __launch_bounds__(NT) void k_gram_sweep2(
     // Per 16 x 16 fragment one max and one ballot (wave-uniform branch); the
     // staging body runs only for fragments where some lane has a candidate
     // (a few per wave and tile at the C2 threshold).
-    auto check = [&](int ct0) {
-        if constexpr (PROBE == 0) {
-            // (global ids fit int32: the outputs are int32 ids)
-            const int cg0 = (int)c_off + ct0 + 128 * wc + 4 * fk;
+    // one 16 x 16 fragment: per-fragment max + ballot (wave-uniform branch);
+    // the staging body runs only where some lane has a candidate
+    auto check_block = [&](int f, int g, int ct0) {
+        const f32x4 a = acc[f][g];
+        const float m4 = fmaxf(fmaxf(a[0], a[1]), fmaxf(a[2], a[3]));
+        if (__builtin_expect(__ballot(m4 > 0.f) == 0, 1)) return;
+        const int ql = 64 * wq + 16 * f + fr;
+        const int qgl = (int)q_off + q0 + ql;  // (global ids fit int32: the outputs are int32)
+        const int c = (int)c_off + ct0 + 128 * wc + 16 * g + 4 * fk;  // id of register 0
+        unsigned pm = 0;
 #pragma unroll
-            for (int f = 0; f < WQF; ++f) {
-                const int ql = 64 * wq + 16 * f + fr;
-                const int qgl = (int)q_off + q0 + ql;
-#pragma unroll
-                for (int g = 0; g < WCF; ++g) {
-                    const f32x4 a = acc[f][g];
-                    const float m4 = fmaxf(fmaxf(a[0], a[1]), fmaxf(a[2], a[3]));
-                    if (__builtin_expect(__ballot(m4 > 0.f) == 0, 1)) continue;
-                    unsigned pm = 0;
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) pm |= a[r] > 0.f ? (1u << r) : 0u;
-                    const int c = cg0 + 16 * g;  // corpus id of register 0
-                    if (excl && (unsigned)(qgl - c) < 4u) pm &= ~(1u << (qgl - c));
-                    if (pm != 0) {
-                        const int mine = __popc(pm);
-                        int pos = atomicAdd(&sm.qcnt[ql], mine);
-                        int e = atomicAdd(&sm.scnt[w], mine);
-                        const float t0l = sm.t0[ql];
-                        while (pm) {
-                            const int r = __builtin_ctz(pm);
-                            pm &= pm - 1;
-                            const uint2 kv = make_uint2(__float_as_uint(t0l - 2.f * a[r]),
-                                                        (uint32_t)(c + r));
-                            if (pos < cap) {
-                                if (e < SCAP) {
-                                    sm.stk[w][e] = kv;
-                                    sm.stp[w][e] = (uint32_t)ql | ((uint32_t)pos << 8);
-                                } else {  // area full: straight out (rare)
-                                    buf[((int64_t)(q0 + ql) * S + sl) * cap + pos] = kv;
-                                    dirty = true;
-                                }
-                            }
-                            ++e;
-                            ++pos;
-                        }
+        for (int r = 0; r < 4; ++r) pm |= a[r] > 0.f ? (1u << r) : 0u;
+        if (excl && (unsigned)(qgl - c) < 4u) pm &= ~(1u << (qgl - c));
+        if (pm != 0) {
+            const int mine = __popc(pm);
+            int pos = atomicAdd(&sm.qcnt[ql], mine);
+            int e = atomicAdd(&sm.scnt[w], mine);
+            const float t0l = sm.t0[ql];
+            while (pm) {
+                const int r = __builtin_ctz(pm);
+                pm &= pm - 1;
+                const uint2 kv = make_uint2(__float_as_uint(t0l - 2.f * a[r]), (uint32_t)(c + r));
+                if (pos < cap) {
+                    if (e < SCAP) {
+                        sm.stk[w][e] = kv;
+                        sm.stp[w][e] = (uint32_t)ql | ((uint32_t)pos << 8);
+                    } else {  // area full: straight out (rare)
+                        buf[((int64_t)(q0 + ql) * S + sl) * cap + pos] = kv;
+                        dirty = true;
                     }
                 }
+                ++e;
+                ++pos;
             }
+        }
+    };
+    // candidates of the tile starting at corpus row ct0: positive accumulators
+    auto check = [&](int ct0) {
+        if constexpr (PROBE == 0) {
+#pragma unroll
+            for (int f = 0; f < WQF; ++f)
+#pragma unroll
+                for (int g = 0; g < WCF; ++g) check_block(f, g, ct0);
             // wave-uniform: spill the area once it is 3/4 full (or overran)
             if (sm.scnt[w] >= SCAP * 3 / 4) flush();
         } else {
@@ -253,7 +256,6 @@ __global__ __launch_bounds__(NT) void k_gram_sweep2(
             if (sum == 12345.678f) sm.qcnt[0] = 1;
         }
     };
-
     // ---- prologue: k-steps 0, 1, 2 in flight; k-step 0 landed everywhere
     issue();
     issue();

@@ -5,7 +5,8 @@ Every op runs on the GPU through the C ABI; there is no CPU fallback.
 """
 from . import _lib
 from ._lib import MnError, lib
-from . import energy, graph, l2f64, laplacian, search, sorted_index, sparsification
+from . import clustering, energy, graph, l2f64, laplacian, search, sorted_index, sparsification
+from .clustering import ClusteringOutput, ClusteringStage, nearest_centroid
 from .graph import (BuilderParams, EigenMaps, GraphFactory, GraphLaplacian, SparsityError,
                     build_laplacian_matrix, standardize_columns)
 from .l2f64 import (estimate_intrinsic_dimension, knn_l2_f64, nearest_subcentroid,
@@ -25,7 +26,8 @@ from .knn import (CandidateEdges, DistanceMetric, MSTConfig, ThicknessWeight, Kn
                   knn_cos_bf16_qc, knn_cos_columns, knn_l2sq,
                   knn_l2sq_qc, last_stats, merge_parts)
 
-__all__ = ["MnError", "lib", "graph", "BuilderParams", "EigenMaps", "GraphFactory",
+__all__ = ["MnError", "lib", "clustering", "ClusteringOutput", "ClusteringStage",
+           "nearest_centroid", "graph", "BuilderParams", "EigenMaps", "GraphFactory",
            "GraphLaplacian", "SparsityError", "build_laplacian_matrix", "standardize_columns", "knn_cos_columns", "knn_cos_bf16", "knn_cos_bf16_qc", "bf16_last_stats", "DistanceMetric", "MSTConfig", "ThicknessWeight", "CandidateEdges", "KnnResult", "build_candidate_graph", "knn_l2sq",
            "knn_l2sq_qc", "last_stats", "merge_parts", "CsrMatrix", "GraphParams",
            "LaplacianConfig", "LaplacianOutput", "build_laplacian_from_knn",

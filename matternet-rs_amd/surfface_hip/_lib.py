@@ -127,6 +127,7 @@ SIGNATURES = {
     "mn_diffuse_rows": (C.c_int, [C.POINTER(Csr), P, I32, I64, I32, C.c_double, I32, P, P]),
     "mn_energy_signals": (C.c_int, [C.POINTER(Csr), P, I64, I32, I32, P, P, P]),
     "mn_bc_knn_f32": (C.c_int, [P, P, I64, I32, I32, C.c_float, C.c_float, P, P, P]),
+    "mn_nearest_centroid_f32": (C.c_int, [P, I64, P, I64, I32, P, P, P]),
     "mn_mst_candidate_graph_f32": (C.c_int, [P, P, I64, I32, I32, I32, I32, P, P, P, P, P, P]),
     "mn_laplacian_matvec_rows": (C.c_int, [C.POINTER(Csr), P, I32, I64, I32, P, P]),
     "mn_normalise_lambdas": (C.c_int, [P, I64, P, P]),

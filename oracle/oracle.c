@@ -1065,6 +1065,37 @@ int or_mst_candidates(const float *means, const float *vars, int64_t c, int32_t 
     return err;
 }
 
+int or_nearest_centroid(const float *batch, int64_t b, const float *cents, int64_t c, int32_t f,
+                        int32_t *out_idx, float *out_dist) {
+    if (!batch || !cents || !out_idx || !out_dist || b < 1 || c < 1 || f < 1) return OR_EINVAL;
+    float *cn = (float *)malloc(sizeof(float) * (size_t)c);
+    if (!cn) return OR_ENOMEM;
+    for (int64_t j = 0; j < c; ++j) {
+        float s = 0.0f;
+        for (int32_t t = 0; t < f; ++t) s = s + cents[j * f + t] * cents[j * f + t];
+        cn[j] = s;
+    }
+#pragma omp parallel for schedule(static)
+    for (int64_t i = 0; i < b; ++i) {
+        const float *x = batch + i * f;
+        float bn = 0.0f;
+        for (int32_t t = 0; t < f; ++t) bn = bn + x[t] * x[t];
+        float best = NAN, first = NAN;
+        int32_t bj = -1;
+        for (int64_t j = 0; j < c; ++j) {
+            float dot = 0.0f;
+            for (int32_t t = 0; t < f; ++t) dot = dot + x[t] * cents[j * f + t];
+            const float dd = sqrtf((bn + cn[j]) - 2.0f * dot);
+            if (j == 0) first = dd;
+            if (dd == dd && (bj < 0 || dd < best)) { best = dd; bj = (int32_t)j; }
+        }
+        out_idx[i] = bj < 0 ? 0 : bj;
+        out_dist[i] = bj < 0 ? first : best;
+    }
+    free(cn);
+    return 0;
+}
+
 typedef struct { float w; int32_t j; } bcent;
 static int cmp_bcent(const void *pa, const void *pb) {
     const bcent *a = (const bcent *)pa, *b = (const bcent *)pb;

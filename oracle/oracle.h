@@ -241,6 +241,14 @@ int or_mst_candidates(const float *means, const float *vars, int64_t c, int32_t 
                       int metric, int tw, const float *thickness, int32_t *out_v,
                       float *out_dist, float *out_cost);
 
+/* surfface-pipeline/src/stages/clustering.rs:42-63 batch nearest centroid,
+ * in the fixed order of mn_nearest_centroid_f32 (Burn's is backend-defined:
+ * parity-unpinned): sequential f32 |x|^2, |c|^2 and x.c folds,
+ * sqrtf((bx + bc) - 2 dot), first index of the minimum, NaN never wins
+ * (an all-NaN row: index 0 and its NaN). */
+int or_nearest_centroid(const float *batch, int64_t b, const float *cents, int64_t c, int32_t f,
+                        int32_t *out_idx, float *out_dist);
+
 /* ---- K5: SF-GRASS ------------------------------------------------------- */
 
 /* src_legacy/sparsification.rs:32-113: avg = sum len / n; avg < 10 => copy;

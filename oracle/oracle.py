@@ -64,6 +64,7 @@ def _declare(L):
     L.or_bc_knn.argtypes = [P, P, I64, I32, I32, C.c_float, C.c_float, P, P]
     L.or_bhattacharyya_distance.argtypes = [P, P, P, P, I64]
     L.or_bhattacharyya_distance.restype = C.c_float
+    L.or_nearest_centroid.argtypes = [P, I64, P, I64, I32, P, P]
     L.or_mst_candidates.argtypes = [P, P, I64, I32, I32, C.c_int, C.c_int, P, P, P, P]
     L.or_diffuse_rows.argtypes = [P, I64, I32, P, P, P, C.c_double, I32, C.c_int, P]
     L.or_range_bylambda.argtypes = [P, P, I64, C.c_double, C.c_double, I64, C.c_double, P, P]
@@ -296,6 +297,18 @@ def mst_candidates(means, variances, k, metric=MST_BHATTACHARYYA, tw=TW_MEAN, th
                                    k, metric, tw, None if th is None else _p(th), _p(v), _p(d),
                                    _p(cost)), "mst_candidates")
     return v, d, cost
+
+
+def nearest_centroid(batch, cents):
+    """stages/clustering.rs:42-63 batch nearest centroid (fixed-order restatement)."""
+    batch = np.ascontiguousarray(batch, np.float32)
+    cents = np.ascontiguousarray(cents, np.float32)
+    b, f = batch.shape
+    idx = np.empty(b, np.int32)
+    dist = np.empty(b, np.float32)
+    _check(lib().or_nearest_centroid(_p(batch), b, _p(cents), cents.shape[0], f, _p(idx),
+                                     _p(dist)), "nearest_centroid")
+    return idx, dist
 
 
 def diffuse_rows(X, indptr, indices, values, eta=0.1, steps=4, matvec=False):

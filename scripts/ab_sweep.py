@@ -21,10 +21,11 @@ X = torch.empty((n, d), dtype=torch.float32, device="cuda")
 _lib.check(_lib.lib().mn_fill_uniform_f32(X.data_ptr(), n, d, 42, 0, None))
 torch.cuda.synchronize()
 ref = None
-res = {1: [], 2: []}
-probe = {1: [], 2: []}
+VERS = [int(v) for v in os.environ.get("AB_VERSIONS", "1,2").split(",")]
+res = {v: [] for v in VERS}
+probe = {v: [] for v in VERS}
 for r in range(rounds):
-    for v in (1, 2):
+    for v in VERS:
         os.environ["MN_X1_SWEEP"] = str(v)
         os.environ.pop("MN_X1_PROBE", None)
         t = time.time()
@@ -47,6 +48,5 @@ for r in range(rounds):
         probe[v].append(round(st["ms_sweep"], 2))
         os.environ.pop("MN_X1_PROBE", None)
         print(json.dumps({"round": r, "v": v, **res[v][-1], "probe_ms": probe[v][-1]}), flush=True)
-flop = 2.0 * n * (n - res[2][-1].get("sample_rows", 0)) * d
-print(json.dumps({"summary": {v: min(x["ms_sweep"] for x in res[v]) for v in (1, 2)},
-                  "probe": {v: min(probe[v]) for v in (1, 2)}}))
+print(json.dumps({"summary": {v: min(x["ms_sweep"] for x in res[v]) for v in VERS},
+                  "probe": {v: min(probe[v]) for v in VERS}}))

@@ -469,3 +469,13 @@ def test_mst_candidates_oracle_semantics():
                                  thickness=np.ones(300, np.float32))
     assert np.array_equal(v4, ridx)
     assert np.array_equal(d4.view(np.uint32), np.sqrt(rdist).view(np.uint32))
+
+
+def test_nearest_centroid_oracle_known_answers():
+    """stages/clustering.rs:42-63 on exact small integers: d = sqrt(|x|^2 +
+    |c|^2 - 2 x.c); ties take the first centroid."""
+    cents = np.array([[0, 0], [3, 4], [0, 0]], np.float32)
+    batch = np.array([[0, 0], [3, 4], [1, 0], [6, 8]], np.float32)
+    idx, dist = O.nearest_centroid(batch, cents)
+    assert idx.tolist() == [0, 1, 0, 1]
+    assert dist.tolist() == [0.0, 0.0, 1.0, 5.0]
