@@ -1551,6 +1551,8 @@ static int knn_x1(const float *Q, int64_t nq, const float *C, int64_t nc, int32_
     // phase-1 sample: the first m0 corpus rows, list length L1 (tau0 ~ the
     // (L1 nc / m0)-th best key); small corpora run phase 1 alone (m0 = nc)
     int L1 = std::min(std::max((k + 1) / 2, 16), 48);
+    const char *fl = getenv("MN_X1_L1");  // experiments: phase-1 list length
+    if (fl && *fl) L1 = std::min(std::max(atoi(fl), 4), 48);
     const char *fs = getenv("MN_X1_SAMPLE_DIV");  // experiments: sample = nc / div
     const int64_t div = (fs && *fs) ? std::max(2, atoi(fs)) : 16;
     int64_t m0 = std::max<int64_t>(nc / div, (int64_t)64 * L1);
