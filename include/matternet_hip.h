@@ -88,7 +88,8 @@ enum mn_knn_algo {
 
 typedef struct mn_knn_stats {
     int64_t n_queries;
-    int64_t n_uncertified;  /* rows resolved by the exact fallback scan         */
+    int64_t n_uncertified;  /* rows no certificate settled (resolved by a batched
+                               split-generator pass or the exact scan)        */
     int32_t slices;         /* corpus split factor used                         */
     int32_t list_len;       /* L = k + margin                                   */
     float ms_norms, ms_gram, ms_rerank, ms_fallback, ms_total; /* timing == 1   */

@@ -14,7 +14,7 @@
 //    from LDS and issues its LDS-DMA pieces, so the MFMA pipe never waits on
 //    LDS latency or on the barrier itself.
 //  * 4-slot LDS ring of 32-deep k-steps (both operands, 32 KB per slot), each
-//    k-step issued 3 ahead by LDS-DMA (`global_load_lds_dwordx4`): a k-step
+//    k-step issued 3 ahead by LDS-DMA (`buffer_load_dwordx4 ... lds`): a k-step
 //    is read 6 windows after its DMA was issued; counted `vmcnt(8)` (never 0
 //    in the loop), raw `s_barrier`.
 //  * One KB32 row is 64 B (4 chunks of 16 B); a 16x16x32 fragment read is 16
@@ -75,7 +75,10 @@ __device__ __forceinline__ int xcd_remap(int orig, int nwg) {
 // Qk [nkb][nq][32], Ck [nkb][nc][32] (KB32 bf16).  Corpus rows [c_begin, nc)
 // in S slices of `chunk` rows (a multiple of BC).  tq / tau0 [nq], hc [nc].
 // Per (query, slice): buf[(q*S + s)*cap + i] = (key bits, global corpus id),
-// cnt[q*S + s] = entries (-1: overflow).  PROBE = 1: K loop only (timing).
+// cnt[q*S + s] = entries (-1: overflow).  PROBE = 1: K loop only (timing);
+// diagnostics (results invalid): PROBE = 2 also without the in-loop LDS-DMA
+// issue, PROBE = 3 also without the fragment reads, PROBE = 4 with the DMA
+// issued but never waited for.
 // A tile's epilogue (candidate check + next accumulator init) runs in the
 // wave's read window (fusing the init into the first MFMA window measured
 // equal within noise: 1240-1274 vs 1271 ms at C2).
@@ -119,20 +122,34 @@ __global__ __launch_bounds__(NT) void k_gram_sweep2(
     const int pch = 8 * ((lane & 3) ^ (((lane >> 5) & 1) << 1));  // source chunk (swizzle)
     const int qo0 = min(q0 + prow0, (int)nq - 1) * KB + pch;
     const int qo1 = min(q0 + prow1, (int)nq - 1) * KB + pch;
-    int co0 = min(bt0 + prow0, cend - 1) * KB + pch;
-    int co1 = min(bt0 + prow1, cend - 1) * KB + pch;
+    const int co0 = min(bt0 + prow0, cend - 1) * KB + pch;
+    const int co1 = min(bt0 + prow1, cend - 1) * KB + pch;
     const uint16_t *cbk = Ck, *qbk = Qk;
     const int cstep = (int)nc * KB, qstep = (int)nq * KB;
-    auto dma = [&](const uint16_t *src, uint16_t *lds) {
-        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)src,
-                                         (__attribute__((address_space(3))) void *)lds, 16, 0, 0);
+    // LDS-DMA through buffer descriptors: one k-block region ([n][32] bf16,
+    // 64-B rows) per descriptor, rebuilt from wave-uniform values per k-step
+    // (SALU only); the per-lane 32-bit byte offsets (co*/qo* x 2) are fixed per
+    // tile, so a piece costs no VALU address arithmetic and no VGPR reuse
+    // hazard (the flat-address form serialised the four pieces on one
+    // 64-bit address register)
+    const int qb0 = 2 * qo0, qb1 = 2 * qo1;
+    int cb0 = 2 * co0, cb1 = 2 * co1;
+    // (nc * 32, nq * 32 < 2^31 is checked by the driver: the byte counts fit 32 bits)
+    const int cbytes = (int)(uint32_t)(nc * 64), qbytes = (int)(uint32_t)(nq * 64);
+    auto dma = [&](__amdgpu_buffer_rsrc_t rs, int voff, uint16_t *lds) {
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void *)lds,
+                                                 16, voff, 0, 0, 0);
     };
     auto issue = [&]() {
         if (bt0 < cend) {
-            dma(cbk + co0, &sm.C[bslot][32 * w][0]);
-            dma(cbk + co1, &sm.C[bslot][32 * w + 16][0]);
-            dma(qbk + qo0, &sm.Q[bslot][32 * w][0]);
-            dma(qbk + qo1, &sm.Q[bslot][32 * w + 16][0]);
+            const __amdgpu_buffer_rsrc_t rc =
+                __builtin_amdgcn_make_buffer_rsrc((void *)cbk, (short)0, cbytes, 0x00020000);
+            const __amdgpu_buffer_rsrc_t rq =
+                __builtin_amdgcn_make_buffer_rsrc((void *)qbk, (short)0, qbytes, 0x00020000);
+            dma(rc, cb0, &sm.C[bslot][32 * w][0]);
+            dma(rc, cb1, &sm.C[bslot][32 * w + 16][0]);
+            dma(rq, qb0, &sm.Q[bslot][32 * w][0]);
+            dma(rq, qb1, &sm.Q[bslot][32 * w + 16][0]);
             bslot = (bslot + 1) & (NSLOT - 1);
             cbk += cstep;
             qbk += qstep;
@@ -141,8 +158,8 @@ __global__ __launch_bounds__(NT) void k_gram_sweep2(
                 bt0 += BC;
                 cbk = Ck;
                 qbk = Qk;
-                co0 = min(bt0 + prow0, cend - 1) * KB + pch;
-                co1 = min(bt0 + prow1, cend - 1) * KB + pch;
+                cb0 = 2 * (min(bt0 + prow0, cend - 1) * KB + pch);
+                cb1 = 2 * (min(bt0 + prow1, cend - 1) * KB + pch);
             }
         }
     };
@@ -281,21 +298,21 @@ __global__ __launch_bounds__(NT) void k_gram_sweep2(
             const float *p = hc + min(c0 + BC + 64 * wq + lane, (int)nc - 1);
             asm volatile("global_load_dword %0, %1, off" : "=v"(hcn) : "v"(p) : "memory");
         }
-        issue();  // k-step g + 3
+        if constexpr (PROBE < 2 || PROBE == 4) issue();  // k-step g + 3
         if (kb == 0 && g > 0) {
             // the previous tile's candidates, then this tile's accumulator
             // init (before the fragment reads: the fragments are dead here)
             check(c0 - BC);
             init_acc(par);
         }
-        read_frags((int)(g & (NSLOT - 1)));
+        if constexpr (PROBE < 3 || PROBE == 4) read_frags((int)(g & (NSLOT - 1)));
         if (kb == nkb - 2 && more && wc == 0) {
             // written 2 k-steps (>= 2 barriers) before init_acc reads it
             const int cb = c0 + BC + 64 * wq + lane;
             sm.hc[par ^ 1][64 * wq + lane] = cb < cend ? hcn : __builtin_inff();
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        if (wc == 1) {
+        if (PROBE != 4 && wc == 1) {
             // trailing group: k-step g+1 landed for the window after this one
             const int rem = gtot - 1 - g;
             if (dirty) MN_VMCNT(0);
@@ -312,7 +329,7 @@ __global__ __launch_bounds__(NT) void k_gram_sweep2(
         mfmas();
         __builtin_amdgcn_s_setprio(0);
         __builtin_amdgcn_sched_barrier(0);
-        if (wc == 0) {
+        if (PROBE != 4 && wc == 0) {
             const int rem = gtot - 1 - g;
             if (dirty) MN_VMCNT(0);
             else if (rem >= 3) MN_VMCNT(8);

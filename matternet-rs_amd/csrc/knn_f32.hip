@@ -1083,11 +1083,11 @@ __global__ __launch_bounds__(256) void k_sqrt_dist(float *__restrict__ dist, int
     }
 }
 
-// Escalation of rows the bf16x1 bound could not certify (dense clusters: the
-// bound scales with |q||c|, not with the neighbour distances): gather them,
-// run the split generator on them with k + 1 neighbours and self included,
-// then drop the query's own id (d = +0: it is in the k + 1 list unless > k
-// exact duplicates precede it, in which case the last entry goes).
+// Rows the bf16x1 path leaves uncertified (after its bf16x3 refill) against a
+// large corpus: gather them, run the split generator on them with k + 1
+// neighbours and self included, then drop the query's own id (d = +0: it is
+// in the k + 1 list unless > k exact duplicates precede it, in which case the
+// last entry goes).
 __global__ __launch_bounds__(256) void k_gather_rows(const float *__restrict__ X, int d,
                                                      const int *__restrict__ rows, int64_t n,
                                                      float *__restrict__ out) {
@@ -1605,14 +1605,21 @@ static int knn_x1(const float *Q, int64_t nq, const float *C, int64_t nc, int32_
         const int64_t grid = nqb * p2.S;
         MN_REQUIRE(grid < INT_MAX && nq * 32 < INT_MAX && nc * 32 < INT_MAX, MN_ENOTSUP,
                    "mn_knn: sweep grid too large (split the queries / corpus)");
-        const bool noepi = probe && !strcmp(probe, "noepi");
+        // timing probes: noepi = K loop only; nodma / noread = also without the
+        // in-loop DMA issue / fragment reads (diagnostics, results invalid)
+        const bool noepi = probe && (!strcmp(probe, "noepi") || !strcmp(probe, "nodma") ||
+                                     !strcmp(probe, "noread") || !strcmp(probe, "nowait"));
         if (sweep_version() == 1) {
             auto kern = noepi ? ksw::k_gram_sweep<1> : ksw::k_gram_sweep<0>;
             hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(ksw::NT), 0, s, QK, nq, CK, nc,
                                nkb, q_off, (int64_t)0, 0, tq, tau0, chc, m0, S2, p2.chunk, cap2,
                                cbuf2, cnt2);
         } else {
-            auto kern = noepi ? ksw2::k_gram_sweep2<1> : ksw2::k_gram_sweep2<0>;
+            auto kern = !noepi ? ksw2::k_gram_sweep2<0>
+                        : !strcmp(probe, "nodma") ? ksw2::k_gram_sweep2<2>
+                        : !strcmp(probe, "noread") ? ksw2::k_gram_sweep2<3>
+                        : !strcmp(probe, "nowait") ? ksw2::k_gram_sweep2<4>
+                                                   : ksw2::k_gram_sweep2<1>;
             hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(ksw2::NT), 0, s, QK, nq, CK, nc,
                                nkb, q_off, (int64_t)0, 0, tq, tau0, chc, m0, S2, p2.chunk, cap2,
                                cbuf2, cnt2);
@@ -1752,19 +1759,58 @@ static int knn_x1(const float *Q, int64_t nq, const float *C, int64_t nc, int32_
         t_stats.n_escalated = nfb;
         t_stats.ms_escalate = te.ms(0, 1);
     }
-    const unsigned fgrid = (unsigned)std::min<int64_t>(nq, 1024);
-    if (vec4)
-        hipLaunchKernelGGL(k_fallback<true>, dim3(fgrid), dim3(FB_THREADS), 0, s, Q, C, nc, d,
-                           q_off, c_off, excl, k, fb_count, fb_list, out_idx, out_dist);
-    else
-        hipLaunchKernelGGL(k_fallback<false>, dim3(fgrid), dim3(FB_THREADS), 0, s, Q, C, nc, d,
-                           q_off, c_off, excl, k, fb_count, fb_list, out_idx, out_dist);
-    MN_KCHECK(s, "k_fallback");
-    tm.mark();
-    int64_t hf[8] = {0};
-    MN_HIP_TRY(hipMemcpyAsync(hf, flags, 64, hipMemcpyDeviceToHost, s));
+    // rows still uncertified: against a large corpus, gather them and run the
+    // split generator (k + 1 neighbours, self included, then the query's own
+    // id dropped) — one batched, certified Gram pass instead of an O(nc d)
+    // exact scan per row on one CU (15 rows cost 228 ms that way at C2);
+    // small corpora keep the exact scan
+    int nfb2 = 0;
+    MN_HIP_TRY(hipMemcpyAsync(&nfb2, fb_count, 4, hipMemcpyDeviceToHost, s));
     MN_HIP_TRY(hipStreamSynchronize(s));
-    t_stats.n_uncertified = ((const int *)hf)[5];
+    if (nfb2 > 0 && nc >= (1 << 16) && k + 1 <= KMAX) {
+        int *rows = nullptr;
+        float *Qg = nullptr, *ed = nullptr;
+        int32_t *ei = nullptr;
+        MN_HIP_TRY(hipMalloc(&rows, sizeof(int) * (size_t)nfb2));
+        MN_HIP_TRY(hipMalloc(&Qg, sizeof(float) * (size_t)nfb2 * d));
+        MN_HIP_TRY(hipMalloc(&ei, sizeof(int32_t) * (size_t)nfb2 * (k + 1)));
+        MN_HIP_TRY(hipMalloc(&ed, sizeof(float) * (size_t)nfb2 * (k + 1)));
+        MN_HIP_TRY(hipMemcpyAsync(rows, fb_list, sizeof(int) * (size_t)nfb2,
+                                  hipMemcpyDeviceToDevice, s));
+        hipLaunchKernelGGL(k_gather_rows, dim3((unsigned)(((int64_t)nfb2 * d + 255) / 256)),
+                           dim3(256), 0, s, Q, d, rows, (int64_t)nfb2, Qg);
+        MN_KCHECK(s, "k_gather_rows");
+        mn_knn_opts o2 = *opts;
+        o2.k = k + 1;
+        o2.exclude_self = 0;
+        o2.metric = MN_L2SQ;
+        o2.timing = 0;
+        o2.algo = (k + 1 + margin <= kb16::LMAX) ? MN_KNN_BF16X3 : MN_KNN_F32;
+        const mn_knn_stats saved = t_stats;
+        const int rc = knn_f32_core(Qg, nfb2, C, nc, d, 0, c_off, &o2, ei, ed, o2.algo);
+        t_stats = saved;
+        if (rc == MN_OK) {
+            hipLaunchKernelGGL(k_scatter_escalated, dim3((unsigned)((nfb2 + 255) / 256)),
+                               dim3(256), 0, s, rows, (int64_t)nfb2, q_off, excl, k, ei, ed,
+                               out_idx, out_dist);
+            MN_KCHECK(s, "k_scatter_escalated");
+        }
+        MN_HIP_TRY(hipStreamSynchronize(s));
+        (void)hipFree(rows); (void)hipFree(Qg); (void)hipFree(ei); (void)hipFree(ed);
+        if (rc != MN_OK) return rc;
+    } else if (nfb2 > 0) {
+        const unsigned fgrid = (unsigned)std::min<int64_t>(nfb2, 1024);
+        if (vec4)
+            hipLaunchKernelGGL(k_fallback<true>, dim3(fgrid), dim3(FB_THREADS), 0, s, Q, C, nc, d,
+                               q_off, c_off, excl, k, fb_count, fb_list, out_idx, out_dist);
+        else
+            hipLaunchKernelGGL(k_fallback<false>, dim3(fgrid), dim3(FB_THREADS), 0, s, Q, C, nc,
+                               d, q_off, c_off, excl, k, fb_count, fb_list, out_idx, out_dist);
+        MN_KCHECK(s, "k_fallback");
+    }
+    tm.mark();
+    MN_HIP_TRY(hipStreamSynchronize(s));
+    t_stats.n_uncertified = nfb2;
     if (tm.on) {
         t_stats.n_candidates = n_cand;
         t_stats.ms_norms = tm.ms(0, 1);

@@ -42,11 +42,13 @@ for r in range(rounds):
                                                                  out.dist.view(torch.int32))
             res[v][-1]["same_as_first"] = bool(same)
         del out
-        os.environ["MN_X1_PROBE"] = "noepi"
-        S.knn_l2sq(X, 32, timing=True, algo="bf16x1")
-        st = S.knn.last_stats()
-        probe[v].append(round(st["ms_sweep"], 2))
+        pm = {}
+        for pk in os.environ.get("AB_PROBES", "noepi").split(","):
+            os.environ["MN_X1_PROBE"] = pk
+            S.knn_l2sq(X, 32, timing=True, algo="bf16x1")
+            pm[pk] = round(S.knn.last_stats()["ms_sweep"], 2)
         os.environ.pop("MN_X1_PROBE", None)
-        print(json.dumps({"round": r, "v": v, **res[v][-1], "probe_ms": probe[v][-1]}), flush=True)
+        probe[v].append(pm.get("noepi", 0.0))
+        print(json.dumps({"round": r, "v": v, **res[v][-1], "probe_ms": pm}), flush=True)
 print(json.dumps({"summary": {v: min(x["ms_sweep"] for x in res[v]) for v in VERS},
                   "probe": {v: min(probe[v]) for v in VERS}}))

@@ -190,3 +190,19 @@ def test_euclidean_metric_sqrt_is_correctly_rounded(algo_e):
                                   np.sqrt(rdist).reshape(-1).view(np.uint32))
     np.testing.assert_array_equal(e.cost.cpu().numpy().view(np.uint32),
                                   e.distance.cpu().numpy().view(np.uint32))
+
+
+def test_uncertified_rows_batched_fallback():
+    """Rows no certificate settles (all-zero rows: exact ties far beyond k)
+    against a corpus >= 2^16 go through the batched split-generator pass
+    (k + 1 with self, own id dropped) — bit-exact with the oracle."""
+    n, d, k = 70000, 32, 32
+    X = datagen.uniform(n, d, seed=11)
+    zero = np.random.default_rng(2).choice(n, 300, replace=False)
+    X[zero] = 0.0
+    idx, dist, st = hip_knn(X, k, algo="bf16x1")
+    rows = np.unique(np.concatenate([zero[:40], np.random.default_rng(3).choice(n, 40, replace=False)]))
+    ridx, rdist = O.knn_l2sq_rows(X, k, rows)
+    np.testing.assert_array_equal(idx[rows], ridx)
+    np.testing.assert_array_equal(dist[rows].view(np.uint32), rdist.view(np.uint32))
+    assert st["n_uncertified"] > 0, st
