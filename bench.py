@@ -58,7 +58,7 @@ def parse():
                     help="rows of the C5 graph checked bit-exact against the oracle (0 = off)")
     ap.add_argument("--no-c3", dest="c3", action="store_false",
                     help="skip the C3 legs (Laplacian assembly, energy pass, sorted index)")
-    ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_gram_latest.json"),
+    ap.add_argument("--pmc-json", default=os.path.join(ROOT, "bench_pmc_gram.json"),
                     help="PMC-derived HBM bytes per launch of the Gram kernel (optional)")
     ap.add_argument("--time-budget-s", type=float, default=420.0,
                     help="N>1: cap warmup+steps so the whole run fits this budget (the cap is "

@@ -80,8 +80,9 @@ __device__ __forceinline__ int xcd_remap(int orig, int nwg) {
 // issue, PROBE = 3 also without the fragment reads, PROBE = 4 with the DMA
 // issued but never waited for.
 // A tile's epilogue (candidate check + next accumulator init) runs in the
-// wave's read window (fusing the init into the first MFMA window measured
-// equal within noise: 1240-1274 vs 1271 ms at C2).
+// wave's read window (fusing the init into the first MFMA window, or one
+// ballot per 2 or 4 fragments before the per-fragment ones, measured equal
+// within noise at C2).
 template <int PROBE>
 __global__ __launch_bounds__(NT) void k_gram_sweep2(
     const uint16_t *__restrict__ Qk, int64_t nq, const uint16_t *__restrict__ Ck, int64_t nc,

@@ -65,7 +65,7 @@ def main():
         out["algorithmic_bytes_per_launch"] = (2 * n * d * 2 if "sweep" in dshort else 2 * n * d * 4)
     with open(os.path.join(dst, f"{tag}_summary.json"), "w") as fh:
         json.dump(out, fh, indent=1)
-    with open(os.path.join(dst, "pmc_gram_latest.json"), "w") as fh:
+    with open(os.path.join(os.path.dirname(dst), "bench_pmc_gram.json"), "w") as fh:
         json.dump(out, fh, indent=1)
     print(json.dumps(out, indent=1))
 
