@@ -177,6 +177,7 @@ __global__ __launch_bounds__(NT) void k_gram_sweep2(
                 *reinterpret_cast<const float4 *>(&sm.hc[par][128 * wc + 16 * g + 4 * fk]);
 #pragma unroll
             for (int f = 0; f < WQF; ++f) {
+                // (hipcc packs these into v_pk_add_f32 pairs)
                 acc[f][g][0] = tql[f] - x.x;
                 acc[f][g][1] = tql[f] - x.y;
                 acc[f][g][2] = tql[f] - x.z;

@@ -21,6 +21,8 @@
 #include <climits>
 #include <cmath>
 
+#include <cstdlib>
+
 #include "common.hpp"
 #include "scan.hpp"
 
@@ -176,8 +178,60 @@ constexpr int STD_CHUNK = 256;  // values per chunk: 64 lanes x 4
 
 constexpr int STD_PF = 4;  // chunks in flight ahead of the chain
 
+// Pass 1 certified in parallel.  Pass 1 only feeds (f32) of the f64 sum, so
+// its bits are known whenever every value the sequential fold can take rounds
+// to the same f32: the fold lies within gamma_n * sum|x| (u = 2^-53) of the
+// exact sum, which a double-double reduction gives to ~n u^2 sum|x|.  When
+// that interval straddles an f32 rounding boundary (rarely: its width is
+// ~1e-10 relative against an f32 ulp of 6e-8 at n = 1e6), or a value is not
+// finite, the sequential pass 1 runs as before.  Pass 2's f32 chain stays
+// sequential (its rounding is large and order-dependent).
+constexpr int SUM_BLOCKS = 512;
+
+__device__ __forceinline__ void two_sum(double a, double b, double &s, double &e) {
+    s = a + b;
+    const double bb = s - a;
+    e = (a - (s - bb)) + (b - bb);
+}
+__device__ __forceinline__ void dd_add(double &hi, double &lo, double x) {
+    double s, e;
+    two_sum(hi, x, s, e);
+    e += lo;
+    two_sum(s, e, hi, lo);
+}
+
+// per block: double-double sum of lam and f64 sum of |lam| (+ non-finite flag)
+__global__ __launch_bounds__(256) void k_sum_dd(const double *__restrict__ lam, int64_t n,
+                                               double *__restrict__ part) {
+    __shared__ double sh[3][256];
+    double hi = 0.0, lo = 0.0, ab = 0.0;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)SUM_BLOCKS * 256) {
+        const double v = lam[i];
+        dd_add(hi, lo, v);
+        ab += __builtin_fabs(v);  // NaN / inf propagate: the check below fails
+    }
+    sh[0][threadIdx.x] = hi; sh[1][threadIdx.x] = lo; sh[2][threadIdx.x] = ab;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+        if ((int)threadIdx.x < o) {
+            double h = sh[0][threadIdx.x], l = sh[1][threadIdx.x];
+            dd_add(h, l, sh[0][threadIdx.x + o]);
+            dd_add(h, l, sh[1][threadIdx.x + o]);
+            sh[0][threadIdx.x] = h; sh[1][threadIdx.x] = l;
+            sh[2][threadIdx.x] += sh[2][threadIdx.x + o];
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        part[3 * blockIdx.x] = sh[0][0];
+        part[3 * blockIdx.x + 1] = sh[1][0];
+        part[3 * blockIdx.x + 2] = sh[2][0];
+    }
+}
+
 __global__ __launch_bounds__(64) void k_std_exact(const double *__restrict__ lam, int64_t n,
-                                                  float *__restrict__ out) {
+                                                  const double *__restrict__ part,
+                                                  float *__restrict__ out, int *__restrict__ seq) {
     __shared__ double b64[2][STD_CHUNK];
     __shared__ float b32[2][STD_CHUNK];
     const int lane = threadIdx.x;
@@ -187,8 +241,30 @@ __global__ __launch_bounds__(64) void k_std_exact(const double *__restrict__ lam
 #pragma unroll
         for (int t = 0; t < 4; ++t) p[t] = lam[c * STD_CHUNK + 4 * lane + t];
     };
-    // ---- pass 1: s = sum(lam) in index order (f64) ----
+    // ---- pass 1: s = sum(lam) in index order (f64), certified from the
+    // double-double partials when possible ----
+    bool certified = false;
+    float sf = 0.0f;
+    if (part) {
+        double hi = 0.0, lo = 0.0, ab = 0.0;
+        for (int b = 0; b < SUM_BLOCKS; ++b) {  // every lane the same (uniform)
+            dd_add(hi, lo, part[3 * b]);
+            dd_add(hi, lo, part[3 * b + 1]);
+            ab += part[3 * b + 2];
+        }
+        const double u = 0x1p-53, nn = (double)n;
+        // sequential-fold bound gamma_n * sum|x| plus the double-double
+        // reduction's own error, an ulp of hi and |lo|, all inflated
+        const double E = (nn * u / (1.0 - nn * u)) * ab * (1.0 + 0x1p-20) +
+                         8.0 * (nn + SUM_BLOCKS) * u * u * ab + __builtin_fabs(lo) +
+                         __builtin_fabs(hi) * 0x1p-52 + 0x1p-1000;
+        if (__builtin_isfinite(hi) && __builtin_isfinite(ab) && __builtin_isfinite(E)) {
+            const float a = (float)(hi - E), b = (float)(hi + E);
+            if (a == b) { certified = true; sf = a; }
+        }
+    }
     double s = -0.0;
+    if (!certified) {
 #pragma unroll
     for (int u = 0; u < STD_PF; ++u)
         if (u < nfull) fetch(u, ring[u]);
@@ -207,7 +283,10 @@ __global__ __launch_bounds__(64) void k_std_exact(const double *__restrict__ lam
         }
     }
     for (int64_t i = nfull * STD_CHUNK; i < n; ++i) s = s + lam[i];
-    const float mean = __fdiv_rn((float)s, (float)n);
+    sf = (float)s;
+    }
+    if (threadIdx.x == 0 && seq) *seq = certified ? 0 : 1;
+    const float mean = __fdiv_rn(sf, (float)n);
     // ---- pass 2: var = sum((mean - (f32)lam)^2) in index order (f32) ----
     float var = -0.0f;
 #pragma unroll
@@ -391,7 +470,17 @@ static int sorted_index_impl(const double *lam, int64_t n, int64_t *order, doubl
         side = side_stream();
         MN_REQUIRE(side, MN_EHIP, "mn_sorted_index: side stream creation failed");
         MN_HIP_TRY(stream_wait(side, s));
-        hipLaunchKernelGGL(k_std_exact, dim3(1), dim3(64), 0, side, lam, n, (float *)sums);
+        // pass-1 certificate partials (the sequential pass 1 runs only if it
+        // fails); MN_STD_SEQ=1 forces the sequential pass (tests)
+        const char *fs = getenv("MN_STD_SEQ");
+        const bool force_seq = fs && *fs == '1';
+        double *part1 = force_seq ? nullptr : (double *)scratch(kSlotNorms2, sizeof(double) * 3 * SUM_BLOCKS + 64);
+        if (part1) {
+            hipLaunchKernelGGL(k_sum_dd, dim3(SUM_BLOCKS), dim3(256), 0, side, lam, n, part1);
+            MN_KCHECK(side, "k_sum_dd");
+        }
+        hipLaunchKernelGGL(k_std_exact, dim3(1), dim3(64), 0, side, lam, n, (const double *)part1,
+                           (float *)sums, (int *)(sums + 1));
         MN_KCHECK(side, "k_std_exact");
     }
     hipLaunchKernelGGL(k_make_keys, dim3(grid(P)), dim3(256), 0, s, lam, n, P, keys);

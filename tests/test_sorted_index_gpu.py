@@ -95,3 +95,49 @@ def test_lambda_lookups_vs_oracle_unique_and_edges():
     _lookup_case(lam, qs, 40, 2.0, 0.001, None)
     _lookup_case(lam, qs, 1, 0.0, 1.0, 0.0)     # base_delta 0: one window
     _lookup_case(lam[:1], qs[:10], 3, 1.0, 0.5, None)  # a single item
+
+
+def _std_both(lam, monkeypatch):
+    """std_dev through the certified pass 1 (default) and through the forced
+    sequential pass 1 (MN_STD_SEQ=1)."""
+    _, _, sd = hip_sort(lam)
+    monkeypatch.setenv("MN_STD_SEQ", "1")
+    _, _, sd_seq = hip_sort(lam)
+    monkeypatch.delenv("MN_STD_SEQ")
+    return sd, sd_seq
+
+
+def _midpoint_case(n, rng, offset_units):
+    """multiples of 2^-30 in [0, 1) whose f64 sum is exact, the last value set
+    so the sum lands on an f32 rounding midpoint (+ offset_units * 2^-30)."""
+    lam = rng.integers(0, 2**30, size=n).astype(np.float64) * 2.0**-30
+    head = float(np.sum(lam[:-1]))  # exact: every partial sum fits in 53 bits
+    e = int(np.floor(np.log2(head + 1.0)))
+    ulp = 2.0 ** (e - 23)
+    target = np.ceil(head / ulp) * ulp + ulp / 2 + offset_units * 2.0**-30
+    lam[-1] = target - head
+    assert 0.0 <= lam[-1] and np.float64(head + lam[-1]) == target
+    return lam
+
+
+@pytest.mark.parametrize("case", ["tie2", "cancel", "mid_1m", "mid_plus_1m", "normal_1m",
+                                  "huge_mixed"])
+def test_std_pass1_certificate_matches_sequential(case, monkeypatch):
+    """K4 std_dev: pass 1's f64 sum is certified from a double-double parallel
+    sum plus the sequential-fold error bound (gamma_n * sum|x|); inputs whose
+    bound straddles an f32 rounding boundary must fall back to the sequential
+    fold.  Both paths bit-equal to the oracle's sequential restatement."""
+    rng = np.random.default_rng(11)
+    lam = {
+        "tie2": lambda: np.array([1.0, 2.0**-24]),           # exact f32 tie -> even
+        "cancel": lambda: np.array([1e16, 1.0, -1e16, 3.0]),  # fold 3, exact 4
+        "mid_1m": lambda: _midpoint_case(1_000_000, rng, 0),
+        "mid_plus_1m": lambda: _midpoint_case(1_000_000, rng, 1),
+        "normal_1m": lambda: rng.normal(size=1_000_000),
+        "huge_mixed": lambda: np.concatenate([rng.normal(size=50_000) * 1e15,
+                                              rng.normal(size=50_000) * 1e-30]),
+    }[case]()
+    sd, sd_seq = _std_both(lam, monkeypatch)
+    _, _, rsd = O.sorted_index(lam)
+    assert np.float32(sd_seq) == np.float32(rsd)
+    assert np.float32(sd) == np.float32(rsd)
