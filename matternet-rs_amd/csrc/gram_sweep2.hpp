@@ -79,11 +79,17 @@ __device__ __forceinline__ int xcd_remap(int orig, int nwg) {
 // diagnostics (results invalid): PROBE = 2 also without the in-loop LDS-DMA
 // issue, PROBE = 3 also without the fragment reads, PROBE = 4 with the DMA
 // issued but never waited for.
+// MODE = SW_COS (C5, knn_bf16.hip): hc holds -|c| and tq = t(q) |q| (t the
+// cosine threshold): acc0 = tq * hc, so acc = q.c - t |q||c| and a pair is a
+// candidate iff q.c / (|q||c|) > t; rows past the slice end are padded with
+// NaN (never positive); key = -acc / |c| (the re-rank maps it back to cos).
 // A tile's epilogue (candidate check + next accumulator init) runs in the
 // wave's read window (fusing the init into the first MFMA window, or one
 // ballot per 2 or 4 fragments before the per-fragment ones, measured equal
 // within noise at C2).
-template <int PROBE>
+enum SweepMode { SW_L2 = 0, SW_COS = 1 };
+
+template <int PROBE, int MODE = SW_L2>
 __global__ __launch_bounds__(NT) void k_gram_sweep2(
     const uint16_t *__restrict__ Qk, int64_t nq, const uint16_t *__restrict__ Ck, int64_t nc,
     int nkb, int64_t q_off, int64_t c_off, int excl, const float *__restrict__ tq,
@@ -102,6 +108,7 @@ __global__ __launch_bounds__(NT) void k_gram_sweep2(
     const int cend = (int)min(nc, (int64_t)cbeg + chunk);
     const int ntile = cend > cbeg ? (cend - cbeg + BC - 1) / BC : 0;
     const int gtot = ntile * nkb;
+    const float pad = MODE == SW_COS ? __builtin_nanf("") : __builtin_inff();
 
     if (tid < NWAVES) sm.scnt[tid] = 0;
     if (tid < BQ) {
@@ -111,7 +118,7 @@ __global__ __launch_bounds__(NT) void k_gram_sweep2(
     }
     if (ntile > 0 && tid < BC) {
         const int c = cbeg + tid;
-        sm.hc[0][tid] = (c < cend) ? hc[c] : __builtin_inff();
+        sm.hc[0][tid] = (c < cend) ? hc[c] : pad;
     }
 
     // ---- LDS-DMA issue state: the next k-step gi to stage (tile row bt0,
@@ -177,11 +184,18 @@ __global__ __launch_bounds__(NT) void k_gram_sweep2(
                 *reinterpret_cast<const float4 *>(&sm.hc[par][128 * wc + 16 * g + 4 * fk]);
 #pragma unroll
             for (int f = 0; f < WQF; ++f) {
-                // (hipcc packs these into v_pk_add_f32 pairs)
-                acc[f][g][0] = tql[f] - x.x;
-                acc[f][g][1] = tql[f] - x.y;
-                acc[f][g][2] = tql[f] - x.z;
-                acc[f][g][3] = tql[f] - x.w;
+                // (hipcc packs these into v_pk_add_f32 / v_pk_mul_f32 pairs)
+                if constexpr (MODE == SW_COS) {
+                    acc[f][g][0] = tql[f] * x.x;
+                    acc[f][g][1] = tql[f] * x.y;
+                    acc[f][g][2] = tql[f] * x.z;
+                    acc[f][g][3] = tql[f] * x.w;
+                } else {
+                    acc[f][g][0] = tql[f] - x.x;
+                    acc[f][g][1] = tql[f] - x.y;
+                    acc[f][g][2] = tql[f] - x.z;
+                    acc[f][g][3] = tql[f] - x.w;
+                }
             }
         }
     };
@@ -223,7 +237,7 @@ __global__ __launch_bounds__(NT) void k_gram_sweep2(
     // (a few per wave and tile at the C2 threshold).
     // one 16 x 16 fragment: per-fragment max + ballot (wave-uniform branch);
     // the staging body runs only where some lane has a candidate
-    auto check_block = [&](int f, int g, int ct0) {
+    auto check_block = [&](int f, int g, int ct0, int hpar) {
         const f32x4 a = acc[f][g];
         const float m4 = fmaxf(fmaxf(a[0], a[1]), fmaxf(a[2], a[3]));
         if (__builtin_expect(__ballot(m4 > 0.f) == 0, 1)) return;
@@ -242,7 +256,12 @@ __global__ __launch_bounds__(NT) void k_gram_sweep2(
             while (pm) {
                 const int r = __builtin_ctz(pm);
                 pm &= pm - 1;
-                const uint2 kv = make_uint2(__float_as_uint(t0l - 2.f * a[r]), (uint32_t)(c + r));
+                float key;
+                if constexpr (MODE == SW_COS)  // hc = -|c|: key = -acc / |c|
+                    key = a[r] / sm.hc[hpar][128 * wc + 16 * g + 4 * fk + r];
+                else
+                    key = t0l - 2.f * a[r];
+                const uint2 kv = make_uint2(__float_as_uint(key), (uint32_t)(c + r));
                 if (pos < cap) {
                     if (e < SCAP) {
                         sm.stk[w][e] = kv;
@@ -258,12 +277,13 @@ __global__ __launch_bounds__(NT) void k_gram_sweep2(
         }
     };
     // candidates of the tile starting at corpus row ct0: positive accumulators
-    auto check = [&](int ct0) {
+    // (hpar: the hc parity of that tile)
+    auto check = [&](int ct0, int hpar) {
         if constexpr (PROBE == 0) {
 #pragma unroll
             for (int f = 0; f < WQF; ++f)
 #pragma unroll
-                for (int g = 0; g < WCF; ++g) check_block(f, g, ct0);
+                for (int g = 0; g < WCF; ++g) check_block(f, g, ct0, hpar);
             // wave-uniform: spill the area once it is 3/4 full (or overran)
             if (sm.scnt[w] >= SCAP * 3 / 4) flush();
         } else {
@@ -304,14 +324,14 @@ __global__ __launch_bounds__(NT) void k_gram_sweep2(
         if (kb == 0 && g > 0) {
             // the previous tile's candidates, then this tile's accumulator
             // init (before the fragment reads: the fragments are dead here)
-            check(c0 - BC);
+            check(c0 - BC, par ^ 1);
             init_acc(par);
         }
         if constexpr (PROBE < 3 || PROBE == 4) read_frags((int)(g & (NSLOT - 1)));
         if (kb == nkb - 2 && more && wc == 0) {
             // written 2 k-steps (>= 2 barriers) before init_acc reads it
             const int cb = c0 + BC + 64 * wq + lane;
-            sm.hc[par ^ 1][64 * wq + lane] = cb < cend ? hcn : __builtin_inff();
+            sm.hc[par ^ 1][64 * wq + lane] = cb < cend ? hcn : pad;
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         if (PROBE != 4 && wc == 1) {
@@ -348,7 +368,7 @@ __global__ __launch_bounds__(NT) void k_gram_sweep2(
         }
     }
     if (wc == 0) __builtin_amdgcn_s_barrier();  // match the trailing group's extra window
-    if (gtot > 0) check(c0 - BC);
+    if (gtot > 0) check(c0 - BC, par ^ 1);
     if (sm.scnt[w] > 0) flush();
     __syncthreads();
     if (tid < BQ && q0 + tid < nq) {

@@ -23,6 +23,19 @@
 //                  |cos~ - cos| <= 2(d+12)2^-24 (f32 accumulation of exact
 //                  products + two f32 scalings), eps/weight filter (a prefix).
 //   k_cos_fallback exact scan for uncertified rows (ties at dist 1, overflow).
+//
+// Two-phase generator (the default for self graphs at scale, C5): the corpus
+// is visited in a golden-ratio order (pos p holds row perm(p)) whose prefix of
+// m0 = n/16 rows is the sample.
+//   phase 1   k_gram_bf16<GM_COS> of every query against the sample, list
+//             length L1: t(q) = -(min over slices of the L1-th best key), the
+//             cosine of about the (16 L1)-th neighbour.
+//   phase 2   gram_sweep2.hpp SW_COS over positions [m0, n) in KB32 layout:
+//             acc = q.c - t |q||c| > 0 buffers the pair (no per-row lists, one
+//             compare per product: the same epilogue as the L2 sweep).
+//   k_cos_rerank_x1  both buffers -> exact f64 distances, (dist, j) order,
+//             certification: every pair never buffered has cos~ <= t, so its
+//             exact cos is <= t + delta and its distance >= 1 - max(t+delta, 0).
 #include <algorithm>
 #include <cmath>
 #include <climits>
@@ -31,6 +44,8 @@
 
 #include "common.hpp"
 #include "gram_bf16.hpp"
+#include "gram_sweep.hpp"
+#include "gram_sweep2.hpp"
 
 namespace mn {
 namespace kb16 {
@@ -317,6 +332,235 @@ __global__ __launch_bounds__(FBT) void k_cos_fallback(
     }
 }
 
+// ---- two-phase generator ------------------------------------------------------
+// visiting order: pos p -> row (a p + b) mod n, gcd(a, n) = 1
+struct Perm {
+    uint64_t a, b, n, ainv;
+    __device__ __forceinline__ int64_t operator()(int64_t p) const {
+        return (int64_t)((a * (uint64_t)p + b) % n);
+    }
+    __device__ __forceinline__ int64_t pos(int64_t r) const {  // inverse
+        return (int64_t)((ainv * (((uint64_t)r + n - b) % n)) % n);
+    }
+};
+
+inline Perm make_perm_ab(int64_t n) {
+    uint64_t a = (uint64_t)((double)n * 0.6180339887498949);
+    if (a == 0) a = 1;
+    auto gcd = [](uint64_t x, uint64_t y) { while (y) { const uint64_t t = x % y; x = y; y = t; } return x; };
+    while (gcd(a, (uint64_t)n) != 1) ++a;
+    a %= (uint64_t)n;
+    if (a == 0) a = 1;
+    // a^-1 mod n (extended Euclid; n < 2^31 so the products fit 64 bits)
+    int64_t r0 = (int64_t)n, r1 = (int64_t)a, t0 = 0, t1 = 1;
+    while (r1) {
+        const int64_t qq = r0 / r1, r2 = r0 - qq * r1, t2 = t0 - qq * t1;
+        r0 = r1; r1 = r2; t0 = t1; t1 = t2;
+    }
+    const uint64_t ainv = (uint64_t)((t0 % (int64_t)n + (int64_t)n) % (int64_t)n);
+    return Perm{a, (uint64_t)n / 3, (uint64_t)n, ainv};
+}
+
+// KB32 copy [dp/32][n][32] (zero-padded past d) of rows perm(p) (perm.n == 0:
+// identity); one thread per 16 B of output, consecutive threads write
+// consecutive bytes of one k-block
+__global__ __launch_bounds__(256) void k_to_kb32(const uint16_t *__restrict__ X, int64_t n, int d,
+                                                 int dp, Perm pm, uint16_t *__restrict__ XK) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t per_kb = n * 4;
+    if (t >= per_kb * (dp / 32)) return;
+    const int kb = (int)(t / per_kb);
+    const int64_t rem = t - (int64_t)kb * per_kb;
+    const int64_t p = rem >> 2;
+    const int cc = (int)(rem & 3);
+    const int64_t src = pm.n ? pm(p) : p;
+    const int e0 = 32 * kb + 8 * cc;
+    uint4 v = make_uint4(0u, 0u, 0u, 0u);
+    if (e0 + 8 <= d) {
+        v = *reinterpret_cast<const uint4 *>(X + src * d + e0);  // d % 8 == 0, 16-B aligned rows
+    } else if (e0 < d) {
+        uint16_t h[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) h[u] = e0 + u < d ? X[src * d + e0 + u] : (uint16_t)0;
+        v = make_uint4(h[0] | ((uint32_t)h[1] << 16), h[2] | ((uint32_t)h[3] << 16),
+                       h[4] | ((uint32_t)h[5] << 16), h[6] | ((uint32_t)h[7] << 16));
+    }
+    *reinterpret_cast<uint4 *>(XK + ((int64_t)kb * n + p) * 32 + 8 * cc) = v;
+}
+
+// row-major copy of the sample positions [0, m) (stride d), 16 B per thread
+__global__ __launch_bounds__(256) void k_sample_rows(const uint16_t *__restrict__ X, int64_t m,
+                                                     int d, Perm pm, uint16_t *__restrict__ XR) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int d8 = d / 8;
+    if (t >= m * d8) return;
+    const int64_t p = t / d8;
+    const int c = (int)(t - p * d8);
+    *reinterpret_cast<uint4 *>(XR + p * d + 8 * c) =
+        *reinterpret_cast<const uint4 *>(X + pm(p) * d + 8 * c);
+}
+
+// per position: 1/|c| (phase 1) and -|c| (sweep), f32 of the exact norms
+__global__ __launch_bounds__(256) void k_perm_norms(const double *__restrict__ nrm,
+                                                    const float *__restrict__ inv, int64_t n,
+                                                    Perm pm, float *__restrict__ invp,
+                                                    float *__restrict__ negn) {
+    const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= n) return;
+    const int64_t r = pm(p);
+    invp[p] = inv[r];
+    negn[p] = -(float)nrm[r];
+}
+
+// per query row q: t = -(min over phase-1 slices of the L1-th best key); a
+// forced slice (-inf) or no full slice (+inf) -> t = +inf (nothing is
+// buffered, the row is rescanned).  tq = t |q| at the query's sweep position.
+__global__ __launch_bounds__(256) void k_tau_cos(int64_t nq, int S1, const float *__restrict__ btau1,
+                                                 const double *__restrict__ qn, Perm pm,
+                                                 float *__restrict__ tcos,
+                                                 float *__restrict__ tq_pos) {
+    const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= nq) return;
+    float T = __builtin_inff();
+    for (int s = 0; s < S1; ++s) T = fminf(T, btau1[q * S1 + s]);
+    const bool ok = __builtin_isfinite(T);
+    const float t = ok ? -T : __builtin_inff();
+    tcos[q] = t;
+    tq_pos[pm.pos(q)] = ok ? (float)((double)t * qn[q]) : __builtin_inff();
+}
+
+// One wave per query: both buffers' candidates in key = -cos~ order (sweep
+// keys mapped back: -cos~ = key / |q| - t), exact distances for the best kq
+// and every other candidate whose lower bound does not exceed the worst of
+// those, (dist, j) order, certification dist_min(never buffered) > D_k.
+template <int NR>
+__global__ __launch_bounds__(256) void k_cos_rerank_x1(
+    const uint16_t *__restrict__ X, int64_t n, int d, Perm pm, const double *__restrict__ xn,
+    const float *__restrict__ xinv, int S1, int cap1, const uint2 *__restrict__ buf1,
+    const int *__restrict__ cnt1, const float *__restrict__ btau1, int S2, int cap2,
+    const uint2 *__restrict__ buf2, const int *__restrict__ cnt2, const float *__restrict__ tcos,
+    int topk, double delta, double eps, double sigma, double p, const int *__restrict__ qlist,
+    const int *__restrict__ qlist_n, int *__restrict__ big_count, int *__restrict__ big_list,
+    int32_t *__restrict__ out_idx, double *__restrict__ out_dist, double *__restrict__ out_w,
+    int *__restrict__ fb_count, int *__restrict__ fb_list) {
+    __shared__ int cand[4][64 * NR];
+    __shared__ float candk[4][64 * NR];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int64_t wq = (int64_t)blockIdx.x * 4 + wid;
+    if (qlist ? wq >= *qlist_n : wq >= n) return;
+    const int64_t q = qlist ? qlist[wq] : wq;
+    const float t = tcos[q];
+    bool forced = !(t < __builtin_inff());
+    int M = 0;
+    const float qi = xinv[q];
+    for (int s = 0; s < S1; ++s) {
+        const int cnt = cnt1[q * S1 + s];
+        const float ts = btau1[q * S1 + s];
+        const uint2 *bp = buf1 + (q * S1 + s) * (int64_t)cap1;
+        for (int e0 = 0; e0 < cnt; e0 += 64) {
+            const int e = e0 + lane;
+            const uint2 v = e < cnt ? bp[e] : make_uint2(0x7f800000u, 0u);
+            const int64_t gid = e < cnt ? pm((int64_t)v.y) : -1;
+            const bool pass = e < cnt && __uint_as_float(v.x) <= ts && gid != q;
+            const uint64_t bm = __ballot(pass);
+            const int pos = M + (int)__popcll(bm & ((1ull << lane) - 1ull));
+            if (pass && pos < 64 * NR) {
+                cand[wid][pos] = (int)gid;
+                candk[wid][pos] = __uint_as_float(v.x);
+            }
+            M += (int)__popcll(bm);
+        }
+    }
+    const int64_t qp = pm.pos(q);  // the sweep ran over positions
+    for (int s = 0; s < S2; ++s) {
+        const int cnt = cnt2[qp * S2 + s];
+        forced |= cnt < 0;
+        const uint2 *bp = buf2 + (qp * S2 + s) * (int64_t)cap2;
+        for (int e0 = 0; e0 < cnt; e0 += 64) {
+            const int e = e0 + lane;
+            const uint2 v = e < cnt ? bp[e] : make_uint2(0u, 0u);
+            const int64_t gid = e < cnt ? pm((int64_t)v.y) : -1;
+            const bool pass = e < cnt && gid != q;
+            const uint64_t bm = __ballot(pass);
+            const int pos = M + (int)__popcll(bm & ((1ull << lane) - 1ull));
+            if (pass && pos < 64 * NR) {
+                cand[wid][pos] = (int)gid;
+                candk[wid][pos] = __uint_as_float(v.x) * qi - t;
+            }
+            M += (int)__popcll(bm);
+        }
+    }
+    if (!forced && M > 64 * NR && big_list) {
+        if (lane == 0) big_list[atomicAdd(big_count, 1)] = (int)q;
+        return;
+    }
+    forced |= M > 64 * NR;
+    M = min(M, 64 * NR);
+    __builtin_amdgcn_wave_barrier();
+    float kk[NR];
+    int ix[NR];
+#pragma unroll
+    for (int r = 0; r < NR; ++r) {
+        const int e = lane + 64 * r;
+        kk[r] = e < M ? candk[wid][e] : __builtin_inff();
+        ix[r] = e < M ? cand[wid][e] : INT_MAX;
+    }
+    wave_bitonic_sort<NR>(kk, ix);
+    const uint16_t *qrow = X + q * (int64_t)d;
+    const int kq = min(topk, M);
+    double dd[NR];
+#pragma unroll
+    for (int r = 0; r < NR; ++r) {
+        const int e = lane + 64 * r;
+        dd[r] = __builtin_inf();
+        if (e < kq) dd[r] = cos_dist(exact_dot(qrow, X + (int64_t)ix[r] * d, d), xn[q], xn[ix[r]]);
+    }
+    double Dp = -__builtin_inf();
+#pragma unroll
+    for (int r = 0; r < NR; ++r) Dp = fmax(Dp, (lane + 64 * r) < kq ? dd[r] : -__builtin_inf());
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) Dp = fmax(Dp, __shfl_xor(Dp, o));
+    // pruning bound: the sweep keys carry two extra f32 roundings (2 delta
+    // covers them with a wide margin)
+    const double dprune = 2.0 * delta + 1e-6;
+#pragma unroll
+    for (int r = 0; r < NR; ++r) {
+        const int e = lane + 64 * r;
+        if (e >= kq && e < M) {
+            const double cub = -(double)kk[r] + dprune;
+            const double lb = 1.0 - (cub > 0.0 ? cub : 0.0);
+            if (lb <= Dp) dd[r] = cos_dist(exact_dot(qrow, X + (int64_t)ix[r] * d, d), xn[q], xn[ix[r]]);
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < NR; ++r)
+        if (lane + 64 * r >= M) ix[r] = INT_MAX;
+    wave_bitonic_sort<NR>(dd, ix);
+    const int keff = (int)min((int64_t)min(topk, M), n - 1);
+    const int kneed = (int)min((int64_t)topk, n - 1);
+    bool cert = !forced && keff >= kneed;
+    if (cert && keff > 0) {
+        const double Dk = wave_elem<NR>(dd, keff - 1);
+        const double cmax = (double)t + delta;
+        const double dmin = 1.0 - (cmax > 0.0 ? cmax : 0.0);
+        cert = dmin > Dk;
+    }
+    if (!cert) {
+        if (lane == 0) fb_list[atomicAdd(fb_count, 1)] = (int)q;
+        return;
+    }
+    const double wv = weight_of(dd[0], sigma, p);
+    const bool keep = lane < keff && dd[0] <= eps && wv > 1e-12;
+    const uint64_t km = __ballot(keep);
+    const int nkeep = (~km) == 0 ? 64 : (int)__builtin_ctzll(~km);
+    if (lane < topk) {
+        const bool k2 = lane < nkeep;
+        out_idx[q * topk + lane] = k2 ? ix[0] : -1;
+        out_dist[q * topk + lane] = k2 ? dd[0] : __builtin_inf();
+        if (out_w) out_w[q * topk + lane] = k2 ? wv : 0.0;
+    }
+}
+
 }  // namespace kb16
 
 static thread_local mn_knn_stats t_bf16_stats{};
@@ -324,6 +568,131 @@ static thread_local mn_knn_stats t_bf16_stats{};
 static int getenv_int(const char *name, int dflt) {
     const char *e = getenv(name);
     return (e && *e) ? atoi(e) : dflt;
+}
+
+// Two-phase generator for self graphs (see the header).  X [n][d] row-major
+// (d % 8 == 0, 16-B aligned), exact norms xn / 1/|x| xinv by row.  Returns
+// MN_OK, or 1 when the inputs do not suit it (the caller runs the one-phase
+// generator).
+static int knn_cos_bf16_x1(const uint16_t *X, int64_t n, int32_t d, const mn_cos_opts *o,
+                           const double *xn, const float *xinv, int *flags, int *fb_list,
+                           int32_t *out_idx, double *out_dist, double *out_w, hipStream_t s) {
+    using namespace kb16;
+    const int topk = o->topk;
+    int L1 = std::min(std::max((topk + 1) / 2, 16), 48);
+    const char *fl = getenv("MN_BF16_L1");  // experiments: phase-1 list length
+    if (fl && *fl) L1 = std::min(std::max(atoi(fl), 4), 48);
+    int64_t m0 = std::max<int64_t>(n / 16, (int64_t)64 * L1);
+    m0 = (m0 + BN - 1) / BN * BN;
+    if (m0 + 4 * ksw2::BC > n || n * 32 >= INT_MAX || n >= INT_MAX) return 1;
+    const int dp = (d + 255) / 256 * 256;  // KB32 k-blocks, nkb >= 8 (sweep2's prefetch)
+    const int nkb = dp / 32;
+    const Perm pm = make_perm_ab(n);
+
+    uint16_t *XK = (uint16_t *)scratch(kSlotX1CK, (size_t)n * dp * 2 + 64);
+    uint16_t *XR = (uint16_t *)scratch(kSlotX1CR, (size_t)m0 * d * 2 + 64);
+    float *aux = (float *)scratch(kSlotX1Aux, (size_t)n * 16 + 256);
+    MN_REQUIRE(XK && XR && aux, MN_ENOMEM, "mn_knn_cos_bf16: two-phase scratch allocation failed");
+    float *invp = aux, *negn = aux + n, *tcos = negn + n, *tq_pos = tcos + n;
+
+    Timer tm;
+    tm.start(o->timing != 0, s);
+    {
+        const int64_t nt = n * 4 * nkb;
+        hipLaunchKernelGGL(k_to_kb32, dim3((unsigned)((nt + 255) / 256)), dim3(256), 0, s, X, n, d,
+                           dp, pm, XK);
+        const int64_t ns = m0 * (d / 8);
+        hipLaunchKernelGGL(k_sample_rows, dim3((unsigned)((ns + 255) / 256)), dim3(256), 0, s, X, m0,
+                           d, pm, XR);
+        hipLaunchKernelGGL(k_perm_norms, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, xn,
+                           xinv, n, pm, invp, negn);
+        MN_KCHECK(s, "k_to_kb32 / k_sample_rows / k_perm_norms");
+    }
+    // phase 1: every query (rows, in place) against the sample (positions [0, m0))
+    const GramPlan pl = plan_gram(n, m0, L1, 1);
+    const size_t nbuf1 = (size_t)n * pl.S * pl.cap;
+    uint2 *buf1 = (uint2 *)scratch(kSlotLists, nbuf1 * sizeof(uint2) + 64);
+    char *meta1 = (char *)scratch(kSlotListMeta, (size_t)n * pl.S * 8 + 64);
+    MN_REQUIRE(buf1 && meta1, MN_ENOMEM, "mn_knn_cos_bf16: phase-1 buffer allocation failed");
+    int *cnt1 = (int *)meta1;
+    float *btau1 = (float *)(meta1 + (size_t)n * pl.S * 4);
+    {
+        const int64_t bq = (n + BM - 1) / BM;
+        hipLaunchKernelGGL((k_gram_bf16<GM_COS, 0>), dim3((unsigned)(bq * pl.S)), dim3(NT), 0, s, X,
+                           n, XR, m0, d, (int64_t)0, (int64_t)0, 0, xinv, invp, L1, (int)pl.S,
+                           pl.chunk, pl.cap, buf1, cnt1, btau1);
+        MN_KCHECK(s, "k_gram_bf16<COS> (sample)");
+        hipLaunchKernelGGL(k_tau_cos, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, n,
+                           (int)pl.S, btau1, xn, pm, tcos, tq_pos);
+        MN_KCHECK(s, "k_tau_cos");
+    }
+    tm.mark();
+    // phase 2: positions [m0, n) x all query positions
+    const double expect = (double)L1 * (double)(n - m0) / (double)m0;
+    const ksw::SweepPlan p2 = ksw::plan_sweep(n, n - m0, expect);
+    const int S2 = (int)p2.S, cap2 = p2.cap;
+    const size_t nbuf2 = (size_t)n * S2 * cap2;
+    uint2 *buf2 = (uint2 *)scratch(kSlotX1Buf2, nbuf2 * sizeof(uint2) + 64);
+    int *cnt2 = (int *)scratch(kSlotX1Meta2, (size_t)n * S2 * 4 + 64);
+    MN_REQUIRE(buf2 && cnt2, MN_ENOMEM, "mn_knn_cos_bf16: sweep buffer allocation failed");
+    {
+        const int64_t grid = (n + ksw2::BQ - 1) / ksw2::BQ * p2.S;
+        MN_REQUIRE(grid < INT_MAX, MN_ENOTSUP, "mn_knn_cos_bf16: sweep grid too large");
+        const char *probe = getenv("MN_BF16_PROBE");
+        auto kern = (probe && !strcmp(probe, "noepi")) ? ksw2::k_gram_sweep2<1, ksw2::SW_COS>
+                                                       : ksw2::k_gram_sweep2<0, ksw2::SW_COS>;
+        hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(ksw2::NT), 0, s, XK, n, XK, n, nkb,
+                           (int64_t)0, (int64_t)0, 0, tq_pos, tq_pos, negn, m0, S2, p2.chunk,
+                           cap2, buf2, cnt2);
+        MN_KCHECK(s, "k_gram_sweep2<COS>");
+    }
+    tm.mark();
+    // certification slack (cosine units): phase 1's f32 accumulation of exact
+    // products scaled by two f32 inverse norms, 2 (d + 12) u; the sweep's
+    // dp + 1 terms (products and acc0 = -t|q||c|, |t| <= 1 + ...) with f32
+    // roundings of t|q|, |c| and acc0: 2.5 (dp + 16) u covers both
+    const double delta = 2.5 * ((double)dp + 16.0) * 0x1p-24;
+    int *fb_count = flags + 2, *big_count = flags + 3;
+    int *big_list = fb_list + n;
+#define MN_RRC(NRV, NB, QL, QN, BC, BL)                                                          \
+    hipLaunchKernelGGL(k_cos_rerank_x1<NRV>, dim3((unsigned)(NB)), dim3(256), 0, s, X, n, d, pm, \
+                       xn, xinv, (int)pl.S, pl.cap, buf1, cnt1, btau1, S2, cap2, buf2, cnt2,     \
+                       tcos, topk, delta, o->eps, o->sigma, o->p, QL, QN, BC, BL, out_idx,      \
+                       out_dist, out_w, fb_count, fb_list)
+    MN_RRC(8, (n + 3) / 4, (const int *)nullptr, (const int *)nullptr, big_count, big_list);
+    MN_KCHECK(s, "k_cos_rerank_x1<8>");
+    int hb[4] = {0, 0, 0, 0};
+    MN_HIP_TRY(hipMemcpyAsync(hb, flags, 16, hipMemcpyDeviceToHost, s));
+    MN_HIP_TRY(hipStreamSynchronize(s));
+    if (hb[3] > 0) {
+        MN_RRC(16, (hb[3] + 3) / 4, (const int *)big_list, (const int *)big_count, (int *)nullptr,
+               (int *)nullptr);
+        MN_KCHECK(s, "k_cos_rerank_x1<16>");
+    }
+#undef MN_RRC
+    tm.mark();
+    hipLaunchKernelGGL(k_cos_fallback, dim3((unsigned)std::min<int64_t>(n, 1024)), dim3(FBT), 0, s,
+                       X, X, n, d, (int64_t)0, (int64_t)0, 1, xn, xn, topk, o->eps, o->sigma, o->p,
+                       fb_count, fb_list, out_idx, out_dist, out_w);
+    MN_KCHECK(s, "k_cos_fallback");
+    tm.mark();
+    MN_HIP_TRY(hipMemcpyAsync(hb, flags, 16, hipMemcpyDeviceToHost, s));
+    MN_HIP_TRY(hipStreamSynchronize(s));
+    t_bf16_stats.n_uncertified = hb[2];
+    t_bf16_stats.algo = MN_KNN_BF16X1;
+    t_bf16_stats.slices = (int)pl.S;
+    t_bf16_stats.list_len = L1;
+    t_bf16_stats.sample_rows = m0;
+    t_bf16_stats.sweep_slices = S2;
+    t_bf16_stats.sweep_cap = cap2;
+    if (tm.on) {
+        t_bf16_stats.ms_sample = tm.ms(0, 1);
+        t_bf16_stats.ms_sweep = tm.ms(1, 2);
+        t_bf16_stats.ms_gram = tm.ms(0, 2);
+        t_bf16_stats.ms_rerank = tm.ms(2, 3);
+        t_bf16_stats.ms_fallback = tm.ms(3, 4);
+    }
+    return MN_OK;
 }
 
 static int knn_cos_bf16_impl(const uint16_t *Q, int64_t nq, const uint16_t *C, int64_t nc,
@@ -357,7 +726,7 @@ static int knn_cos_bf16_impl(const uint16_t *Q, int64_t nq, const uint16_t *C, i
     char *g = (char *)scratch(kSlotNorms, (size_t)(nq + nc) * 12 + 256);
     uint2 *cbuf = (uint2 *)scratch(kSlotLists, (size_t)nq * S * cap * sizeof(uint2) + 64);
     char *meta = (char *)scratch(kSlotListMeta, (size_t)nq * S * 8 + 64);
-    int *fb_list = (int *)scratch(kSlotFallback, sizeof(int) * (size_t)nq + 64);
+    int *fb_list = (int *)scratch(kSlotFallback, sizeof(int) * (size_t)nq * 2 + 64);
     int *flags = (int *)scratch(kSlotFlags, 64);
     MN_REQUIRE(g && cbuf && meta && fb_list && flags, MN_ENOMEM,
                "mn_knn_cos_bf16: scratch allocation failed (candidate buffer %zu MB)",
@@ -400,6 +769,23 @@ static int knn_cos_bf16_impl(const uint16_t *Q, int64_t nq, const uint16_t *C, i
     MN_HIP_TRY(hipStreamSynchronize(s));
     MN_REQUIRE(hf[1] == 0, MN_ENONFINITE, "mn_knn_cos_bf16: input contains NaN/inf");
     tm.mark();
+    {
+        // self graphs at scale: the two-phase generator (MN_BF16_X1=0: one phase)
+        const char *xe = getenv("MN_BF16_X1");
+        if (same && !(xe && *xe == '0')) {
+            const float ms_norms = tm.on ? tm.ms(0, 1) : 0.f;
+            const int rc = knn_cos_bf16_x1(Q, nq, d, o, qn, qinv, flags, fb_list, out_idx, out_dist,
+                                           out_w, s);
+            if (rc != 1) {
+                if (tm.on) {
+                    t_bf16_stats.ms_norms = ms_norms;
+                    t_bf16_stats.ms_total = ms_norms + t_bf16_stats.ms_gram +
+                                            t_bf16_stats.ms_rerank + t_bf16_stats.ms_fallback;
+                }
+                return rc;
+            }
+        }
+    }
     if (nc > 0) {
         const char *probe = getenv("MN_BF16_PROBE");
         auto kern = !probe ? k_gram_bf16<GM_COS, 0>

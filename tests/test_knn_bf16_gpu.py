@@ -122,3 +122,35 @@ def test_errors():
     bad[3, 3] = float("nan")
     with pytest.raises(S.MnError):
         S.knn_cos_bf16(bad, 4)
+
+
+def test_two_phase_edge_rows_and_one_phase_agree(monkeypatch):
+    """The two-phase generator (sample thresholds + SW_COS sweep, n >= 2048):
+    zero rows, tiny norms, an antipodal pair, 150 identical rows (ties beyond
+    any threshold -> uncertified -> exact scan) and clustered duplicates, all
+    bit-exact vs the oracle and vs the one-phase generator (MN_BF16_X1=0)."""
+    X = datagen.clustered(6000, 96, seed=13, blobs=30, sigma=0.05, dup_frac=0.02,
+                          zero_frac=0.002)
+    X[20] = -X[21]
+    X[30] *= 1e-7
+    X[40:190] = X[40]
+    Xt, Xf = bf16_rows(X)
+    kw = dict(eps=0.8, sigma=0.5, p=2.0)
+    i, d, w, st = hip(Xt, 16, **kw)
+    assert st["algo"] == 3 and st["sample_rows"] > 0  # MN_KNN_BF16X1
+    assert st["n_uncertified"] >= 150
+    exact((i, d, w), O.knn_cos(Xf, 16, **kw))
+    monkeypatch.setenv("MN_BF16_X1", "0")
+    i1, d1, w1, st1 = hip(Xt, 16, **kw)
+    assert st1["sample_rows"] == 0
+    exact((i, d, w), (i1, d1, w1))
+
+
+@pytest.mark.parametrize("n,d,topk", [(2048 + 1024, 768, 32), (9000, 40, 3), (4500, 3072, 64)])
+def test_two_phase_shapes(n, d, topk):
+    """two-phase at the smallest size it runs at, a d that is not a multiple
+    of 32 (zero-padded KB32 k-blocks), and topk = 64 (L1 = 32)."""
+    Xt, Xf = bf16_rows(datagen.uniform(n, d, seed=n))
+    i, dd, w, st = hip(Xt, topk)
+    assert st["sample_rows"] > 0
+    exact((i, dd, w), O.knn_cos(Xf, topk))
