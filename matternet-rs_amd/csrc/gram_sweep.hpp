@@ -30,6 +30,7 @@
 // query (h = 0, 1 in the two waves of its corpus halves) take positions from
 // one LDS counter per query.
 #pragma once
+#include <cstdlib>
 #include <climits>
 
 #include "common.hpp"
@@ -345,6 +346,8 @@ inline SweepPlan plan_sweep(int64_t nq, int64_t nc2, double expect) {
     SweepPlan p;
     const int64_t nqb = (nq + BQ - 1) / BQ;
     int64_t S = std::max<int64_t>(8, (2048 + nqb - 1) / nqb);
+    const char *es = getenv("MN_SWEEP_S");  // experiments: corpus slices
+    if (es && *es) S = std::max(1, atoi(es));
     S = std::min<int64_t>(S, std::max<int64_t>(1, nc2 / (4 * BC)));
     S = std::max<int64_t>(S, 1);
     int64_t chunk = (nc2 + S - 1) / S;

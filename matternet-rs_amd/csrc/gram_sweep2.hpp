@@ -89,7 +89,13 @@ __device__ __forceinline__ int xcd_remap(int orig, int nwg) {
 // within noise at C2).
 enum SweepMode { SW_L2 = 0, SW_COS = 1 };
 
-template <int PROBE, int MODE = SW_L2>
+// TM (tile-major layout): element (row r, feature e) of Qk / Ck at
+// ((r / 256) nkb + e / 32) * 8192 + (r % 256) * 32 + e % 32, rows padded to a
+// multiple of 256 (allocated; never candidates): a block's k-steps are then
+// consecutive 16-KB pieces of one contiguous 256-row panel instead of pieces
+// n * 64 B apart (one page per k-step and operand), and c_begin / chunk must
+// be multiples of BC.
+template <int PROBE, int MODE = SW_L2, bool TM = false>
 __global__ __launch_bounds__(NT) void k_gram_sweep2(
     const uint16_t *__restrict__ Qk, int64_t nq, const uint16_t *__restrict__ Ck, int64_t nc,
     int nkb, int64_t q_off, int64_t c_off, int excl, const float *__restrict__ tq,
@@ -112,7 +118,8 @@ __global__ __launch_bounds__(NT) void k_gram_sweep2(
 
     if (tid < NWAVES) sm.scnt[tid] = 0;
     if (tid < BQ) {
-        sm.tq[tid] = q0 + tid < nq ? tq[q0 + tid] : -__builtin_inff();
+        // padded queries never qualify (COS: NaN, as -inf * -|c| would be +inf)
+        sm.tq[tid] = q0 + tid < nq ? tq[q0 + tid] : (MODE == SW_COS ? pad : -__builtin_inff());
         sm.qcnt[tid] = 0;
         sm.t0[tid] = q0 + tid < nq ? tau0[q0 + tid] : 0.f;
     }
@@ -128,12 +135,15 @@ __global__ __launch_bounds__(NT) void k_gram_sweep2(
     int bkb = 0, bslot = 0;
     const int prow0 = 32 * w + (lane >> 2), prow1 = prow0 + 16;
     const int pch = 8 * ((lane & 3) ^ (((lane >> 5) & 1) << 1));  // source chunk (swizzle)
-    const int qo0 = min(q0 + prow0, (int)nq - 1) * KB + pch;
-    const int qo1 = min(q0 + prow1, (int)nq - 1) * KB + pch;
-    const int co0 = min(bt0 + prow0, cend - 1) * KB + pch;
-    const int co1 = min(bt0 + prow1, cend - 1) * KB + pch;
-    const uint16_t *cbk = Ck, *qbk = Qk;
-    const int cstep = (int)nc * KB, qstep = (int)nq * KB;
+    const int qo0 = TM ? prow0 * KB + pch : min(q0 + prow0, (int)nq - 1) * KB + pch;
+    const int qo1 = TM ? prow1 * KB + pch : min(q0 + prow1, (int)nq - 1) * KB + pch;
+    const int co0 = TM ? prow0 * KB + pch : min(bt0 + prow0, cend - 1) * KB + pch;
+    const int co1 = TM ? prow1 * KB + pch : min(bt0 + prow1, cend - 1) * KB + pch;
+    const int64_t panel = (int64_t)nkb * BC * KB;  // TM: elements per 256-row panel
+    const uint16_t *const qpan = TM ? Qk + (int64_t)(q0 / BQ) * panel : Qk;
+    auto cpan = [&](int row0) { return TM ? Ck + (int64_t)(row0 / BC) * panel : Ck; };
+    const uint16_t *cbk = cpan(bt0), *qbk = qpan;
+    const int cstep = TM ? BC * KB : (int)nc * KB, qstep = TM ? BQ * KB : (int)nq * KB;
     // LDS-DMA through buffer descriptors: one k-block region ([n][32] bf16,
     // 64-B rows) per descriptor, rebuilt from wave-uniform values per k-step
     // (SALU only); the per-lane 32-bit byte offsets (co*/qo* x 2) are fixed per
@@ -143,7 +153,8 @@ __global__ __launch_bounds__(NT) void k_gram_sweep2(
     const int qb0 = 2 * qo0, qb1 = 2 * qo1;
     int cb0 = 2 * co0, cb1 = 2 * co1;
     // (nc * 32, nq * 32 < 2^31 is checked by the driver: the byte counts fit 32 bits)
-    const int cbytes = (int)(uint32_t)(nc * 64), qbytes = (int)(uint32_t)(nq * 64);
+    const int cbytes = TM ? BC * KB * 2 : (int)(uint32_t)(nc * 64);
+    const int qbytes = TM ? BQ * KB * 2 : (int)(uint32_t)(nq * 64);
     auto dma = [&](__amdgpu_buffer_rsrc_t rs, int voff, uint16_t *lds) {
         __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void *)lds,
                                                  16, voff, 0, 0, 0);
@@ -164,10 +175,12 @@ __global__ __launch_bounds__(NT) void k_gram_sweep2(
             if (++bkb == nkb) {
                 bkb = 0;
                 bt0 += BC;
-                cbk = Ck;
-                qbk = Qk;
-                cb0 = 2 * (min(bt0 + prow0, cend - 1) * KB + pch);
-                cb1 = 2 * (min(bt0 + prow1, cend - 1) * KB + pch);
+                cbk = cpan(bt0);
+                qbk = qpan;
+                if constexpr (!TM) {
+                    cb0 = 2 * (min(bt0 + prow0, cend - 1) * KB + pch);
+                    cb1 = 2 * (min(bt0 + prow1, cend - 1) * KB + pch);
+                }
             }
         }
     };

@@ -364,15 +364,36 @@ inline Perm make_perm_ab(int64_t n) {
 // KB32 copy [dp/32][n][32] (zero-padded past d) of rows perm(p) (perm.n == 0:
 // identity); one thread per 16 B of output, consecutive threads write
 // consecutive bytes of one k-block
+// tm: the tile-major variant (gram_sweep2.hpp TM; rows padded to 256 with
+// zeros, n_pad = n rounded up), output written linearly
 __global__ __launch_bounds__(256) void k_to_kb32(const uint16_t *__restrict__ X, int64_t n, int d,
-                                                 int dp, Perm pm, uint16_t *__restrict__ XK) {
+                                                 int dp, Perm pm, uint16_t *__restrict__ XK,
+                                                 int tm) {
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const int64_t per_kb = n * 4;
-    if (t >= per_kb * (dp / 32)) return;
-    const int kb = (int)(t / per_kb);
-    const int64_t rem = t - (int64_t)kb * per_kb;
-    const int64_t p = rem >> 2;
-    const int cc = (int)(rem & 3);
+    const int nkb = dp / 32;
+    const int64_t rows = tm ? (n + 255) / 256 * 256 : n;
+    const int64_t per_kb = rows * 4;
+    if (t >= per_kb * nkb) return;
+    int kb, cc;
+    int64_t p, o;
+    if (tm) {
+        cc = (int)(t & 3);
+        const int r = (int)((t >> 2) & 255);
+        const int64_t pk = t >> 10;  // panel * nkb + kb
+        kb = (int)(pk % nkb);
+        p = (pk / nkb) * 256 + r;
+        o = t * 8;
+    } else {
+        kb = (int)(t / per_kb);
+        const int64_t rem = t - (int64_t)kb * per_kb;
+        p = rem >> 2;
+        cc = (int)(rem & 3);
+        o = ((int64_t)kb * n + p) * 32 + 8 * cc;
+    }
+    if (p >= n) {  // padded rows (tile-major only)
+        *reinterpret_cast<uint4 *>(XK + o) = make_uint4(0u, 0u, 0u, 0u);
+        return;
+    }
     const int64_t src = pm.n ? pm(p) : p;
     const int e0 = 32 * kb + 8 * cc;
     uint4 v = make_uint4(0u, 0u, 0u, 0u);
@@ -385,7 +406,7 @@ __global__ __launch_bounds__(256) void k_to_kb32(const uint16_t *__restrict__ X,
         v = make_uint4(h[0] | ((uint32_t)h[1] << 16), h[2] | ((uint32_t)h[3] << 16),
                        h[4] | ((uint32_t)h[5] << 16), h[6] | ((uint32_t)h[7] << 16));
     }
-    *reinterpret_cast<uint4 *>(XK + ((int64_t)kb * n + p) * 32 + 8 * cc) = v;
+    *reinterpret_cast<uint4 *>(XK + o) = v;
 }
 
 // row-major copy of the sample positions [0, m) (stride d), 16 B per thread
@@ -583,13 +604,16 @@ static int knn_cos_bf16_x1(const uint16_t *X, int64_t n, int32_t d, const mn_cos
     const char *fl = getenv("MN_BF16_L1");  // experiments: phase-1 list length
     if (fl && *fl) L1 = std::min(std::max(atoi(fl), 4), 48);
     int64_t m0 = std::max<int64_t>(n / 16, (int64_t)64 * L1);
-    m0 = (m0 + BN - 1) / BN * BN;
+    m0 = (m0 + 255) / 256 * 256;  // whole sweep tiles (TM) and phase-1 tiles
     if (m0 + 4 * ksw2::BC > n || n * 32 >= INT_MAX || n >= INT_MAX) return 1;
     const int dp = (d + 255) / 256 * 256;  // KB32 k-blocks, nkb >= 8 (sweep2's prefetch)
     const int nkb = dp / 32;
     const Perm pm = make_perm_ab(n);
 
-    uint16_t *XK = (uint16_t *)scratch(kSlotX1CK, (size_t)n * dp * 2 + 64);
+    const char *te = getenv("MN_BF16_TM");  // layout A/B: 0 = k-block-major KB32
+    const int tmaj = (te && *te == '0') ? 0 : 1;
+    const int64_t nrows = tmaj ? (n + 255) / 256 * 256 : n;
+    uint16_t *XK = (uint16_t *)scratch(kSlotX1CK, (size_t)nrows * dp * 2 + 64);
     uint16_t *XR = (uint16_t *)scratch(kSlotX1CR, (size_t)m0 * d * 2 + 64);
     float *aux = (float *)scratch(kSlotX1Aux, (size_t)n * 16 + 256);
     MN_REQUIRE(XK && XR && aux, MN_ENOMEM, "mn_knn_cos_bf16: two-phase scratch allocation failed");
@@ -598,9 +622,9 @@ static int knn_cos_bf16_x1(const uint16_t *X, int64_t n, int32_t d, const mn_cos
     Timer tm;
     tm.start(o->timing != 0, s);
     {
-        const int64_t nt = n * 4 * nkb;
+        const int64_t nt = nrows * 4 * nkb;
         hipLaunchKernelGGL(k_to_kb32, dim3((unsigned)((nt + 255) / 256)), dim3(256), 0, s, X, n, d,
-                           dp, pm, XK);
+                           dp, pm, XK, tmaj);
         const int64_t ns = m0 * (d / 8);
         hipLaunchKernelGGL(k_sample_rows, dim3((unsigned)((ns + 255) / 256)), dim3(256), 0, s, X, m0,
                            d, pm, XR);
@@ -639,12 +663,27 @@ static int knn_cos_bf16_x1(const uint16_t *X, int64_t n, int32_t d, const mn_cos
         const int64_t grid = (n + ksw2::BQ - 1) / ksw2::BQ * p2.S;
         MN_REQUIRE(grid < INT_MAX, MN_ENOTSUP, "mn_knn_cos_bf16: sweep grid too large");
         const char *probe = getenv("MN_BF16_PROBE");
-        auto kern = (probe && !strcmp(probe, "noepi")) ? ksw2::k_gram_sweep2<1, ksw2::SW_COS>
-                                                       : ksw2::k_gram_sweep2<0, ksw2::SW_COS>;
+        const bool noepi = probe && !strcmp(probe, "noepi");
+        auto kern = tmaj ? (noepi ? ksw2::k_gram_sweep2<1, ksw2::SW_COS, true>
+                                  : ksw2::k_gram_sweep2<0, ksw2::SW_COS, true>)
+                         : (noepi ? ksw2::k_gram_sweep2<1, ksw2::SW_COS, false>
+                                  : ksw2::k_gram_sweep2<0, ksw2::SW_COS, false>);
         hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(ksw2::NT), 0, s, XK, n, XK, n, nkb,
                            (int64_t)0, (int64_t)0, 0, tq_pos, tq_pos, negn, m0, S2, p2.chunk,
                            cap2, buf2, cnt2);
         MN_KCHECK(s, "k_gram_sweep2<COS>");
+        if (probe && *probe) {  // timing probe: no outputs are produced
+            tm.mark();
+            MN_HIP_TRY(hipStreamSynchronize(s));
+            if (tm.on) {
+                t_bf16_stats.ms_sample = tm.ms(0, 1);
+                t_bf16_stats.ms_sweep = tm.ms(1, 2);
+                t_bf16_stats.ms_gram = tm.ms(0, 2);
+            }
+            t_bf16_stats.sample_rows = m0;
+            t_bf16_stats.sweep_slices = S2;
+            return MN_OK;
+        }
     }
     tm.mark();
     // certification slack (cosine units): phase 1's f32 accumulation of exact

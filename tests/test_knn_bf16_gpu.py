@@ -140,6 +140,9 @@ def test_two_phase_edge_rows_and_one_phase_agree(monkeypatch):
     assert st["algo"] == 3 and st["sample_rows"] > 0  # MN_KNN_BF16X1
     assert st["n_uncertified"] >= 150
     exact((i, d, w), O.knn_cos(Xf, 16, **kw))
+    monkeypatch.setenv("MN_BF16_TM", "0")  # k-block-major sweep layout
+    exact((i, d, w), hip(Xt, 16, **kw)[:3])
+    monkeypatch.delenv("MN_BF16_TM")
     monkeypatch.setenv("MN_BF16_X1", "0")
     i1, d1, w1, st1 = hip(Xt, 16, **kw)
     assert st1["sample_rows"] == 0
