@@ -658,6 +658,13 @@ __global__ __launch_bounds__(256) void k_rerank_buf(
 // (d + 3) u (|T| + 2E).
 // ---------------------------------------------------------------------------
 
+// element offset of (row, k-block kb) in a KB32 copy of n rows: k-block-major
+// [nkb][n][32], or tile-major (tm, gram_sweep2.hpp TM) [n/256][nkb][256][32]
+__device__ __forceinline__ int64_t kb32_at(int64_t row, int kb, int64_t n, int nkb, int tm) {
+    return tm ? ((((row >> 8) * nkb + kb) << 13) + ((row & 255) << 5))
+              : (((int64_t)kb * n + row) << 5);
+}
+
 // bounds must never round down: v >= 0
 __device__ __forceinline__ float f32_up(double v) {
     float f = (float)v;
@@ -677,7 +684,7 @@ __global__ __launch_bounds__(256) void k_prep_x1(const float *__restrict__ X, in
                                                  float *__restrict__ hcv, float *__restrict__ hn,
                                                  float *__restrict__ rn,
                                                  unsigned *__restrict__ maxbits,
-                                                 int *__restrict__ flags, int corpus) {
+                                                 int *__restrict__ flags, int corpus, int tm) {
     const int lane = threadIdx.x & 63, hl = lane >> 5, ll = lane & 31;
     const int64_t wave0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
@@ -720,7 +727,7 @@ __global__ __launch_bounds__(256) void k_prep_x1(const float *__restrict__ X, in
             if (live) {
                 const uint4 pk = make_uint4(wv[0], wv[1], wv[2], wv[3]);
                 *reinterpret_cast<uint4 *>(XR + row * (int64_t)dp + t0) = pk;
-                *reinterpret_cast<uint4 *>(XK + ((int64_t)(t0 >> 5) * n + row) * 32 + (t0 & 31)) =
+                *reinterpret_cast<uint4 *>(XK + kb32_at(row, t0 >> 5, n, dp >> 5, tm) + (t0 & 31)) =
                     pk;
             }
         }
@@ -784,7 +791,7 @@ __global__ __launch_bounds__(256) void k_prep_x3(const float *__restrict__ X, in
                                                  uint16_t *__restrict__ XK, int corpus,
                                                  float *__restrict__ nrm, float *__restrict__ hn,
                                                  float *__restrict__ ln, float *__restrict__ r2n,
-                                                 unsigned *__restrict__ cmax3) {
+                                                 unsigned *__restrict__ cmax3, int tm) {
     const int lane = threadIdx.x & 63, hl = lane >> 5, ll = lane & 31;
     const int64_t wave0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
@@ -833,10 +840,12 @@ __global__ __launch_bounds__(256) void k_prep_x3(const float *__restrict__ X, in
             if (live) {
                 const uint4 H = make_uint4(hw[0], hw[1], hw[2], hw[3]);
                 const uint4 Lo = make_uint4(lw[0], lw[1], lw[2], lw[3]);
-                const int64_t kb = t0 >> 5, off = row * 32 + (t0 & 31);
-                *reinterpret_cast<uint4 *>(XK + (kb * n) * 32 + off) = H;
-                *reinterpret_cast<uint4 *>(XK + ((kb + nkb) * n) * 32 + off) = corpus ? Lo : H;
-                *reinterpret_cast<uint4 *>(XK + ((kb + 2 * nkb) * n) * 32 + off) = corpus ? H : Lo;
+                const int kb = t0 >> 5, ko = t0 & 31, n3 = 3 * nkb;
+                *reinterpret_cast<uint4 *>(XK + kb32_at(row, kb, n, n3, tm) + ko) = H;
+                *reinterpret_cast<uint4 *>(XK + kb32_at(row, kb + nkb, n, n3, tm) + ko) =
+                    corpus ? Lo : H;
+                *reinterpret_cast<uint4 *>(XK + kb32_at(row, kb + 2 * nkb, n, n3, tm) + ko) =
+                    corpus ? H : Lo;
             }
         }
 #pragma unroll
@@ -1506,9 +1515,14 @@ static int knn_x1(const float *Q, int64_t nq, const float *C, int64_t nc, int32_
     // perm[p]), so the phase-1 sample is the contiguous prefix [0, m0) and the
     // sweep covers [m0, nc); ids are mapped back through perm in the re-rank
     uint16_t *QR = (uint16_t *)scratch(kSlotX1QR, (size_t)nq * dp * 2 + 64);
-    uint16_t *QK = (uint16_t *)scratch(kSlotX1QK, (size_t)nq * dp * 2 + 64);
+    // sweep2 reads tile-major KB32 (rows padded to whole 256-row panels; the
+    // pad rows are never candidates); the legacy sweep the k-block-major form
+    const char *tme = getenv("MN_X1_TM");  // layout A/B: 0 = k-block-major for sweep2 too
+    const int tmaj = (sweep_version() == 1 || (tme && *tme == '0')) ? 0 : 1;
+    auto pad256 = [&](int64_t r) { return tmaj ? (r + 255) / 256 * 256 : r; };
+    uint16_t *QK = (uint16_t *)scratch(kSlotX1QK, (size_t)pad256(nq) * dp * 2 + 64);
     uint16_t *CR = (uint16_t *)scratch(kSlotX1CR, (size_t)nc * dp * 2 + 64);
-    uint16_t *CK = (uint16_t *)scratch(kSlotX1CK, (size_t)nc * dp * 2 + 64);
+    uint16_t *CK = (uint16_t *)scratch(kSlotX1CK, (size_t)pad256(nc) * dp * 2 + 64);
     char *aux = (char *)scratch(kSlotX1Aux, (size_t)nq * 28 + (size_t)nc * 8 + 256);
     int *flags = (int *)scratch(kSlotFlags, 64);
     int *fb_list = (int *)scratch(kSlotFallback, sizeof(int) * (size_t)nq * 2 + 64);
@@ -1532,10 +1546,10 @@ static int knn_x1(const float *Q, int64_t nq, const float *C, int64_t nc, int32_
         const int64_t blocks = std::min<int64_t>((n + 7) / 8, 16384);
         if (vec4)
             hipLaunchKernelGGL(k_prep_x1<true>, dim3((unsigned)blocks), dim3(256), 0, s, X, n, d,
-                               dp, pm, R, K, nv, hcv, hv, rv, cmax, flags + 3, corpus);
+                               dp, pm, R, K, nv, hcv, hv, rv, cmax, flags + 3, corpus, tmaj);
         else
             hipLaunchKernelGGL(k_prep_x1<false>, dim3((unsigned)blocks), dim3(256), 0, s, X, n, d,
-                               dp, pm, R, K, nv, hcv, hv, rv, cmax, flags + 3, corpus);
+                               dp, pm, R, K, nv, hcv, hv, rv, cmax, flags + 3, corpus, tmaj);
     };
     prep(Q, nq, nullptr, QR, QK, qn, nullptr, qhn, qrn, 0);
     prep(C, nc, perm, CR, CK, cnv, chc, nullptr, nullptr, 1);
@@ -1556,7 +1570,7 @@ static int knn_x1(const float *Q, int64_t nq, const float *C, int64_t nc, int32_
     const char *fs = getenv("MN_X1_SAMPLE_DIV");  // experiments: sample = nc / div
     const int64_t div = (fs && *fs) ? std::max(2, atoi(fs)) : 16;
     int64_t m0 = std::max<int64_t>(nc / div, (int64_t)64 * L1);
-    m0 = (m0 + kb16::BN - 1) / kb16::BN * kb16::BN;
+    m0 = (m0 + 255) / 256 * 256;  // whole phase-1 tiles and whole sweep panels
     const bool two = m0 + 4 * ksw::BC <= nc;
     if (!two) {
         m0 = nc;
@@ -1615,11 +1629,13 @@ static int knn_x1(const float *Q, int64_t nq, const float *C, int64_t nc, int32_
                                nkb, q_off, (int64_t)0, 0, tq, tau0, chc, m0, S2, p2.chunk, cap2,
                                cbuf2, cnt2);
         } else {
-            auto kern = !noepi ? ksw2::k_gram_sweep2<0>
-                        : !strcmp(probe, "nodma") ? ksw2::k_gram_sweep2<2>
-                        : !strcmp(probe, "noread") ? ksw2::k_gram_sweep2<3>
-                        : !strcmp(probe, "nowait") ? ksw2::k_gram_sweep2<4>
-                                                   : ksw2::k_gram_sweep2<1>;
+            using ksw2::SW_L2;
+            auto kern = !noepi ? (tmaj ? ksw2::k_gram_sweep2<0, SW_L2, true>
+                                     : ksw2::k_gram_sweep2<0, SW_L2, false>)
+                        : !strcmp(probe, "nodma") ? ksw2::k_gram_sweep2<2, SW_L2, true>
+                        : !strcmp(probe, "noread") ? ksw2::k_gram_sweep2<3, SW_L2, true>
+                        : !strcmp(probe, "nowait") ? ksw2::k_gram_sweep2<4, SW_L2, true>
+                                                   : ksw2::k_gram_sweep2<1, SW_L2, true>;
             hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(ksw2::NT), 0, s, QK, nq, CK, nc,
                                nkb, q_off, (int64_t)0, 0, tq, tau0, chc, m0, S2, p2.chunk, cap2,
                                cbuf2, cnt2);
@@ -1687,8 +1703,8 @@ static int knn_x1(const float *Q, int64_t nq, const float *C, int64_t nc, int32_
         const int nkb3 = 3 * nkb;
         char *eb = (char *)scratch(kSlotX1Esc, (size_t)nfb * 32 + 256);
         // the row-major phase-1 copies are dead: their slots hold the 3 dp copies
-        uint16_t *CK3 = (uint16_t *)scratch(kSlotX1CR, (size_t)nc * dp * 6 + 64);
-        uint16_t *QK3 = (uint16_t *)scratch(kSlotX1QR, (size_t)nfb * dp * 6 + 64);
+        uint16_t *CK3 = (uint16_t *)scratch(kSlotX1CR, (size_t)pad256(nc) * dp * 6 + 64);
+        uint16_t *QK3 = (uint16_t *)scratch(kSlotX1QR, (size_t)pad256(nfb) * dp * 6 + 64);
         MN_REQUIRE(eb && CK3 && QK3, MN_ENOMEM, "mn_knn: refill scratch allocation failed");
         int *erows = (int *)eb;
         float *qn3 = (float *)(eb + (((size_t)nfb * 4 + 15) & ~(size_t)15));
@@ -1703,10 +1719,10 @@ static int knn_x1(const float *Q, int64_t nq, const float *C, int64_t nc, int32_
             const int64_t blocks = std::min<int64_t>((n + 7) / 8, 16384);
             if (vec4)
                 hipLaunchKernelGGL(k_prep_x3<true>, dim3((unsigned)blocks), dim3(256), 0, s, X, n,
-                                   d, dp, src, K, corpus, nv, hv, lv, rv, cmax3);
+                                   d, dp, src, K, corpus, nv, hv, lv, rv, cmax3, tmaj);
             else
                 hipLaunchKernelGGL(k_prep_x3<false>, dim3((unsigned)blocks), dim3(256), 0, s, X, n,
-                                   d, dp, src, K, corpus, nv, hv, lv, rv, cmax3);
+                                   d, dp, src, K, corpus, nv, hv, lv, rv, cmax3, tmaj);
         };
         prep3(C, nc, perm, CK3, 1, nullptr, nullptr, nullptr, nullptr);
         prep3(Q, nfb, erows, QK3, 0, qn3, qh3, ql3, q23);
@@ -1730,7 +1746,9 @@ static int knn_x1(const float *Q, int64_t nq, const float *C, int64_t nc, int32_
                                QK3, (int64_t)nfb, CK3, nc, nkb3, (int64_t)0, (int64_t)0, 0, tq3,
                                tau3, chc, (int64_t)0, (int)p3.S, p3.chunk, p3.cap, cbuf3, cnt3);
         else
-            hipLaunchKernelGGL(ksw2::k_gram_sweep2<0>, dim3((unsigned)grid3), dim3(ksw2::NT), 0, s,
+            hipLaunchKernelGGL((tmaj ? ksw2::k_gram_sweep2<0, ksw2::SW_L2, true>
+                                   : ksw2::k_gram_sweep2<0, ksw2::SW_L2, false>),
+                               dim3((unsigned)grid3), dim3(ksw2::NT), 0, s,
                                QK3, (int64_t)nfb, CK3, nc, nkb3, (int64_t)0, (int64_t)0, 0, tq3,
                                tau3, chc, (int64_t)0, (int)p3.S, p3.chunk, p3.cap, cbuf3, cnt3);
         MN_KCHECK(s, "k_gram_sweep<x3>");

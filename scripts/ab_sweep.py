@@ -1,7 +1,9 @@
 """A/B of the two phase-2 sweep kernels (MN_X1_SWEEP=1 gram_sweep.hpp vs 2
 gram_sweep2.hpp) in ONE process on the same device and data (guide rule 24):
 C2 shape by default, interleaved rounds, outputs compared bit for bit.
-  python scripts/ab_sweep.py [n] [d] [rounds]"""
+  python scripts/ab_sweep.py [n] [d] [rounds]
+AB_ENVS="MN_X1_TM=1;MN_X1_TM=0" compares environment variants instead
+(';' between variants, ',' between assignments)."""
 import json
 import os
 import sys
@@ -21,12 +23,17 @@ X = torch.empty((n, d), dtype=torch.float32, device="cuda")
 _lib.check(_lib.lib().mn_fill_uniform_f32(X.data_ptr(), n, d, 42, 0, None))
 torch.cuda.synchronize()
 ref = None
-VERS = [int(v) for v in os.environ.get("AB_VERSIONS", "1,2").split(",")]
+if os.environ.get("AB_ENVS"):
+    VERS = os.environ["AB_ENVS"].split(";")
+else:
+    VERS = ["MN_X1_SWEEP=" + v for v in os.environ.get("AB_VERSIONS", "1,2").split(",")]
 res = {v: [] for v in VERS}
 probe = {v: [] for v in VERS}
 for r in range(rounds):
     for v in VERS:
-        os.environ["MN_X1_SWEEP"] = str(v)
+        for kv in v.split(","):
+            k_, val = kv.split("=")
+            os.environ[k_] = val
         os.environ.pop("MN_X1_PROBE", None)
         t = time.time()
         out = S.knn_l2sq(X, 32, timing=True, algo="bf16x1")
