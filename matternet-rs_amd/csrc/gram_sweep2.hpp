@@ -90,7 +90,8 @@ __device__ __forceinline__ int xcd_remap(int orig, int nwg) {
 enum SweepMode { SW_L2 = 0, SW_COS = 1 };
 
 // TM (tile-major layout): element (row r, feature e) of Qk / Ck at
-// ((r / 256) nkb + e / 32) * 8192 + (r % 256) * 32 + e % 32, rows padded to a
+// ((r / 256) pst + e / 32) * 8192 + (r % 256) * 32 + e % 32 (pst >= nkb: the
+// panel stride in k-steps, padded so panels do not alias), rows padded to a
 // multiple of 256 (allocated; never candidates): a block's k-steps are then
 // consecutive 16-KB pieces of one contiguous 256-row panel instead of pieces
 // n * 64 B apart (one page per k-step and operand), and c_begin / chunk must
@@ -100,7 +101,7 @@ __global__ __launch_bounds__(NT) void k_gram_sweep2(
     const uint16_t *__restrict__ Qk, int64_t nq, const uint16_t *__restrict__ Ck, int64_t nc,
     int nkb, int64_t q_off, int64_t c_off, int excl, const float *__restrict__ tq,
     const float *__restrict__ tau0, const float *__restrict__ hc, int64_t c_begin, int S,
-    int64_t chunk, int cap, uint2 *__restrict__ buf, int *__restrict__ cnt) {
+    int64_t chunk, int cap, uint2 *__restrict__ buf, int *__restrict__ cnt, int pst = 0) {
     __shared__ Smem sm;
     const int tid = threadIdx.x, lane = tid & 63;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -139,7 +140,7 @@ __global__ __launch_bounds__(NT) void k_gram_sweep2(
     const int qo1 = TM ? prow1 * KB + pch : min(q0 + prow1, (int)nq - 1) * KB + pch;
     const int co0 = TM ? prow0 * KB + pch : min(bt0 + prow0, cend - 1) * KB + pch;
     const int co1 = TM ? prow1 * KB + pch : min(bt0 + prow1, cend - 1) * KB + pch;
-    const int64_t panel = (int64_t)nkb * BC * KB;  // TM: elements per 256-row panel
+    const int64_t panel = (int64_t)pst * BC * KB;  // TM: elements between 256-row panels
     const uint16_t *const qpan = TM ? Qk + (int64_t)(q0 / BQ) * panel : Qk;
     auto cpan = [&](int row0) { return TM ? Ck + (int64_t)(row0 / BC) * panel : Ck; };
     const uint16_t *cbk = cpan(bt0), *qbk = qpan;

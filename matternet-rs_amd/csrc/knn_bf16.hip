@@ -364,8 +364,8 @@ inline Perm make_perm_ab(int64_t n) {
 // KB32 copy [dp/32][n][32] (zero-padded past d) of rows perm(p) (perm.n == 0:
 // identity); one thread per 16 B of output, consecutive threads write
 // consecutive bytes of one k-block
-// tm: the tile-major variant (gram_sweep2.hpp TM; rows padded to 256 with
-// zeros, n_pad = n rounded up), output written linearly
+// tm > 0: the tile-major variant with panel stride tm k-blocks (gram_sweep2.hpp
+// TM; rows padded to 256 with zeros, n_pad = n rounded up)
 __global__ __launch_bounds__(256) void k_to_kb32(const uint16_t *__restrict__ X, int64_t n, int d,
                                                  int dp, Perm pm, uint16_t *__restrict__ XK,
                                                  int tm) {
@@ -381,8 +381,9 @@ __global__ __launch_bounds__(256) void k_to_kb32(const uint16_t *__restrict__ X,
         const int r = (int)((t >> 2) & 255);
         const int64_t pk = t >> 10;  // panel * nkb + kb
         kb = (int)(pk % nkb);
-        p = (pk / nkb) * 256 + r;
-        o = t * 8;
+        const int64_t panel = pk / nkb;
+        p = panel * 256 + r;
+        o = ((panel * tm + kb) << 13) + (r << 5) + 8 * cc;
     } else {
         kb = (int)(t / per_kb);
         const int64_t rem = t - (int64_t)kb * per_kb;
@@ -612,8 +613,10 @@ static int knn_cos_bf16_x1(const uint16_t *X, int64_t n, int32_t d, const mn_cos
 
     const char *te = getenv("MN_BF16_TM");  // layout A/B: 0 = k-block-major KB32
     const int tmaj = (te && *te == '0') ? 0 : 1;
+    const char *tpe = getenv("MN_TM_PAD");  // panel stride nkb + pad k-blocks (default 1)
+    const int pst = tmaj ? nkb + ((tpe && *tpe) ? std::max(0, atoi(tpe)) : 1) : 0;
     const int64_t nrows = tmaj ? (n + 255) / 256 * 256 : n;
-    uint16_t *XK = (uint16_t *)scratch(kSlotX1CK, (size_t)nrows * dp * 2 + 64);
+    uint16_t *XK = (uint16_t *)scratch(kSlotX1CK, (size_t)nrows * (tmaj ? pst * 32 : dp) * 2 + 64);
     uint16_t *XR = (uint16_t *)scratch(kSlotX1CR, (size_t)m0 * d * 2 + 64);
     float *aux = (float *)scratch(kSlotX1Aux, (size_t)n * 16 + 256);
     MN_REQUIRE(XK && XR && aux, MN_ENOMEM, "mn_knn_cos_bf16: two-phase scratch allocation failed");
@@ -624,7 +627,7 @@ static int knn_cos_bf16_x1(const uint16_t *X, int64_t n, int32_t d, const mn_cos
     {
         const int64_t nt = nrows * 4 * nkb;
         hipLaunchKernelGGL(k_to_kb32, dim3((unsigned)((nt + 255) / 256)), dim3(256), 0, s, X, n, d,
-                           dp, pm, XK, tmaj);
+                           dp, pm, XK, pst);
         const int64_t ns = m0 * (d / 8);
         hipLaunchKernelGGL(k_sample_rows, dim3((unsigned)((ns + 255) / 256)), dim3(256), 0, s, X, m0,
                            d, pm, XR);
@@ -670,7 +673,7 @@ static int knn_cos_bf16_x1(const uint16_t *X, int64_t n, int32_t d, const mn_cos
                                   : ksw2::k_gram_sweep2<0, ksw2::SW_COS, false>);
         hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(ksw2::NT), 0, s, XK, n, XK, n, nkb,
                            (int64_t)0, (int64_t)0, 0, tq_pos, tq_pos, negn, m0, S2, p2.chunk,
-                           cap2, buf2, cnt2);
+                           cap2, buf2, cnt2, pst);
         MN_KCHECK(s, "k_gram_sweep2<COS>");
         if (probe && *probe) {  // timing probe: no outputs are produced
             tm.mark();

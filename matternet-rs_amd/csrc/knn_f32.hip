@@ -659,9 +659,10 @@ __global__ __launch_bounds__(256) void k_rerank_buf(
 // ---------------------------------------------------------------------------
 
 // element offset of (row, k-block kb) in a KB32 copy of n rows: k-block-major
-// [nkb][n][32], or tile-major (tm, gram_sweep2.hpp TM) [n/256][nkb][256][32]
-__device__ __forceinline__ int64_t kb32_at(int64_t row, int kb, int64_t n, int nkb, int tm) {
-    return tm ? ((((row >> 8) * nkb + kb) << 13) + ((row & 255) << 5))
+// [nkb][n][32], or tile-major (tm = the panel stride in k-blocks, >= nkb;
+// gram_sweep2.hpp TM) [n/256][tm][256][32]
+__device__ __forceinline__ int64_t kb32_at(int64_t row, int kb, int64_t n, int tm) {
+    return tm ? ((((row >> 8) * tm + kb) << 13) + ((row & 255) << 5))
               : (((int64_t)kb * n + row) << 5);
 }
 
@@ -727,7 +728,7 @@ __global__ __launch_bounds__(256) void k_prep_x1(const float *__restrict__ X, in
             if (live) {
                 const uint4 pk = make_uint4(wv[0], wv[1], wv[2], wv[3]);
                 *reinterpret_cast<uint4 *>(XR + row * (int64_t)dp + t0) = pk;
-                *reinterpret_cast<uint4 *>(XK + kb32_at(row, t0 >> 5, n, dp >> 5, tm) + (t0 & 31)) =
+                *reinterpret_cast<uint4 *>(XK + kb32_at(row, t0 >> 5, n, tm) + (t0 & 31)) =
                     pk;
             }
         }
@@ -840,11 +841,11 @@ __global__ __launch_bounds__(256) void k_prep_x3(const float *__restrict__ X, in
             if (live) {
                 const uint4 H = make_uint4(hw[0], hw[1], hw[2], hw[3]);
                 const uint4 Lo = make_uint4(lw[0], lw[1], lw[2], lw[3]);
-                const int kb = t0 >> 5, ko = t0 & 31, n3 = 3 * nkb;
-                *reinterpret_cast<uint4 *>(XK + kb32_at(row, kb, n, n3, tm) + ko) = H;
-                *reinterpret_cast<uint4 *>(XK + kb32_at(row, kb + nkb, n, n3, tm) + ko) =
+                const int kb = t0 >> 5, ko = t0 & 31;
+                *reinterpret_cast<uint4 *>(XK + kb32_at(row, kb, n, tm) + ko) = H;
+                *reinterpret_cast<uint4 *>(XK + kb32_at(row, kb + nkb, n, tm) + ko) =
                     corpus ? Lo : H;
-                *reinterpret_cast<uint4 *>(XK + kb32_at(row, kb + 2 * nkb, n, n3, tm) + ko) =
+                *reinterpret_cast<uint4 *>(XK + kb32_at(row, kb + 2 * nkb, n, tm) + ko) =
                     corpus ? H : Lo;
             }
         }
@@ -1519,10 +1520,15 @@ static int knn_x1(const float *Q, int64_t nq, const float *C, int64_t nc, int32_
     // pad rows are never candidates); the legacy sweep the k-block-major form
     const char *tme = getenv("MN_X1_TM");  // layout A/B: 0 = k-block-major for sweep2 too
     const int tmaj = (sweep_version() == 1 || (tme && *tme == '0')) ? 0 : 1;
+    // tile-major panel stride: nkb + TM_PAD k-blocks (MN_TM_PAD, default 1)
+    const char *tpe = getenv("MN_TM_PAD");
+    const int tpad = (tpe && *tpe) ? std::max(0, atoi(tpe)) : 1;
+    const int pst1 = tmaj ? nkb + tpad : 0, pst3 = tmaj ? 3 * nkb + tpad : 0;
     auto pad256 = [&](int64_t r) { return tmaj ? (r + 255) / 256 * 256 : r; };
-    uint16_t *QK = (uint16_t *)scratch(kSlotX1QK, (size_t)pad256(nq) * dp * 2 + 64);
+    const int64_t kbw1 = tmaj ? (int64_t)pst1 * 32 : dp, kbw3 = tmaj ? (int64_t)pst3 * 32 : 3 * dp;
+    uint16_t *QK = (uint16_t *)scratch(kSlotX1QK, (size_t)pad256(nq) * kbw1 * 2 + 64);
     uint16_t *CR = (uint16_t *)scratch(kSlotX1CR, (size_t)nc * dp * 2 + 64);
-    uint16_t *CK = (uint16_t *)scratch(kSlotX1CK, (size_t)pad256(nc) * dp * 2 + 64);
+    uint16_t *CK = (uint16_t *)scratch(kSlotX1CK, (size_t)pad256(nc) * kbw1 * 2 + 64);
     char *aux = (char *)scratch(kSlotX1Aux, (size_t)nq * 28 + (size_t)nc * 8 + 256);
     int *flags = (int *)scratch(kSlotFlags, 64);
     int *fb_list = (int *)scratch(kSlotFallback, sizeof(int) * (size_t)nq * 2 + 64);
@@ -1546,10 +1552,10 @@ static int knn_x1(const float *Q, int64_t nq, const float *C, int64_t nc, int32_
         const int64_t blocks = std::min<int64_t>((n + 7) / 8, 16384);
         if (vec4)
             hipLaunchKernelGGL(k_prep_x1<true>, dim3((unsigned)blocks), dim3(256), 0, s, X, n, d,
-                               dp, pm, R, K, nv, hcv, hv, rv, cmax, flags + 3, corpus, tmaj);
+                               dp, pm, R, K, nv, hcv, hv, rv, cmax, flags + 3, corpus, pst1);
         else
             hipLaunchKernelGGL(k_prep_x1<false>, dim3((unsigned)blocks), dim3(256), 0, s, X, n, d,
-                               dp, pm, R, K, nv, hcv, hv, rv, cmax, flags + 3, corpus, tmaj);
+                               dp, pm, R, K, nv, hcv, hv, rv, cmax, flags + 3, corpus, pst1);
     };
     prep(Q, nq, nullptr, QR, QK, qn, nullptr, qhn, qrn, 0);
     prep(C, nc, perm, CR, CK, cnv, chc, nullptr, nullptr, 1);
@@ -1638,7 +1644,7 @@ static int knn_x1(const float *Q, int64_t nq, const float *C, int64_t nc, int32_
                                                    : ksw2::k_gram_sweep2<1, SW_L2, true>;
             hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(ksw2::NT), 0, s, QK, nq, CK, nc,
                                nkb, q_off, (int64_t)0, 0, tq, tau0, chc, m0, S2, p2.chunk, cap2,
-                               cbuf2, cnt2);
+                               cbuf2, cnt2, pst1);
         }
         MN_KCHECK(s, "k_gram_sweep");
     }
@@ -1703,8 +1709,8 @@ static int knn_x1(const float *Q, int64_t nq, const float *C, int64_t nc, int32_
         const int nkb3 = 3 * nkb;
         char *eb = (char *)scratch(kSlotX1Esc, (size_t)nfb * 32 + 256);
         // the row-major phase-1 copies are dead: their slots hold the 3 dp copies
-        uint16_t *CK3 = (uint16_t *)scratch(kSlotX1CR, (size_t)pad256(nc) * dp * 6 + 64);
-        uint16_t *QK3 = (uint16_t *)scratch(kSlotX1QR, (size_t)pad256(nfb) * dp * 6 + 64);
+        uint16_t *CK3 = (uint16_t *)scratch(kSlotX1CR, (size_t)pad256(nc) * kbw3 * 2 + 64);
+        uint16_t *QK3 = (uint16_t *)scratch(kSlotX1QR, (size_t)pad256(nfb) * kbw3 * 2 + 64);
         MN_REQUIRE(eb && CK3 && QK3, MN_ENOMEM, "mn_knn: refill scratch allocation failed");
         int *erows = (int *)eb;
         float *qn3 = (float *)(eb + (((size_t)nfb * 4 + 15) & ~(size_t)15));
@@ -1719,10 +1725,10 @@ static int knn_x1(const float *Q, int64_t nq, const float *C, int64_t nc, int32_
             const int64_t blocks = std::min<int64_t>((n + 7) / 8, 16384);
             if (vec4)
                 hipLaunchKernelGGL(k_prep_x3<true>, dim3((unsigned)blocks), dim3(256), 0, s, X, n,
-                                   d, dp, src, K, corpus, nv, hv, lv, rv, cmax3, tmaj);
+                                   d, dp, src, K, corpus, nv, hv, lv, rv, cmax3, pst3);
             else
                 hipLaunchKernelGGL(k_prep_x3<false>, dim3((unsigned)blocks), dim3(256), 0, s, X, n,
-                                   d, dp, src, K, corpus, nv, hv, lv, rv, cmax3, tmaj);
+                                   d, dp, src, K, corpus, nv, hv, lv, rv, cmax3, pst3);
         };
         prep3(C, nc, perm, CK3, 1, nullptr, nullptr, nullptr, nullptr);
         prep3(Q, nfb, erows, QK3, 0, qn3, qh3, ql3, q23);
@@ -1750,7 +1756,8 @@ static int knn_x1(const float *Q, int64_t nq, const float *C, int64_t nc, int32_
                                    : ksw2::k_gram_sweep2<0, ksw2::SW_L2, false>),
                                dim3((unsigned)grid3), dim3(ksw2::NT), 0, s,
                                QK3, (int64_t)nfb, CK3, nc, nkb3, (int64_t)0, (int64_t)0, 0, tq3,
-                               tau3, chc, (int64_t)0, (int)p3.S, p3.chunk, p3.cap, cbuf3, cnt3);
+                               tau3, chc, (int64_t)0, (int)p3.S, p3.chunk, p3.cap, cbuf3, cnt3,
+                               pst3);
         MN_KCHECK(s, "k_gram_sweep<x3>");
         int *big_count3 = flags + 6;
         int *big_list3 = fb_list + nq;
