@@ -481,7 +481,11 @@ struct GramPlan {
     int cap, NR;
 };
 
-inline GramPlan plan_gram(int64_t nq, int64_t nc, int L, int64_t min_slices) {
+// max_slices > 0 caps S (the two-phase generators' sample pass: their
+// threshold is the L-th best of the WHOLE sample only with one slice; with S
+// slices it is the best of S per-slice L-th bests, about S x more candidates)
+inline GramPlan plan_gram(int64_t nq, int64_t nc, int L, int64_t min_slices,
+                          int64_t max_slices = 0) {
     GramPlan p;
     const int64_t blocks_q = (nq + BM - 1) / BM;
     // corpus slices: enough blocks to fill the chip, and at least min_slices
@@ -494,6 +498,7 @@ inline GramPlan plan_gram(int64_t nq, int64_t nc, int L, int64_t min_slices) {
     const int64_t max_sl = (msl && *msl) ? std::min(480, std::max(64, atoi(msl))) : 256;
     S = std::min<int64_t>(S, std::max<int64_t>(1, max_sl / L));
     S = std::min<int64_t>(S, std::max<int64_t>(1, (nc + BN - 1) / BN));
+    if (max_slices > 0) S = std::min(S, max_slices);
     S = std::max<int64_t>(S, 1);
     int64_t chunk = (nc + S - 1) / S;
     chunk = std::max<int64_t>(BN, ((chunk + BN - 1) / BN) * BN);

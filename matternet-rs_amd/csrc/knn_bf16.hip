@@ -638,7 +638,7 @@ static int knn_cos_bf16_x1(const uint16_t *X, int64_t n, int32_t d, const mn_cos
         MN_KCHECK(s, "k_to_kb32 / k_sample_rows / k_perm_norms");
     }
     // phase 1: every query (rows, in place) against the sample (positions [0, m0))
-    const GramPlan pl = plan_gram(n, m0, L1, 1);
+    const GramPlan pl = plan_gram(n, m0, L1, 1, 1);
     const size_t nbuf1 = (size_t)n * pl.S * pl.cap;
     uint2 *buf1 = (uint2 *)scratch(kSlotLists, nbuf1 * sizeof(uint2) + 64);
     char *meta1 = (char *)scratch(kSlotListMeta, (size_t)n * pl.S * 8 + 64);
@@ -693,9 +693,12 @@ static int knn_cos_bf16_x1(const uint16_t *X, int64_t n, int32_t d, const mn_cos
     tm.mark();
     // certification slack (cosine units): phase 1's f32 accumulation of exact
     // products scaled by two f32 inverse norms, 2 (d + 12) u; the sweep's
-    // dp + 1 terms (products and acc0 = -t|q||c|, |t| <= 1 + ...) with f32
-    // roundings of t|q|, |c| and acc0: 2.5 (dp + 16) u covers both
-    const double delta = 2.5 * ((double)dp + 16.0) * 0x1p-24;
+    // dk + 1 terms (products and acc0 = -t|q||c|, |t| <= 1 + ...) with f32
+    // roundings of t|q|, |c| and acc0: 2.5 (dk + 16) u covers both.  dk = d
+    // rounded up to the MFMA's 32: the all-zero k-blocks of the padding add
+    // exactly 0 to the accumulator
+    const int dk = (d + 31) / 32 * 32;
+    const double delta = 2.5 * ((double)dk + 16.0) * 0x1p-24;
     int *fb_count = flags + 2, *big_count = flags + 3;
     int *big_list = fb_list + n;
 #define MN_RRC(NRV, NB, QL, QN, BC, BL)                                                          \

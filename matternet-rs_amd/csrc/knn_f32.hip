@@ -1584,7 +1584,7 @@ static int knn_x1(const float *Q, int64_t nq, const float *C, int64_t nc, int32_
     }
     t_stats.sample_rows = m0;
     t_stats.list_len = L1;
-    const kb16::GramPlan pl = kb16::plan_gram(nq, m0, L1, 1);
+    const kb16::GramPlan pl = kb16::plan_gram(nq, m0, L1, 1, two ? 1 : 0);
     t_stats.slices = (int)pl.S;
     const size_t nbuf1 = (size_t)nq * pl.S * pl.cap;
     uint2 *cbuf1 = (uint2 *)scratch(kSlotLists, nbuf1 * sizeof(uint2) + 64);
