@@ -583,6 +583,112 @@ __global__ __launch_bounds__(256) void k_cos_rerank_x1(
     }
 }
 
+// ---- split exact scan (few uncertified rows over a large corpus) ------------
+// Block (f, p) scans corpus part p of fallback row f into its keff best
+// (dist, id) — the same per-thread insertion lists and block selection as
+// k_cos_fallback — and k_cos_fb_merge merges the P part lists of a row (each
+// sorted) with the same selection, then applies the eps / weight prefix.
+// Block-level selection of the r-th best over the threads' sorted lists.
+template <typename Emit>
+__device__ void fb_select(FbSmem &sm, int cnt, int keff, Emit emit) {
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    int head = 0;
+    for (int r = 0; r < keff; ++r) {
+        double bd = head < cnt ? sm.ld[tid][head] : __builtin_inf();
+        int bi = head < cnt ? sm.li[tid][head] : INT_MAX;
+        int bt = tid;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            const double od = __shfl_xor(bd, o);
+            const int oi = __shfl_xor(bi, o), ot = __shfl_xor(bt, o);
+            if (key_less(od, oi, bd, bi)) { bd = od; bi = oi; bt = ot; }
+        }
+        if (lane == 0) { sm.rd[w] = bd; sm.ri[w] = bi; sm.rt[w] = bt; }
+        __syncthreads();
+        const int win = key_less(sm.rd[1], sm.ri[1], sm.rd[0], sm.ri[0]) ? 1 : 0;
+        if (tid == sm.rt[win]) {
+            ++head;
+            emit(r, sm.rd[win], sm.ri[win]);
+        }
+        __syncthreads();
+    }
+}
+
+__global__ __launch_bounds__(FBT) void k_cos_fb_part(
+    const uint16_t *__restrict__ X, int64_t n, int d, const double *__restrict__ xn, int topk,
+    int P, int64_t cs, const int *__restrict__ fb_list, double *__restrict__ pd,
+    int *__restrict__ pi, int *__restrict__ pc) {
+    __shared__ FbSmem sm;
+    const int tid = threadIdx.x;
+    const int f = blockIdx.x / P, p = blockIdx.x % P;
+    const int64_t q = fb_list[f];
+    const int keff = (int)min((int64_t)topk, n - 1);
+    const int64_t j0 = (int64_t)p * cs, j1 = min(n, j0 + cs);
+    const uint16_t *qrow = X + q * (int64_t)d;
+    int cnt = 0;
+    for (int64_t j = j0 + tid; keff > 0 && j < j1; j += FBT) {
+        if (j == q) continue;
+        const double dist = cos_dist(exact_dot(qrow, X + j * d, d), xn[q], xn[j]);
+        const int gi = (int)j;
+        if (cnt == keff && !key_less(dist, gi, sm.ld[tid][keff - 1], sm.li[tid][keff - 1]))
+            continue;
+        int pp = cnt < keff ? cnt : keff - 1;
+        while (pp > 0 && key_less(dist, gi, sm.ld[tid][pp - 1], sm.li[tid][pp - 1])) {
+            sm.ld[tid][pp] = sm.ld[tid][pp - 1];
+            sm.li[tid][pp] = sm.li[tid][pp - 1];
+            --pp;
+        }
+        sm.ld[tid][pp] = dist;
+        sm.li[tid][pp] = gi;
+        if (cnt < keff) ++cnt;
+    }
+    __syncthreads();
+    // entries of the part: every valid j in range beyond the query itself
+    const int64_t valid = (j1 > j0 ? j1 - j0 : 0) - ((q >= j0 && q < j1) ? 1 : 0);
+    const int kp = (int)min((int64_t)keff, max<int64_t>(valid, 0));
+    const int64_t o = ((int64_t)f * P + p) * KMAX;
+    fb_select(sm, cnt, kp, [&](int r, double dv, int iv) { pd[o + r] = dv; pi[o + r] = iv; });
+    if (tid == 0) pc[(int64_t)f * P + p] = kp;
+}
+
+__global__ __launch_bounds__(FBT) void k_cos_fb_merge(
+    int64_t n, int topk, int P, double eps, double sigma, double p_, const int *__restrict__ fb_list,
+    const double *__restrict__ pd, const int *__restrict__ pi, const int *__restrict__ pc,
+    int32_t *__restrict__ out_idx, double *__restrict__ out_dist, double *__restrict__ out_w) {
+    __shared__ FbSmem sm;
+    __shared__ int sstop;
+    const int tid = threadIdx.x, f = blockIdx.x;
+    const int64_t q = fb_list[f];
+    const int keff = (int)min((int64_t)topk, n - 1);
+    int cnt = 0;
+    if (tid == 0) sstop = 0;
+    if (tid < P) {
+        const int64_t o = ((int64_t)f * P + tid) * KMAX;
+        cnt = pc[(int64_t)f * P + tid];
+        for (int r = 0; r < cnt; ++r) {
+            sm.ld[tid][r] = pd[o + r];
+            sm.li[tid][r] = pi[o + r];
+        }
+    }
+    __syncthreads();
+    // the eps / weight filter keeps a prefix: the first failing entry stops
+    // the list (sstop: each round's emitter is ordered after the previous
+    // round's by fb_select's barrier)
+    fb_select(sm, cnt, keff, [&](int r, double dv, int iv) {
+        const double wv = weight_of(dv, sigma, p_);
+        const bool st = sstop || !(dv <= eps && wv > 1e-12);
+        if (st) sstop = 1;
+        out_idx[q * topk + r] = st ? -1 : iv;
+        out_dist[q * topk + r] = st ? __builtin_inf() : dv;
+        if (out_w) out_w[q * topk + r] = st ? 0.0 : wv;
+    });
+    for (int r = keff + tid; r < topk; r += FBT) {
+        out_idx[q * topk + r] = -1;
+        out_dist[q * topk + r] = __builtin_inf();
+        if (out_w) out_w[q * topk + r] = 0.0;
+    }
+}
+
 }  // namespace kb16
 
 static thread_local mn_knn_stats t_bf16_stats{};
@@ -718,10 +824,32 @@ static int knn_cos_bf16_x1(const uint16_t *X, int64_t n, int32_t d, const mn_cos
     }
 #undef MN_RRC
     tm.mark();
-    hipLaunchKernelGGL(k_cos_fallback, dim3((unsigned)std::min<int64_t>(n, 1024)), dim3(FBT), 0, s,
-                       X, X, n, d, (int64_t)0, (int64_t)0, 1, xn, xn, topk, o->eps, o->sigma, o->p,
-                       fb_count, fb_list, out_idx, out_dist, out_w);
-    MN_KCHECK(s, "k_cos_fallback");
+    MN_HIP_TRY(hipMemcpyAsync(hb, flags, 16, hipMemcpyDeviceToHost, s));
+    MN_HIP_TRY(hipStreamSynchronize(s));
+    const int nfb = hb[2];
+    // few rows: each row's exact scan split over P blocks + a merge (one block
+    // per row would leave the chip idle); many rows: one block per row
+    const int P = (int)std::min<int64_t>(128, std::max<int64_t>(1, (2048 + nfb - 1) / std::max(nfb, 1)));
+    const char *fse = getenv("MN_BF16_FB_SPLIT");  // 0: always one block per row (A/B)
+    if (nfb > 0 && P >= 4 && !(fse && *fse == '0')) {
+        const int64_t cs = (n + P - 1) / P;
+        const size_t np = (size_t)nfb * P;
+        char *fbp = (char *)scratch(kSlotGeneric3, np * KMAX * 12 + np * 4 + 256);
+        MN_REQUIRE(fbp, MN_ENOMEM, "mn_knn_cos_bf16: split-scan scratch allocation failed");
+        double *pd = (double *)fbp;
+        int *pi = (int *)(pd + np * KMAX), *pc = pi + np * KMAX;
+        hipLaunchKernelGGL(k_cos_fb_part, dim3((unsigned)np), dim3(FBT), 0, s, X, n, d, xn, topk, P,
+                           cs, fb_list, pd, pi, pc);
+        MN_KCHECK(s, "k_cos_fb_part");
+        hipLaunchKernelGGL(k_cos_fb_merge, dim3((unsigned)nfb), dim3(FBT), 0, s, n, topk, P, o->eps,
+                           o->sigma, o->p, fb_list, pd, pi, pc, out_idx, out_dist, out_w);
+        MN_KCHECK(s, "k_cos_fb_merge");
+    } else {
+        hipLaunchKernelGGL(k_cos_fallback, dim3((unsigned)std::min<int64_t>(n, 1024)), dim3(FBT), 0,
+                           s, X, X, n, d, (int64_t)0, (int64_t)0, 1, xn, xn, topk, o->eps, o->sigma,
+                           o->p, fb_count, fb_list, out_idx, out_dist, out_w);
+        MN_KCHECK(s, "k_cos_fallback");
+    }
     tm.mark();
     MN_HIP_TRY(hipMemcpyAsync(hb, flags, 16, hipMemcpyDeviceToHost, s));
     MN_HIP_TRY(hipStreamSynchronize(s));
