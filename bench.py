@@ -285,7 +285,7 @@ def main():
             "c3_legs": c3,
             "c5_leg": c5,
             "knn_stats": {kk: (round(v, 3) if isinstance(v, float) else v)
-                          for kk, v in st.items() if kk != "reserved1"},
+                          for kk, v in st.items()},
         }
         if world > 1:
             line["time_budget"] = {"budget_s": a.time_budget_s, "steps_requested": steps_req,

@@ -54,6 +54,13 @@ int mn_stream_synchronize(void *stream);
 int mn_fill_uniform_f32(float *X, int64_t n, int32_t d, uint64_t seed,
                         int64_t row0, void *stream);
 
+/* The library's f32 ln / exp on device arrays (fn 0 = logf, 1 = expf): the
+ * platform glibc's logf / expf restated on the device, which the reference's
+ * f32::ln / f32::exp call (distance.rs:102, 283-289) — used by the
+ * Bhattacharyya kernels; exported so callers and tests can check them.  x ==
+ * NULL evaluates the consecutive f32 bit patterns bits0 + i (i < n). */
+int mn_libm_f32(const float *x, int64_t n, uint32_t bits0, int32_t fn, float *out, void *stream);
+
 /* ---------------------------------------------------------------------- */
 /* K1 — brute-force kNN (Gram on MFMA + LDS top-k + exact re-rank)        */
 /* ---------------------------------------------------------------------- */
@@ -104,7 +111,7 @@ typedef struct mn_knn_stats {
     int64_t n_escalated;    /* rows the bf16x1 bound could not certify, refilled
                                by the bf16x3 sweep at their own threshold      */
     float ms_escalate;
-    int32_t reserved1;
+    int32_t n_root_rescan;  /* MN_L2: rows rescanned for the root order (k_l2_order) */
 } mn_knn_stats;
 
 /* Self kNN over the rows of X [n][d] f32 (device, row-major): replaces
@@ -468,10 +475,29 @@ enum mn_sparsify_mode {
  * input position), the rest -1 / 0.0.  When the average degree does not
  * enable pruning the rows are copied (compacted, slot order).  ratio: SF-GRASS
  * target ratio (SfGrassSparsifier::new() = 0.5; with_target_ratio clamps to
- * [0.1, 1]).  applied_host (host, may be NULL) = 1 if pruning ran.  Bit-exact. */
+ * [0.1, 1]).  degrees [n] (device, may be NULL): deg_i for the scores and the
+ * average-degree switch; NULL = the row lengths (SF-GRASS).  The inline
+ * pruning passes the eps-valid neighbour counts, taken BEFORE the weight
+ * filter (laplacian.rs:219-229).  applied_host (host, may be NULL) = 1 if
+ * pruning ran.  Bit-exact. */
 int mn_sparsify_rows(const int32_t *nbr_idx, const double *nbr_w, int64_t n, int32_t k,
-                     double ratio, int32_t mode, int32_t *out_idx, double *out_w,
-                     int32_t *applied_host, void *stream);
+                     double ratio, int32_t mode, const int32_t *degrees, int32_t *out_idx,
+                     double *out_w, int32_t *applied_host, void *stream);
+
+/* SfGrassSparsifier::sparsify_graph (src_legacy/sparsification.rs:32-101) on
+ * CSR rows of ANY length (the reference's &[Vec<(usize, f64)>]; e.g. a
+ * symmetrised adjacency with hub rows): `in` (device CSR, f64 values, indptr
+ * from 0) -> `out` (library-allocated, release with mn_csr_free, or the
+ * caller's buffers when out->caller_owned == 1; too small: MN_ECAP with
+ * out->nnz = the need).  n_nodes: the reference's n_nodes argument (the
+ * average-degree divisor; <= 0: in->n_rows).  avg = nnz / n_nodes < 10: the
+ * rows unchanged; else per row keep min(max(ceil(len ratio), 1), len) entries
+ * by descending w * sqrt((deg_i deg_j) as f64), deg = row lengths, in score
+ * order (ties by input position = ascending j for a column-sorted CSR; the
+ * reference's sort_unstable leaves them unspecified).  applied_host (host,
+ * may be NULL) = 1 if pruning ran.  Bit-exact. */
+int mn_sparsify_sfgrass(const mn_csr *in, int64_t n_nodes, double ratio, mn_csr *out,
+                        int32_t *applied_host, void *stream);
 
 
 /* ---------------------------------------------------------------------- */

@@ -14,9 +14,10 @@
 //
 // Parity: the fold order, every +, *, / and the square root are the
 // reference's (sqrt correctly rounded via mn::sqrt_rn_f32, f32 division is
-// correctly rounded); ln / exp are the device's (OCML, <= 2 ulp) where the
-// reference calls the host libm, so BC agrees within ~1e-6 relative and the
-// neighbour sets agree up to near-ties at that level.
+// correctly rounded); ln / exp are glibc's logf / expf restated on the device
+// (glibc_f32.hpp: bit-identical to the platform libm the reference's f32::ln /
+// f32::exp call, checked on every f32 input), so BC and the neighbour sets are
+// bit-exact.
 //
 // GPU design: BC is symmetric bit for bit (every operation commutes in i, j),
 // so only the upper 64 x 64 tiles are computed; a block stages a 32-centroid
@@ -29,6 +30,7 @@
 #include <climits>
 
 #include "common.hpp"
+#include "glibc_f32.hpp"
 
 namespace mn {
 namespace bc {
@@ -81,7 +83,8 @@ __global__ __launch_bounds__(256) void k_bc_matrix(const float *__restrict__ mu,
                     const float vs = va[a] + vb[b];
                     const float d = ma[a] - mb[b];
                     const float mean_term = (d * d) / (4.0f * vs);
-                    const float log_term = 0.5f * logf(vs / (2.0f * sqrt_rn_f32(va[a] * vb[b])));
+                    const float log_term =
+                        0.5f * glibc::logf(vs / (2.0f * sqrt_rn_f32(va[a] * vb[b])));
                     db[a][b] = db[a][b] + (mean_term + log_term);
                 }
         }
@@ -94,7 +97,7 @@ __global__ __launch_bounds__(256) void k_bc_matrix(const float *__restrict__ mu,
         for (int b = 0; b < 4; ++b) {
             const int i = i0 + a, j = j0 + b;
             if (i >= F || j >= F) continue;
-            float w = expf(-db[a][b]);
+            float w = glibc::expf(-db[a][b]);
             bad |= (w != w);
             w = w < 0.f ? 0.f : (w > 1.f ? 1.f : w);  // NaN stays NaN
             BC[(int64_t)i * F + j] = w;

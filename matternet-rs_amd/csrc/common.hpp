@@ -42,6 +42,7 @@ enum ScratchSlot {
     kSlotX1Meta2,  //                phase-2 counts
     kSlotX1Esc,    //                escalated rows (gathered queries, lists)
     kSlotPerm,     // corpus visiting order (+ permuted norms / sample rows)
+    kSlotL2List,   // MN_L2: the extended L2^2 list before the root order
     kNumSlots
 };
 

@@ -256,6 +256,7 @@ __global__ __launch_bounds__(256) void k_cos_rerank(
 }
 
 constexpr int FBT = 128;
+static_assert(FBT >= 128, "k_cos_fb_merge: one part list per thread, P <= FBT");
 struct alignas(16) FbSmem {
     double ld[FBT][KMAX];
     int li[FBT][KMAX];
@@ -829,7 +830,8 @@ static int knn_cos_bf16_x1(const uint16_t *X, int64_t n, int32_t d, const mn_cos
     const int nfb = hb[2];
     // few rows: each row's exact scan split over P blocks + a merge (one block
     // per row would leave the chip idle); many rows: one block per row
-    const int P = (int)std::min<int64_t>(128, std::max<int64_t>(1, (2048 + nfb - 1) / std::max(nfb, 1)));
+    // (k_cos_fb_merge loads the P part lists one per thread: P <= FBT)
+    const int P = (int)std::min<int64_t>(FBT, std::max<int64_t>(1, (2048 + nfb - 1) / std::max(nfb, 1)));
     const char *fse = getenv("MN_BF16_FB_SPLIT");  // 0: always one block per row (A/B)
     if (nfb > 0 && P >= 4 && !(fse && *fse == '0')) {
         const int64_t cs = (n + P - 1) / P;

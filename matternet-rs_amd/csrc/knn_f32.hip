@@ -1083,13 +1083,44 @@ __global__ __launch_bounds__(256) void k_count_cands(const int *__restrict__ c, 
     if (threadIdx.x == 0) atomicAdd(out, part[0] + part[1] + part[2] + part[3]);
 }
 
-// MN_L2: distances of the L2SQ result -> correctly rounded f32 sqrt
-// (Rust f32::sqrt; gfx950 sqrtf is not correctly rounded, common.hpp)
-__global__ __launch_bounds__(256) void k_sqrt_dist(float *__restrict__ dist, int64_t n) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) {
-        const float v = dist[i];
-        if (v < __builtin_inff()) dist[i] = sqrt_rn_f32(v);
+// MN_L2 (distance.rs:195-203; mst.rs:344 stable sort of the ROOTED f32
+// distances): two different L2^2 values can round to the same f32 root, and
+// then the reference orders them by index, not by the squared value.  The
+// L2^2 list is computed k2 = k + 8 long; one wave per row takes the correctly
+// rounded roots (Rust f32::sqrt; gfx950 sqrtf is not correctly rounded,
+// common.hpp), re-sorts by (root, idx) — which only permutes runs of equal
+// roots — and keeps k.  Entries beyond the list have roots >= the last one,
+// so the result is exact unless the run of roots equal to the k-th one
+// reaches the end of a full list: those rows go to the exact root-keyed scan.
+__global__ __launch_bounds__(256) void k_l2_order(const int32_t *__restrict__ idx2,
+                                                  const float *__restrict__ d2, int64_t nq, int k2,
+                                                  int k, int64_t nc, int64_t q_off, int64_t c_off,
+                                                  int excl, int32_t *__restrict__ out_idx,
+                                                  float *__restrict__ out_dist,
+                                                  int *__restrict__ fb_count,
+                                                  int *__restrict__ fb_list) {
+    const int lane = threadIdx.x & 63;
+    const int64_t q = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    if (q >= nq) return;
+    const int id = lane < k2 ? idx2[q * k2 + lane] : -1;
+    const float sq = lane < k2 ? d2[q * k2 + lane] : __builtin_inff();
+    float key[1] = {id >= 0 ? sqrt_rn_f32(sq) : __builtin_inff()};
+    int ix[1] = {id >= 0 ? id : INT_MAX};
+    const int m = (int)__popcll(__ballot(id >= 0));
+    wave_bitonic_sort<1>(key, ix);
+    const int64_t gq = q_off + q;
+    const int64_t valid = nc - ((excl && gq >= c_off && gq < c_off + nc) ? 1 : 0);
+    const float rk = __shfl(key[0], min(k, m) - 1 < 0 ? 0 : min(k, m) - 1);
+    const float rl = __shfl(key[0], k2 - 1);
+    const bool more = m == k2 && (int64_t)k2 < valid;
+    if (more && k <= m && rl == rk) {
+        if (lane == 0) fb_list[atomicAdd(fb_count, 1)] = (int)q;
+        return;
+    }
+    if (lane < k) {
+        const bool ok = lane < m;
+        out_idx[q * k + lane] = ok ? ix[0] : -1;
+        out_dist[q * k + lane] = ok ? key[0] : __builtin_inff();
     }
 }
 
@@ -1141,7 +1172,9 @@ struct alignas(16) FallbackSmem {
     int rt[2];
 };
 
-template <bool VEC4>
+// SQRT: keys are the correctly rounded f32 roots (MN_L2 rows whose equal-root
+// run reaches past the extended list, k_l2_order)
+template <bool VEC4, bool SQRT = false>
 __global__ __launch_bounds__(FB_THREADS) void k_fallback(
     const float *__restrict__ Q, const float *__restrict__ C, int64_t nc, int d, int64_t q_off,
     int64_t c_off, int excl, int k, const int *__restrict__ fb_count,
@@ -1161,7 +1194,8 @@ __global__ __launch_bounds__(FB_THREADS) void k_fallback(
         for (int64_t j = tid; keff > 0 && j < nc; j += FB_THREADS) {
             const int64_t gj = c_off + j;
             if (excl && gj == gq) continue;
-            const float dist = exact_l2sq<VEC4>(qrow, C + j * (int64_t)d, d);
+            float dist = exact_l2sq<VEC4>(qrow, C + j * (int64_t)d, d);
+            if constexpr (SQRT) dist = sqrt_rn_f32(dist);
             const int gi = (int)gj;
             if (cnt == keff && !key_less(dist, gi, sm.ld[tid][keff - 1], sm.li[tid][keff - 1]))
                 continue;
@@ -1793,13 +1827,17 @@ static int knn_x1(const float *Q, int64_t nq, const float *C, int64_t nc, int32_
     MN_HIP_TRY(hipMemcpyAsync(&nfb2, fb_count, 4, hipMemcpyDeviceToHost, s));
     MN_HIP_TRY(hipStreamSynchronize(s));
     if (nfb2 > 0 && nc >= (1 << 16) && k + 1 <= KMAX) {
-        int *rows = nullptr;
-        float *Qg = nullptr, *ed = nullptr;
-        int32_t *ei = nullptr;
-        MN_HIP_TRY(hipMalloc(&rows, sizeof(int) * (size_t)nfb2));
-        MN_HIP_TRY(hipMalloc(&Qg, sizeof(float) * (size_t)nfb2 * d));
-        MN_HIP_TRY(hipMalloc(&ei, sizeof(int32_t) * (size_t)nfb2 * (k + 1)));
-        MN_HIP_TRY(hipMalloc(&ed, sizeof(float) * (size_t)nfb2 * (k + 1)));
+        // the refill slot is dead here (knn_f32_core below does not use it):
+        // rows, the gathered queries and the (k + 1)-lists, 16-B aligned parts
+        auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
+        const size_t b_rows = al(sizeof(int) * (size_t)nfb2), b_q = al(sizeof(float) * (size_t)nfb2 * d),
+                     b_l = al(sizeof(int32_t) * (size_t)nfb2 * (k + 1));
+        char *gb = (char *)scratch(kSlotX1Esc, b_rows + b_q + 2 * b_l + 256);
+        MN_REQUIRE(gb, MN_ENOMEM, "mn_knn: escalation scratch allocation failed");
+        int *rows = (int *)gb;
+        float *Qg = (float *)(gb + b_rows);
+        int32_t *ei = (int32_t *)(gb + b_rows + b_q);
+        float *ed = (float *)(gb + b_rows + b_q + b_l);
         MN_HIP_TRY(hipMemcpyAsync(rows, fb_list, sizeof(int) * (size_t)nfb2,
                                   hipMemcpyDeviceToDevice, s));
         hipLaunchKernelGGL(k_gather_rows, dim3((unsigned)(((int64_t)nfb2 * d + 255) / 256)),
@@ -1821,7 +1859,6 @@ static int knn_x1(const float *Q, int64_t nq, const float *C, int64_t nc, int32_
             MN_KCHECK(s, "k_scatter_escalated");
         }
         MN_HIP_TRY(hipStreamSynchronize(s));
-        (void)hipFree(rows); (void)hipFree(Qg); (void)hipFree(ei); (void)hipFree(ed);
         if (rc != MN_OK) return rc;
     } else if (nfb2 > 0) {
         const unsigned fgrid = (unsigned)std::min<int64_t>(nfb2, 1024);
@@ -1871,28 +1908,61 @@ static int knn_f32_impl(const float *Q, int64_t nq, const float *C, int64_t nc, 
     MN_REQUIRE(q_off >= 0 && c_off >= 0 && q_off + nq <= INT_MAX && c_off + nc <= INT_MAX,
                MN_EINVAL, "mn_knn: global ids must fit int32");
     t_stats.n_queries = nq;
+    // MN_L2: the L2^2 graph k2 = k + 8 long, then k_l2_order (root order)
+    const bool l2 = opts->metric == MN_L2 && nq > 0;
+    const int k2 = l2 ? std::min(k + 8, KMAX) : k;
+    mn_knn_opts o2 = *opts;
+    o2.k = k2;
+    o2.metric = MN_L2SQ;
+    int32_t *ri = out_idx;
+    float *rd = out_dist;
+    if (l2) {
+        char *t = (char *)scratch(kSlotL2List, (size_t)nq * k2 * 8 + 256);
+        MN_REQUIRE(t, MN_ENOMEM, "mn_knn: MN_L2 list allocation failed");
+        ri = (int32_t *)t;
+        rd = (float *)(t + (((size_t)nq * k2 * 4 + 255) & ~(size_t)255));
+    }
     int rc = 1;
     const bool x1 = algo == MN_KNN_BF16X1 || (algo == MN_KNN_AUTO && nc >= (1 << 17));
     if (x1 && nq > 0 && nc > 0) {
-        rc = knn_x1(Q, nq, C, nc, d, q_off, c_off, opts, out_idx, out_dist);
+        rc = knn_x1(Q, nq, C, nc, d, q_off, c_off, &o2, ri, rd);
         if (rc < 0) return rc;
     }
     if (rc == 1) {
         int a = algo == MN_KNN_BF16X1 ? MN_KNN_AUTO : algo;
         if (a == MN_KNN_AUTO) {
             const int margin = opts->margin > 0 ? opts->margin : 16;
-            a = (k + margin <= kb16::LMAX) ? MN_KNN_BF16X3 : MN_KNN_F32;
+            a = (k2 + margin <= kb16::LMAX) ? MN_KNN_BF16X3 : MN_KNN_F32;
         }
-        rc = knn_f32_core(Q, nq, C, nc, d, q_off, c_off, opts, out_idx, out_dist, a);
+        rc = knn_f32_core(Q, nq, C, nc, d, q_off, c_off, &o2, ri, rd, a);
         if (rc != MN_OK) return rc;
     }
-    if (opts->metric == MN_L2 && nq > 0) {
-        const int64_t n = nq * k;
+    if (l2) {
         hipStream_t s = (hipStream_t)opts->stream;
-        hipLaunchKernelGGL(k_sqrt_dist, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s,
-                           out_dist, n);
-        MN_KCHECK(s, "k_sqrt_dist");
+        int *fl = (int *)scratch(kSlotFlags, 64);
+        int *fbl = (int *)scratch(kSlotFallback, sizeof(int) * (size_t)nq * 2 + 64);
+        MN_REQUIRE(fl && fbl, MN_ENOMEM, "mn_knn: MN_L2 scratch allocation failed");
+        const int excl = opts->exclude_self ? 1 : 0;
+        MN_HIP_TRY(hipMemsetAsync(fl, 0, 4, s));
+        hipLaunchKernelGGL(k_l2_order, dim3((unsigned)((nq * 64 + 255) / 256)), dim3(256), 0, s,
+                           ri, rd, nq, k2, k, nc, q_off, c_off, excl, out_idx, out_dist, fl, fbl);
+        MN_KCHECK(s, "k_l2_order");
+        int nfb = 0;
+        MN_HIP_TRY(hipMemcpyAsync(&nfb, fl, 4, hipMemcpyDeviceToHost, s));
         MN_HIP_TRY(hipStreamSynchronize(s));
+        if (nfb > 0) {
+            const bool vec4 = (d % 4 == 0) && (((uintptr_t)Q | (uintptr_t)C) % 16 == 0);
+            const unsigned fgrid = (unsigned)std::min<int64_t>(nfb, 1024);
+            if (vec4)
+                hipLaunchKernelGGL((k_fallback<true, true>), dim3(fgrid), dim3(FB_THREADS), 0, s,
+                                   Q, C, nc, d, q_off, c_off, excl, k, fl, fbl, out_idx, out_dist);
+            else
+                hipLaunchKernelGGL((k_fallback<false, true>), dim3(fgrid), dim3(FB_THREADS), 0, s,
+                                   Q, C, nc, d, q_off, c_off, excl, k, fl, fbl, out_idx, out_dist);
+            MN_KCHECK(s, "k_fallback<sqrt>");
+            MN_HIP_TRY(hipStreamSynchronize(s));
+        }
+        t_stats.n_root_rescan = nfb;  // rows rescanned for the root order
     }
     return MN_OK;
 }

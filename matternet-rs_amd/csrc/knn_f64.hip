@@ -205,7 +205,8 @@ extern "C" int mn_knn_l2_f64(const void *Q, int64_t nq, const void *C, int64_t n
     MN_REQUIRE(g && flag, MN_ENOMEM, "mn_knn_l2_f64: scratch allocation failed");
     double *cd = (double *)g;
     int32_t *ci = (int32_t *)(cd + per);
-    double *cd2 = (double *)(g + per * 12 + 64);
+    // (16-B aligned whatever the parity of per: the merge reads f64 pairs)
+    double *cd2 = (double *)(g + ((per * 12 + 64 + 15) & ~(size_t)15));
     int32_t *ci2 = (int32_t *)(cd2 + (size_t)nq * ((ntiles + 7) / 8) * k);
     MN_HIP_TRY(hipMemsetAsync(flag, 0, 4, s));
     const dim3 grid((unsigned)ntiles, (unsigned)nqb);

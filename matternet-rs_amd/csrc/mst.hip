@@ -17,18 +17,16 @@
 //
 // Parity: the fold order and every +, *, / are the reference's; the square
 // root is correctly rounded (mn::sqrt_rn_f32) like Rust's f32::sqrt, and ln is
-// the f64 log rounded to f32 — correctly rounded except when ln(x) lies within
-// ~2^-29 relative of an f32 rounding boundary — where the reference calls the
-// host libm logf (glibc: < 1 ulp, correctly rounded in all but rare cases).
-// Distances therefore agree bit for bit on all but rare terms (then within an
-// ulp of the fold), and neighbour lists agree up to such near-ties.
+// glibc's logf restated on the device (glibc_f32.hpp: bit-identical to the
+// platform libm the reference's f32::ln calls, checked on every f32 input).
+// Distances and neighbour lists are therefore bit-exact.
 //
 // GPU design: D(i, j) is symmetric bit for bit (md is negated, squared; ss,
 // sp commute), so only the upper 64 x 64 node tiles are computed; a block
 // stages a 32-feature chunk of both tiles' means and floored variances in LDS
 // (transposed, padded) and every thread folds a 4 x 4 pair block in feature
-// order (VALU / transcendental bound: a division pair, a sqrt and an f64 log
-// per term — not a Gram).  The C x C f32 matrix lives in HBM (C <= 65536:
+// order (VALU / transcendental bound: a division pair, a sqrt and a table
+// log per term — not a Gram).  The C x C f32 matrix lives in HBM (C <= 65536:
 // <= 16 GiB of 288).  Then one wave per node keeps its k best (dist, j) in
 // registers over 1024-slot passes of a wave bitonic sort (the carried prefix
 // plus the next row chunk), and writes edges + costs.
@@ -36,6 +34,7 @@
 #include <climits>
 
 #include "common.hpp"
+#include "glibc_f32.hpp"
 
 namespace mn {
 namespace mst {
@@ -53,7 +52,7 @@ __device__ __forceinline__ float bd_term(float mi, float si, float mj, float sj)
     const float md = mi - mj;
     const float mahal = (0.25f * (md * md)) / ss;
     const float r = fmaxf(ss / (2.0f * sqrt_rn_f32(sp)), EPS);
-    const float lt = 0.25f * (float)::log((double)r);
+    const float lt = 0.25f * glibc::logf(r);
     return mahal + lt;
 }
 

@@ -7,6 +7,7 @@
 #include <cstdlib>
 
 #include "common.hpp"
+#include "glibc_f32.hpp"
 
 namespace mn {
 
@@ -139,6 +140,17 @@ __global__ void k_fill_uniform_f32(float *__restrict__ X, int64_t total, int32_t
 
 }  // namespace mn
 
+namespace mn {
+__global__ __launch_bounds__(256) void k_libm_f32(const float *__restrict__ x, int64_t n,
+                                                  uint32_t bits0, int fn, float *__restrict__ out) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const float v = x ? x[i] : __uint_as_float(bits0 + (uint32_t)i);
+        out[i] = fn == 0 ? glibc::logf(v) : glibc::expf(v);
+    }
+}
+}  // namespace mn
+
 extern "C" {
 
 int mn_version(void) { return 100; }
@@ -195,6 +207,22 @@ int mn_fill_uniform_f32(float *X, int64_t n, int32_t d, uint64_t seed, int64_t r
     hipStream_t s = (hipStream_t)stream;
     hipLaunchKernelGGL(mn::k_fill_uniform_f32, dim3((unsigned)blocks), dim3(256), 0, s, X, total,
                        d, seed, row0);
+    MN_HIP_TRY(hipGetLastError());
+    MN_HIP_TRY(hipStreamSynchronize(s));
+    return MN_OK;
+}
+
+// The library's f32 ln / exp (glibc_f32.hpp) on device arrays: fn 0 = logf,
+// 1 = expf; x == NULL evaluates the consecutive bit patterns bits0 + i.
+int mn_libm_f32(const float *x, int64_t n, uint32_t bits0, int32_t fn, float *out,
+                void *stream) {
+    MN_REQUIRE(out && n >= 0 && (fn == 0 || fn == 1), MN_EINVAL, "mn_libm_f32: bad args");
+    if (n == 0) return MN_OK;
+    int64_t blocks = (n + 255) / 256;
+    if (blocks > 65536) blocks = 65536;
+    hipStream_t s = (hipStream_t)stream;
+    hipLaunchKernelGGL(mn::k_libm_f32, dim3((unsigned)blocks), dim3(256), 0, s, x, n, bits0, fn,
+                       out);
     MN_HIP_TRY(hipGetLastError());
     MN_HIP_TRY(hipStreamSynchronize(s));
     return MN_OK;

@@ -13,7 +13,7 @@ from .l2f64 import (estimate_intrinsic_dimension, knn_l2_f64, nearest_subcentroi
                     prepare_query_items_energy, topk_by_l2, topk_by_l2_rows)
 from .search import (normalise_query_lambda, prepare_query_lambdas, search_lambda_aware,
                      search_lambda_aware_hybrid)
-from .sparsification import SfGrassSparsifier, sparsify_rows
+from .sparsification import SfGrassSparsifier, sparsify_rows, sparsify_sfgrass_csr
 from .sorted_index import SortedLambdas
 from .energy import (TauMode, compute_lambdas_gpu, compute_tau_mode_gpu, compute_taumode_lambdas,
                      diffuse_rows, energy_rows, laplacian_matvec_rows,
@@ -36,7 +36,7 @@ __all__ = ["MnError", "lib", "clustering", "ClusteringOutput", "ClusteringStage"
            "compute_lambdas_gpu", "compute_tau_mode_gpu", "diffuse_rows",
            "laplacian_matvec_rows", "signal_energy_and_dispersion",
            "normalise_lambdas", "sorted_index", "SortedLambdas", "sparsification",
-           "SfGrassSparsifier", "sparsify_rows", "search", "search_lambda_aware",
+           "SfGrassSparsifier", "sparsify_rows", "sparsify_sfgrass_csr", "search", "search_lambda_aware",
            "normalise_query_lambda", "prepare_query_lambdas",
            "search_lambda_aware_hybrid", "l2f64", "knn_l2_f64", "topk_by_l2", "topk_by_l2_rows",
            "nearest_subcentroid", "prepare_query_items_energy", "estimate_intrinsic_dimension"]

@@ -42,7 +42,7 @@ class KnnStats(C.Structure):
                 ("algo", C.c_int32), ("ms_sample", C.c_float), ("ms_sweep", C.c_float),
                 ("sample_rows", C.c_int64), ("n_candidates", C.c_int64),
                 ("sweep_slices", C.c_int32), ("sweep_cap", C.c_int32),
-                ("n_escalated", C.c_int64), ("ms_escalate", C.c_float), ("reserved1", C.c_int32)]
+                ("n_escalated", C.c_int64), ("ms_escalate", C.c_float), ("n_root_rescan", C.c_int32)]
 
     def as_dict(self):
         return {f: getattr(self, f) for f, _ in self._fields_}
@@ -111,6 +111,7 @@ SIGNATURES = {
     "mn_memcpy_d2d": (C.c_int, [P, P, C.c_size_t, P]),
     "mn_stream_synchronize": (C.c_int, [P]),
     "mn_fill_uniform_f32": (C.c_int, [P, I64, I32, C.c_uint64, I64, P]),
+    "mn_libm_f32": (C.c_int, [P, I64, C.c_uint32, I32, P, P]),
     "mn_knn_f32": (C.c_int, [P, I64, I32, C.POINTER(KnnOpts), P, P]),
     "mn_knn_f32_qc": (C.c_int, [P, I64, P, I64, I32, I64, I64, C.POINTER(KnnOpts), P, P]),
     "mn_knn_merge_f32": (C.c_int, [P, P, I32, I64, I32, P, P, P]),
@@ -138,7 +139,8 @@ SIGNATURES = {
     "mn_sorted_k_nearest_by_lambda": (C.c_int, [P, P, I64, C.c_double, P, I64, C.c_int32,
                                                 C.c_double, C.c_int32, C.c_double, C.c_double,
                                                 C.c_double, P, P, P, P]),
-    "mn_sparsify_rows": (C.c_int, [P, P, I64, I32, C.c_double, I32, P, P, P, P]),
+    "mn_sparsify_rows": (C.c_int, [P, P, I64, I32, C.c_double, I32, P, P, P, P, P]),
+    "mn_sparsify_sfgrass": (C.c_int, [C.POINTER(Csr), I64, C.c_double, C.POINTER(Csr), P, P]),
     "mn_knn_cos_columns_f32": (C.c_int, [P, I64, I32, C.POINTER(CosOpts), P, P, P]),
     "mn_knn_cos_columns_f64": (C.c_int, [P, I64, I32, C.POINTER(CosOpts), P, P, P]),
     "mn_standardize_columns_f64": (C.c_int, [P, I64, I32, P, P]),

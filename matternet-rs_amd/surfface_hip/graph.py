@@ -34,6 +34,8 @@ distance <= eps maps below 1e-12).
 """
 from __future__ import annotations
 
+import math
+
 from dataclasses import dataclass, field
 from typing import Optional
 
@@ -97,11 +99,42 @@ def _cos_graph(items: torch.Tensor, params: GraphParams):
     else:
         idx, _, w, _ = knn_cos_columns(X.float(), params.topk, eps=params.eps, sigma=sigma,
                                        p=params.p)
-    # degrees = eps-valid neighbours (:219-229) = row lengths of the filtered
-    # lists; sparsify iff their average > 10, keep max(len/2, 1) of rows with
-    # len > 2 by w * sqrt(deg_i deg_j) (:231-282)
-    oi, ow, applied = sparsify_rows(idx, w, 0.5, _lib.MN_SPARSIFY_INLINE)
+    # degrees = the eps-valid neighbours among the topk nearest others
+    # (:219-229), counted BEFORE the weight > 1e-12 filter (:255-258); sparsify
+    # iff their average > 10, keep max(len/2, 1) of rows with len > 2 by
+    # w * sqrt(deg_i deg_j) (:231-282).  The kernels' rows hold the entries
+    # passing both filters, so where the weight filter can drop an eps-valid
+    # entry the counts come from a second, weight-neutral query (sigma 1, p 1:
+    # w = 1/(1 + d) >= 1/2); otherwise they are the row lengths.
+    deg = None
+    if _weight_can_drop(params.eps, sigma, params.p):
+        if X.dtype == torch.float64:
+            i2, _, _ = _knn_cos_columns_f64(X, params.topk, params.eps, 1.0, 1.0)
+        else:
+            i2, _, _, _ = knn_cos_columns(X.float(), params.topk, eps=params.eps, sigma=1.0, p=1.0)
+        deg = (i2 >= 0).sum(dim=1, dtype=torch.int32)
+    oi, ow, applied = sparsify_rows(idx, w, 0.5, _lib.MN_SPARSIFY_INLINE, degrees=deg)
     return oi, ow, applied, n
+
+
+def _weight_can_drop(eps: float, sigma: float, p: float) -> bool:
+    """Can w = 1/(1 + (d/sigma)^p) <= 1e-12 for an eps-valid rectified cosine
+    distance d in [0, min(eps, 1)]?  w is monotone in d, so the ends decide."""
+    dmax = min(eps, 1.0)
+    if not dmax >= 0.0:
+        return False
+
+    def w(d):
+        x = d / sigma
+        if x == 0.0:
+            t = 0.0 if p > 0 else (1.0 if p == 0 else math.inf)
+        else:
+            try:
+                t = math.pow(x, p)
+            except OverflowError:
+                t = math.inf
+        return 1.0 / (1.0 + t)
+    return not (min(w(0.0), w(dmax)) > 1e-12)
 
 
 @on_device
@@ -129,10 +162,12 @@ def build_laplacian_matrix(transposed: torch.Tensor, params: GraphParams,
     if not (n >= 2 and d >= 2):
         raise ValueError(f"items should be at least of shape (2,2): ({d},{n})")
     items = standardize_columns(transposed) if params.normalise else transposed
-    idx, w, _, nn = _cos_graph(items, params)
+    idx, w, _, _ = _cos_graph(items, params)
     L, _ = build_laplacian_from_knn(idx, w, weight_kernel="given", symmetrise="union")
+    # laplacian.rs:129,165-168: nnodes = n_items, else n (the column count of
+    # `transposed`, i.e. the profile length), not the node count d
     return GraphLaplacian(init_data=items, matrix=L,
-                          nnodes=n_items if n_items is not None else nn,
+                          nnodes=n_items if n_items is not None else n,
                           graph_params=params, energy=energy)
 
 

@@ -150,8 +150,36 @@ def laplacian_stage_from_edges(nbr_idx: torch.Tensor, weights: torch.Tensor,
                                       symmetrise="max", normalize=config.normalize,
                                       weight_threshold=config.weight_threshold)
     f = nbr_idx.shape[0]
-    return LaplacianOutput(matrix=m, n_features=f, nnz=m.nnz, degrees=deg,
-                           sparsity=1.0 - m.nnz / float(f * f))
+    nnz = _stage_c_nnz(nbr_idx, weights, deg, config)
+    # laplacian.rs:187: `1.0 - (nnz as f32 / total as f32)`, all in f32
+    sp = np.float32(1.0) - np.float32(np.float32(nnz) / np.float32(f * f))
+    return LaplacianOutput(matrix=m, n_features=f, nnz=nnz, degrees=deg, sparsity=float(sp))
+
+
+def _stage_c_nnz(nbr_idx: torch.Tensor, weights: torch.Tensor, deg: torch.Tensor,
+                 config: LaplacianConfig) -> int:
+    """The reference's nnz count (surfface-core/src/laplacian.rs:344-391): taken
+    while the dense L is written, BEFORE the `|v| > 1e-9` filter of the CSR
+    conversion (:215): the diagonal entries with d_i > thr plus 2 per
+    undirected edge (key (min, max), i != j, w > thr), in normalized mode only
+    the edges whose both degrees exceed thr."""
+    thr = config.weight_threshold
+    f = nbr_idx.shape[0]
+    k = nbr_idx.shape[1]
+    i = torch.arange(f, device=nbr_idx.device, dtype=torch.int64).repeat_interleave(k)
+    j = nbr_idx.reshape(-1).to(torch.int64)
+    w = weights.reshape(-1).float()
+    keep = (j >= 0) & (j < f) & (i != j) & (w > thr)
+    i, j = i[keep], j[keep]
+    key = torch.unique(torch.minimum(i, j) * f + torch.maximum(i, j))
+    a, b = key // f, key % f
+    dg = deg.float()
+    n_diag = int((dg > thr).sum().item())
+    if config.normalize:
+        n_edges = int(((dg[a] > thr) & (dg[b] > thr)).sum().item())
+    else:
+        n_edges = int(key.numel())
+    return n_diag + 2 * n_edges
 
 
 @on_device

@@ -150,6 +150,60 @@ static int knn_l2sq_core(const float *X, int64_t n, int32_t d, int32_t k,
     return err;
 }
 
+/* A.1 in the per-shard form of the row-sharded build: query
+ * rows Q[t] (global ids q_ids[t]) against a corpus shard C (global ids c_off +
+ * j); the pair whose global ids are equal is skipped when excl.  Output ids
+ * are global; (dist, id) order; restated-efficient heap (mode 1).  The
+ * reference's mst.rs:330-360 over the shard's rows. */
+int or_knn_l2sq_qc_f32(const float *Q, int64_t nq, const int64_t *q_ids, const float *C,
+                       int64_t nc, int32_t d, int64_t c_off, int32_t k, int excl, int nthreads,
+                       int32_t *out_idx, float *out_dist) {
+    if (!Q || !C || !q_ids || !out_idx || !out_dist || nq < 0 || nc < 1 || d < 1 || k < 1)
+        return OR_EINVAL;
+    int err = 0;
+    set_threads(nthreads);
+#pragma omp parallel
+    {
+        cand_f32 *buf = (cand_f32 *)malloc(sizeof(cand_f32) * (size_t)k);
+        if (!buf) {
+#pragma omp atomic write
+            err = OR_ENOMEM;
+        }
+#pragma omp for schedule(dynamic, 1)
+        for (int64_t t = 0; t < nq; ++t) {
+            if (!buf) continue;
+            const float *xq = Q + t * (int64_t)d;
+            int32_t cnt = 0;
+            int bad = 0;
+            for (int64_t j = 0; j < nc; ++j) {
+                const int64_t g = c_off + j;
+                if (excl && g == q_ids[t]) continue;
+                const float dist = fold_l2sq_f32(xq, C + j * (int64_t)d, d);
+                if (dist != dist) { bad = 1; break; }
+                if (cnt < k) {
+                    buf[cnt].d = dist; buf[cnt].j = (int32_t)g;
+                    heap_sift_up(buf, cnt); ++cnt;
+                } else if (lt_f32(dist, (int32_t)g, buf[0].d, buf[0].j)) {
+                    buf[0].d = dist; buf[0].j = (int32_t)g;
+                    heap_sift_down(buf, cnt, 0);
+                }
+            }
+            if (bad) {
+#pragma omp atomic write
+                err = OR_ENONFINITE;
+                continue;
+            }
+            qsort(buf, (size_t)cnt, sizeof(cand_f32), cmp_cand_f32);
+            for (int32_t r = 0; r < k; ++r) {
+                out_idx[t * k + r] = r < cnt ? buf[r].j : -1;
+                out_dist[t * k + r] = r < cnt ? buf[r].d : INFINITY;
+            }
+        }
+        free(buf);
+    }
+    return err;
+}
+
 /* ------------------------------------------------------------------------ */
 /* K1 — A.1c rectified cosine, f64                                           */
 /* ------------------------------------------------------------------------ */

@@ -54,6 +54,13 @@ int or_knn_l2sq_rows_f32(const float *X, int64_t n, int32_t d, int32_t k,
                          const int64_t *rows, int64_t nrows, int nthreads,
                          int32_t *out_idx, float *out_dist);
 
+/* A.1 per-shard form: queries Q [nq][d] with global ids
+ * q_ids[nq] against corpus C [nc][d] with global ids c_off + j; the equal-id
+ * pair skipped when excl; output ids global, (dist, id) order. */
+int or_knn_l2sq_qc_f32(const float *Q, int64_t nq, const int64_t *q_ids, const float *C,
+                       int64_t nc, int32_t d, int64_t c_off, int32_t k, int excl, int nthreads,
+                       int32_t *out_idx, float *out_dist);
+
 /* A.1c rectified-cosine kNN, f64 arithmetic on exactly-widened f32 inputs.
  *   src_legacy/tests/test_helpers.rs:77-126 (build_adjacency_matrix):
  *   norms sqrt(sum x*x) sequential f64; dot sequential f64;
@@ -285,6 +292,13 @@ int or_search_lambda_aware_hybrid(const double *X, int64_t n, int32_t f, const d
                                   const double *Q, const double *lambda_q, int64_t nq,
                                   int64_t k, double alpha, int nthreads, int64_t *out_idx,
                                   double *out_score, int64_t *out_count);
+
+/* glibc_check.c: the host glibc logf / expf (what the reference's f32::ln /
+ * f32::exp call) and a host copy of the device restatement (csrc/glibc_f32.hpp). */
+int or_libm_f32(const float *x, int64_t n, uint32_t bits0, int fn, float *out, int nthreads);
+int64_t or_libm_mismatch(uint32_t bits0, int64_t n, int fn, const float *got);
+int64_t or_glibc_restated_check(int fn, int64_t stride);
+int or_glibc_tables(int which, uint64_t *out);
 
 #ifdef __cplusplus
 }

@@ -48,6 +48,13 @@ F = C.c_float
 def _declare(L):
     L.or_knn_l2sq_f32.argtypes = [P, I64, I32, I32, I64, I64, C.c_int, C.c_int, P, P]
     L.or_knn_l2sq_rows_f32.argtypes = [P, I64, I32, I32, P, I64, C.c_int, P, P]
+    L.or_libm_f32.argtypes = [P, I64, C.c_uint32, C.c_int, P, C.c_int]
+    L.or_libm_mismatch.argtypes = [C.c_uint32, I64, C.c_int, P]
+    L.or_libm_mismatch.restype = I64
+    L.or_glibc_restated_check.argtypes = [C.c_int, I64]
+    L.or_glibc_restated_check.restype = I64
+    L.or_glibc_tables.argtypes = [C.c_int, P]
+    L.or_knn_l2sq_qc_f32.argtypes = [P, I64, P, P, I64, I32, I64, I32, C.c_int, C.c_int, P, P]
     L.or_knn_l2_f64.argtypes = [P, I64, P, I64, I32, P, I32, C.c_int, C.c_int, P, P]
     L.or_knn_cos_f64.argtypes = [P, I64, I32, I32, D, D, D, I64, I64, C.c_int, P, P, P]
     L.or_knn_cos_f64d.argtypes = [P, I64, I32, I32, D, D, D, I64, I64, C.c_int, P, P, P]
@@ -107,6 +114,20 @@ def knn_l2sq_rows(X, k, rows, nthreads=0):
     dist = np.empty((len(rows), k), np.float32)
     _check(lib().or_knn_l2sq_rows_f32(_p(X), n, d, k, _p(rows), len(rows), nthreads, _p(idx),
                                       _p(dist)), "knn_l2sq_rows")
+    return idx, dist
+
+
+def knn_l2sq_qc(Q, q_ids, Cm, c_off, k, excl=True, nthreads=0):
+    """Per-shard L2^2 kNN (or_knn_l2sq_qc_f32): queries with global ids against
+    a corpus shard whose rows have global ids c_off + j."""
+    Q = np.ascontiguousarray(Q, dtype=np.float32)
+    Cm = np.ascontiguousarray(Cm, dtype=np.float32)
+    q_ids = np.ascontiguousarray(q_ids, dtype=np.int64)
+    nq, d = Q.shape
+    idx = np.empty((nq, k), np.int32)
+    dist = np.empty((nq, k), np.float32)
+    _check(lib().or_knn_l2sq_qc_f32(_p(Q), nq, _p(q_ids), _p(Cm), Cm.shape[0], d, c_off, k,
+                                    int(excl), nthreads, _p(idx), _p(dist)), "knn_l2sq_qc")
     return idx, dist
 
 
@@ -377,3 +398,67 @@ def search_lambda_aware(X, lambdas, Q, lambda_q, k, alpha, nthreads=0, hybrid=Fa
     _check(fn(_p(X), n, f, _p(lam), _p(Q), _p(lq), nq, k, alpha, nthreads, _p(oi), _p(os_),
               _p(oc)), "search_lambda_aware")
     return oi[:, :k], os_[:, :k], oc
+
+
+# ---- glibc logf / expf (glibc_check.c) -------------------------------------
+def libm_f32(x=None, n=None, bits0=0, fn=0):
+    """The HOST glibc logf (fn 0) / expf (fn 1) of x, or of the bit patterns
+    bits0 .. bits0 + n - 1."""
+    if x is not None:
+        x = np.ascontiguousarray(x, dtype=np.float32)
+        n = len(x)
+    out = np.empty(n, np.float32)
+    _check(lib().or_libm_f32(None if x is None else _p(x), n, bits0, fn, _p(out), 0), "libm_f32")
+    return out
+
+
+def libm_mismatch(bits0, got, fn):
+    """How many of got[i] differ from the host glibc value at bit pattern
+    bits0 + i (NaN matches NaN)."""
+    got = np.ascontiguousarray(got, dtype=np.float32)
+    return int(lib().or_libm_mismatch(bits0, len(got), fn, _p(got)))
+
+
+def glibc_restated_check(fn, stride):
+    """Mismatches of the host copy of the device restatement vs host glibc
+    over every stride-th f32 bit pattern."""
+    return int(lib().or_glibc_restated_check(fn, stride))
+
+
+def glibc_tables(which):
+    out = np.zeros(40, np.uint64)
+    m = lib().or_glibc_tables(which, _p(out))
+    return out[:m]
+
+
+def glibc_tables_from_libm(path=None):
+    """Re-derive the restatement's tables from the host libm's bytes: the
+    logf table is the 16 {1/c, log c} pairs right before ln2 (followed by the
+    3 polynomial coefficients, e_logf_data.c layout); the expf data is the 32
+    table words + shift_scaled + poly[3] + shift + invln2_scaled +
+    poly_scaled[3] (e_exp2f_data.c layout) around invln2_scaled = 32/ln2."""
+    import ctypes.util
+    import struct
+    path = path or "/lib/x86_64-linux-gnu/libm.so.6"
+    data = open(path, "rb").read()
+    ln2 = struct.pack("<d", float.fromhex("0x1.62e42fefa39efp-1"))
+    log = None
+    p = data.find(ln2)
+    while p >= 0:
+        if p >= 256:
+            tab = np.frombuffer(data[p - 256:p], dtype="<f8").reshape(16, 2)
+            if np.all((tab[:, 0] > 0.6) & (tab[:, 0] < 1.6)) and \
+                    np.allclose(tab[:, 1], -np.log(tab[:, 0]), atol=1e-6):
+                poly = np.frombuffer(data[p + 8:p + 32], dtype="<u8")
+                log = np.concatenate([tab.reshape(-1).view(np.uint64), poly[[0, 1, 2]],
+                                      np.frombuffer(ln2, dtype="<u8")])
+                break
+        p = data.find(ln2, p + 1)
+    inv = struct.pack("<d", float.fromhex("0x1.71547652b82fep+5"))
+    q = data.find(inv)
+    base = q - 256 - 8 - 24 - 8
+    tab = np.frombuffer(data[base:base + 256], dtype="<u8")
+    rest = np.frombuffer(data[base + 256:base + 256 + 72], dtype="<u8")
+    # rest: shift_scaled, poly[3], shift, invln2_scaled, poly_scaled[3]
+    exp = np.concatenate([tab, rest[[6, 7, 8]], rest[[5]], rest[[4]]])
+    return log, exp

@@ -58,3 +58,21 @@ def to_bf16_bits(x: np.ndarray) -> np.ndarray:
 
 def bf16_bits_to_f32(b: np.ndarray) -> np.ndarray:
     return (b.astype(np.uint32) << np.uint32(16)).view(np.float32)
+
+
+def sorted_rows(n: int, d: int, kind: str, seed: int = 3) -> np.ndarray:
+    """Adversarial row ORDERS for the two-phase generators: rows
+    sorted so that the corpus order keeps improving every row's candidates.
+      near_1d    — x = t v + 0.05 noise + 0.2 with t sorted (the original
+                   stress case of the round-2 cosine test: almost every row's
+                   neighbours are its index neighbours)
+      projection — a normal cloud (+0.3) sorted by one random projection."""
+    rng = np.random.default_rng(seed)
+    if kind == "near_1d":
+        t = np.sort(rng.uniform(-1.0, 1.0, n))
+        v = rng.normal(size=d)
+        return (np.outer(t, v) + 0.05 * rng.normal(size=(n, d)) + 0.2).astype(np.float32)
+    if kind == "projection":
+        X = rng.normal(size=(n, d)) + 0.3
+        return X[np.argsort(X @ rng.normal(size=d))].astype(np.float32)
+    raise ValueError(kind)

@@ -62,7 +62,7 @@ def test_c2_1m_uniform_sampled_rows_bit_exact(c2):
     rows = np.random.default_rng(0).choice(N, 128, replace=False)
     _check_graph(X.cpu().numpy(), r.idx.cpu().numpy(), r.dist.cpu().numpy(), rows)
     st = r.stats
-    print("C2 stats", json.dumps({k: v for k, v in st.items() if k != "reserved1"}))
+    print("C2 stats", json.dumps({k: v for k, v in st.items()}))
     assert st["n_uncertified"] == 0 and st["n_escalated"] == 0
 
 
@@ -82,7 +82,7 @@ def test_c2_1m_clustered_stress_bounded():
     st = r.stats
     rec = {"gen_s": round(t1 - t0, 1), "knn_wall_s": round(t2 - t1, 2),
            **{k: (round(v, 2) if isinstance(v, float) else v) for k, v in st.items()
-              if k != "reserved1"}}
+             }}
     print("C2-clustered stats", json.dumps(rec))
     # bounded: the escalation / exact-scan cost stays within a small multiple
     # of the uniform build (2 s)
@@ -132,6 +132,27 @@ def test_c3_chain_1m(c2):
         cols, vals = exp[int(i)]
         np.testing.assert_array_equal(ix[ip[i]:ip[i + 1]], cols)
         np.testing.assert_array_equal(iv[ip[i]:ip[i + 1]].view(np.uint64), vals.view(np.uint64))
+    # 1b. SF-GRASS over the symmetrised item graph (rows of any length: the
+    #     hub rows of this graph hold thousands of entries): W = -offdiag(L),
+    #     whole graph bit-exact vs the oracle (sparsification.rs:32-101)
+    rid = torch.repeat_interleave(torch.arange(N, device="cuda"), L.indptr[1:] - L.indptr[:-1])
+    off = L.indices.to(torch.int64) != rid
+    cnt = torch.zeros(N + 1, dtype=torch.int64, device="cuda")
+    cnt[1:] = torch.cumsum(torch.bincount(rid[off], minlength=N), 0)
+    W = S.CsrMatrix(cnt, L.indices[off].contiguous(), (-L.values[off]).contiguous(), (N, N))
+    lens = (cnt[1:] - cnt[:-1])
+    print("C3 item adjacency: max row length", int(lens.max()), "rows > 512:",
+          int((lens > 512).sum()))
+    assert int(lens.max()) > 512  # long rows: the block sort
+    Ws, applied = S.sparsify_sfgrass_csr(W, 0.5)
+    assert applied
+    wip, wix, wiv = W.to_numpy()
+    rip, rix, riw = O.sfgrass(wip, wix, wiv, 0.5)
+    sip, six, siv = Ws.to_numpy()
+    np.testing.assert_array_equal(sip, rip)
+    np.testing.assert_array_equal(six, rix)
+    np.testing.assert_array_equal(siv.view(np.uint64), riw.view(np.uint64))
+    del W, Ws, rid, off
     # 2. feature graph (768 column nodes, topk 4) + its Laplacian
     fi, fd, fw, fst = S.knn_cos_columns(X, 4, eps=1.0, sigma=1.0, p=2.0)
     assert fst["n_uncertified"] == 0
@@ -166,8 +187,10 @@ def test_c5_1m_3072_bf16_cosine_sampled_rows():
         Xb[r0:r0 + (1 << 17)].copy_(tmp)
     del tmp
     idx, dist, w, st = S.knn_cos_bf16(Xb, K, eps=1.0, sigma=1.0, p=2.0, timing=True)
-    print("C5 stats", json.dumps({k: v for k, v in st.items() if k != "reserved1"}))
-    rows = np.array([0, 77_777, 524_287, n - 1])
+    print("C5 stats", json.dumps({k: v for k, v in st.items()}))
+    # 64 rows (>= 64): fixed edge rows + random ones
+    rows = np.unique(np.concatenate([[0, 1, 77_777, 524_287, n - 2, n - 1],
+                                     np.random.default_rng(5).choice(n, 58, replace=False)]))
     bits = Xb.view(torch.int16).cpu().numpy().view(np.uint16)
     ri, rd, rw = O.knn_cos_bf16_rows(bits, K, rows, nthreads=THREADS)
     sel = torch.from_numpy(rows).cuda()

@@ -20,12 +20,14 @@ from oracle import oracle as O
 pytestmark = pytest.mark.gpu
 
 
-def _inline(idx, w):
-    """laplacian.rs:216-282 on the eps-filtered rows: deg = row length,
-    sparsify iff avg > 10, rows with len > 2 keep max(len/2, 1) by
+def _inline(idx, w, deg=None):
+    """laplacian.rs:216-282 on the eps-filtered rows: deg = the eps-valid
+    neighbour counts (default: the row lengths, equal when no weight is
+    filtered), sparsify iff avg > 10, rows with len > 2 keep max(len/2, 1) by
     w * sqrt(deg_i deg_j) desc (ties: input position)."""
     n, k = idx.shape
-    deg = (idx >= 0).sum(1)
+    if deg is None:
+        deg = (idx >= 0).sum(1)
     if not deg.sum() / n > 10.0:
         return idx, w
     oi = np.full_like(idx, -1)
@@ -44,11 +46,12 @@ def _inline(idx, w):
 
 def _oracle_graph(items, topk, eps, sigma, p):
     items = np.asarray(items)
-    if items.dtype == np.float64:
-        idx, _, w = O.knn_cos_f64(items, topk, eps, sigma, p)
-    else:
-        idx, _, w = O.knn_cos(items, topk, eps, sigma, p)
-    oi, ow = _inline(idx, w)
+    knn = O.knn_cos_f64 if items.dtype == np.float64 else O.knn_cos
+    idx, _, w = knn(items, topk, eps, sigma, p)
+    # laplacian.rs:219-229: degrees count the eps-valid neighbours before the
+    # weight filter (:255-258): the same query with a weight that never drops
+    i2, _, _ = knn(items, topk, eps, 1.0, 1.0)
+    oi, ow = _inline(idx, w, (i2 >= 0).sum(1))
     return O.laplacian_union(oi, ow)
 
 
@@ -86,11 +89,33 @@ def test_f64_items_and_sigma_p():
     T = rng.normal(size=(70, 500)) + 0.3  # rows = nodes
     params = S.GraphParams(eps=0.9, k=6, topk=12, p=1.5, sigma=0.4)
     gl = S.build_laplacian_matrix(torch.from_numpy(T).cuda(), params)
-    assert gl.nnodes == 70
+    assert gl.nnodes == 500  # laplacian.rs:129,165-168: n = the column count of `transposed`
     _csr_equal(gl.matrix, _oracle_graph(T, 12, 0.9, 0.4, 1.5), rtol=1e-15)
     params2 = S.GraphParams(eps=0.9, k=6, topk=12, p=2.0, sigma=0.4)
     gl2 = S.build_laplacian_matrix(torch.from_numpy(T).cuda(), params2)
     _csr_equal(gl2.matrix, _oracle_graph(T, 12, 0.9, 0.4, 2.0))
+
+
+def test_inline_degree_counts_eps_valid_before_the_weight_filter():
+    """laplacian.rs:219-229 counts a node's neighbours with dist <= eps, before
+    the weight > 1e-12 filter of :255-258.  sigma = 1e-7, p = 2 drops every
+    edge with d >= 0.1: 7 groups of 10 near-identical nodes keep 9 weighted
+    edges each (row length 9, avg < 10) while every node has 16 eps-valid
+    neighbours (avg 16 > 10), so the reference prunes and a row-length
+    degree rule would not."""
+    import surfface_hip as S
+    rng = np.random.default_rng(12)
+    base = rng.normal(size=(7, 400))
+    T = np.repeat(base, 10, axis=0) + 0.02 * rng.normal(size=(70, 400))
+    params = S.GraphParams(eps=1.0, k=6, topk=16, p=2.0, sigma=1e-7)
+    gl = S.build_laplacian_matrix(torch.from_numpy(T).cuda(), params)
+    ref = _oracle_graph(T, 16, 1.0, 1e-7, 2.0)
+    _csr_equal(gl.matrix, ref)
+    # pruned: 4 = max(9 // 2, 1) kept per row before symmetrisation, so fewer
+    # than the 9 + 1 entries per row of the unpruned groups
+    assert gl.matrix.nnz < 70 * 10
+    idx, _, w = O.knn_cos_f64(T, 16, 1.0, 1e-7, 2.0)
+    assert ((idx >= 0).sum(1) == 9).all()
 
 
 def test_spectral_signals_laplacian_of_laplacian():

@@ -159,19 +159,22 @@ def test_two_phase_shapes(n, d, topk):
     exact((i, dd, w), O.knn_cos(Xf, topk))
 
 
-def test_two_phase_sorted_rows_stay_certified():
-    """Rows sorted along one principal direction (a corpus order
-    that keeps improving the candidates): the golden-ratio visiting order
-    keeps the sample representative, so the thresholds hold and almost every
-    row certifies; sampled rows bit-exact."""
-    rng = np.random.default_rng(3)
+@pytest.mark.parametrize("kind", ["near_1d", "projection"])
+def test_two_phase_sorted_rows_stay_certified(kind):
+    """Rows in an adversarial order (ADVICE r1 / VERDICT r2): near_1d is the
+    ORIGINAL round-2 stress case (t v + 0.05 noise + 0.2, rows sorted by t),
+    projection a normal cloud sorted by one projection.  Every row of the
+    graph is bit-exact vs the oracle; the uncertified rows (resolved by the
+    exact scan) and the fallback time are recorded, and the projection case
+    keeps almost every row certified."""
+    import json
     n, d = 20_000, 64
-    X = rng.normal(size=(n, d)) + 0.3
-    X = X[np.argsort(X @ rng.normal(size=d))].astype(np.float32)  # sorted by a projection
+    X = datagen.sorted_rows(n, d, kind)
     Xt, Xf = bf16_rows(X)
-    i, dd, w, st = hip(Xt, 10)
+    i, dd, w, st = hip(Xt, 10, timing=True)
+    print(f"sorted-rows cosine {kind}", json.dumps(
+        {k: (round(v, 3) if isinstance(v, float) else v) for k, v in st.items()}))
     assert st["sample_rows"] > 0
-    assert st["n_uncertified"] <= n // 100, {k: st[k] for k in ("n_uncertified", "slices", "sample_rows", "sweep_slices", "sweep_cap")}
-    for r in (0, 1, 777, n // 2, n - 1):
-        ri, rd, rw = O.knn_cos(Xf, 10, q_begin=r, q_end=r + 1)
-        exact((i[r:r + 1], dd[r:r + 1], w[r:r + 1]), (ri, rd, rw))
+    exact((i, dd, w), O.knn_cos(Xf, 10))
+    if kind == "projection":
+        assert st["n_uncertified"] <= n // 100, st

@@ -178,18 +178,82 @@ def test_euclidean_metric_sqrt_is_correctly_rounded(algo_e):
     import surfface_hip as S
     X = datagen.clustered(4000, 40, seed=21, blobs=9, dup_frac=0.01, zero_frac=0.002)
     r = S.knn_l2sq(torch.from_numpy(X).cuda(), 12, euclidean=True, algo=algo_e)
-    ridx, rdist = O.knn_l2sq(X, 12)
+    ridx, rdist = oracle_euclidean(X, 12)
     np.testing.assert_array_equal(r.idx.cpu().numpy(), ridx)
-    np.testing.assert_array_equal(r.dist.cpu().numpy().view(np.uint32),
-                                  np.sqrt(rdist).view(np.uint32))
+    np.testing.assert_array_equal(r.dist.cpu().numpy().view(np.uint32), rdist.view(np.uint32))
     # candidate-graph mirror (mst.rs:312-363) with the Euclidean metric
     e = S.build_candidate_graph(X, None, 12, S.DistanceMetric.Euclidean,
                                 S.ThicknessWeight.NoWeight, thickness=np.ones(len(X), np.float32))
     np.testing.assert_array_equal(e.v.cpu().numpy(), ridx.reshape(-1))
     np.testing.assert_array_equal(e.distance.cpu().numpy().view(np.uint32),
-                                  np.sqrt(rdist).reshape(-1).view(np.uint32))
+                                  rdist.reshape(-1).view(np.uint32))
     np.testing.assert_array_equal(e.cost.cpu().numpy().view(np.uint32),
                                   e.distance.cpu().numpy().view(np.uint32))
+
+
+def oracle_euclidean(X, k):
+    """The reference's Euclidean candidate graph (mst.rs:330-360 with
+    euclidean_distance_slice, distance.rs:195-203): the oracle's f32 fold,
+    sqrtf, then the stable sort of the ROOTS (ties by index)."""
+    v, d, _ = O.mst_candidates(X, None, k, O.MST_EUCLIDEAN, O.TW_NONE,
+                               thickness=np.ones(len(X), np.float32))
+    return v, d
+
+
+def _root_tie_rows():
+    """[0, 0, ...] and rows whose squared distances to it are 1.25 + 2^-23 and
+    1.25: different f32 L2^2 values with the same correctly rounded root."""
+    hi = np.float32(0.5) + np.float32(2.0 ** -23)
+    assert np.float32(1.0) + hi * hi != np.float32(1.25)
+    assert np.sqrt(np.float32(1.0) + hi * hi) == np.sqrt(np.float32(1.25))
+    return np.array([1.0, hi], np.float32), np.array([1.0, 0.5], np.float32)
+
+
+@pytest.mark.parametrize("algo_e", ["bf16x1", "bf16x3", "f32"])
+def test_euclidean_root_ties_order_by_index(algo_e):
+    """the reference sorts the ROOTED distances (stable, so equal
+    roots go by index).  A larger L2^2 on a smaller index that shares its root
+    with a smaller L2^2 must come first, and win the last kept slot.  Case 2:
+    the equal-root run extends past the extended k + 8 list (the root-keyed
+    exact rescan)."""
+    import surfface_hip as S
+    hi, lo = _root_tie_rows()
+    far = np.stack([np.array([10.0 + j, 3.0], np.float32) for j in range(60)])
+    X = np.concatenate([np.zeros((1, 2), np.float32), hi[None], lo[None], far])
+    X = np.concatenate([X, np.zeros((len(X), 6), np.float32)], axis=1)  # d = 8
+    for k in (1, 2, 5):
+        r = S.knn_l2sq(torch.from_numpy(X).cuda(), k, euclidean=True, algo=algo_e)
+        ridx, rdist = oracle_euclidean(X, k)
+        assert ridx[0, 0] == 1  # the larger L2^2 on the smaller index
+        np.testing.assert_array_equal(r.idx.cpu().numpy(), ridx)
+        np.testing.assert_array_equal(r.dist.cpu().numpy().view(np.uint32), rdist.view(np.uint32))
+    # 20 hi rows (ids 1..20) and 20 lo rows (ids 21..40): L2^2 order puts
+    # every lo row first, the root order the hi rows
+    X2 = np.concatenate([np.zeros((1, 2), np.float32), np.repeat(hi[None], 20, 0),
+                         np.repeat(lo[None], 20, 0), far])
+    X2 = np.concatenate([X2, np.zeros((len(X2), 6), np.float32)], axis=1)
+    r = S.knn_l2sq(torch.from_numpy(X2).cuda(), 4, euclidean=True, algo=algo_e)
+    ridx, rdist = oracle_euclidean(X2, 4)
+    assert list(ridx[0]) == [1, 2, 3, 4]
+    np.testing.assert_array_equal(r.idx.cpu().numpy(), ridx)
+    np.testing.assert_array_equal(r.dist.cpu().numpy().view(np.uint32), rdist.view(np.uint32))
+    assert r.stats["n_root_rescan"] >= 1
+
+
+@pytest.mark.parametrize("kind", ["near_1d", "projection"])
+def test_bf16x1_two_phase_sorted_rows(kind):
+    """The headline L2 generator (bf16x1 two-phase) on rows in an adversarial
+    order: every row bit-exact vs the oracle; uncertified rows and
+    the fallback cost recorded."""
+    import json
+    n, d, k = 20_000, 64, 10
+    X = datagen.sorted_rows(n, d, kind)
+    idx, dist, st = hip_knn(X, k, algo="bf16x1", timing=True)
+    print(f"sorted-rows L2 {kind}", json.dumps(
+        {kk: (round(v, 3) if isinstance(v, float) else v) for kk, v in st.items()}))
+    assert st["algo"] == 3 and st["sample_rows"] > 0
+    ridx, rdist = O.knn_l2sq(X, k)
+    assert_exact(idx, dist, ridx, rdist)
 
 
 def test_uncertified_rows_batched_fallback():

@@ -18,6 +18,8 @@ from oracle import oracle as O
 
 import datagen
 
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
 HERE = os.path.dirname(os.path.abspath(__file__))
 KA = json.load(open(os.path.join(HERE, "golden", "reference_known_answers.json")))
 GS = np.load(os.path.join(HERE, "golden", "golden_small.npz"))
@@ -479,3 +481,34 @@ def test_nearest_centroid_oracle_known_answers():
     idx, dist = O.nearest_centroid(batch, cents)
     assert idx.tolist() == [0, 1, 0, 1]
     assert dist.tolist() == [0.0, 0.0, 1.0, 5.0]
+
+
+def test_glibc_logf_expf_restatement():
+    """The kernels' f32 ln / exp (csrc/glibc_f32.hpp) restate the platform
+    glibc logf / expf the reference's f32::ln / f32::exp call.  CPU checks:
+    (1) the restatement's tables are the bytes of the host libm's
+    e_logf_data / e_exp2f_data (re-derived from the binary), (2) the device
+    header holds the same literals, (3) the host copy of the algorithm equals
+    the host glibc on every 61st f32 bit pattern (a stride-1 run over all
+    2^32 inputs: 0 mismatches; the device code is checked exhaustively by
+    tests/test_libm_gpu.py)."""
+    import re
+    import struct
+    lg, ex = O.glibc_tables_from_libm()
+    assert lg is not None
+    np.testing.assert_array_equal(lg, O.glibc_tables(0))
+    np.testing.assert_array_equal(ex, O.glibc_tables(1))
+    hdr = open(os.path.join(ROOT, "matternet-rs_amd", "csrc", "glibc_f32.hpp")).read()
+    body = hdr[hdr.index("kLogT"):hdr.index("// glibc logf")]
+    lits = re.findall(r"-?0x[0-9a-f]+\.?[0-9a-f]*p[+-]\d+|0x[0-9a-f]{16}", body)
+    vals = []
+    for t in lits:
+        if "p" in t:
+            vals.append(struct.unpack("<Q", struct.pack("<d", float.fromhex(t)))[0])
+        else:
+            vals.append(int(t, 16))
+    # header order: log table (32), A0 A1 A2, Ln2, exp table (32), C0 C1 C2, InvLn2N, Shift
+    np.testing.assert_array_equal(np.array(vals[:36], np.uint64), O.glibc_tables(0))
+    np.testing.assert_array_equal(np.array(vals[36:], np.uint64), O.glibc_tables(1))
+    assert O.glibc_restated_check(0, 61) == 0
+    assert O.glibc_restated_check(1, 61) == 0

@@ -99,3 +99,61 @@ def test_inline_mode_vs_restatement():
             exp = [j for j, _, _ in row]
         got = [int(v) for v in oi[i] if v >= 0]
         assert got == exp, i
+
+
+def _csr_hip(ip, ix, w, ratio=0.5, n_nodes=0):
+    import surfface_hip as S
+    n = len(ip) - 1
+    A = S.CsrMatrix(torch.from_numpy(np.asarray(ip, np.int64)).cuda(),
+                    torch.from_numpy(np.asarray(ix, np.int32)).cuda(),
+                    torch.from_numpy(np.asarray(w, np.float64)).cuda(), (n, n))
+    out, applied = S.sparsify_sfgrass_csr(A, ratio, n_nodes)
+    oip, oix, oiw = out.to_numpy()
+    return oip, oix, oiw, applied
+
+
+@pytest.mark.parametrize("ratio", [0.5, 0.1, 0.37, 1.0])
+def test_csr_rows_of_any_length_vs_oracle(ratio):
+    """mn_sparsify_sfgrass: CSR rows of ANY length — empty,
+    single, wave-sized, block-sized (LDS) and hub rows beyond the LDS image
+    (global-scratch bitonic) — with quantised weights (score ties by input
+    position), bit-exact vs or_sfgrass (sparsification.rs:32-101)."""
+    rng = np.random.default_rng(11)
+    n = 30_000
+    lens = rng.integers(0, 40, size=n)
+    lens[:5] = [0, 1, 2, 3, 0]
+    lens[100:110] = rng.integers(65, 512, size=10)      # wave tiers
+    lens[200:220] = rng.integers(513, 8192, size=20)    # LDS block sort
+    lens[300] = 8192
+    lens[301] = 8193                                    # first hub size
+    lens[302] = 20_000
+    lens[303] = 70_001                                  # > 2^16
+    ip = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+    ix = rng.integers(0, n, size=int(ip[-1])).astype(np.int32)
+    w = np.round(rng.random(int(ip[-1])) * 8) / 8.0
+    oip, oix, oiw, applied = _csr_hip(ip, ix, w, ratio)
+    assert applied
+    rip, rix, riw = O.sfgrass(ip, ix, w, ratio)
+    np.testing.assert_array_equal(oip, rip)
+    np.testing.assert_array_equal(oix, rix)
+    np.testing.assert_array_equal(oiw.view(np.uint64), riw.view(np.uint64))
+
+
+def test_csr_sparse_graph_unchanged_and_n_nodes():
+    """avg = edges / n_nodes < 10: the rows come back unchanged
+    (sparsification.rs:41-53); the same rows with a smaller n_nodes divisor
+    cross the switch."""
+    rng = np.random.default_rng(2)
+    n = 1000
+    lens = rng.integers(0, 12, size=n)                   # avg ~5.5
+    ip = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+    ix = rng.integers(0, n, size=int(ip[-1])).astype(np.int32)
+    w = rng.random(int(ip[-1]))
+    oip, oix, oiw, applied = _csr_hip(ip, ix, w)
+    assert not applied
+    np.testing.assert_array_equal(oip, ip)
+    np.testing.assert_array_equal(oix, ix)
+    np.testing.assert_array_equal(oiw, w)
+    oip, oix, oiw, applied = _csr_hip(ip, ix, w, n_nodes=400)  # avg ~13.8
+    assert applied
+    assert oip[-1] < ip[-1]
