@@ -43,6 +43,9 @@ enum ScratchSlot {
     kSlotX1Esc,    //                escalated rows (gathered queries, lists)
     kSlotPerm,     // corpus visiting order (+ permuted norms / sample rows)
     kSlotL2List,   // MN_L2: the extended L2^2 list before the root order
+    kSlotSymOrd,   // MN_KNN_BF16X1 symmetric sweep: tau0 order + per-position arrays
+    kSlotSymTab,   //                block table
+    kSlotSortTmp,  // radix-sort temporary storage
     kNumSlots
 };
 

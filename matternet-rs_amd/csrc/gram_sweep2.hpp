@@ -30,6 +30,7 @@
 //    wave's READ window, beside its partner's MFMAs.
 #pragma once
 #include <climits>
+#include <type_traits>
 
 #include "common.hpp"
 
@@ -38,6 +39,7 @@ namespace ksw2 {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 
 constexpr int BQ = 256;      // queries per block
 constexpr int BC = 256;      // corpus rows per tile
@@ -53,7 +55,11 @@ struct alignas(16) Smem {
     uint16_t C[NSLOT][BC][KB];   // corpus k-step, 16 KB per slot
     uint16_t Q[NSLOT][BQ][KB];   // query k-step, 16 KB per slot
     float hc[2][BC];             // |c|^2 / 2 of a tile (+inf past the slice end)
-    int qcnt[BQ];                // candidates written per query of the block
+    float tc[2][BC];             // SW_SYM: tau0 of a tile's rows (off-diagonal keys)
+    union {
+        int qcnt[BQ];            // candidates written per query of the block
+        float ta[BQ];            // SW_SYM: -|q|^2 / 2 (off-diagonal tiles)
+    };
     float t0[BQ];                // tau0 of the block's queries
     float tq[BQ];                // (tau0 - |q|^2) / 2 of the block's queries
     int scnt[NWAVES];            // staged entries per wave
@@ -87,7 +93,27 @@ __device__ __forceinline__ int xcd_remap(int orig, int nwg) {
 // wave's read window (fusing the init into the first MFMA window, or one
 // ballot per 2 or 4 fragments before the per-fragment ones, measured equal
 // within noise at C2).
-enum SweepMode { SW_L2 = 0, SW_COS = 1 };
+enum SweepMode { SW_L2 = 0, SW_COS = 1, SW_SYM = 2 };
+
+// SW_SYM (self kNN, X both operands, rows in ascending-tau0 order): the
+// sweep covers each unordered pair once.  Block b takes row block I = tab[b].x
+// against column tiles [tab[b].y, tab[b].z) with every tile J >= I.  The
+// diagonal tile (J == I, only ever a block's first tile) runs as SW_L2: acc0 =
+// tq(q) - hc(c), a pair is row q's candidate iff acc > 0, key = tau0(q) -
+// 2 acc.  An off-diagonal tile (J > I, so tau0(c) >= tau0(q): sorted order)
+// folds the COLUMN's threshold: acc0 = aoff(q) - hoff(c) with aoff = -|q|^2/2,
+// hoff = (|c|^2 - tau0(c)) / 2, so acc > 0 iff key = tau0(c) - 2 acc < tau0(c),
+// the test of row c; row q's own test key < tau0(q) <= tau0(c) implies it and
+// is checked only on those hits.  Both rows' candidates go to per-ROW
+// buffers buf[row][cap] through global counters cnt[row] (returned atomics at
+// the flush of the per-wave LDS staging area; counts past cap mean overflow).
+struct SymArgs {
+    const int4 *tab;    // per block: (I, Jbeg, Jend) in 256-row blocks
+    const float *aoff;  // [n] -|x|^2 / 2
+    const float *hoff;  // [n] (|x|^2 - tau0) / 2
+    int kexp;           // F16: operands hold x 2^e, the folds (tq, hc, aoff, hoff)
+                        // are scaled by 2^2e; keys = tau0 - 2 acc 2^kexp, kexp = -2e
+};
 
 // TM (tile-major layout): element (row r, feature e) of Qk / Ck at
 // ((r / 256) pst + e / 32) * 8192 + (r % 256) * 32 + e % 32 (pst >= nkb: the
@@ -96,12 +122,17 @@ enum SweepMode { SW_L2 = 0, SW_COS = 1 };
 // consecutive 16-KB pieces of one contiguous 256-row panel instead of pieces
 // n * 64 B apart (one page per k-step and operand), and c_begin / chunk must
 // be multiples of BC.
-template <int PROBE, int MODE = SW_L2, bool TM = false>
+// F16: the operands are fp16 copies of x 2^e (one v_mfma_f32_16x16x32_f16 per
+// 32 features: the same rate as bf16, 11 significant bits instead of 8, so the
+// residual-norm bound is ~8x tighter); SW_SYM only.
+template <int PROBE, int MODE = SW_L2, bool TM = false, bool F16 = false>
 __global__ __launch_bounds__(NT) void k_gram_sweep2(
     const uint16_t *__restrict__ Qk, int64_t nq, const uint16_t *__restrict__ Ck, int64_t nc,
     int nkb, int64_t q_off, int64_t c_off, int excl, const float *__restrict__ tq,
     const float *__restrict__ tau0, const float *__restrict__ hc, int64_t c_begin, int S,
-    int64_t chunk, int cap, uint2 *__restrict__ buf, int *__restrict__ cnt, int pst = 0) {
+    int64_t chunk, int cap, uint2 *__restrict__ buf, int *__restrict__ cnt, int pst = 0,
+    SymArgs sym = SymArgs{}) {
+    constexpr bool SYM = MODE == SW_SYM;
     __shared__ Smem sm;
     const int tid = threadIdx.x, lane = tid & 63;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -109,24 +140,40 @@ __global__ __launch_bounds__(NT) void k_gram_sweep2(
     const int fr = lane & 15, fk = lane >> 4;
     const int v = xcd_remap((int)blockIdx.x, (int)gridDim.x);
     // (32-bit row / step counters: nq * 32, nc * 32 < 2^31 is checked by the driver)
-    const int q0 = (v / S) * BQ;
-    const int sl = v % S;
-    const int cbeg = (int)(c_begin + (int64_t)sl * chunk);
-    const int cend = (int)min(nc, (int64_t)cbeg + chunk);
+    int q0, sl, cbeg, cend;
+    if constexpr (SYM) {
+        const int4 e = sym.tab[v];
+        q0 = e.x * BQ;
+        sl = 0;
+        cbeg = e.y * BC;
+        cend = (int)min(nc, (int64_t)e.z * BC);
+    } else {
+        q0 = (v / S) * BQ;
+        sl = v % S;
+        cbeg = (int)(c_begin + (int64_t)sl * chunk);
+        cend = (int)min(nc, (int64_t)cbeg + chunk);
+    }
     const int ntile = cend > cbeg ? (cend - cbeg + BC - 1) / BC : 0;
     const int gtot = ntile * nkb;
     const float pad = MODE == SW_COS ? __builtin_nanf("") : __builtin_inff();
+    const bool diag0 = SYM && cbeg == q0;  // SW_SYM: the first tile is the diagonal one
 
     if (tid < NWAVES) sm.scnt[tid] = 0;
     if (tid < BQ) {
         // padded queries never qualify (COS: NaN, as -inf * -|c| would be +inf)
         sm.tq[tid] = q0 + tid < nq ? tq[q0 + tid] : (MODE == SW_COS ? pad : -__builtin_inff());
-        sm.qcnt[tid] = 0;
         sm.t0[tid] = q0 + tid < nq ? tau0[q0 + tid] : 0.f;
+        if constexpr (SYM) sm.ta[tid] = q0 + tid < nq ? sym.aoff[q0 + tid] : -__builtin_inff();
+        else sm.qcnt[tid] = 0;
     }
     if (ntile > 0 && tid < BC) {
         const int c = cbeg + tid;
-        sm.hc[0][tid] = (c < cend) ? hc[c] : pad;
+        if constexpr (SYM) {
+            sm.hc[0][tid] = (c < cend) ? (diag0 ? hc[c] : sym.hoff[c]) : pad;
+            sm.tc[0][tid] = (c < cend) ? tau0[c] : pad;
+        } else {
+            sm.hc[0][tid] = (c < cend) ? hc[c] : pad;
+        }
     }
 
     // ---- LDS-DMA issue state: the next k-step gi to stage (tile row bt0,
@@ -186,12 +233,14 @@ __global__ __launch_bounds__(NT) void k_gram_sweep2(
         }
     };
 
+    typedef typename std::conditional<F16, f16x8, bf16x8>::type frag_t;
     f32x4 acc[WQF][WCF];
-    bf16x8 fq[WQF], fc[WCF];
-    auto init_acc = [&](int par) {
+    frag_t fq[WQF], fc[WCF];
+    auto init_acc = [&](int par, bool diag) {
         float tql[WQF];  // this lane's queries, one per 16-query fragment
+        const float *qa = (SYM && !diag) ? sm.ta : sm.tq;
 #pragma unroll
-        for (int f = 0; f < WQF; ++f) tql[f] = sm.tq[64 * wq + 16 * f + fr];
+        for (int f = 0; f < WQF; ++f) tql[f] = qa[64 * wq + 16 * f + fr];
 #pragma unroll
         for (int g = 0; g < WCF; ++g) {
             const float4 x =
@@ -217,17 +266,20 @@ __global__ __launch_bounds__(NT) void k_gram_sweep2(
         const int chs = 8 * swz(fr, fk);
 #pragma unroll
         for (int f = 0; f < WQF; ++f)
-            fq[f] = *reinterpret_cast<const bf16x8 *>(&sm.Q[slot][64 * wq + 16 * f + fr][chs]);
+            fq[f] = *reinterpret_cast<const frag_t *>(&sm.Q[slot][64 * wq + 16 * f + fr][chs]);
 #pragma unroll
         for (int g = 0; g < WCF; ++g)
-            fc[g] = *reinterpret_cast<const bf16x8 *>(&sm.C[slot][128 * wc + 16 * g + fr][chs]);
+            fc[g] = *reinterpret_cast<const frag_t *>(&sm.C[slot][128 * wc + 16 * g + fr][chs]);
     };
     auto mfmas = [&]() {
 #pragma unroll
         for (int f = 0; f < WQF; ++f)
 #pragma unroll
             for (int g = 0; g < WCF; ++g)
-                acc[f][g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fc[g], fq[f], acc[f][g], 0, 0, 0);
+                if constexpr (F16)
+                    acc[f][g] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fc[g], fq[f], acc[f][g], 0, 0, 0);
+                else
+                    acc[f][g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fc[g], fq[f], acc[f][g], 0, 0, 0);
     };
 
     bool dirty = false;  // candidate stores issued since the last counted wait
@@ -239,11 +291,29 @@ __global__ __launch_bounds__(NT) void k_gram_sweep2(
         const int n = min(sm.scnt[w], SCAP);
         for (int e = lane; e < n; e += 64) {
             const uint32_t pq = sm.stp[w][e];
-            const int ql = (int)(pq & 255u), pos = (int)(pq >> 8);
-            buf[((int64_t)(q0 + ql) * S + sl) * cap + pos] = sm.stk[w][e];
+            if constexpr (SYM) {  // pq = the row; its slot from the row's counter
+                const int pos = atomicAdd(&cnt[pq], 1);
+                if (pos < cap) buf[(int64_t)pq * cap + pos] = sm.stk[w][e];
+            } else {
+                const int ql = (int)(pq & 255u), pos = (int)(pq >> 8);
+                buf[((int64_t)(q0 + ql) * S + sl) * cap + pos] = sm.stk[w][e];
+            }
         }
         sm.scnt[w] = 0;
         dirty = true;
+    };
+    // SW_SYM: one candidate (row, id, key) into the wave's staging area
+    auto emit_sym = [&](uint32_t row, uint32_t id, float key) {
+        const uint2 kv = make_uint2(__float_as_uint(key), id);
+        const int e = atomicAdd(&sm.scnt[w], 1);
+        if (e < SCAP) {
+            sm.stk[w][e] = kv;
+            sm.stp[w][e] = row;
+        } else {  // area full: straight out (rare)
+            const int pos = atomicAdd(&cnt[row], 1);
+            if (pos < cap) buf[(int64_t)row * cap + pos] = kv;
+            dirty = true;
+        }
     };
     // candidates of the tile starting at corpus row ct0: positive accumulators.
     // Per 16 x 16 fragment one max and one ballot (wave-uniform branch); the
@@ -251,7 +321,7 @@ __global__ __launch_bounds__(NT) void k_gram_sweep2(
     // (a few per wave and tile at the C2 threshold).
     // one 16 x 16 fragment: per-fragment max + ballot (wave-uniform branch);
     // the staging body runs only where some lane has a candidate
-    auto check_block = [&](int f, int g, int ct0, int hpar) {
+    auto check_block = [&](int f, int g, int ct0, int hpar, bool diag) {
         const f32x4 a = acc[f][g];
         const float m4 = fmaxf(fmaxf(a[0], a[1]), fmaxf(a[2], a[3]));
         if (__builtin_expect(__ballot(m4 > 0.f) == 0, 1)) return;
@@ -262,6 +332,22 @@ __global__ __launch_bounds__(NT) void k_gram_sweep2(
 #pragma unroll
         for (int r = 0; r < 4; ++r) pm |= a[r] > 0.f ? (1u << r) : 0u;
         if (excl && (unsigned)(qgl - c) < 4u) pm &= ~(1u << (qgl - c));
+        if constexpr (SYM) {
+            const float t0l = sm.t0[ql];
+            while (pm) {
+                const int r = __builtin_ctz(pm);
+                pm &= pm - 1;
+                const float a2 = 2.f * (F16 ? __builtin_ldexpf(a[r], sym.kexp) : a[r]);
+                if (diag) {  // row q's test, as SW_L2
+                    emit_sym((uint32_t)qgl, (uint32_t)(c + r), t0l - a2);
+                } else {     // row c's test (acc > 0); row q's only on these hits
+                    const float key = sm.tc[hpar][128 * wc + 16 * g + 4 * fk + r] - a2;
+                    emit_sym((uint32_t)(c + r), (uint32_t)qgl, key);
+                    if (key < t0l) emit_sym((uint32_t)qgl, (uint32_t)(c + r), key);
+                }
+            }
+            return;
+        }
         if (pm != 0) {
             const int mine = __popc(pm);
             int pos = atomicAdd(&sm.qcnt[ql], mine);
@@ -292,12 +378,12 @@ __global__ __launch_bounds__(NT) void k_gram_sweep2(
     };
     // candidates of the tile starting at corpus row ct0: positive accumulators
     // (hpar: the hc parity of that tile)
-    auto check = [&](int ct0, int hpar) {
+    auto check = [&](int ct0, int hpar, bool diag) {
         if constexpr (PROBE == 0) {
 #pragma unroll
             for (int f = 0; f < WQF; ++f)
 #pragma unroll
-                for (int g = 0; g < WCF; ++g) check_block(f, g, ct0, hpar);
+                for (int g = 0; g < WCF; ++g) check_block(f, g, ct0, hpar, diag);
             // wave-uniform: spill the area once it is 3/4 full (or overran)
             if (sm.scnt[w] >= SCAP * 3 / 4) flush();
         } else {
@@ -317,12 +403,12 @@ __global__ __launch_bounds__(NT) void k_gram_sweep2(
     else if (gtot == 2) MN_VMCNT(4);
     else MN_VMCNT(0);
     __syncthreads();  // also publishes sm.hc[0], qcnt, t0
-    if (gtot > 0) init_acc(0);
+    if (gtot > 0) init_acc(0, diag0);
     if (wc == 1) __builtin_amdgcn_s_barrier();  // the trailing group starts one window late
 
     int c0 = cbeg;  // first corpus row of the current tile
     int kb = 0, par = 0;
-    float hcn = 0.f;  // next tile's hc (waves 0-3, one value per lane)
+    float hcn = 0.f, tcn = 0.f;  // next tile's hc (and SW_SYM tau0), waves 0-3
     for (int g = 0; g < gtot; ++g) {
         // ================= READ window of k-step g =================
         const bool more = c0 + BC < cend;
@@ -330,22 +416,28 @@ __global__ __launch_bounds__(NT) void k_gram_sweep2(
             // the next tile's |c|^2 / 2: waves 0-3 load one value per lane
             // (asm loads: the compiler's own waits would drain the DMA queue);
             // older than the DMA issued just below, so the counted waits
-            // retire them
-            const float *p = hc + min(c0 + BC + 64 * wq + lane, (int)nc - 1);
+            // retire them.  SW_SYM: the next tile is off-diagonal: hoff, tau0
+            const int cn = min(c0 + BC + 64 * wq + lane, (int)nc - 1);
+            const float *p = SYM ? sym.hoff + cn : hc + cn;
             asm volatile("global_load_dword %0, %1, off" : "=v"(hcn) : "v"(p) : "memory");
+            if constexpr (SYM) {
+                const float *pt = tau0 + cn;
+                asm volatile("global_load_dword %0, %1, off" : "=v"(tcn) : "v"(pt) : "memory");
+            }
         }
         if constexpr (PROBE < 2 || PROBE == 4) issue();  // k-step g + 3
         if (kb == 0 && g > 0) {
             // the previous tile's candidates, then this tile's accumulator
             // init (before the fragment reads: the fragments are dead here)
-            check(c0 - BC, par ^ 1);
-            init_acc(par);
+            check(c0 - BC, par ^ 1, diag0 && c0 - BC == cbeg);
+            init_acc(par, false);
         }
         if constexpr (PROBE < 3 || PROBE == 4) read_frags((int)(g & (NSLOT - 1)));
         if (kb == nkb - 2 && more && wc == 0) {
             // written 2 k-steps (>= 2 barriers) before init_acc reads it
             const int cb = c0 + BC + 64 * wq + lane;
             sm.hc[par ^ 1][64 * wq + lane] = cb < cend ? hcn : pad;
+            if constexpr (SYM) sm.tc[par ^ 1][64 * wq + lane] = cb < cend ? tcn : pad;
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         if (PROBE != 4 && wc == 1) {
@@ -382,8 +474,9 @@ __global__ __launch_bounds__(NT) void k_gram_sweep2(
         }
     }
     if (wc == 0) __builtin_amdgcn_s_barrier();  // match the trailing group's extra window
-    if (gtot > 0) check(c0 - BC, par ^ 1);
+    if (gtot > 0) check(c0 - BC, par ^ 1, diag0 && c0 - BC == cbeg);
     if (sm.scnt[w] > 0) flush();
+    if constexpr (SYM) return;  // the per-row counters are final
     __syncthreads();
     if (tid < BQ && q0 + tid < nq) {
         const int c = sm.qcnt[tid];

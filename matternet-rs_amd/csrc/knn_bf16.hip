@@ -782,7 +782,7 @@ static int knn_cos_bf16_x1(const uint16_t *X, int64_t n, int32_t d, const mn_cos
                                   : ksw2::k_gram_sweep2<0, ksw2::SW_COS, false>);
         hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(ksw2::NT), 0, s, XK, n, XK, n, nkb,
                            (int64_t)0, (int64_t)0, 0, tq_pos, tq_pos, negn, m0, S2, p2.chunk,
-                           cap2, buf2, cnt2, pst);
+                           cap2, buf2, cnt2, pst, ksw2::SymArgs{});
         MN_KCHECK(s, "k_gram_sweep2<COS>");
         if (probe && *probe) {  // timing probe: no outputs are produced
             tm.mark();

@@ -33,6 +33,7 @@
 #include <climits>
 #include <cstdlib>
 #include <cstring>
+#include <vector>
 
 #include "common.hpp"
 #include "gram_bf16.hpp"
@@ -40,6 +41,11 @@
 #include "gram_sweep2.hpp"
 
 namespace mn {
+
+// sortkeys.hip
+hipError_t sort_f32_pairs(const float *keys_in, float *keys_out, const int *vals_in,
+                          int *vals_out, int64_t n, hipStream_t s);
+
 namespace knn {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
@@ -685,10 +691,12 @@ __global__ __launch_bounds__(256) void k_prep_x1(const float *__restrict__ X, in
                                                  float *__restrict__ hcv, float *__restrict__ hn,
                                                  float *__restrict__ rn,
                                                  unsigned *__restrict__ maxbits,
-                                                 int *__restrict__ flags, int corpus, int tm) {
+                                                 int *__restrict__ flags, int corpus, int tm,
+                                                 unsigned *__restrict__ amax) {
     const int lane = threadIdx.x & 63, hl = lane >> 5, ll = lane & 31;
     const int64_t wave0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+    float am = 0.f;  // max |x| (amax != NULL: the fp16 sweep's scale)
     for (int64_t r2 = 2 * wave0; r2 < n; r2 += 2 * nwaves) {
         const int64_t row = r2 + hl;
         const bool live = row < n;
@@ -715,6 +723,7 @@ __global__ __launch_bounds__(256) void k_prep_x1(const float *__restrict__ X, in
                 for (int v = 0; v < 2; ++v) {
                     const float x = xv[u + v];
                     bad |= !__builtin_isfinite(x);
+                    if (live) am = fmaxf(am, __builtin_fabsf(x));
                     const uint32_t hb = __builtin_fabsf(x) >= 0x1p-126f ? bf16_rne(x) : 0u;
                     const float hf = __uint_as_float(hb << 16);
                     const float r = x - hf;  // exact
@@ -727,9 +736,10 @@ __global__ __launch_bounds__(256) void k_prep_x1(const float *__restrict__ X, in
             }
             if (live) {
                 const uint4 pk = make_uint4(wv[0], wv[1], wv[2], wv[3]);
-                *reinterpret_cast<uint4 *>(XR + row * (int64_t)dp + t0) = pk;
-                *reinterpret_cast<uint4 *>(XK + kb32_at(row, t0 >> 5, n, tm) + (t0 & 31)) =
-                    pk;
+                if (XR) *reinterpret_cast<uint4 *>(XR + row * (int64_t)dp + t0) = pk;
+                if (XK)
+                    *reinterpret_cast<uint4 *>(XK + kb32_at(row, t0 >> 5, n, tm) + (t0 & 31)) =
+                        pk;
             }
         }
 #pragma unroll
@@ -756,6 +766,82 @@ __global__ __launch_bounds__(256) void k_prep_x1(const float *__restrict__ X, in
                 atomicMax(maxbits + 1, __float_as_uint(hf));
                 atomicMax(maxbits + 2, __float_as_uint(rf));
             }
+        }
+    }
+    if (amax) {
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) am = fmaxf(am, __shfl_xor(am, o));
+        if (lane == 0 && am > 0.f) atomicMax(amax, __float_as_uint(am));
+    }
+}
+
+// fp16 copy for the symmetric sweep (gram_sweep2.hpp F16): h = fp16(x 2^e)
+// (round to nearest even; |x 2^e| < 2^-14 flushed to 0, so the MFMA never
+// sees a subnormal), stored tile-major KB32 like k_prep_x1; in UNSCALED units
+// |h 2^-e| and |x - h 2^-e| per row (the residual is exact) and their maxima
+// over all rows (maxbits[0..1]).  Position `row` holds source row perm[row].
+template <bool VEC4>
+__global__ __launch_bounds__(256) void k_prep_f16(const float *__restrict__ X, int64_t n, int d,
+                                                  int dp, const int *__restrict__ perm,
+                                                  uint16_t *__restrict__ XK, int e,
+                                                  float *__restrict__ hn, float *__restrict__ rn,
+                                                  unsigned *__restrict__ maxbits, int tm) {
+    const int lane = threadIdx.x & 63, hl = lane >> 5, ll = lane & 31;
+    const int64_t wave0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+    for (int64_t r2 = 2 * wave0; r2 < n; r2 += 2 * nwaves) {
+        const int64_t row = r2 + hl;
+        const bool live = row < n;
+        const int64_t srow = perm ? (int64_t)perm[min(row, n - 1)] : min(row, n - 1);
+        const float *p = X + srow * (int64_t)d;
+        double sh = 0.0, sr = 0.0;
+        for (int t0 = 8 * ll; t0 < dp; t0 += 256) {
+            uint32_t wv[4];
+            float xv[8];
+            if (VEC4 && t0 + 8 <= d) {
+                const float4 a = *reinterpret_cast<const float4 *>(p + t0);
+                const float4 b = *reinterpret_cast<const float4 *>(p + t0 + 4);
+                xv[0] = a.x; xv[1] = a.y; xv[2] = a.z; xv[3] = a.w;
+                xv[4] = b.x; xv[5] = b.y; xv[6] = b.z; xv[7] = b.w;
+            } else {
+#pragma unroll
+                for (int u = 0; u < 8; ++u) xv[u] = t0 + u < d ? p[t0 + u] : 0.f;
+            }
+#pragma unroll
+            for (int u = 0; u < 8; u += 2) {
+                uint32_t hb2[2];
+#pragma unroll
+                for (int v = 0; v < 2; ++v) {
+                    const float x = xv[u + v];
+                    const float xs = __builtin_ldexpf(x, e);  // exact (|x 2^e| < 2^14)
+                    _Float16 h = __builtin_fabsf(xs) >= 0x1p-14f ? (_Float16)xs : (_Float16)0.f;
+                    uint16_t hbits;
+                    __builtin_memcpy(&hbits, &h, 2);
+                    const float hf = __builtin_ldexpf((float)h, -e);
+                    const float r = x - hf;  // exact
+                    sh += (double)hf * (double)hf;
+                    sr += (double)r * (double)r;
+                    hb2[v] = hbits;
+                }
+                wv[u >> 1] = hb2[0] | (hb2[1] << 16);
+            }
+            if (live) {
+                const uint4 pk = make_uint4(wv[0], wv[1], wv[2], wv[3]);
+                *reinterpret_cast<uint4 *>(XK + kb32_at(row, t0 >> 5, n, tm) + (t0 & 31)) = pk;
+            }
+        }
+#pragma unroll
+        for (int o = 16; o > 0; o >>= 1) {
+            sh += __shfl_xor(sh, o);
+            sr += __shfl_xor(sr, o);
+        }
+        if (ll == 0 && live) {
+            const float hf = f32_up(__builtin_sqrt(sh) * (1.0 + 0x1p-50));
+            const float rf = f32_up(__builtin_sqrt(sr) * (1.0 + 0x1p-50));
+            hn[row] = hf;
+            rn[row] = rf;
+            atomicMax(maxbits + 0, __float_as_uint(hf));
+            atomicMax(maxbits + 1, __float_as_uint(rf));
         }
     }
 }
@@ -918,14 +1004,48 @@ __global__ __launch_bounds__(256) void k_tau_x3(int64_t n, const int *__restrict
     delta[i] = f32_up(delta3_at(__builtin_fabs((double)T), qn, qh, ql, q2, Mn, Mh, Ml, M2, d, dp));
 }
 
-// Per query: T = min over phase-1 slices of tau (-inf: forced), tq, delta.
+// delta of the bf16x1 bound: Tf = |threshold| magnitude in the
+// accumulator terms, qn / qh / qr the row's |q|^2, |bf16(q)|, |q - bf16(q)|,
+// Mn the corpus max |c|^2, Mh / Mr the corpus maxima of |ch| / |c - ch|.
+// The error of the approximate key d~ = |q|^2 + |c|^2 - 2 (acc0 + qh.ch)
+// against the exact distance: the omitted products |q.c - qh.ch| <= |qh||rc|
+// + |rq||ch| + |rq||rc| (Cauchy-Schwarz), the f32 accumulation of acc0 and
+// the dp exact products, the roundings of the norms / folds / stored key
+// (4 u M), and the reference fold's own error (d + 3) u (|T| + 2 E).
+//   tight = 0: accumulation gamma (4 dp + 64) u (M + qh Mh) (the original,
+//              generous constant);
+//   tight = 1: 2 (dp + 33) u (M / 2 + qh Mh): <= 2 u per addition in ANY
+//              order (Higham's gamma_n sum |terms| with a factor 2 for a
+//              non-nearest internal rounding), |acc0| <= M / 2, sum |products|
+//              <= |qh||ch|; the probe scripts/probes/probe_mfma_accum.hip
+//              measures the MFMA chains well inside it (profiles/).
+__device__ __forceinline__ float delta_x1(double Tf, float qn, double qh, double qr, double Mn,
+                                          double Mh, double Mr, int d, int dp, int tight = 0) {
+    const double u = 0x1p-24;
+    const double M = Tf + (double)qn + Mn;
+    const double Eprod = qh * Mr + qr * Mh + qr * Mr;
+    const double acc = tight ? 2.0 * (dp + 33.0) * u * (0.5 * M + qh * Mh)
+                             : (4.0 * dp + 64.0) * u * (M + qh * Mh);
+    const double E = Eprod + acc + 4.0 * u * M;
+    const double dl = 2.0 * E + (d + 3.0) * u * (Tf + 2.0 * E) + 0x1p-100;
+    return f32_up(dl * (1.0 + 0x1p-20));
+}
+__device__ __forceinline__ float delta_x1(double Tf, float qn, double qh, double qr,
+                                          const unsigned *__restrict__ cmax, int d, int dp) {
+    return delta_x1(Tf, qn, qh, qr, __uint_as_float(cmax[0]), __uint_as_float(cmax[1]),
+                    __uint_as_float(cmax[2]), d, dp, 0);
+}
+
+// Per query: T = min over phase-1 slices of tau (-inf: forced), tq, delta;
+// tmax (may be NULL) collects max |T| over the finite T (uint bits).
 __global__ __launch_bounds__(256) void k_tau_x1(int64_t nq, int S1, const float *__restrict__ btau1,
                                                 const float *__restrict__ nq_f,
                                                 const float *__restrict__ hn_q,
                                                 const float *__restrict__ rn_q,
                                                 const unsigned *__restrict__ cmax, int d, int dp,
                                                 float *__restrict__ tq, float *__restrict__ tau0,
-                                                float *__restrict__ delta) {
+                                                float *__restrict__ delta,
+                                                unsigned *__restrict__ tmax) {
     const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (q >= nq) return;
     float T = __builtin_inff();
@@ -933,17 +1053,51 @@ __global__ __launch_bounds__(256) void k_tau_x1(int64_t nq, int S1, const float 
     const float qn = nq_f[q];
     tau0[q] = T;
     tq[q] = (T - qn) * 0.5f;
-    const double u = 0x1p-24;
-    const double Mn = __uint_as_float(cmax[0]), Mh = __uint_as_float(cmax[1]),
-                 Mr = __uint_as_float(cmax[2]);
-    const double qh = hn_q[q], qr = rn_q[q];
     const double Tf = __builtin_isfinite(T) ? __builtin_fabs((double)T) : 0.0;
-    const double M = Tf + (double)qn + Mn;
-    const double Eprod = qh * Mr + qr * Mh + qr * Mr;
-    const double gam = (4.0 * dp + 64.0) * u;
-    const double E = Eprod + gam * (M + qh * Mh) + 4.0 * u * M;
-    const double dl = 2.0 * E + (d + 3.0) * u * (Tf + 2.0 * E) + 0x1p-100;
-    delta[q] = f32_up(dl * (1.0 + 0x1p-20));
+    delta[q] = delta_x1(Tf, qn, hn_q[q], rn_q[q], cmax, d, dp);
+    if (tmax && __builtin_isfinite(T)) atomicMax(tmax, __float_as_uint(__builtin_fabsf(T)));
+}
+
+// SW_SYM per-position arrays (position p holds row pi[p]): the threshold,
+// both accumulator folds (gram_sweep2.hpp SW_SYM), scaled by 2^(2e) for the
+// fp16 operands (e = 0: bf16), and the certification bound with the
+// accumulator magnitude of any column's threshold (max |T|).  hq / rq: the
+// operand copy's |h| and |x - h| per POSITION (fp16) or per row (pos_hr = 0);
+// cmh: their maxima.
+__global__ __launch_bounds__(256) void k_sym_pos(int64_t n, const int *__restrict__ pi,
+                                                 const float *__restrict__ tau0,
+                                                 const float *__restrict__ nq_f,
+                                                 const float *__restrict__ hq,
+                                                 const float *__restrict__ rq, int pos_hr,
+                                                 const unsigned *__restrict__ cmax,
+                                                 const unsigned *__restrict__ cmh,
+                                                 const unsigned *__restrict__ tmax, int d, int dp,
+                                                 int e, int tight, float *__restrict__ tauP,
+                                                 float *__restrict__ tqP, float *__restrict__ hcP,
+                                                 float *__restrict__ hcS, float *__restrict__ aoff,
+                                                 float *__restrict__ hoff,
+                                                 float *__restrict__ dltP) {
+    const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= n) return;
+    const int r = pi[p];
+    const float T = tau0[r], qn = nq_f[r];
+    const float tq = (T - qn) * 0.5f, hc = 0.5f * qn;
+    tauP[p] = T;
+    tqP[p] = __builtin_ldexpf(tq, 2 * e);     // diagonal tile: row fold (as k_tau_x1)
+    hcS[p] = __builtin_ldexpf(hc, 2 * e);     //   and its column term
+    hcP[p] = hc;                              // (unscaled: the bf16x3 refill's corpus term)
+    aoff[p] = __builtin_ldexpf(-hc, 2 * e);   // off-diagonal tiles: acc0 = aoff(q) - hoff(c)
+    hoff[p] = __builtin_ldexpf(-tq, 2 * e);   //   = -|q|^2/2 + (tau0(c) - |c|^2)/2
+    const double Tf = __builtin_isfinite(T) ? __builtin_fabs((double)T) : 0.0;
+    const double Tm = fmax(Tf, (double)__uint_as_float(*tmax));
+    const int64_t hr = pos_hr ? p : r;
+    dltP[p] = delta_x1(Tm, qn, hq[hr], rq[hr], __uint_as_float(cmax[0]),
+                       __uint_as_float(cmh[0]), __uint_as_float(cmh[1]), d, dp, tight);
+}
+
+__global__ __launch_bounds__(256) void k_iota(int *__restrict__ v, int64_t n) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) v[i] = (int)i;
 }
 
 // One wave per query: gather both phases' buffered candidates with key < T
@@ -996,8 +1150,9 @@ __global__ __launch_bounds__(64 * WPB) void k_rerank_x1(
     for (int s = 0; s < S1; ++s)
         gather(buf1 + (q * S1 + s) * (int64_t)cap1, cnt1[q * S1 + s], true);
     for (int j = 0; j < S2; ++j) {
-        const int c = cnt2[q * S2 + j];
-        forced |= c < 0;
+        int c = cnt2[q * S2 + j];
+        forced |= c < 0 || c > cap2;  // -1: overflow; SW_SYM: a count past cap
+        c = min(c, cap2);
         if (c > 0) gather(buf2 + (q * S2 + j) * (int64_t)cap2, c, false);
     }
     if (!forced && M > 64 * NR && big_list) {
@@ -1564,7 +1719,7 @@ static int knn_x1(const float *Q, int64_t nq, const float *C, int64_t nc, int32_
     uint16_t *CR = (uint16_t *)scratch(kSlotX1CR, (size_t)nc * dp * 2 + 64);
     uint16_t *CK = (uint16_t *)scratch(kSlotX1CK, (size_t)pad256(nc) * kbw1 * 2 + 64);
     char *aux = (char *)scratch(kSlotX1Aux, (size_t)nq * 28 + (size_t)nc * 8 + 256);
-    int *flags = (int *)scratch(kSlotFlags, 64);
+    int *flags = (int *)scratch(kSlotFlags, 128);
     int *fb_list = (int *)scratch(kSlotFallback, sizeof(int) * (size_t)nq * 2 + 64);
     int *perm = make_perm(nc, kSlotPerm, 0, s);
     MN_REQUIRE(QR && QK && CR && CK && aux && flags && fb_list && perm, MN_ENOMEM,
@@ -1576,31 +1731,6 @@ static int knn_x1(const float *Q, int64_t nq, const float *C, int64_t nc, int32_
     unsigned *cmax = (unsigned *)flags;  // [0..2]: max |c|^2, |ch|, |rc|
     int *fb_count = flags + 5;  // [3]: non-finite input, [4]: too large for bf16x1
     unsigned long long *ncand = (unsigned long long *)(flags + 8);
-
-    Timer tm;
-    tm.start(opts->timing != 0, s);
-    MN_HIP_TRY(hipMemsetAsync(flags, 0, 64, s));
-    auto prep = [&](const float *X, int64_t n, const int *pm, uint16_t *R, uint16_t *K, float *nv,
-                    float *hcv, float *hv, float *rv, int corpus) {
-        if (n == 0) return;
-        const int64_t blocks = std::min<int64_t>((n + 7) / 8, 16384);
-        if (vec4)
-            hipLaunchKernelGGL(k_prep_x1<true>, dim3((unsigned)blocks), dim3(256), 0, s, X, n, d,
-                               dp, pm, R, K, nv, hcv, hv, rv, cmax, flags + 3, corpus, pst1);
-        else
-            hipLaunchKernelGGL(k_prep_x1<false>, dim3((unsigned)blocks), dim3(256), 0, s, X, n, d,
-                               dp, pm, R, K, nv, hcv, hv, rv, cmax, flags + 3, corpus, pst1);
-    };
-    prep(Q, nq, nullptr, QR, QK, qn, nullptr, qhn, qrn, 0);
-    prep(C, nc, perm, CR, CK, cnv, chc, nullptr, nullptr, 1);
-    MN_KCHECK(s, "k_prep_x1");
-    int hflags[8] = {0};
-    MN_HIP_TRY(hipMemcpyAsync(hflags, flags, 32, hipMemcpyDeviceToHost, s));
-    MN_HIP_TRY(hipStreamSynchronize(s));
-    MN_REQUIRE(hflags[3] == 0, MN_ENONFINITE,
-               "mn_knn: input contains NaN/inf (the reference panics in partial_cmp().unwrap())");
-    if (hflags[4] != 0) return 1;
-    tm.mark();
 
     // phase-1 sample: the first m0 corpus rows, list length L1 (tau0 ~ the
     // (L1 nc / m0)-th best key); small corpora run phase 1 alone (m0 = nc)
@@ -1616,6 +1746,48 @@ static int knn_x1(const float *Q, int64_t nq, const float *C, int64_t nc, int32_
         m0 = nc;
         L1 = std::min(k + margin, kb16::LMAX);
     }
+    // self kNN: the symmetric sweep (gram_sweep2.hpp SW_SYM: each unordered
+    // pair once, rows in ascending-tau0 order; MN_X1_SYM=0 for the
+    // query-major sweep of the rows outside the sample)
+    const char *sye = getenv("MN_X1_SYM");
+    bool sym = same && excl && two && tmaj && sweep_version() == 2 && !(sye && *sye == '0') &&
+               !(getenv("MN_X1_PROBE") && *getenv("MN_X1_PROBE"));
+
+    // flags: [0..2] cmax, [3] non-finite input, [4] too large for bf16x1,
+    // [5] fb_count, [6] big_count, [7] max |tau0|, [8..9] ncand, [10..13]
+    // refill maxima, [14] max |x|, [16..17] fp16 maxima (SW_SYM)
+    Timer tm;
+    tm.start(opts->timing != 0, s);
+    MN_HIP_TRY(hipMemsetAsync(flags, 0, 128, s));
+    auto prep = [&](const float *X, int64_t n, const int *pm, uint16_t *R, uint16_t *K, float *nv,
+                    float *hcv, float *hv, float *rv, int corpus, unsigned *amax = nullptr) {
+        if (n == 0) return;
+        const int64_t blocks = std::min<int64_t>((n + 7) / 8, 16384);
+        if (vec4)
+            hipLaunchKernelGGL(k_prep_x1<true>, dim3((unsigned)blocks), dim3(256), 0, s, X, n, d,
+                               dp, pm, R, K, nv, hcv, hv, rv, cmax, flags + 3, corpus, pst1, amax);
+        else
+            hipLaunchKernelGGL(k_prep_x1<false>, dim3((unsigned)blocks), dim3(256), 0, s, X, n, d,
+                               dp, pm, R, K, nv, hcv, hv, rv, cmax, flags + 3, corpus, pst1, amax);
+    };
+    if (sym) {
+        // phase 1 only: the rows (maxima over them: Q == C) and the sample;
+        // the sweep copy is built in tau0 order below
+        prep(Q, nq, nullptr, QR, nullptr, qn, nullptr, qhn, qrn, 1, (unsigned *)(flags + 14));
+        prep(C, m0, perm, CR, nullptr, cnv, chc, nullptr, nullptr, 0);
+    } else {
+        prep(Q, nq, nullptr, QR, QK, qn, nullptr, qhn, qrn, 0);
+        prep(C, nc, perm, CR, CK, cnv, chc, nullptr, nullptr, 1);
+    }
+    MN_KCHECK(s, "k_prep_x1");
+    int hflags[8] = {0};
+    MN_HIP_TRY(hipMemcpyAsync(hflags, flags, 32, hipMemcpyDeviceToHost, s));
+    MN_HIP_TRY(hipStreamSynchronize(s));
+    MN_REQUIRE(hflags[3] == 0, MN_ENONFINITE,
+               "mn_knn: input contains NaN/inf (the reference panics in partial_cmp().unwrap())");
+    if (hflags[4] != 0) return 1;
+    tm.mark();
+
     t_stats.sample_rows = m0;
     t_stats.list_len = L1;
     const kb16::GramPlan pl = kb16::plan_gram(nq, m0, L1, 1, two ? 1 : 0);
@@ -1634,16 +1806,128 @@ static int knn_x1(const float *Q, int64_t nq, const float *C, int64_t nc, int32_
                            L1, (int)pl.S, pl.chunk, pl.cap, cbuf1, bcnt1, btau1);
         MN_KCHECK(s, "k_gram_bf16<L2H>");
     }
+    unsigned *tmaxb = (unsigned *)(flags + 7);  // max |tau0| (SW_SYM bound)
     hipLaunchKernelGGL(k_tau_x1, dim3((unsigned)((nq + 255) / 256)), dim3(256), 0, s, nq,
-                       (int)pl.S, btau1, qn, qhn, qrn, cmax, d, dp, tq, tau0, dlt);
+                       (int)pl.S, btau1, qn, qhn, qrn, cmax, d, dp, tq, tau0, dlt, tmaxb);
     MN_KCHECK(s, "k_tau_x1");
     tm.mark();
 
     int S2 = 0, cap2 = 0;
     uint2 *cbuf2 = nullptr;
     int *cnt2 = nullptr;
+    // what the re-rank reads: per-query thresholds / bounds, the phase-1
+    // lists (S1 slices), the id map (positions -> rows) and the row map
+    int S1r = (int)pl.S;
+    const float *tau_r = tau0, *dlt_r = dlt;
+    const int *perm_r = perm, *qmap_r = nullptr;
+    const float *chc_r = chc;
     const char *probe = getenv("MN_X1_PROBE");  // noepi: sweep K loop only, no results
-    if (two) {
+    if (sym) {
+        // rows in ascending tau0 (position p holds row pi[p]); rows with a
+        // non-finite threshold at the top end would break the column fold
+        const size_t nn = (size_t)nc;
+        char *so = (char *)scratch(kSlotSymOrd, nn * 4 * 14 + 4096);
+        uint16_t *XK = (uint16_t *)scratch(kSlotX1CK, (size_t)pad256(nc) * kbw1 * 2 + 64);
+        MN_REQUIRE(so && XK, MN_ENOMEM, "mn_knn: symmetric-sweep scratch allocation failed");
+        auto arr = [&](int i) { return so + (size_t)i * (((nn * 4) + 255) & ~(size_t)255); };
+        float *skey = (float *)arr(0);
+        int *pi = (int *)arr(1), *iota = (int *)arr(2);
+        float *tauP = (float *)arr(3), *tqP = (float *)arr(4), *hcP = (float *)arr(5),
+              *aoff = (float *)arr(6), *hoff = (float *)arr(7), *dltP = (float *)arr(8),
+              *nrmP = (float *)arr(9), *hcS = (float *)arr(10), *h16 = (float *)arr(11),
+              *r16 = (float *)arr(12);
+        hipLaunchKernelGGL(k_iota, dim3((unsigned)((nc + 255) / 256)), dim3(256), 0, s, iota, nc);
+        MN_HIP_TRY(sort_f32_pairs(tau0, skey, iota, pi, nc, s));
+        float kmax = 0.f;
+        unsigned amaxb = 0;
+        MN_HIP_TRY(hipMemcpyAsync(&kmax, skey + nc - 1, 4, hipMemcpyDeviceToHost, s));
+        MN_HIP_TRY(hipMemcpyAsync(&amaxb, flags + 14, 4, hipMemcpyDeviceToHost, s));
+        MN_HIP_TRY(hipStreamSynchronize(s));
+        // fp16 operands (MN_SYM_F16=0: bf16): x 2^e with max |x 2^e| < 2^14
+        const char *f16e = getenv("MN_SYM_F16");
+        const bool f16 = !(f16e && *f16e == '0');
+        int e16 = 0;
+        if (f16) {
+            float am;
+            memcpy(&am, &amaxb, 4);
+            int E = 0;
+            if (am > 0.f) frexpf(am, &E);  // am < 2^E
+            e16 = 14 - E;
+        }
+        if (!(kmax < __builtin_inff())) {
+            // fall back to the query-major sweep: its copies were skipped
+            sym = false;
+            prep(Q, nq, nullptr, nullptr, QK, qn, nullptr, qhn, qrn, 0);
+            prep(C, nc, perm, nullptr, CK, cnv, chc, nullptr, nullptr, 1);
+            MN_KCHECK(s, "k_prep_x1");
+        } else {
+            unsigned *cm16 = (unsigned *)(flags + 16);
+            if (f16) {
+                const int64_t blocks = std::min<int64_t>((nc + 7) / 8, 16384);
+                if (vec4)
+                    hipLaunchKernelGGL(k_prep_f16<true>, dim3((unsigned)blocks), dim3(256), 0, s,
+                                       C, nc, d, dp, pi, XK, e16, h16, r16, cm16, pst1);
+                else
+                    hipLaunchKernelGGL(k_prep_f16<false>, dim3((unsigned)blocks), dim3(256), 0, s,
+                                       C, nc, d, dp, pi, XK, e16, h16, r16, cm16, pst1);
+                MN_KCHECK(s, "k_prep_f16");
+            } else {
+                prep(C, nc, pi, nullptr, XK, nrmP, nullptr, nullptr, nullptr, 0);
+            }
+            hipLaunchKernelGGL(k_sym_pos, dim3((unsigned)((nc + 255) / 256)), dim3(256), 0, s,
+                               nc, pi, tau0, qn, f16 ? h16 : qhn, f16 ? r16 : qrn, f16 ? 1 : 0,
+                               cmax, f16 ? cm16 : cmax + 1, tmaxb, d, dp, e16, f16 ? 1 : 0, tauP,
+                               tqP, hcP, hcS, aoff, hoff, dltP);
+            MN_KCHECK(s, "k_sym_pos");
+            // block table: row block I against column tiles [J0, J1), J >= I,
+            // at most TPB tiles per block, the longest first
+            const int nbk = (int)((nc + ksw2::BC - 1) / ksw2::BC);
+            const char *tpe2 = getenv("MN_SYM_TPB");
+            const int TPB = (tpe2 && *tpe2) ? std::max(1, atoi(tpe2)) : 256;
+            std::vector<int4> tab;
+            tab.reserve((size_t)nbk * ((size_t)nbk / TPB + 2) / 2 + 16);
+            for (int I = 0; I < nbk; ++I)
+                for (int J0 = I; J0 < nbk; J0 += TPB)
+                    tab.push_back(make_int4(I, J0, std::min(J0 + TPB, nbk), 0));
+            std::stable_sort(tab.begin(), tab.end(), [](const int4 &a, const int4 &b) {
+                return (a.z - a.y) > (b.z - b.y);
+            });
+            int4 *dtab = (int4 *)scratch(kSlotSymTab, tab.size() * sizeof(int4) + 64);
+            MN_REQUIRE(dtab, MN_ENOMEM, "mn_knn: block table allocation failed");
+            MN_HIP_TRY(hipMemcpyAsync(dtab, tab.data(), tab.size() * sizeof(int4),
+                                      hipMemcpyHostToDevice, s));
+            // per-row buffers: expect ~ L1 nc / m0 candidates a row
+            const double expect = (double)L1 * (double)nc / (double)m0;
+            const char *cpe = getenv("MN_SYM_CAP");
+            cap2 = (cpe && *cpe) ? std::max(64, atoi(cpe))
+                                 : std::max(256, (int)((2.5 * expect + 64.0 + 15.0) / 16.0) * 16);
+            S2 = 1;
+            t_stats.sweep_slices = -1;  // symmetric: one per-row buffer
+            t_stats.sweep_cap = cap2;
+            cbuf2 = (uint2 *)scratch(kSlotX1Buf2, nn * cap2 * sizeof(uint2) + 64);
+            cnt2 = (int *)scratch(kSlotX1Meta2, nn * 4 + 64);
+            MN_REQUIRE(cbuf2 && cnt2, MN_ENOMEM,
+                       "mn_knn: symmetric sweep buffer allocation failed (%zu MB)",
+                       (nn * cap2 * sizeof(uint2)) >> 20);
+            MN_HIP_TRY(hipMemsetAsync(cnt2, 0, nn * 4, s));
+            MN_REQUIRE(tab.size() < INT_MAX && nc * 32 < INT_MAX, MN_ENOTSUP,
+                       "mn_knn: sweep grid too large (split the queries / corpus)");
+            ksw2::SymArgs sa{dtab, aoff, hoff, -2 * e16};
+            auto sk = f16 ? ksw2::k_gram_sweep2<0, ksw2::SW_SYM, true, true>
+                          : ksw2::k_gram_sweep2<0, ksw2::SW_SYM, true, false>;
+            hipLaunchKernelGGL(sk, dim3((unsigned)tab.size()), dim3(ksw2::NT), 0, s, XK, nc, XK,
+                               nc, nkb, (int64_t)0, (int64_t)0, 1, tqP, tauP, hcS, (int64_t)0, 1,
+                               (int64_t)0, cap2, cbuf2, cnt2, pst1, sa);
+            MN_KCHECK(s, "k_gram_sweep2<SYM>");
+            S1r = 0;
+            tau_r = tauP;
+            dlt_r = dltP;
+            perm_r = pi;
+            qmap_r = pi;
+            chc_r = hcP;
+        }
+    }
+    if (two && !sym) {
         const double expect = (double)L1 * (double)(nc - m0) / (double)m0;
         const ksw::SweepPlan p2 = ksw::plan_sweep(nq, nc - m0, expect);
         S2 = (int)p2.S;
@@ -1678,7 +1962,7 @@ static int knn_x1(const float *Q, int64_t nq, const float *C, int64_t nc, int32_
                                                    : ksw2::k_gram_sweep2<1, SW_L2, true>;
             hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(ksw2::NT), 0, s, QK, nq, CK, nc,
                                nkb, q_off, (int64_t)0, 0, tq, tau0, chc, m0, S2, p2.chunk, cap2,
-                               cbuf2, cnt2, pst1);
+                               cbuf2, cnt2, pst1, ksw2::SymArgs{});
         }
         MN_KCHECK(s, "k_gram_sweep");
     }
@@ -1701,9 +1985,9 @@ static int knn_x1(const float *Q, int64_t nq, const float *C, int64_t nc, int32_
     // rows with more): up to 1024, one row per block
 #define MN_RRX(NRV, WPB, V, NB, QL, QN, BC, BL)                                                 \
     hipLaunchKernelGGL((k_rerank_x1<NRV, WPB, V>), dim3((unsigned)(NB)), dim3(64 * WPB), 0, s, \
-                       Q, nq, C, d, c_off, (int)pl.S, pl.cap, cbuf1, bcnt1, tau0, S2, cap2,     \
-                       cbuf2, cnt2, dlt, k, nvalid, QL, QN, BC, BL, perm, q_off, excl,          \
-                       (const int *)nullptr, ubv, out_idx, out_dist, fb_count, fb_list)
+                       Q, nq, C, d, c_off, S1r, pl.cap, cbuf1, bcnt1, tau_r, S2, cap2,          \
+                       cbuf2, cnt2, dlt_r, k, nvalid, QL, QN, BC, BL, perm_r, q_off, excl,      \
+                       qmap_r, ubv, out_idx, out_dist, fb_count, fb_list)
     const int64_t nb1 = (nq + 3) / 4;
     if (vec4) MN_RRX(8, 4, true, nb1, (const int *)nullptr, (const int *)nullptr, big_count, big_list);
     else MN_RRX(8, 4, false, nb1, (const int *)nullptr, (const int *)nullptr, big_count, big_list);
@@ -1721,8 +2005,9 @@ static int knn_x1(const float *Q, int64_t nq, const float *C, int64_t nc, int32_
     // statistics of the buffers now: an escalation below reuses (and may
     // reallocate) the scratch slots that hold them
     if (tm.on) {
-        hipLaunchKernelGGL(k_count_cands, dim3(1024), dim3(256), 0, s, bcnt1, nq * pl.S, pl.cap,
-                           ncand);
+        if (S1r > 0)
+            hipLaunchKernelGGL(k_count_cands, dim3(1024), dim3(256), 0, s, bcnt1, nq * pl.S,
+                               pl.cap, ncand);
         if (two)
             hipLaunchKernelGGL(k_count_cands, dim3(1024), dim3(256), 0, s, cnt2, nq * S2, cap2,
                                ncand);
@@ -1764,7 +2049,7 @@ static int knn_x1(const float *Q, int64_t nq, const float *C, int64_t nc, int32_
                 hipLaunchKernelGGL(k_prep_x3<false>, dim3((unsigned)blocks), dim3(256), 0, s, X, n,
                                    d, dp, src, K, corpus, nv, hv, lv, rv, cmax3, pst3);
         };
-        prep3(C, nc, perm, CK3, 1, nullptr, nullptr, nullptr, nullptr);
+        prep3(C, nc, perm_r, CK3, 1, nullptr, nullptr, nullptr, nullptr);
         prep3(Q, nfb, erows, QK3, 0, qn3, qh3, ql3, q23);
         MN_KCHECK(s, "k_prep_x3");
         hipLaunchKernelGGL(k_tau_x3, dim3((unsigned)((nfb + 255) / 256)), dim3(256), 0, s,
@@ -1784,14 +2069,14 @@ static int knn_x1(const float *Q, int64_t nq, const float *C, int64_t nc, int32_
         if (sweep_version() == 1)
             hipLaunchKernelGGL(ksw::k_gram_sweep<0>, dim3((unsigned)grid3), dim3(ksw::NT), 0, s,
                                QK3, (int64_t)nfb, CK3, nc, nkb3, (int64_t)0, (int64_t)0, 0, tq3,
-                               tau3, chc, (int64_t)0, (int)p3.S, p3.chunk, p3.cap, cbuf3, cnt3);
+                               tau3, chc_r, (int64_t)0, (int)p3.S, p3.chunk, p3.cap, cbuf3, cnt3);
         else
             hipLaunchKernelGGL((tmaj ? ksw2::k_gram_sweep2<0, ksw2::SW_L2, true>
                                    : ksw2::k_gram_sweep2<0, ksw2::SW_L2, false>),
                                dim3((unsigned)grid3), dim3(ksw2::NT), 0, s,
                                QK3, (int64_t)nfb, CK3, nc, nkb3, (int64_t)0, (int64_t)0, 0, tq3,
-                               tau3, chc, (int64_t)0, (int)p3.S, p3.chunk, p3.cap, cbuf3, cnt3,
-                               pst3);
+                               tau3, chc_r, (int64_t)0, (int)p3.S, p3.chunk, p3.cap, cbuf3, cnt3,
+                               pst3, ksw2::SymArgs{});
         MN_KCHECK(s, "k_gram_sweep<x3>");
         int *big_count3 = flags + 6;
         int *big_list3 = fb_list + nq;
@@ -1799,7 +2084,7 @@ static int knn_x1(const float *Q, int64_t nq, const float *C, int64_t nc, int32_
     hipLaunchKernelGGL((k_rerank_x1<NRV, WPB, V>), dim3((unsigned)(NB)), dim3(64 * WPB), 0, s, \
                        Q, (int64_t)nfb, C, d, c_off, 0, 0, (const uint2 *)nullptr,            \
                        (const int *)nullptr, tau3, (int)p3.S, p3.cap, cbuf3, cnt3, dlt3, k,    \
-                       nvalid, QL, QN, BC, BL, perm, q_off, excl, erows, (float *)nullptr,     \
+                       nvalid, QL, QN, BC, BL, perm_r, q_off, excl, erows, (float *)nullptr,     \
                        out_idx, out_dist, fb_count, fb_list)
         const int64_t nb3 = (nfb + 3) / 4;
         if (vec4) MN_RR3(8, 4, true, nb3, (const int *)nullptr, (const int *)nullptr, big_count3, big_list3);
