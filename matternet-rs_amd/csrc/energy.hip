@@ -32,6 +32,7 @@
 #include <algorithm>
 #include <climits>
 #include <cmath>
+#include <cstdlib>
 #include <vector>
 
 #include "common.hpp"
@@ -202,6 +203,101 @@ __device__ uint32_t wave_select(const uint32_t (&keys)[NR], int nr, int rank, in
     return prefix;
 }
 
+// Same result, faster for spread values: one histogram pass over 256 buckets
+// LINEAR IN THE VALUE between the row's min and max (b = floor((v - vmin) *
+// 256 / (vmax - vmin)), monotone under rounding, so buckets before the
+// target's hold only smaller-or-equal values), then the target bucket's
+// members (<= 64) are sorted in one wave.  The radix select's first pass
+// (sign + exponent byte) piles the keys of a row onto a few LDS addresses;
+// these buckets do not.  Falls back to wave_select for a bucket of > 64
+// members or non-finite / degenerate ranges.
+template <int NR>
+__device__ uint32_t wave_select_lin(const uint32_t (&keys)[NR], int f, int rank, int *hist) {
+    const int lane = threadIdx.x & 63;
+    uint32_t kmin = 0xFFFFFFFFu, kmax = 0u;
+#pragma unroll
+    for (int r = 0; r < NR; ++r) {
+        if (lane + 64 * r < f) {
+            kmin = keys[r] < kmin ? keys[r] : kmin;
+            kmax = keys[r] > kmax ? keys[r] : kmax;
+        }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const uint32_t a = __shfl_xor(kmin, o), b = __shfl_xor(kmax, o);
+        kmin = a < kmin ? a : kmin;
+        kmax = b > kmax ? b : kmax;
+    }
+    if (kmin == kmax) return kmin;
+    const float vmin = key2f(kmin), vmax = key2f(kmax);
+    const float scale = 256.0f / (vmax - vmin);
+    if (!__builtin_isfinite(vmin) || !__builtin_isfinite(vmax) || !(scale < 1e30f))
+        return wave_select<NR>(keys, NR, rank, hist);
+    hist[lane * 4 + 0] = 0; hist[lane * 4 + 1] = 0;
+    hist[lane * 4 + 2] = 0; hist[lane * 4 + 3] = 0;
+    __builtin_amdgcn_wave_barrier();
+    int bk[NR];
+#pragma unroll
+    for (int r = 0; r < NR; ++r) {
+        const float v = key2f(keys[r]);
+        int b = (int)((v - vmin) * scale);
+        b = b < 0 ? 0 : (b > 255 ? 255 : b);
+        bk[r] = lane + 64 * r < f ? b : -1;
+        if (bk[r] >= 0) atomicAdd(&hist[b], 1);
+    }
+    __builtin_amdgcn_wave_barrier();
+    const int c0 = hist[lane * 4], c1 = hist[lane * 4 + 1], c2 = hist[lane * 4 + 2],
+              c3 = hist[lane * 4 + 3];
+    const int tot = c0 + c1 + c2 + c3;
+    int incl = tot;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(incl, o);
+        if (lane >= o) incl += y;
+    }
+    const int excl = incl - tot;
+    const bool mine = rank >= excl && rank < incl;
+    int bin = 0, before = excl, cb = c0;
+    if (mine) {
+        if (rank < excl + c0) { bin = 0; cb = c0; }
+        else if (rank < excl + c0 + c1) { bin = 1; before += c0; cb = c1; }
+        else if (rank < excl + c0 + c1 + c2) { bin = 2; before += c0 + c1; cb = c2; }
+        else { bin = 3; before += c0 + c1 + c2; cb = c3; }
+    }
+    const uint64_t who = __ballot(mine);
+    const int src = (int)__builtin_ctzll(who);
+    const int B = __shfl(lane * 4 + bin, src);
+    const int bef = __shfl(before, src);
+    const int cnt = __shfl(cb, src);
+    if (cnt > 64) return wave_select<NR>(keys, NR, rank, hist);
+    __builtin_amdgcn_wave_barrier();  // histogram read before its words are reused
+    uint32_t *cand = (uint32_t *)hist;
+    int base = 0;
+#pragma unroll
+    for (int r = 0; r < NR; ++r) {
+        const bool in = bk[r] == B;
+        const uint64_t m = __ballot(in);
+        if (in) cand[base + (int)__popcll(m & ((1ull << lane) - 1ull))] = keys[r];
+        base += (int)__popcll(m);
+    }
+    __builtin_amdgcn_wave_barrier();
+    // bitonic sort of the bucket's keys (unsigned words, one per lane)
+    uint32_t u = lane < cnt ? cand[lane] : 0xFFFFFFFFu;
+#pragma unroll
+    for (int k2 = 2; k2 <= 64; k2 <<= 1) {
+#pragma unroll
+        for (int j = k2 >> 1; j > 0; j >>= 1) {
+            const uint32_t pu = __shfl_xor(u, j);
+            const bool asc = (lane & k2) == 0, lower = (lane & j) == 0;
+            const bool keep_min = asc == lower;
+            u = keep_min ? (pu < u ? pu : u) : (pu > u ? pu : u);
+        }
+    }
+    const uint32_t res = __shfl(u, rank - bef);
+    __builtin_amdgcn_wave_barrier();
+    return res;
+}
+
 __device__ __forceinline__ double wave_sum(double x) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o);
@@ -217,7 +313,7 @@ __device__ double row_tau(const uint32_t (&keys)[NR], int f, double msum, int ta
     if (tau_mode == MN_TAU_MEAN) return fmax(wave_sum(msum) / (double)f, 1e-10);
     const int lane = threadIdx.x & 63;
     const int rank = (tau_mode == MN_TAU_PERCENTILE) ? pct_rank : ((f % 2 == 1) ? f / 2 : f / 2 - 1);
-    const uint32_t ka = wave_select<NR>(keys, NR, rank, hist);
+    const uint32_t ka = wave_select_lin<NR>(keys, f, rank, hist);
     double med = (double)key2f(ka);
     if (tau_mode == MN_TAU_MEDIAN && f % 2 == 0) {
         // element rank+1: equal to ka if >= rank+2 keys are <= ka, else min{key > ka}
@@ -360,6 +456,139 @@ __global__ __launch_bounds__(NR <= 16 ? 1024 : 256) void k_energy_rows(
                 if (g_mode == MN_G_TAUMODE) {
                     const double tau =
                         row_tau<NR>(keys[t], f, msum[t], tau_mode, tau_param, pct_rank, hist);
+                    const double ebv = e_raw / (e_raw + tau);
+                    lam = tau * ebv + (1.0 - tau) * g_raw;
+                } else {
+                    lam = e_raw;
+                }
+            }
+            if (lane == 0 && r0 + t < n) {
+                if (Eo) Eo[r0 + t] = e_raw;
+                if (Go) Go[r0 + t] = g_raw;
+                if (Lo) Lo[r0 + t] = lam;
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+    }
+}
+
+// ---- register-resident entry lists (the C3 shape: ne <= 64 NE) -------------
+// The entry lists are the same for every row, so each lane keeps its slots
+// p = lane + 64 t in registers for the whole launch (list A padded to whole
+// slots with zero-weight entries, then list B from slot tA on): a pass over
+// two rows then needs only the two 16-B gathers (f64 pair of both rows) per
+// entry, all addresses known up front — no per-entry LDS list reads and no
+// load -> gather dependency, which left the LDS-list kernel latency-bound
+// (SQ wait_any 0.60).  Rows are staged in LDS as f64 pairs (no per-entry
+// conversions).  Same arithmetic as k_energy_rows (f64, the A/B multiplicities
+// applied once per row).
+template <int NR, int NE>
+__global__ __launch_bounds__(NE <= 16 ? 512 : 256) void k_energy_rows_reg(
+    const float *__restrict__ X, int64_t n, int f, int64_t na, int64_t ne,
+    const uint32_t *__restrict__ geij, const double *__restrict__ gev, double mA_num,
+    double mA_g, int g_mode, int tau_mode, double tau_param, int pct_rank,
+    double *__restrict__ Eo, double *__restrict__ Go, double *__restrict__ Lo) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char dsm[];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    double2 *xs = (double2 *)dsm + (size_t)w * f;
+    int *hist = (int *)((double2 *)dsm + (size_t)nw * f) + w * 256;
+    // this lane's slots: A (padded to whole slots) then B
+    const int tA = (int)((na + 63) / 64);
+    const int64_t nb = ne - na;
+    uint32_t eij[NE];
+    double ev[NE];
+#pragma unroll
+    for (int t = 0; t < NE; ++t) {
+        int64_t p;
+        bool ok;
+        if (t < tA) {
+            p = (int64_t)t * 64 + lane;
+            ok = p < na;
+        } else {
+            p = na + (int64_t)(t - tA) * 64 + lane;
+            ok = p < ne && (t - tA) * 64 + lane < nb;
+        }
+        eij[t] = ok ? geij[p] : 0u;
+        ev[t] = ok ? gev[p] : 0.0;
+    }
+    const int64_t npass = (n + 1) / 2;
+    for (int64_t ps = (int64_t)blockIdx.x * nw + w; ps < npass; ps += (int64_t)gridDim.x * nw) {
+        const int64_t r0 = ps * 2;
+        double den[2], msum[2];
+        bool nonzero[2];
+        {
+            const float *x0 = X + r0 * (int64_t)f;
+            const float *x1 = X + min(r0 + 1, n - 1) * (int64_t)f;  // a missing last row repeats
+            double dn0 = 0.0, dn1 = 0.0, ms0 = 0.0, ms1 = 0.0;
+            bool nz0 = false, nz1 = false;
+#pragma unroll
+            for (int r = 0; r < NR; ++r) {
+                const int c = lane + 64 * r;
+                if (c < f) {
+                    const double a = (double)x0[c], b = (double)x1[c];
+                    xs[c] = make_double2(a, b);
+                    dn0 += a * a;
+                    dn1 += b * b;
+                    ms0 += a;
+                    ms1 += b;
+                    nz0 |= !(fabs(a) <= 1e-10);
+                    nz1 |= !(fabs(b) <= 1e-10);
+                }
+            }
+            den[0] = wave_sum(dn0);
+            den[1] = wave_sum(dn1);
+            msum[0] = ms0;
+            msum[1] = ms1;
+            nonzero[0] = __any(nz0) != 0;
+            nonzero[1] = __any(nz1) != 0;
+        }
+        __builtin_amdgcn_wave_barrier();
+        double nA0 = 0.0, nA1 = 0.0, nB0 = 0.0, nB1 = 0.0, S0 = 0.0, S1 = 0.0, Q0 = 0.0, Q1 = 0.0;
+#pragma unroll
+        for (int t = 0; t < NE; ++t) {
+            const int i = (int)(eij[t] & 0xFFFFu), j = (int)(eij[t] >> 16);
+            const double2 gi = xs[i], gj = xs[j];
+            if (t < tA) {  // list A: num -= w x_i x_j, e = w (x_i - x_j)^2
+                nA0 = __builtin_fma(-ev[t], gi.x * gj.x, nA0);
+                nA1 = __builtin_fma(-ev[t], gi.y * gj.y, nA1);
+                const double d0 = gi.x - gj.x, d1 = gi.y - gj.y;
+                const double e0 = (d0 * d0) * ev[t], e1 = (d1 * d1) * ev[t];
+                S0 += e0;
+                S1 += e1;
+                Q0 = __builtin_fma(e0, e0, Q0);
+                Q1 = __builtin_fma(e1, e1, Q1);
+            } else {       // list B: num only
+                nB0 = __builtin_fma(ev[t], gi.x * gj.x, nB0);
+                nB1 = __builtin_fma(ev[t], gi.y * gj.y, nB1);
+            }
+        }
+        const double nAs[2] = {nA0, nA1}, nBs[2] = {nB0, nB1}, Sv[2] = {S0, S1}, Qv[2] = {Q0, Q1};
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+            const double num = wave_sum(mA_num * nAs[t] + nBs[t]);
+            const double Ss = mA_g * wave_sum(Sv[t]);
+            const double Qs = mA_g * wave_sum(Qv[t]);
+            double e_raw = 0.0, g_raw = 0.0, lam = 0.0;
+            if (g_mode == MN_G_SPECTRAL) {
+                const double r = num / (den[t] + 1e-9);
+                e_raw = r < -1e6 ? -1e6 : (r > 1e6 ? 1e6 : r);
+                g_raw = Ss;
+                lam = e_raw;
+            } else if (!(g_mode == MN_G_TAUMODE && !nonzero[t])) {  // zero vector: lambda 0
+                e_raw = den[t] > 1e-12 ? fmax(num / den[t], 0.0) : 0.0;
+                if (Ss > 1e-12) {
+                    const double g = Qs / (Ss * Ss);
+                    g_raw = g < 0.0 ? 0.0 : (g > 1.0 ? 1.0 : g);
+                }
+                if (g_mode == MN_G_TAUMODE) {
+                    uint32_t keys[NR];
+#pragma unroll
+                    for (int r = 0; r < NR; ++r) {
+                        const int c = lane + 64 * r;
+                        keys[r] = c < f ? f2key((float)(t == 0 ? xs[c].x : xs[c].y)) : 0xFFFFFFFFu;
+                    }
+                    const double tau =
+                        row_tau<NR>(keys, f, msum[t], tau_mode, tau_param, pct_rank, hist);
                     const double ebv = e_raw / (e_raw + tau);
                     lam = tau * ebv + (1.0 - tau) * g_raw;
                 } else {
@@ -722,6 +951,34 @@ static int energy_impl(const mn_csr *L, const float *X, int64_t n, int32_t f,
     const size_t shmem = (in_lds ? ebytes : 0) + (size_t)nw * per_wave;
     const int64_t npass = (n + ROWS - 1) / ROWS;
     const int64_t blocks = std::min<int64_t>((npass + nw - 1) / nw, 1024);
+    // register-resident entry lists (k_energy_rows_reg): the lists fit 48
+    // slots a lane (list A padded to whole slots), rows of <= 1024 features
+    const int64_t slots = (na + 63) / 64 + (ne - na + 63) / 64;
+    const char *rge = getenv("MN_ENERGY_REG");  // 0: the LDS-list kernel (A/B)
+    const bool reg = slots <= 48 && nr <= 16 && !(rge && *rge == '0');
+    if (reg) {
+        const int nwr = slots <= 16 ? 8 : 4;  // = launch bounds / 64
+        const size_t shr = (size_t)nwr * f * 16 + (size_t)nwr * 256 * 4;
+        const int64_t blocks_r = std::min<int64_t>((npass + nwr - 1) / nwr, 1024);
+#define MN_ERR(NRV, NEV)                                                                        \
+    do {                                                                                        \
+        MN_HIP_TRY(hipFuncSetAttribute((const void *)k_energy_rows_reg<NRV, NEV>,               \
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)shr));  \
+        hipLaunchKernelGGL((k_energy_rows_reg<NRV, NEV>), dim3((unsigned)blocks_r),             \
+                           dim3(64 * nwr), shr, s, X, n, f, na, ne, eij, ev, mA_num, mA_g,       \
+                           opts->g_mode, opts->tau_mode, opts->tau_param, pct_rank, E, G, lam); \
+    } while (0)
+        if (nr <= 4) {
+            if (slots <= 16) MN_ERR(4, 16); else if (slots <= 32) MN_ERR(4, 32); else MN_ERR(4, 48);
+        } else if (nr <= 8) {
+            if (slots <= 16) MN_ERR(8, 16); else if (slots <= 32) MN_ERR(8, 32); else MN_ERR(8, 48);
+        } else if (nr <= 12) {
+            if (slots <= 16) MN_ERR(12, 16); else if (slots <= 32) MN_ERR(12, 32); else MN_ERR(12, 48);
+        } else {
+            if (slots <= 16) MN_ERR(16, 16); else if (slots <= 32) MN_ERR(16, 32); else MN_ERR(16, 48);
+        }
+#undef MN_ERR
+    }
 #define MN_ER(NRV)                                                                              \
     do {                                                                                        \
         MN_HIP_TRY(hipFuncSetAttribute((const void *)k_energy_rows<NRV>,                        \
@@ -730,7 +987,8 @@ static int energy_impl(const mn_csr *L, const float *X, int64_t n, int32_t f,
                            X, n, f, na, ne, in_lds, eij, ev, mA_num, mA_g, opts->g_mode,        \
                            opts->tau_mode, opts->tau_param, pct_rank, E, G, lam);               \
     } while (0)
-    if (nr <= 4) MN_ER(4);
+    if (reg) {
+    } else if (nr <= 4) MN_ER(4);
     else if (nr <= 8) MN_ER(8);
     else if (nr <= 12) MN_ER(12);
     else if (nr <= 16) MN_ER(16);

@@ -18,14 +18,22 @@ _lib.check(_lib.lib().mn_fill_uniform_f32(X.data_ptr(), n, d, 42, 0, None))
 fi, fd, fw, _ = S.knn_cos_columns(X, 4, eps=1.0, sigma=1.0, p=2.0)
 L, _ = S.build_laplacian_from_knn(fi, fw, weight_kernel="given", symmetrise="union")
 modes = {"median": S.TauMode.Median, "mean": S.TauMode.Mean, "fixed": S.TauMode.Fixed(0.5)}
-ref = None
+ref = {}
 for rep in range(3):
-    for name, tm in modes.items():
-        torch.cuda.synchronize()
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-        E, G, lam = S.energy_rows(X, L, _lib.MN_G_TAUMODE, tm)
-        e1.record()
-        torch.cuda.synchronize()
-        print(json.dumps({"rep": rep, "mode": name, "ms": round(e0.elapsed_time(e1), 3),
-                          "nnz": L.nnz}), flush=True)
+    for kern in ("reg", "lds"):  # MN_ENERGY_REG A/B: register-resident lists vs LDS lists
+        os.environ["MN_ENERGY_REG"] = "1" if kern == "reg" else "0"
+        for name, tm in modes.items():
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            E, G, lam = S.energy_rows(X, L, _lib.MN_G_TAUMODE, tm)
+            e1.record()
+            torch.cuda.synchronize()
+            same = None
+            if name in ref:
+                same = bool(torch.allclose(lam, ref[name], rtol=1e-12, atol=1e-15))
+            else:
+                ref[name] = lam.clone()
+            print(json.dumps({"rep": rep, "kernel": kern, "mode": name,
+                              "ms": round(e0.elapsed_time(e1), 3), "nnz": L.nnz,
+                              "same_as_first": same}), flush=True)

@@ -232,3 +232,35 @@ def test_item_graph_signal_orientation(gm):
     rE2, rG2, _ = O.energy_rows(np.ascontiguousarray(X.T), ip, ix, iv2, og, O.TAU_MEDIAN)
     np.testing.assert_allclose(E2.cpu().numpy(), rE2, rtol=RTOL, atol=ATOL)
     np.testing.assert_allclose(G2.cpu().numpy(), rG2, rtol=RTOL, atol=ATOL)
+
+
+@pytest.mark.parametrize("tau", ["median", "pct"])
+def test_tau_order_statistic_adversarial_rows(tau):
+    """tau = the row's median / percentile (taumode.rs:29-70) through the
+    value-linear bucket select (energy.hip wave_select_lin) and its radix
+    fallback: rows whose values pile into one bucket (> 64 members: exponential
+    tails, a 1e30 outlier), half-tied rows, two-valued rows, negative rows,
+    huge / tiny ranges, subnormals — lambdas within the K3 tolerance."""
+    import surfface_hip as S
+    ip, ix, iv = feature_laplacian()
+    rng = np.random.default_rng(5)
+    n, f = 4096, 768
+    X = datagen.uniform(n, f, seed=33)
+    X[0] = rng.exponential(size=f).astype(np.float32) ** 6       # heavy tail
+    X[1] = np.float32(0.5)
+    X[1, ::3] = rng.random(len(range(0, f, 3))).astype(np.float32)
+    X[2] = np.where(rng.random(f) < 0.5, 1.0, 2.0).astype(np.float32)
+    X[3] = -np.abs(X[3])
+    X[4] = datagen.uniform(1, f, seed=4)[0] * np.float32(1e-30)
+    X[5, 7] = np.float32(1e30)                                   # one outlier: all else in bucket 0
+    X[6] = (rng.random(f) * 1e-40).astype(np.float32)             # subnormals
+    X[7] = np.float32(3.0)
+    X[7, 100] = np.float32(3.0000002)
+    X[8:64] = (rng.standard_normal((56, f)) ** 3).astype(np.float32)
+    tm = {"median": (S.TauMode.Median, O.TAU_MEDIAN, 0.0),
+          "pct": (S.TauMode.Percentile(0.77), O.TAU_PERCENTILE, 0.77)}[tau]
+    E, G, lam = run(X, ip, ix, iv, 0, tm[0])
+    rE, rG, rl = O.energy_rows(X, ip, ix, iv, O.G_TAUMODE, tm[1], tm[2])
+    np.testing.assert_allclose(E, rE, rtol=RTOL, atol=ATOL)
+    np.testing.assert_allclose(G, rG, rtol=RTOL, atol=ATOL)
+    np.testing.assert_allclose(lam, rl, rtol=RTOL, atol=ATOL)
