@@ -193,29 +193,12 @@ int mn_knn_last_stats(mn_knn_stats *out);
  * sort_unstable leaves ties unspecified): out_idx [f][k] (int32, -1 pad),
  * out_w [f][k] (f32, 0 pad) — the directed edges the Stage C Laplacian
  * (mn_laplacian_from_knn, MN_SYM_MAX) symmetrises.  f32 arithmetic and fold
- * order as the reference; ln / exp are the device's (<= 2 ulp): weights within
- * 1e-5 relative, neighbour sets equal up to near-ties.  2 <= f <= 4096,
- * k >= 1.  MN_ENONFINITE on NaN coefficients (the reference panics). */
+ * order as the reference; ln / exp are glibc's logf / expf restated
+ * (mn_libm_f32): bit-exact.  2 <= f <= 4096, k >= 1.  MN_ENONFINITE on NaN
+ * coefficients (the reference panics). */
 int mn_bc_knn_f32(const float *means, const float *vars, int64_t c, int32_t f, int32_t k,
                   float var_reg, float weight_thr, int32_t *out_idx, float *out_w, void *stream);
 
-/* MST stage candidate graph (surfface-core/src/mst.rs:312-363
- * MSTStage::build_candidate_graph + compute_distance :366-397 +
- * compute_edge_cost :400-412).  Nodes are the C centroid ROWS of means /
- * vars [C][F] (device, f32).  Per node i, the k = min(k_neighbors, C-1)
- * nearest j != i by (distance asc, j asc) — the reference's stable sort —
- * as edges out_v / out_dist / out_cost [C][k] (u = i implicit), cost =
- * distance * phi(t_i, t_j) (MN_TW_NONE: cost = distance).  thickness [C]
- * (device) or NULL = the mean variance per row (centroid.rs:107-109;
- * sequential f32 sum / F — Burn's summation order is backend-defined, so
- * that default is parity-unpinned); out_thickness [C] optional.
- * MN_MST_BHATTACHARYYA (the default metric, mst.rs:77-84) folds
- * bhattacharyya_distance_diagonal (distance.rs:78-108) in feature order with
- * the reference's f32 operations (sqrt correctly rounded; ln = f64 log
- * rounded to f32 where the reference calls libm logf: bit-exact but for rare
- * ulp-level terms); C <= 65536, k <= 512.  MN_MST_EUCLIDEAN /
- * MN_MST_SQEUCLIDEAN run mn_knn_f32 (bit-exact).  MN_ENONFINITE on a NaN
- * distance (the reference's partial_cmp().unwrap()). */
 /* Clustering stage, batch nearest centroid (surfface-pipeline/src/stages/
  * clustering.rs:42-63): per item of batch [b][f] the nearest of the c
  * centroids [c][f] (device, f32) by sqrt((|x|^2 + |c|^2) - 2 x.c), out_idx /
@@ -239,6 +222,22 @@ enum mn_thickness_weight { /* mst.rs:58-74 ThicknessWeight */
     MN_TW_GEOMEAN = 3, /* sqrt(t_i * t_j) */
     MN_TW_NONE = 4
 };
+/* MST stage candidate graph (surfface-core/src/mst.rs:312-363
+ * MSTStage::build_candidate_graph + compute_distance :366-397 +
+ * compute_edge_cost :400-412).  Nodes are the C centroid ROWS of means /
+ * vars [C][F] (device, f32).  Per node i, the k = min(k_neighbors, C-1)
+ * nearest j != i by (distance asc, j asc) — the reference's stable sort —
+ * as edges out_v / out_dist / out_cost [C][k] (u = i implicit), cost =
+ * distance * phi(t_i, t_j) (MN_TW_NONE: cost = distance).  thickness [C]
+ * (device) or NULL = the mean variance per row (centroid.rs:107-109;
+ * sequential f32 sum / F — Burn's summation order is backend-defined, so
+ * that default is parity-unpinned); out_thickness [C] optional.
+ * MN_MST_BHATTACHARYYA (the default metric, mst.rs:77-84) folds
+ * bhattacharyya_distance_diagonal (distance.rs:78-108) in feature order with
+ * the reference's f32 operations (sqrt correctly rounded; ln = glibc's logf
+ * restated, mn_libm_f32): bit-exact; C <= 65536, k <= 512.  MN_MST_EUCLIDEAN /
+ * MN_MST_SQEUCLIDEAN run mn_knn_f32 (bit-exact).  MN_ENONFINITE on a NaN
+ * distance (the reference's partial_cmp().unwrap()). */
 int mn_mst_candidate_graph_f32(const float *means, const float *vars, int64_t c, int32_t f,
                                int32_t k_neighbors, int32_t metric, int32_t thickness_weight,
                                const float *thickness, float *out_thickness, int32_t *out_v,

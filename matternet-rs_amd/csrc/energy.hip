@@ -33,6 +33,7 @@
 #include <climits>
 #include <cmath>
 #include <cstdlib>
+#include <type_traits>
 #include <vector>
 
 #include "common.hpp"
@@ -307,13 +308,15 @@ __device__ __forceinline__ double wave_sum(double x) {
 // tau of one row (taumode.rs:29-70) from its keys
 template <int NR>
 __device__ double row_tau(const uint32_t (&keys)[NR], int f, double msum, int tau_mode,
-                          double tau_param, int pct_rank, int *hist) {
+                          double tau_param, int pct_rank, int *hist, int sel = 0) {
     if (tau_mode == MN_TAU_FIXED)
         return (isfinite(tau_param) && tau_param > 0.0) ? tau_param : 1e-10;
     if (tau_mode == MN_TAU_MEAN) return fmax(wave_sum(msum) / (double)f, 1e-10);
     const int lane = threadIdx.x & 63;
     const int rank = (tau_mode == MN_TAU_PERCENTILE) ? pct_rank : ((f % 2 == 1) ? f / 2 : f / 2 - 1);
-    const uint32_t ka = wave_select_lin<NR>(keys, f, rank, hist);
+    // sel 1: value-linear buckets (wave_select_lin), else the radix select
+    const uint32_t ka = sel == 1 ? wave_select_lin<NR>(keys, f, rank, hist)
+                                 : wave_select<NR>(keys, NR, rank, hist);
     double med = (double)key2f(ka);
     if (tau_mode == MN_TAU_MEDIAN && f % 2 == 0) {
         // element rank+1: equal to ka if >= rank+2 keys are <= ka, else min{key > ka}
@@ -341,12 +344,13 @@ __device__ double row_tau(const uint32_t (&keys)[NR], int f, double msum, int ta
 
 // LDS: [ev f64 x ne | eij u32 x ne] (when in_lds) | xs f32 [waves][ROWS][fpad]
 //      | hist int [waves][256]
-template <int NR>
+template <int NR, int ROWS = 2>
 __global__ __launch_bounds__(NR <= 16 ? 1024 : 256) void k_energy_rows(
     const float *__restrict__ X, int64_t n, int f, int64_t na, int64_t ne, int in_lds,
     const uint32_t *__restrict__ geij, const double *__restrict__ gev, double mA_num,
     double mA_g, int g_mode, int tau_mode, double tau_param, int pct_rank,
-    double *__restrict__ Eo, double *__restrict__ Go, double *__restrict__ Lo) {
+    double *__restrict__ Eo, double *__restrict__ Go, double *__restrict__ Lo, int sel) {
+    typedef typename std::conditional<ROWS == 4, float4, float2>::type gat_t;
     extern __shared__ __attribute__((aligned(16))) unsigned char dsm[];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
     const int fpad = (f + 3) & ~3;
@@ -398,17 +402,24 @@ __global__ __launch_bounds__(NR <= 16 ? 1024 : 256) void k_energy_rows(
 #pragma unroll
         for (int t = 0; t < ROWS; ++t) nA[t] = nB[t] = S[t] = Q[t] = 0.0;
         // list A: num += v x_i x_j (v = -w), S += e, Q += e^2, e = w (x_i - x_j)^2
-        // the ROWS values of one feature are adjacent: one 8-B gather per
-        // endpoint serves both rows of the pass
-        static_assert(ROWS == 2, "gathers are float2");
+        // the ROWS values of one feature are adjacent: one 8-B (16-B) gather
+        // per endpoint serves the 2 (4) rows of the pass
+        static_assert(ROWS == 2 || ROWS == 4, "gathers are float2 / float4");
+        auto unpack = [](const gat_t &g, float (&a)[ROWS]) {
+            const float *q = reinterpret_cast<const float *>(&g);
+#pragma unroll
+            for (int t = 0; t < ROWS; ++t) a[t] = q[t];
+        };
 #pragma unroll 2
         for (int64_t p = lane; p < na; p += 64) {
             const uint32_t ij = EIJ[p];
             const double wv = EV[p];
             const int i = (int)(ij & 0xFFFFu), j = (int)(ij >> 16);
-            const float2 gi = *reinterpret_cast<const float2 *>(&xs[i * ROWS]);
-            const float2 gj = *reinterpret_cast<const float2 *>(&xs[j * ROWS]);
-            const float ai[2] = {gi.x, gi.y}, aj[2] = {gj.x, gj.y};
+            const gat_t gi = *reinterpret_cast<const gat_t *>(&xs[i * ROWS]);
+            const gat_t gj = *reinterpret_cast<const gat_t *>(&xs[j * ROWS]);
+            float ai[ROWS], aj[ROWS];
+            unpack(gi, ai);
+            unpack(gj, aj);
 #pragma unroll
             for (int t = 0; t < ROWS; ++t) {
                 const double xi = (double)ai[t], xj = (double)aj[t];
@@ -425,9 +436,11 @@ __global__ __launch_bounds__(NR <= 16 ? 1024 : 256) void k_energy_rows(
             const uint32_t ij = EIJ[p];
             const double v = EV[p];
             const int i = (int)(ij & 0xFFFFu), j = (int)(ij >> 16);
-            const float2 gi = *reinterpret_cast<const float2 *>(&xs[i * ROWS]);
-            const float2 gj = *reinterpret_cast<const float2 *>(&xs[j * ROWS]);
-            const float ai[2] = {gi.x, gi.y}, aj[2] = {gj.x, gj.y};
+            const gat_t gi = *reinterpret_cast<const gat_t *>(&xs[i * ROWS]);
+            const gat_t gj = *reinterpret_cast<const gat_t *>(&xs[j * ROWS]);
+            float ai[ROWS], aj[ROWS];
+            unpack(gi, ai);
+            unpack(gj, aj);
 #pragma unroll
             for (int t = 0; t < ROWS; ++t) {
                 const double xi = (double)ai[t], xj = (double)aj[t];
@@ -454,8 +467,8 @@ __global__ __launch_bounds__(NR <= 16 ? 1024 : 256) void k_energy_rows(
                     g_raw = g < 0.0 ? 0.0 : (g > 1.0 ? 1.0 : g);
                 }
                 if (g_mode == MN_G_TAUMODE) {
-                    const double tau =
-                        row_tau<NR>(keys[t], f, msum[t], tau_mode, tau_param, pct_rank, hist);
+                    const double tau = row_tau<NR>(keys[t], f, msum[t], tau_mode, tau_param,
+                                                   pct_rank, hist, sel);
                     const double ebv = e_raw / (e_raw + tau);
                     lam = tau * ebv + (1.0 - tau) * g_raw;
                 } else {
@@ -943,19 +956,25 @@ static int energy_impl(const mn_csr *L, const float *X, int64_t n, int32_t f,
     const int fpad = (f + 3) & ~3;
     const size_t ebytes = (((size_t)ne * 12) + 15) & ~(size_t)15;
     const int in_lds = ebytes <= EDGE_LDS_MAX ? 1 : 0;
-    const size_t per_wave = (size_t)ROWS * fpad * 4 + 256 * 4;
+    // rows per wave pass: MN_ENERGY_ROWS (2 or 4; 4 halves the entry-list
+    // reads per row, 16-B gathers, half the waves); tau select MN_TAU_SEL
+    const char *rwe = getenv("MN_ENERGY_ROWS");
+    const int rows = (rwe && *rwe == '4' && nr <= 16) ? 4 : 2;
+    const char *sle = getenv("MN_TAU_SEL");
+    const int sel = (sle && *sle == '1') ? 1 : 0;
+    const size_t per_wave = (size_t)rows * fpad * 4 + 256 * 4;
     const size_t avail = LDS_BUDGET - (in_lds ? ebytes : 0);
     const int wmax = nr <= 16 ? 16 : 4;  // = launch bounds / 64
     const int nw = (int)std::min<size_t>((size_t)wmax, avail / per_wave);
     MN_REQUIRE(nw >= 1, MN_ENOTSUP, "mn_energy_rows: f=%d does not fit the LDS plan", f);
     const size_t shmem = (in_lds ? ebytes : 0) + (size_t)nw * per_wave;
-    const int64_t npass = (n + ROWS - 1) / ROWS;
+    const int64_t npass = (n + rows - 1) / rows;
     const int64_t blocks = std::min<int64_t>((npass + nw - 1) / nw, 1024);
     // register-resident entry lists (k_energy_rows_reg): the lists fit 48
     // slots a lane (list A padded to whole slots), rows of <= 1024 features
     const int64_t slots = (na + 63) / 64 + (ne - na + 63) / 64;
-    const char *rge = getenv("MN_ENERGY_REG");  // 0: the LDS-list kernel (A/B)
-    const bool reg = slots <= 48 && nr <= 16 && !(rge && *rge == '0');
+    const char *rge = getenv("MN_ENERGY_REG");  // 1: register lists (A/B; slower so far)
+    const bool reg = slots <= 48 && nr <= 16 && (rge && *rge == '1');
     if (reg) {
         const int nwr = slots <= 16 ? 8 : 4;  // = launch bounds / 64
         const size_t shr = (size_t)nwr * f * 16 + (size_t)nwr * 256 * 4;
@@ -979,13 +998,19 @@ static int energy_impl(const mn_csr *L, const float *X, int64_t n, int32_t f,
         }
 #undef MN_ERR
     }
+#define MN_ER2(NRV, RW)                                                                         \
+    do {                                                                                        \
+        MN_HIP_TRY(hipFuncSetAttribute((const void *)k_energy_rows<NRV, RW>,                    \
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)shmem)); \
+        hipLaunchKernelGGL((k_energy_rows<NRV, RW>), dim3((unsigned)blocks), dim3(64 * nw),     \
+                           shmem, s, X, n, f, na, ne, in_lds, eij, ev, mA_num, mA_g,             \
+                           opts->g_mode, opts->tau_mode, opts->tau_param, pct_rank, E, G, lam,  \
+                           sel);                                                                \
+    } while (0)
 #define MN_ER(NRV)                                                                              \
     do {                                                                                        \
-        MN_HIP_TRY(hipFuncSetAttribute((const void *)k_energy_rows<NRV>,                        \
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)shmem)); \
-        hipLaunchKernelGGL(k_energy_rows<NRV>, dim3((unsigned)blocks), dim3(64 * nw), shmem, s, \
-                           X, n, f, na, ne, in_lds, eij, ev, mA_num, mA_g, opts->g_mode,        \
-                           opts->tau_mode, opts->tau_param, pct_rank, E, G, lam);               \
+        if (rows == 4 && NRV <= 16) MN_ER2(NRV, 4);                                             \
+        else MN_ER2(NRV, 2);                                                                    \
     } while (0)
     if (reg) {
     } else if (nr <= 4) MN_ER(4);
@@ -995,6 +1020,7 @@ static int energy_impl(const mn_csr *L, const float *X, int64_t n, int32_t f,
     else if (nr <= 32) MN_ER(32);
     else MN_ER(64);  // f <= 4096
 #undef MN_ER
+#undef MN_ER2
     MN_KCHECK(s, "k_energy_rows");
     if (spec) {
         double *part = (double *)scratch(kSlotNorms2, (size_t)n * 16 + 8 * SUM_BLOCKS + 64) + 2 * n;

@@ -1750,8 +1750,7 @@ static int knn_x1(const float *Q, int64_t nq, const float *C, int64_t nc, int32_
     // pair once, rows in ascending-tau0 order; MN_X1_SYM=0 for the
     // query-major sweep of the rows outside the sample)
     const char *sye = getenv("MN_X1_SYM");
-    bool sym = same && excl && two && tmaj && sweep_version() == 2 && !(sye && *sye == '0') &&
-               !(getenv("MN_X1_PROBE") && *getenv("MN_X1_PROBE"));
+    bool sym = same && excl && two && tmaj && sweep_version() == 2 && !(sye && *sye == '0');
 
     // flags: [0..2] cmax, [3] non-finite input, [4] too large for bf16x1,
     // [5] fb_count, [6] big_count, [7] max |tau0|, [8..9] ncand, [10..13]
@@ -1818,6 +1817,7 @@ static int knn_x1(const float *Q, int64_t nq, const float *C, int64_t nc, int32_
     // what the re-rank reads: per-query thresholds / bounds, the phase-1
     // lists (S1 slices), the id map (positions -> rows) and the row map
     int S1r = (int)pl.S;
+    int sym_mark = 0;  // 1: an extra timer mark before the SW_SYM sweep
     const float *tau_r = tau0, *dlt_r = dlt;
     const int *perm_r = perm, *qmap_r = nullptr;
     const float *chc_r = chc;
@@ -1880,18 +1880,35 @@ static int knn_x1(const float *Q, int64_t nq, const float *C, int64_t nc, int32_
                                tqP, hcP, hcS, aoff, hoff, dltP);
             MN_KCHECK(s, "k_sym_pos");
             // block table: row block I against column tiles [J0, J1), J >= I,
-            // at most TPB tiles per block, the longest first
+            // at most TPB tiles per block.  MN_SYM_ORDER 0: ranges from the
+            // diagonal, the longest first (co-resident blocks of an XCD share
+            // a row panel); 1: column ranges aligned to a TPB grid, ordered by
+            // range then row (co-resident blocks share the column stream)
             const int nbk = (int)((nc + ksw2::BC - 1) / ksw2::BC);
             const char *tpe2 = getenv("MN_SYM_TPB");
             const int TPB = (tpe2 && *tpe2) ? std::max(1, atoi(tpe2)) : 256;
+            const char *ore = getenv("MN_SYM_ORDER");
+            const int order = (ore && *ore) ? atoi(ore) : 0;
             std::vector<int4> tab;
             tab.reserve((size_t)nbk * ((size_t)nbk / TPB + 2) / 2 + 16);
-            for (int I = 0; I < nbk; ++I)
-                for (int J0 = I; J0 < nbk; J0 += TPB)
-                    tab.push_back(make_int4(I, J0, std::min(J0 + TPB, nbk), 0));
-            std::stable_sort(tab.begin(), tab.end(), [](const int4 &a, const int4 &b) {
-                return (a.z - a.y) > (b.z - b.y);
-            });
+            if (order == 1) {
+                for (int I = 0; I < nbk; ++I)
+                    for (int J0 = I; J0 < nbk;) {
+                        const int J1 = std::min((J0 / TPB + 1) * TPB, nbk);
+                        tab.push_back(make_int4(I, J0, J1, J0 / TPB));
+                        J0 = J1;
+                    }
+                std::stable_sort(tab.begin(), tab.end(), [](const int4 &a, const int4 &b) {
+                    return a.w != b.w ? a.w < b.w : a.x < b.x;
+                });
+            } else {
+                for (int I = 0; I < nbk; ++I)
+                    for (int J0 = I; J0 < nbk; J0 += TPB)
+                        tab.push_back(make_int4(I, J0, std::min(J0 + TPB, nbk), 0));
+                std::stable_sort(tab.begin(), tab.end(), [](const int4 &a, const int4 &b) {
+                    return (a.z - a.y) > (b.z - b.y);
+                });
+            }
             int4 *dtab = (int4 *)scratch(kSlotSymTab, tab.size() * sizeof(int4) + 64);
             MN_REQUIRE(dtab, MN_ENOMEM, "mn_knn: block table allocation failed");
             MN_HIP_TRY(hipMemcpyAsync(dtab, tab.data(), tab.size() * sizeof(int4),
@@ -1912,8 +1929,17 @@ static int knn_x1(const float *Q, int64_t nq, const float *C, int64_t nc, int32_
             MN_HIP_TRY(hipMemsetAsync(cnt2, 0, nn * 4, s));
             MN_REQUIRE(tab.size() < INT_MAX && nc * 32 < INT_MAX, MN_ENOTSUP,
                        "mn_knn: sweep grid too large (split the queries / corpus)");
+            tm.mark();  // SW_SYM: sort / fp16 copy / table -> ms_norms
+            sym_mark = 1;
             ksw2::SymArgs sa{dtab, aoff, hoff, -2 * e16};
-            auto sk = f16 ? ksw2::k_gram_sweep2<0, ksw2::SW_SYM, true, true>
+            // timing probes (results invalid): noepi = K loop only, nodma /
+            // noread = also without the DMA issue / fragment reads
+            const int pk = !probe || !*probe ? 0 : !strcmp(probe, "nodma") ? 2
+                           : !strcmp(probe, "noread") ? 3 : 1;
+            auto sk = f16 ? (pk == 0 ? ksw2::k_gram_sweep2<0, ksw2::SW_SYM, true, true>
+                             : pk == 1 ? ksw2::k_gram_sweep2<1, ksw2::SW_SYM, true, true>
+                             : pk == 2 ? ksw2::k_gram_sweep2<2, ksw2::SW_SYM, true, true>
+                                       : ksw2::k_gram_sweep2<3, ksw2::SW_SYM, true, true>)
                           : ksw2::k_gram_sweep2<0, ksw2::SW_SYM, true, false>;
             hipLaunchKernelGGL(sk, dim3((unsigned)tab.size()), dim3(ksw2::NT), 0, s, XK, nc, XK,
                                nc, nkb, (int64_t)0, (int64_t)0, 1, tqP, tauP, hcS, (int64_t)0, 1,
@@ -1970,10 +1996,11 @@ static int knn_x1(const float *Q, int64_t nq, const float *C, int64_t nc, int32_
     if (probe && *probe) {  // timing probe: outputs are not produced
         MN_HIP_TRY(hipStreamSynchronize(s));
         if (tm.on) {
-            t_stats.ms_norms = tm.ms(0, 1);
+            const int o = sym_mark;
+            t_stats.ms_norms = tm.ms(0, 1) + (o ? tm.ms(2, 3) : 0.f);
             t_stats.ms_sample = tm.ms(1, 2);
-            t_stats.ms_sweep = tm.ms(2, 3);
-            t_stats.ms_gram = tm.ms(1, 3);
+            t_stats.ms_sweep = tm.ms(2 + o, 3 + o);
+            t_stats.ms_gram = t_stats.ms_sample + t_stats.ms_sweep;
         }
         return MN_OK;
     }
@@ -2160,13 +2187,14 @@ static int knn_x1(const float *Q, int64_t nq, const float *C, int64_t nc, int32_
     t_stats.n_uncertified = nfb2;
     if (tm.on) {
         t_stats.n_candidates = n_cand;
-        t_stats.ms_norms = tm.ms(0, 1);
+        const int o = sym_mark;
+        t_stats.ms_norms = tm.ms(0, 1) + (o ? tm.ms(2, 3) : 0.f);
         t_stats.ms_sample = tm.ms(1, 2);
-        t_stats.ms_sweep = tm.ms(2, 3);
-        t_stats.ms_gram = tm.ms(1, 3);
-        t_stats.ms_rerank = tm.ms(3, 4);
-        t_stats.ms_fallback = tm.ms(4, 5);
-        t_stats.ms_total = tm.ms(0, 5);
+        t_stats.ms_sweep = tm.ms(2 + o, 3 + o);
+        t_stats.ms_gram = t_stats.ms_sample + t_stats.ms_sweep;
+        t_stats.ms_rerank = tm.ms(3 + o, 4 + o);
+        t_stats.ms_fallback = tm.ms(4 + o, 5 + o);
+        t_stats.ms_total = tm.ms(0, 5 + o);
     }
     return MN_OK;
 }

@@ -51,6 +51,8 @@ for r in range(rounds):
         del out
         pm = {}
         for pk in os.environ.get("AB_PROBES", "noepi").split(","):
+            if not pk:
+                continue
             os.environ["MN_X1_PROBE"] = pk
             S.knn_l2sq(X, 32, timing=True, algo="bf16x1")
             pm[pk] = round(S.knn.last_stats()["ms_sweep"], 2)

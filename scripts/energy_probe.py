@@ -20,8 +20,13 @@ L, _ = S.build_laplacian_from_knn(fi, fw, weight_kernel="given", symmetrise="uni
 modes = {"median": S.TauMode.Median, "mean": S.TauMode.Mean, "fixed": S.TauMode.Fixed(0.5)}
 ref = {}
 for rep in range(3):
-    for kern in ("reg", "lds"):  # MN_ENERGY_REG A/B: register-resident lists vs LDS lists
-        os.environ["MN_ENERGY_REG"] = "1" if kern == "reg" else "0"
+    # A/B in one process: LDS entry lists x 2 rows (default) / x 4 rows, the
+    # value-linear tau select, the register-resident lists
+    for kern, env in (("lds2", {}), ("lds4", {"MN_ENERGY_ROWS": "4"}),
+                      ("lds2_lin", {"MN_TAU_SEL": "1"}), ("reg", {"MN_ENERGY_REG": "1"})):
+        for kk in ("MN_ENERGY_ROWS", "MN_TAU_SEL", "MN_ENERGY_REG"):
+            os.environ.pop(kk, None)
+        os.environ.update(env)
         for name, tm in modes.items():
             torch.cuda.synchronize()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

@@ -1,0 +1,36 @@
+"""K2 item-Laplacian timing (C3 shape): wall time per call vs the library's
+HIP-event span (mn_lap_last_stats.ms_total) for caller-owned (the Python
+wrapper) output, to separate kernel time from call overhead.  Run under
+rocprofv3 --kernel-trace for the per-kernel timeline.
+    python scripts/lap_probe.py [n]"""
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "matternet-rs_amd")]
+import torch  # noqa: E402
+
+import surfface_hip as S  # noqa: E402
+from surfface_hip import _lib  # noqa: E402
+
+n = int(sys.argv[1]) if len(sys.argv) > 1 else 1_000_000
+d, k = 768, 32
+X = torch.empty((n, d), dtype=torch.float32, device="cuda")
+_lib.check(_lib.lib().mn_fill_uniform_f32(X.data_ptr(), n, d, 42, 0, None))
+r = S.knn_l2sq(X, k)
+del X
+torch.cuda.synchronize()
+for rep in range(6):
+    t0 = time.perf_counter()
+    L, _ = S.build_laplacian_from_knn(r.idx, r.dist, weight_kernel="rational", symmetrise="union",
+                                      eps=float("inf"), sigma=1.0, p=2.0)
+    torch.cuda.synchronize()
+    wall = (time.perf_counter() - t0) * 1e3
+    st = S.laplacian.last_stats()
+    byt = n * k * 8 + L.nnz * 12 + (n + 1) * 8
+    print(json.dumps({"rep": rep, "wall_ms": round(wall, 3), "lib_ms": round(st["ms_total"], 3),
+                      "nnz": L.nnz, "GB_per_s_wall": round(byt / wall / 1e6, 1),
+                      "GB_per_s_lib": round(byt / st["ms_total"] / 1e6, 1)}), flush=True)
+    del L

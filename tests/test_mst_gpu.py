@@ -95,7 +95,7 @@ def test_reference_thickness_case():
     means = np.ones((4, 3), np.float32)
     var = np.repeat(np.array([[0.5], [1.0], [0.2], [0.8]], np.float32), 3, axis=1)
     for tw in range(5):
-        e = _check(means, var, 3, tw=tw, exact_frac=1.0)
+        e = _check(means, var, 3, tw=tw)
         th = e.thickness.cpu().numpy()
         np.testing.assert_array_equal(th, np.array([0.5, 1.0, 0.2, 0.8], np.float32))
         assert (e.cost.cpu().numpy() > 0).all()
