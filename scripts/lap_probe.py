@@ -22,6 +22,15 @@ _lib.check(_lib.lib().mn_fill_uniform_f32(X.data_ptr(), n, d, 42, 0, None))
 r = S.knn_l2sq(X, k)
 del X
 torch.cuda.synchronize()
+# row segment lengths before the dedupe: k forward slots + in-degree
+indeg = torch.bincount(r.idx.reshape(-1).long().clamp(min=0), minlength=n)
+seg = indeg + k
+edges = [0, 64, 128, 256, 512, 1024, 2048, 4096, 8192, 1 << 40]
+hist = {f"<={edges[i + 1]}": int(((seg > edges[i]) & (seg <= edges[i + 1])).sum())
+        for i in range(len(edges) - 1)}
+big = seg[seg > 512]
+print(json.dumps({"seg_hist": hist, "entries_in_rows_gt512": int(big.sum()),
+                  "max_seg": int(seg.max())}), flush=True)
 for rep in range(6):
     t0 = time.perf_counter()
     L, _ = S.build_laplacian_from_knn(r.idx, r.dist, weight_kernel="rational", symmetrise="union",
@@ -32,5 +41,6 @@ for rep in range(6):
     byt = n * k * 8 + L.nnz * 12 + (n + 1) * 8
     print(json.dumps({"rep": rep, "wall_ms": round(wall, 3), "lib_ms": round(st["ms_total"], 3),
                       "nnz": L.nnz, "GB_per_s_wall": round(byt / wall / 1e6, 1),
-                      "GB_per_s_lib": round(byt / st["ms_total"] / 1e6, 1)}), flush=True)
+                      "GB_per_s_lib": round(byt / st["ms_total"] / 1e6, 1),
+                      "big_rows": st["big_rows"], "hub_rows": st["hub_rows"]}), flush=True)
     del L
