@@ -160,6 +160,15 @@ __device__ __forceinline__ void wave_bitonic_sort(T (&d)[NR], int (&ix)[NR]) {
 // __fsqrt_rn() are NOT correctly rounded (measured: 1-ulp misses, e.g.
 // sqrt(0x3da6a80c)); the f64 square root rounded to f32 is (53 >= 2*24+2, so
 // the double rounding is innocuous) and matches Rust's IEEE f32::sqrt.
+// Maxima of non-negative float bit patterns over a loop: keep them in
+// registers and issue ONE atomic per wave at the end (a per-row atomicMax on
+// one address serialises a whole launch at the memory-side atomic unit).
+__device__ __forceinline__ void wave_atomic_umax(unsigned *p, unsigned v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = max(v, (unsigned)__shfl_xor((int)v, o));
+    if ((threadIdx.x & 63) == 0 && v != 0u) atomicMax(p, v);
+}
+
 __device__ __forceinline__ float sqrt_rn_f32(float x) { return (float)__builtin_sqrt((double)x); }
 
 // Ordered fold acc = (((acc + b[0]) + b[1]) + ...) over N values in LDS that

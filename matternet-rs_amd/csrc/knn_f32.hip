@@ -87,6 +87,7 @@ __global__ __launch_bounds__(256) void k_row_norms(const float *__restrict__ X, 
     const int lane = threadIdx.x & 63;
     const int64_t wave0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+    unsigned mx = 0u;  // max |x|^2 bits (one atomic per wave)
     for (int64_t row = wave0; row < n; row += nwaves) {
         const float *p = X + row * (int64_t)d;
         float s = 0.f;
@@ -114,9 +115,10 @@ __global__ __launch_bounds__(256) void k_row_norms(const float *__restrict__ X, 
         if (lane == 0) {
             nrm[row] = s;
             if (anybad) atomicOr(nonfinite, 1);
-            atomicMax(maxbits, __builtin_isfinite(s) ? __float_as_uint(s) : 0x7f800000u);
+            mx = max(mx, __builtin_isfinite(s) ? __float_as_uint(s) : 0x7f800000u);
         }
     }
+    wave_atomic_umax(maxbits, mx);
 }
 
 // ---------------------------------------------------------------------------
@@ -697,6 +699,7 @@ __global__ __launch_bounds__(256) void k_prep_x1(const float *__restrict__ X, in
     const int64_t wave0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
     float am = 0.f;  // max |x| (amax != NULL: the fp16 sweep's scale)
+    unsigned mx0 = 0u, mx1 = 0u, mx2 = 0u;  // corpus maxima (one atomic per wave)
     for (int64_t r2 = 2 * wave0; r2 < n; r2 += 2 * nwaves) {
         const int64_t row = r2 + hl;
         const bool live = row < n;
@@ -762,11 +765,16 @@ __global__ __launch_bounds__(256) void k_prep_x1(const float *__restrict__ X, in
             // keys stay far from f32 overflow (and bf16(x) finite) below 2^100
             if (!(s <= 0x1p100)) atomicOr(flags + 1, 1);
             if (corpus) {
-                atomicMax(maxbits + 0, __float_as_uint(nf));
-                atomicMax(maxbits + 1, __float_as_uint(hf));
-                atomicMax(maxbits + 2, __float_as_uint(rf));
+                mx0 = max(mx0, __float_as_uint(nf));
+                mx1 = max(mx1, __float_as_uint(hf));
+                mx2 = max(mx2, __float_as_uint(rf));
             }
         }
+    }
+    if (corpus) {
+        wave_atomic_umax(maxbits + 0, mx0);
+        wave_atomic_umax(maxbits + 1, mx1);
+        wave_atomic_umax(maxbits + 2, mx2);
     }
     if (amax) {
 #pragma unroll
@@ -789,6 +797,7 @@ __global__ __launch_bounds__(256) void k_prep_f16(const float *__restrict__ X, i
     const int lane = threadIdx.x & 63, hl = lane >> 5, ll = lane & 31;
     const int64_t wave0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+    unsigned mx0 = 0u, mx1 = 0u;  // maxima (one atomic per wave)
     for (int64_t r2 = 2 * wave0; r2 < n; r2 += 2 * nwaves) {
         const int64_t row = r2 + hl;
         const bool live = row < n;
@@ -840,10 +849,12 @@ __global__ __launch_bounds__(256) void k_prep_f16(const float *__restrict__ X, i
             const float rf = f32_up(__builtin_sqrt(sr) * (1.0 + 0x1p-50));
             hn[row] = hf;
             rn[row] = rf;
-            atomicMax(maxbits + 0, __float_as_uint(hf));
-            atomicMax(maxbits + 1, __float_as_uint(rf));
+            mx0 = max(mx0, __float_as_uint(hf));
+            mx1 = max(mx1, __float_as_uint(rf));
         }
     }
+    wave_atomic_umax(maxbits + 0, mx0);
+    wave_atomic_umax(maxbits + 1, mx1);
 }
 
 // ---------------------------------------------------------------------------
@@ -883,6 +894,7 @@ __global__ __launch_bounds__(256) void k_prep_x3(const float *__restrict__ X, in
     const int64_t wave0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
     const int nkb = dp >> 5;
+    unsigned mx[4] = {0u, 0u, 0u, 0u};  // corpus maxima (one atomic per wave)
     for (int64_t r2 = 2 * wave0; r2 < n; r2 += 2 * nwaves) {
         const int64_t row = r2 + hl;
         const bool live = row < n;
@@ -952,13 +964,15 @@ __global__ __launch_bounds__(256) void k_prep_x3(const float *__restrict__ X, in
             if (ln) ln[row] = lf;
             if (r2n) r2n[row] = rf;
             if (corpus) {
-                atomicMax(cmax3 + 0, __float_as_uint(nf));
-                atomicMax(cmax3 + 1, __float_as_uint(hf));
-                atomicMax(cmax3 + 2, __float_as_uint(lf));
-                atomicMax(cmax3 + 3, __float_as_uint(rf));
+                mx[0] = max(mx[0], __float_as_uint(nf));
+                mx[1] = max(mx[1], __float_as_uint(hf));
+                mx[2] = max(mx[2], __float_as_uint(lf));
+                mx[3] = max(mx[3], __float_as_uint(rf));
             }
         }
     }
+    if (corpus)
+        for (int c = 0; c < 4; ++c) wave_atomic_umax(cmax3 + c, mx[c]);
 }
 
 __device__ __forceinline__ double delta3_at(double Tf, double qn, double qh, double ql, double q2,
@@ -1047,15 +1061,18 @@ __global__ __launch_bounds__(256) void k_tau_x1(int64_t nq, int S1, const float 
                                                 float *__restrict__ delta,
                                                 unsigned *__restrict__ tmax) {
     const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (q >= nq) return;
-    float T = __builtin_inff();
-    for (int s = 0; s < S1; ++s) T = fminf(T, btau1[q * S1 + s]);
-    const float qn = nq_f[q];
-    tau0[q] = T;
-    tq[q] = (T - qn) * 0.5f;
-    const double Tf = __builtin_isfinite(T) ? __builtin_fabs((double)T) : 0.0;
-    delta[q] = delta_x1(Tf, qn, hn_q[q], rn_q[q], cmax, d, dp);
-    if (tmax && __builtin_isfinite(T)) atomicMax(tmax, __float_as_uint(__builtin_fabsf(T)));
+    unsigned tb = 0u;
+    if (q < nq) {
+        float T = __builtin_inff();
+        for (int s = 0; s < S1; ++s) T = fminf(T, btau1[q * S1 + s]);
+        const float qn = nq_f[q];
+        tau0[q] = T;
+        tq[q] = (T - qn) * 0.5f;
+        const double Tf = __builtin_isfinite(T) ? __builtin_fabs((double)T) : 0.0;
+        delta[q] = delta_x1(Tf, qn, hn_q[q], rn_q[q], cmax, d, dp);
+        if (__builtin_isfinite(T)) tb = __float_as_uint(__builtin_fabsf(T));
+    }
+    if (tmax) wave_atomic_umax(tmax, tb);  // every lane of the wave takes part
 }
 
 // SW_SYM per-position arrays (position p holds row pi[p]): the threshold,
@@ -1395,6 +1412,233 @@ __global__ __launch_bounds__(FB_THREADS) void k_fallback(
         }
         __syncthreads();
     }
+}
+
+// Split exact scan for a FEW uncertified rows (k_fallback gives a whole row
+// to one block: ~60 ms per row at 1M x 768).  Launch over a batch of up to
+// FSQ rows: block b scans corpus part [b chunk, (b+1) chunk) (chunk <= FSC
+// rows) for every row of the batch (the rows in LDS, one corpus row per
+// thread, the reference fold per (row, corpus row) in feature order), keeps
+// the part's survivors — dist <= ub[row] (an exact upper bound of D_k from
+// the re-rank, +inf when none) — and writes the part's best keff by (dist,
+// id).  k_fb_merge then reduces groups of part lists to one list per row.
+constexpr int FSQ = 8;      // rows per launch
+constexpr int FSC = 1024;   // corpus rows per part (one sort of <= FSC survivors)
+constexpr int FST = 256;    // threads
+constexpr int FMG = 4096;   // merge: entries per group (sorted in LDS)
+
+__device__ __forceinline__ void lds_bitonic(float *kd, int *ki, int P) {
+    for (int kk = 2; kk <= P; kk <<= 1)
+        for (int j = kk >> 1; j > 0; j >>= 1) {
+            for (int e = threadIdx.x; e < P; e += blockDim.x) {
+                const int pe = e ^ j;
+                if (pe > e) {
+                    const bool asc = (e & kk) == 0;
+                    const bool sw = asc ? key_less(kd[pe], ki[pe], kd[e], ki[e])
+                                        : key_less(kd[e], ki[e], kd[pe], ki[pe]);
+                    if (sw) {
+                        const float td = kd[e]; kd[e] = kd[pe]; kd[pe] = td;
+                        const int ti = ki[e]; ki[e] = ki[pe]; ki[pe] = ti;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+}
+
+template <bool VEC4, bool SQRT>
+__global__ __launch_bounds__(FST) void k_fb_part(
+    const float *__restrict__ Q, const float *__restrict__ C, int64_t nc, int d, int64_t q_off,
+    int64_t c_off, int excl, int keff_max, const int *__restrict__ rows, int nb,
+    const float *__restrict__ ub, int64_t chunk, float2 *__restrict__ plist,
+    int *__restrict__ pcnt) {
+    extern __shared__ float fsm[];
+    float *qs = fsm;                                // [nb][d]
+    float *dv = qs + (size_t)nb * d;                // [nb][FSC]
+    float *sd = dv + (size_t)nb * FSC;              // [FSC] sort keys
+    int *si = (int *)(sd + FSC);                    // [FSC] sort ids
+    int *scnt = si + FSC;
+    const int P = gridDim.x, b = blockIdx.x, t = threadIdx.x;
+    const int64_t c0 = (int64_t)b * chunk, c1 = min(nc, c0 + chunk);
+    for (int e = t; e < nb * d; e += FST) qs[e] = Q[(int64_t)rows[e / d] * d + (e % d)];
+    __syncthreads();
+    for (int64_t c = c0 + t; c < c1; c += FST) {
+        const float *crow = C + c * (int64_t)d;
+        float acc[FSQ];
+#pragma unroll
+        for (int r = 0; r < FSQ; ++r) acc[r] = -0.0f;
+        if (VEC4) {
+            for (int f = 0; f < d; f += 4) {
+                const float4 y = *reinterpret_cast<const float4 *>(crow + f);
+#pragma unroll
+                for (int r = 0; r < FSQ; ++r) {
+                    if (r < nb) {
+                        const float4 x = *reinterpret_cast<const float4 *>(qs + r * d + f);
+                        float df = x.x - y.x; acc[r] = acc[r] + df * df;
+                        df = x.y - y.y; acc[r] = acc[r] + df * df;
+                        df = x.z - y.z; acc[r] = acc[r] + df * df;
+                        df = x.w - y.w; acc[r] = acc[r] + df * df;
+                    }
+                }
+            }
+        } else {
+            for (int f = 0; f < d; ++f) {
+                const float y = crow[f];
+#pragma unroll
+                for (int r = 0; r < FSQ; ++r)
+                    if (r < nb) {
+                        const float df = qs[r * d + f] - y;
+                        acc[r] = acc[r] + df * df;
+                    }
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < FSQ; ++r)
+            if (r < nb) dv[r * FSC + (c - c0)] = SQRT ? sqrt_rn_f32(acc[r]) : acc[r];
+    }
+    __syncthreads();
+    for (int r = 0; r < nb; ++r) {
+        const int64_t q = rows[r], gq = q_off + q;
+        const float u = ub ? ub[q] : __builtin_inff();
+        if (t == 0) *scnt = 0;
+        __syncthreads();
+        for (int64_t c = c0 + t; c < c1; c += FST) {
+            const float dist = dv[r * FSC + (c - c0)];
+            const int64_t gj = c_off + c;
+            if (!(excl && gj == gq) && dist <= u) {
+                const int p = atomicAdd(scnt, 1);
+                sd[p] = dist;
+                si[p] = (int)gj;
+            }
+        }
+        __syncthreads();
+        const int m = *scnt;
+        int keep = m;
+        if (m > keff_max) {
+            int Pw = 1;
+            while (Pw < m) Pw <<= 1;
+            for (int e = m + t; e < Pw; e += FST) {
+                sd[e] = __builtin_inff();
+                si[e] = INT_MAX;
+            }
+            __syncthreads();
+            lds_bitonic(sd, si, Pw);
+            keep = keff_max;
+        }
+        float2 *out = plist + ((int64_t)r * P + b) * keff_max;
+        for (int e = t; e < keep; e += FST) out[e] = make_float2(sd[e], __int_as_float(si[e]));
+        if (t == 0) pcnt[r * P + b] = keep;
+        __syncthreads();
+    }
+}
+
+// groups of gs part lists (<= FMG entries) of each row -> that group's best
+// keff; with one group left, the row's output (keff = min(k, valid), padded)
+template <bool FINAL>
+__global__ __launch_bounds__(FST) void k_fb_merge(
+    const float2 *__restrict__ plist, const int *__restrict__ pcnt, int P, int keff_max, int gs,
+    float2 *__restrict__ olist, int *__restrict__ ocnt, const int *__restrict__ rows,
+    int64_t nc, int64_t q_off, int64_t c_off, int excl, int k, int32_t *__restrict__ out_idx,
+    float *__restrict__ out_dist) {
+    __shared__ float sd[FMG];
+    __shared__ int si[FMG];
+    __shared__ int base[FMG / 8 + 1];
+    const int G = (P + gs - 1) / gs;
+    const int r = blockIdx.x / G, g = blockIdx.x % G, t = threadIdx.x;
+    const int p0 = g * gs, p1 = min(P, p0 + gs);
+    if (t == 0) {
+        int a = 0;
+        for (int p = p0; p < p1; ++p) {
+            base[p - p0] = a;
+            a += pcnt[r * P + p];
+        }
+        base[p1 - p0] = a;
+    }
+    __syncthreads();
+    const int m = base[p1 - p0];
+    for (int p = p0; p < p1; ++p) {
+        const int o = base[p - p0], n = base[p - p0 + 1] - o;
+        const float2 *src = plist + ((int64_t)r * P + p) * keff_max;
+        for (int e = t; e < n; e += FST) {
+            sd[o + e] = src[e].x;
+            si[o + e] = __float_as_int(src[e].y);
+        }
+    }
+    int Pw = 1;
+    while (Pw < m) Pw <<= 1;
+    for (int e = m + t; e < Pw; e += FST) {
+        sd[e] = __builtin_inff();
+        si[e] = INT_MAX;
+    }
+    __syncthreads();
+    lds_bitonic(sd, si, Pw);
+    const int keep = min(m, keff_max);
+    if constexpr (FINAL) {
+        const int64_t q = rows[r], gq = q_off + q;
+        const bool self_in = excl && gq >= c_off && gq < c_off + nc;
+        const int keff = (int)min((int64_t)k, nc - (self_in ? 1 : 0));
+        for (int e = t; e < k; e += FST) {
+            const bool ok = e < keff && e < keep;
+            out_idx[q * k + e] = ok ? si[e] : -1;
+            out_dist[q * k + e] = ok ? sd[e] : __builtin_inff();
+        }
+    } else {
+        float2 *out = olist + ((int64_t)r * G + g) * keff_max;
+        for (int e = t; e < keep; e += FST) out[e] = make_float2(sd[e], __int_as_float(si[e]));
+        if (t == 0) ocnt[r * G + g] = keep;
+    }
+}
+
+// Host driver of the split scan: the nfb rows listed (device) in rows, in
+// batches; part lists in the kSlotX1Esc scratch.  Returns 1 when the shape is
+// outside its limits (the caller keeps its other path).
+static int fb_split_scan(const float *Q, const float *C, int64_t nc, int d, int64_t q_off,
+                         int64_t c_off, int excl, int k, const int *rows, int nfb,
+                         const float *ub, bool sqrt_keys, int32_t *out_idx, float *out_dist,
+                         hipStream_t s) {
+    const int keff_max = k;
+    const size_t fixed = (size_t)FSC * 8 + 64;
+    const int nbm = (int)std::min<int64_t>(FSQ, (int64_t)((65536 - fixed) / ((size_t)(d + FSC) * 4)));
+    if (nbm < 1 || nc < 1 || k > KMAX) return 1;
+    const int64_t P = (nc + FSC - 1) / FSC;
+    const int64_t chunk = (nc + P - 1) / P;
+    const int gs = FMG / keff_max;
+    // ping-pong part lists: [nb][P][keff] and the first merge level
+    const size_t l0 = (size_t)nbm * P * keff_max, l1 = (size_t)nbm * ((P + gs - 1) / gs) * keff_max;
+    const size_t b0 = (l0 * 8 + 255) & ~(size_t)255, b1 = (l1 * 8 + 255) & ~(size_t)255;
+    const size_t c0b = ((size_t)nbm * P * 4 + 255) & ~(size_t)255;
+    char *g = (char *)scratch(kSlotX1Esc, b0 + b1 + 2 * c0b + 256);
+    if (!g) return MN_ENOMEM;
+    float2 *la = (float2 *)g, *lb = (float2 *)(g + b0);
+    int *ca = (int *)(g + b0 + b1), *cb = (int *)(g + b0 + b1 + c0b);
+    const bool vec4 = (d % 4 == 0) && (((uintptr_t)Q | (uintptr_t)C) % 16 == 0);
+    for (int r0 = 0; r0 < nfb; r0 += nbm) {
+        const int nb = std::min(nbm, nfb - r0);
+        const size_t lds = ((size_t)nb * (d + FSC)) * 4 + fixed;
+        auto kp = vec4 ? (sqrt_keys ? k_fb_part<true, true> : k_fb_part<true, false>)
+                       : (sqrt_keys ? k_fb_part<false, true> : k_fb_part<false, false>);
+        hipLaunchKernelGGL(kp, dim3((unsigned)P), dim3(FST), lds, s, Q, C, nc, d, q_off, c_off,
+                           excl, keff_max, rows + r0, nb, ub, chunk, la, ca);
+        MN_KCHECK(s, "k_fb_part");
+        int Pl = (int)P;
+        float2 *src = la, *dst = lb;
+        int *sc = ca, *dc = cb;
+        while (Pl > gs) {
+            const int G = (Pl + gs - 1) / gs;
+            hipLaunchKernelGGL(k_fb_merge<false>, dim3((unsigned)(nb * G)), dim3(FST), 0, s, src,
+                               sc, Pl, keff_max, gs, dst, dc, rows + r0, nc, q_off, c_off, excl,
+                               k, out_idx, out_dist);
+            MN_KCHECK(s, "k_fb_merge");
+            std::swap(src, dst);
+            std::swap(sc, dc);
+            Pl = G;
+        }
+        hipLaunchKernelGGL(k_fb_merge<true>, dim3((unsigned)nb), dim3(FST), 0, s, src, sc, Pl,
+                           keff_max, gs, dst, dc, rows + r0, nc, q_off, c_off, excl, k, out_idx,
+                           out_dist);
+        MN_KCHECK(s, "k_fb_merge<final>");
+    }
+    return MN_OK;
 }
 
 // ---------------------------------------------------------------------------
@@ -2138,7 +2382,18 @@ static int knn_x1(const float *Q, int64_t nq, const float *C, int64_t nc, int32_
     int nfb2 = 0;
     MN_HIP_TRY(hipMemcpyAsync(&nfb2, fb_count, 4, hipMemcpyDeviceToHost, s));
     MN_HIP_TRY(hipStreamSynchronize(s));
-    if (nfb2 > 0 && nc >= (1 << 16) && k + 1 <= KMAX) {
+    // a few rows: the split exact scan (every corpus part in parallel, pruned
+    // by the rows' exact upper bounds of D_k), ~1 ms per 8 rows at C2
+    int split = 1;
+    const char *fse = getenv("MN_FB_SPLIT");  // 0: the batched split-generator pass (A/B)
+    if (nfb2 > 0 && nfb2 <= 256 && nc >= (1 << 16) && !(fse && *fse == '0')) {
+        split = fb_split_scan(Q, C, nc, d, q_off, c_off, excl, k, fb_list, nfb2, ubv, false,
+                              out_idx, out_dist, s);
+        if (split < 0) return split;
+    }
+    if (split == MN_OK) {
+        // done
+    } else if (nfb2 > 0 && nc >= (1 << 16) && k + 1 <= KMAX) {
         // the refill slot is dead here (knn_f32_core below does not use it):
         // rows, the gathered queries and the (k + 1)-lists, 16-B aligned parts
         auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
@@ -2263,7 +2518,14 @@ static int knn_f32_impl(const float *Q, int64_t nq, const float *C, int64_t nc, 
         int nfb = 0;
         MN_HIP_TRY(hipMemcpyAsync(&nfb, fl, 4, hipMemcpyDeviceToHost, s));
         MN_HIP_TRY(hipStreamSynchronize(s));
-        if (nfb > 0) {
+        int split = 1;
+        if (nfb > 0 && nfb <= 256 && nc >= (1 << 16)) {
+            split = fb_split_scan(Q, C, nc, d, q_off, c_off, excl, k, fbl, nfb, nullptr, true,
+                                  out_idx, out_dist, s);
+            if (split < 0) return split;
+            MN_HIP_TRY(hipStreamSynchronize(s));
+        }
+        if (nfb > 0 && split != MN_OK) {
             const bool vec4 = (d % 4 == 0) && (((uintptr_t)Q | (uintptr_t)C) % 16 == 0);
             const unsigned fgrid = (unsigned)std::min<int64_t>(nfb, 1024);
             if (vec4)

@@ -295,3 +295,65 @@ def test_uncertified_rows_batched_fallback():
     np.testing.assert_array_equal(idx[rows], ridx)
     np.testing.assert_array_equal(dist[rows].view(np.uint32), rdist.view(np.uint32))
     assert st["n_uncertified"] > 0, st
+
+
+@pytest.mark.parametrize("split", ["1", "0"], ids=["split_scan", "batched"])
+def test_uncertified_rows_split_scan(split, monkeypatch):
+    """Uncertified rows (all-zero rows: exact ties far beyond k, plus exact
+    duplicate pairs) against a corpus >= 2^16: up to 256 of them go through
+    the split exact scan (corpus parts in parallel, pruned by each row's exact
+    upper bound of D_k, part lists merged by (dist, id)); MN_FB_SPLIT=0 keeps
+    the batched split-generator pass.  Both bit-exact with the oracle."""
+    import json
+    n, d, k = 70000, 32, 32
+    X = datagen.uniform(n, d, seed=11)
+    zero = np.random.default_rng(2).choice(n, 300, replace=False)
+    X[zero] = 0.0
+    dup = np.setdiff1d(np.arange(1, 12), zero)
+    X[dup + 20000] = X[dup]
+    monkeypatch.setenv("MN_FB_SPLIT", split)
+    idx, dist, st = hip_knn(X, k, algo="bf16x1", timing=True)
+    print(f"uncertified split={split}", json.dumps(
+        {kk: (round(v, 3) if isinstance(v, float) else v) for kk, v in st.items()}))
+    assert 0 < st["n_uncertified"] <= 256, st
+    rows = np.unique(np.concatenate([zero[:64], dup, dup + 20000,
+                                     np.random.default_rng(6).choice(n, 24, replace=False)]))
+    ridx, rdist = O.knn_l2sq_rows(X, k, rows)
+    np.testing.assert_array_equal(idx[rows], ridx)
+    np.testing.assert_array_equal(dist[rows].view(np.uint32), rdist.view(np.uint32))
+
+
+def _euclid_rows_np(X, rows, k):
+    """Reference Euclidean lists of `rows` (distance.rs:195-213 f32 fold from
+    -0.0 in feature order, IEEE sqrt, stable sort of the roots, self
+    excluded) — vectorised over corpus rows, sequential over features."""
+    out_i, out_d = [], []
+    for q in rows:
+        acc = np.full(len(X), -0.0, np.float32)
+        for t in range(X.shape[1]):
+            df = (X[q, t] - X[:, t]).astype(np.float32)
+            acc = (acc + df * df).astype(np.float32)
+        r = np.sqrt(acc)
+        r[q] = np.inf
+        o = np.argsort(r, kind="stable")[:k]
+        out_i.append(o.astype(np.int32))
+        out_d.append(r[o])
+    return np.stack(out_i), np.stack(out_d)
+
+
+def test_euclidean_root_ties_rescan_large_corpus():
+    """The root-keyed rescan (equal-root run past the extended list) against a
+    corpus >= 2^16: the split scan with root keys."""
+    import surfface_hip as S
+    hi, lo = _root_tie_rows()
+    far = (datagen.uniform(70000, 2, seed=13) + np.float32(20.0)).astype(np.float32)
+    X = np.concatenate([np.zeros((1, 2), np.float32), np.repeat(hi[None], 20, 0),
+                        np.repeat(lo[None], 20, 0), far])
+    X = np.ascontiguousarray(np.concatenate([X, np.zeros((len(X), 6), np.float32)], axis=1))
+    r = S.knn_l2sq(torch.from_numpy(X).cuda(), 4, euclidean=True, algo="bf16x1")
+    rows = np.array([0, 1, 25, 100, 5000], np.int64)
+    ridx, rdist = _euclid_rows_np(X, rows, 4)
+    assert list(ridx[0]) == [1, 2, 3, 4]
+    np.testing.assert_array_equal(r.idx.cpu().numpy()[rows], ridx)
+    np.testing.assert_array_equal(r.dist.cpu().numpy()[rows].view(np.uint32), rdist.view(np.uint32))
+    assert r.stats["n_root_rescan"] >= 1
