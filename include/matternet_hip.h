@@ -288,7 +288,7 @@ typedef struct mn_csr {
 
 typedef struct mn_lap_stats {
     int64_t nnz;
-    int64_t big_rows;  /* rows sorted by the block kernel (> 256 entries)      */
+    int64_t big_rows;  /* rows sorted by the wider kernels (> 256 entries)     */
     int64_t hub_rows;  /* rows resolved by the dense column map (> 8192)       */
     float ms_total;
     float reserved0;

@@ -2385,8 +2385,11 @@ static int knn_x1(const float *Q, int64_t nq, const float *C, int64_t nc, int32_
     // a few rows: the split exact scan (every corpus part in parallel, pruned
     // by the rows' exact upper bounds of D_k), ~1 ms per 8 rows at C2
     int split = 1;
-    const char *fse = getenv("MN_FB_SPLIT");  // 0: the batched split-generator pass (A/B)
-    if (nfb2 > 0 && nfb2 <= 256 && nc >= (1 << 16) && !(fse && *fse == '0')) {
+    // MN_FB_SPLIT: the row limit of the split scan (default 256; 0 = always
+    // the batched split-generator pass; A/B and tests)
+    const char *fse = getenv("MN_FB_SPLIT");
+    const int fb_lim = (fse && *fse) ? std::max(0, atoi(fse)) : 256;
+    if (nfb2 > 0 && nfb2 <= fb_lim && nc >= (1 << 16)) {
         split = fb_split_scan(Q, C, nc, d, q_off, c_off, excl, k, fb_list, nfb2, ubv, false,
                               out_idx, out_dist, s);
         if (split < 0) return split;

@@ -47,9 +47,10 @@ struct Params {
     double eps, sigma, p, thr;
 };
 
-constexpr int WAVE_CAP = 512;
+constexpr int WAVE_CAP = 512;   // general (col, w) wave sort
 constexpr int BLOCK_CAP = 8192;
 constexpr int EMPTY = INT_MAX;  // sentinel column of an invalid forward slot
+constexpr uint64_t SENT = ~0ull;  // sentinel packed key (column << 32 | entry)
 
 __device__ __forceinline__ double pw(double x, double p) {
     if (p == 2.0) return x * x;
@@ -136,8 +137,11 @@ __device__ __forceinline__ double readlane_f64(double x, int l) {
 }
 
 // Sort, dedupe and fold one row of m <= 64*NR entries held by one wave.
+// Source (cs, ws at o) and destination (col, wt at od) may differ: the
+// bucket kernel sorts rows staged in LDS into their global segments.
 template <int NR>
 __device__ __forceinline__ void row_sort_fold(int64_t i, int64_t o, int m, int sym,
+                                              const int32_t *cs, const double *ws, int64_t od,
                                               int32_t *__restrict__ col, double *__restrict__ wt,
                                               int32_t *__restrict__ uniq,
                                               int32_t *__restrict__ kept,
@@ -149,8 +153,8 @@ __device__ __forceinline__ void row_sort_fold(int64_t i, int64_t o, int m, int s
 #pragma unroll
     for (int r = 0; r < NR; ++r) {
         const int e = lane + 64 * r;
-        c[r] = e < m ? col[o + e] : EMPTY;
-        w[r] = e < m ? wt[o + e] : 0.0;
+        c[r] = e < m ? cs[o + e] : EMPTY;
+        w[r] = e < m ? ws[o + e] : 0.0;
     }
 #pragma unroll
     for (int kk = 2; kk <= 64 * NR; kk <<= 1) {
@@ -203,8 +207,8 @@ __device__ __forceinline__ void row_sort_fold(int64_t i, int64_t o, int m, int s
         uint64_t mk = __ballot(keep);
         if (keep) {
             const int pos = base + (int)__popcll(mk & ((1ull << lane) - 1ull));
-            col[o + pos] = c[r];
-            wt[o + pos] = w[r];
+            col[od + pos] = c[r];
+            wt[od + pos] = w[r];
         }
         base += (int)__popcll(mk);
         if (sym == MN_SYM_UNION) {
@@ -234,6 +238,162 @@ __device__ __forceinline__ void row_sort_fold(int64_t i, int64_t o, int m, int s
 
 // one wave per row; rows with more than WAVE_CAP entries are listed for the
 // block kernel
+// Packed-key row (the default for rows of <= 64 NR entries): sort keys
+// (column << 32 | entry index e) in registers — one 64-bit compare per
+// exchange, the weights stay where they are — then each column run's first
+// entry is kept with the run's largest weight (the (col asc, w desc) order of
+// row_sort_fold), gathered through wf(e) for the kept entries and their run
+// partners only; then the ascending-column degree fold.  keyf(e), e < m: the
+// key of entry e (SENT for an empty slot).  Every gather is issued before the
+// first store, so the destination may be the source segment.  Returns false
+// (nothing written) for a run of 3 or more equal columns (duplicate ids in one
+// kNN row): the caller then runs row_sort_fold.
+template <int NR, class KeyF, class WF>
+__device__ __forceinline__ bool packed_row(KeyF keyf, WF wf, int m, int64_t i, int64_t od, int sym,
+                                           int32_t *__restrict__ col, double *__restrict__ wt,
+                                           int32_t *__restrict__ uniq, int32_t *__restrict__ kept,
+                                           double *__restrict__ deg64,
+                                           float *__restrict__ deg32) {
+    const int lane = threadIdx.x & 63;
+    uint64_t x[NR];
+#pragma unroll
+    for (int r = 0; r < NR; ++r) {
+        const int e = lane + 64 * r;
+        x[r] = e < m ? keyf(e) : SENT;
+    }
+#pragma unroll
+    for (int q = 2; q <= 64 * NR; q <<= 1) {
+#pragma unroll
+        for (int j = q >> 1; j > 0; j >>= 1) {
+            if (j >= 64) {
+#pragma unroll
+                for (int r = 0; r < NR; ++r) {
+                    const int pr = r ^ (j >> 6);
+                    if (pr > r) {
+                        const bool asc = ((lane + 64 * r) & q) == 0;
+                        if (asc ? x[pr] < x[r] : x[r] < x[pr]) {
+                            const uint64_t t = x[r]; x[r] = x[pr]; x[pr] = t;
+                        }
+                    }
+                }
+            } else {
+#pragma unroll
+                for (int r = 0; r < NR; ++r) {
+                    const int e = lane + 64 * r;
+                    const uint64_t p = (uint64_t)__shfl_xor((long long)x[r], j);
+                    const bool asc = (e & q) == 0, lower = (e & j) == 0;
+                    if ((asc == lower) ? p < x[r] : x[r] < p) x[r] = p;
+                }
+            }
+        }
+    }
+    auto colof = [](uint64_t v) { return v == SENT ? EMPTY : (int)(v >> 32); };
+    // neighbours in sorted order: previous column, next key, next-but-one column
+    bool run3 = false;
+    uint64_t xn[NR];
+    int cp[NR];
+#pragma unroll
+    for (int r = 0; r < NR; ++r) {
+        const int c = colof(x[r]);
+        int up = __shfl_up(c, 1);
+        const int prevlast = __shfl(colof(x[r > 0 ? r - 1 : 0]), 63);
+        if (lane == 0) up = r == 0 ? INT_MIN : prevlast;
+        cp[r] = up;
+        uint64_t dn = (uint64_t)__shfl_down((long long)x[r], 1);
+        const uint64_t nx0 = (uint64_t)__shfl((long long)x[r + 1 < NR ? r + 1 : r], 0);
+        if (lane == 63) dn = r + 1 < NR ? nx0 : SENT;
+        xn[r] = dn;
+        int dn2 = __shfl_down(c, 2);
+        const int n0 = colof(nx0), n1 = __shfl(colof(x[r + 1 < NR ? r + 1 : r]), 1);
+        if (lane >= 62) dn2 = r + 1 < NR ? (lane == 62 ? n0 : n1) : EMPTY;
+        run3 |= c != EMPTY && c == dn2;
+    }
+    if (__any(run3)) return false;
+    double w[NR];
+#pragma unroll
+    for (int r = 0; r < NR; ++r) {
+        const int c = colof(x[r]);
+        const bool keep = c != EMPTY && c != cp[r];
+        w[r] = 0.0;
+        if (keep) {
+            w[r] = wf((uint32_t)x[r]);
+            if (colof(xn[r]) == c) {
+                const double wp = wf((uint32_t)xn[r]);
+                if (wp > w[r]) w[r] = wp;
+            }
+        }
+    }
+    int base = 0;
+    double s64 = -0.0;  // laplacian.rs:367 s.iter().map(w).sum() in ascending j
+    float s32 = 0.0f;   // surfface-core/src/laplacian.rs:331-340 (order: ascending column)
+#pragma unroll
+    for (int r = 0; r < NR; ++r) {
+        const int c = colof(x[r]);
+        const bool keep = c != EMPTY && c != cp[r];
+        uint64_t mk = __ballot(keep);
+        if (keep) {
+            const int pos = base + (int)__popcll(mk & ((1ull << lane) - 1ull));
+            col[od + pos] = c;
+            wt[od + pos] = w[r];
+        }
+        base += (int)__popcll(mk);
+        if (sym == MN_SYM_UNION) {
+            while (mk) {
+                const int l = __builtin_ctzll(mk);
+                mk &= mk - 1;
+                s64 = s64 + readlane_f64(w[r], l);
+            }
+        } else {
+            while (mk) {
+                const int l = __builtin_ctzll(mk);
+                mk &= mk - 1;
+                s32 = s32 + (float)readlane_f64(w[r], l);
+            }
+        }
+    }
+    if (lane == 0) {
+        uniq[i] = base;
+        if (sym == MN_SYM_UNION) {
+            deg64[i] = s64;
+            kept[i] = base + 1;
+        } else {
+            deg32[i] = s32;
+        }
+    }
+    return true;
+}
+
+// 1: done; 0: a run of >= 3 equal columns (general path); -1: too long
+template <int NRMAX, class KeyF, class WF, typename... A>
+__device__ __forceinline__ int packed_row_any(KeyF keyf, WF wf, int m, A... a) {
+    if (m <= 64) return packed_row<1>(keyf, wf, m, a...) ? 1 : 0;
+    if (m <= 128) return packed_row<2>(keyf, wf, m, a...) ? 1 : 0;
+    if (m <= 256) return packed_row<4>(keyf, wf, m, a...) ? 1 : 0;
+    if constexpr (NRMAX >= 8)
+        if (m <= 512) return packed_row<8>(keyf, wf, m, a...) ? 1 : 0;
+    if constexpr (NRMAX >= 16)
+        if (m <= 1024) return packed_row<16>(keyf, wf, m, a...) ? 1 : 0;
+    return -1;
+}
+
+template <typename... A>
+__device__ __forceinline__ bool row_sort_fold_any(int64_t i, int64_t o, int m, int sym,
+                                                  const int32_t *cs, const double *ws, int64_t od,
+                                                  A... a) {
+    if (m <= 64) row_sort_fold<1>(i, o, m, sym, cs, ws, od, a...);
+    else if (m <= 128) row_sort_fold<2>(i, o, m, sym, cs, ws, od, a...);
+    else if (m <= 256) row_sort_fold<4>(i, o, m, sym, cs, ws, od, a...);
+    else if (m <= WAVE_CAP) row_sort_fold<8>(i, o, m, sym, cs, ws, od, a...);
+    else return false;
+    return true;
+}
+
+// list == NULL: row i = the wave's index; else rows list[0 .. *list_n).
+// NRMAX 4 (the full pass / the bucket kernel's leftovers): rows of <= 256
+// entries, longer ones (and rows with duplicate ids) to next_list; NRMAX 16
+// (that list): rows of <= 1024 entries (duplicate ids: the general (col, w)
+// sort up to WAVE_CAP), longer ones to next_list (the block kernel).
+template <int NRMAX>
 __global__ __launch_bounds__(256) void k_row_sort_wave(const int64_t *__restrict__ offs,
                                                        int64_t n, int sym,
                                                        int32_t *__restrict__ col,
@@ -242,18 +402,33 @@ __global__ __launch_bounds__(256) void k_row_sort_wave(const int64_t *__restrict
                                                        int32_t *__restrict__ kept,
                                                        double *__restrict__ deg64,
                                                        float *__restrict__ deg32,
-                                                       int32_t *__restrict__ big_list,
-                                                       int *__restrict__ big_count) {
+                                                       int32_t *__restrict__ next_list,
+                                                       int *__restrict__ next_count,
+                                                       const int32_t *__restrict__ list,
+                                                       const int *__restrict__ list_n) {
     const int lane = threadIdx.x & 63;
-    const int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-    if (i >= n) return;
-    const int64_t o = offs[i];
-    const int m = (int)(offs[i + 1] - o);
-    if (m <= 64) row_sort_fold<1>(i, o, m, sym, col, wt, uniq, kept, deg64, deg32);
-    else if (m <= 128) row_sort_fold<2>(i, o, m, sym, col, wt, uniq, kept, deg64, deg32);
-    else if (m <= 256) row_sort_fold<4>(i, o, m, sym, col, wt, uniq, kept, deg64, deg32);
-    else if (m <= WAVE_CAP) row_sort_fold<8>(i, o, m, sym, col, wt, uniq, kept, deg64, deg32);
-    else if (lane == 0) big_list[atomicAdd(big_count, 1)] = (int32_t)i;
+    const int64_t wv = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
+    const int64_t nrows = list ? (int64_t)*list_n : n;
+    for (int64_t x = wv; x < nrows; x += nw) {
+        const int64_t i = list ? (int64_t)list[x] : x;
+        const int64_t o = offs[i];
+        const int m = (int)(offs[i + 1] - o);
+        auto keyf = [&](int e) {
+            const int c = col[o + e];
+            return c == EMPTY ? SENT : (((uint64_t)(uint32_t)c << 32) | (uint32_t)e);
+        };
+        auto wf = [&](uint32_t e) { return wt[o + e]; };
+        const int rc = packed_row_any<NRMAX>(keyf, wf, m, i, o, sym, col, wt, uniq, kept, deg64,
+                                             deg32);
+        if (rc == 1) continue;
+        if constexpr (NRMAX >= 16) {
+            if (rc == 0 && row_sort_fold_any(i, o, m, sym, col, wt, o, col, wt, uniq, kept, deg64,
+                                             deg32))
+                continue;
+        }
+        if (lane == 0) next_list[atomicAdd(next_count, 1)] = (int32_t)i;
+    }
 }
 
 // one 1024-thread block per row with WAVE_CAP < m <= BLOCK_CAP (bitonic in LDS)
@@ -335,17 +510,32 @@ __global__ __launch_bounds__(1024) void k_row_sort_block(const int64_t *__restri
             col[o + q] = sm.c[sm.flag[q]];
             wt[o + q] = sm.w[sm.flag[q]];
         }
-        if (threadIdx.x == 0) {
-            uniq[i] = base;
-            if (sym == MN_SYM_UNION) {
-                double s = -0.0;
-                for (int q = 0; q < base; ++q) s = s + sm.w[sm.flag[q]];
-                deg64[i] = s;
-                kept[i] = base + 1;
-            } else {
-                float s = 0.0f;
-                for (int q = 0; q < base; ++q) s = s + (float)sm.w[sm.flag[q]];
-                deg32[i] = s;
+        // the ascending-column fold: wave 0 loads 64 kept weights at a time
+        // (parallel LDS gathers) and chains them through v_readlane, so the
+        // chain waits on the add latency, not on two dependent LDS reads
+        if (threadIdx.x < 64) {
+            const int lane = threadIdx.x;
+            double s64 = -0.0;
+            float s32 = 0.0f;
+            double nx = lane < base ? sm.w[sm.flag[lane]] : 0.0;
+            for (int c0 = 0; c0 < base; c0 += 64) {
+                const double v = nx;
+                const int e = c0 + 64 + lane;
+                nx = e < base ? sm.w[sm.flag[e]] : 0.0;
+                const int cnt = min(64, base - c0);
+                if (sym == MN_SYM_UNION)
+                    for (int l = 0; l < cnt; ++l) s64 = s64 + readlane_f64(v, l);
+                else
+                    for (int l = 0; l < cnt; ++l) s32 = s32 + (float)readlane_f64(v, l);
+            }
+            if (lane == 0) {
+                uniq[i] = base;
+                if (sym == MN_SYM_UNION) {
+                    deg64[i] = s64;
+                    kept[i] = base + 1;
+                } else {
+                    deg32[i] = s32;
+                }
             }
         }
         __syncthreads();
@@ -538,6 +728,225 @@ __global__ __launch_bounds__(1024) void k_row_sort_hub(const int64_t *__restrict
     }
 }
 
+// ---- bucketed assembly (default) -------------------------------------------
+// The transpose of the kNN rows without global atomics: destination rows are
+// grouped in buckets of BR rows; every reverse entry (j <- i) is written once
+// into its bucket's contiguous region (runs per (slot block, bucket) placed
+// by a 2-D count/scan, ranks inside a slot block from LDS atomics), then one
+// block per bucket stages its rows' forward slots + reverse entries in LDS
+// (counting sort by row), sorts / dedupes / folds each row there and writes
+// the rows' kept entries to their segments.  Rows longer than WAVE_CAP, and
+// every row of a bucket that does not fit the LDS stage (hub rows), go to the
+// global-memory kernels above.
+constexpr int BSH = 6, BR = 1 << BSH;  // rows per bucket
+constexpr int ACH = 65536;             // slots per counting block
+constexpr int ANT = 1024;
+constexpr int NBMAX = 16384;           // buckets (LDS counters of the slot blocks)
+
+__global__ __launch_bounds__(ANT) void k_lap_bhist(const int32_t *__restrict__ nbr,
+                                                   const void *__restrict__ val, int val_f64,
+                                                   int64_t n, int k, Params P, int NB,
+                                                   int32_t *__restrict__ cnt,
+                                                   int *__restrict__ bad) {
+    __shared__ int h[NBMAX];
+    const int b = blockIdx.x, t = threadIdx.x;
+    for (int q = t; q < NB; q += ANT) h[q] = 0;
+    __syncthreads();
+    const int64_t s0 = (int64_t)b * ACH, s1 = min(n * k, s0 + ACH);
+    bool anybad = false;
+    for (int64_t sl = s0 + t; sl < s1; sl += ANT) {
+        int32_t j;
+        double w;
+        bool bd;
+        if (slot_edge(nbr, val, val_f64, n, sl / k, sl, P, j, w, bd)) atomicAdd(&h[j >> BSH], 1);
+        anybad |= bd;
+    }
+    if (anybad) atomicOr(bad, 1);
+    __syncthreads();
+    for (int q = t; q < NB; q += ANT) cnt[(int64_t)b * NB + q] = h[q];
+}
+
+// per bucket: exclusive prefix over the slot blocks (in place) and the
+// total; one wave per bucket, 64 slot blocks per step
+__global__ __launch_bounds__(256) void k_lap_bscan(int32_t *__restrict__ cnt, int nA, int NB,
+                                                   int32_t *__restrict__ tot) {
+    const int q = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, lane = threadIdx.x & 63;
+    if (q >= NB) return;
+    int carry = 0;
+    for (int b0 = 0; b0 < nA; b0 += 64) {
+        const int b = b0 + lane;
+        const int v = b < nA ? cnt[(int64_t)b * NB + q] : 0;
+        int x = v;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int y = __shfl_up(x, o);
+            if (lane >= o) x += y;
+        }
+        if (b < nA) cnt[(int64_t)b * NB + q] = carry + x - v;
+        carry += __shfl(x, 63);
+    }
+    if (lane == 0) tot[q] = carry;
+}
+
+// reverse entry record: source row, destination row within its bucket, weight
+__global__ __launch_bounds__(ANT) void k_lap_bscatter(const int32_t *__restrict__ nbr,
+                                                      const void *__restrict__ val, int val_f64,
+                                                      int64_t n, int k, Params P, int NB,
+                                                      const int32_t *__restrict__ off,
+                                                      const int64_t *__restrict__ bstart,
+                                                      int4 *__restrict__ rec) {
+    __shared__ int pos[NBMAX];
+    const int b = blockIdx.x, t = threadIdx.x;
+    for (int q = t; q < NB; q += ANT) pos[q] = (int)bstart[q] + off[(int64_t)b * NB + q];
+    __syncthreads();
+    const int64_t s0 = (int64_t)b * ACH, s1 = min(n * k, s0 + ACH);
+    for (int64_t sl = s0 + t; sl < s1; sl += ANT) {
+        int32_t j;
+        double w;
+        bool bd;
+        const int64_t i = sl / k;
+        if (slot_edge(nbr, val, val_f64, n, i, sl, P, j, w, bd)) {
+            const int p = atomicAdd(&pos[j >> BSH], 1);
+            const long long wb = __double_as_longlong(w);
+            rec[p] = make_int4((int)i, j & (BR - 1), (int)(wb & 0xFFFFFFFFll), (int)(wb >> 32));
+        }
+    }
+}
+
+// Bucket stage: packed sort keys (column << 32 | entry index) — the weights
+// stay where they are (forward: recomputed from the slot, reverse: the
+// record) and are gathered only for the kept entries, so a bucket is 8 B per
+// entry of LDS and two buckets share a CU.  Entry index e < BR k: forward
+// slot e of the bucket; else reverse record e0 + e - BR k.
+constexpr int BT = 512;        // threads per bucket block
+constexpr int BKEYS = 8192;    // LDS-staged entries per bucket
+
+struct alignas(16) BucketSmem {
+    uint64_t key[BKEYS];
+    int rlen[BR];
+    int roff[BR + 1];
+    int rfill[BR];
+    int nbig;
+    int big[BR];
+};
+
+__device__ __forceinline__ double bucket_w(uint32_t e, int64_t row0, int k, int64_t e0,
+                                           const int32_t *__restrict__ nbr,
+                                           const void *__restrict__ val, int val_f64, int64_t n,
+                                           const Params &P, const int4 *__restrict__ rec) {
+    if (e < (uint32_t)(BR * k)) {
+        const int64_t i = row0 + e / k, sl = row0 * k + e;
+        int32_t j;
+        double w;
+        bool bd;
+        slot_edge(nbr, val, val_f64, n, i, sl, P, j, w, bd);
+        return w;
+    }
+    const int4 rc = rec[e0 + (e - (uint32_t)(BR * k))];
+    return __longlong_as_double(((long long)rc.w << 32) | (long long)(unsigned)rc.z);
+}
+
+// one block per bucket of BR rows; offs (the rows' segment starts, int64) is
+// written here: segment = k forward slots + the reverse entries, bucket
+// regions in bucket order.  Kept entries go to the segment starts (the
+// layout k_write_csr reads).
+__global__ __launch_bounds__(BT) __attribute__((amdgpu_waves_per_eu(4))) void k_lap_bucket(
+    const int32_t *__restrict__ nbr, const void *__restrict__ val, int val_f64, int64_t n, int k,
+    Params P, const int64_t *__restrict__ bstart, const int4 *__restrict__ rec,
+    int64_t *__restrict__ offs, int32_t *__restrict__ col, double *__restrict__ wt,
+    int32_t *__restrict__ uniq, int32_t *__restrict__ kept, double *__restrict__ deg64,
+    float *__restrict__ deg32, int32_t *__restrict__ wave_list, int *__restrict__ wave_count,
+    int32_t *__restrict__ mid_list, int *__restrict__ mid_count) {
+    __shared__ BucketSmem sm;
+    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    const int64_t row0 = (int64_t)blockIdx.x * BR;
+    const int nr = (int)min((int64_t)BR, n - row0);
+    const int64_t e0 = bstart[blockIdx.x], e1 = bstart[blockIdx.x + 1];
+    const int64_t gbase = row0 * k + e0;
+    if (t < BR) {
+        sm.rlen[t] = 0;
+        sm.rfill[t] = 0;
+    }
+    if (t == 0) sm.nbig = 0;
+    __syncthreads();
+    for (int64_t e = e0 + t; e < e1; e += BT) atomicAdd(&sm.rlen[rec[e].y], 1);
+    __syncthreads();
+    if (t < 64) {  // exclusive scan of the BR = 64 segment lengths
+        const int a = lane < nr ? k + sm.rlen[lane] : 0;
+        int x = a;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int y = __shfl_up(x, o);
+            if (lane >= o) x += y;
+        }
+        sm.roff[lane] = x - a;
+        if (lane == 63) sm.roff[BR] = x;
+        if (lane < nr) offs[row0 + lane] = gbase + x - a;
+        if (lane == 63 && row0 + nr == n) offs[n] = gbase + x;
+    }
+    __syncthreads();
+    const int m = sm.roff[BR];
+    const bool staged = m <= BKEYS;
+    for (int e = t; e < nr * k; e += BT) {
+        const int r = e / k, q = e - r * k;
+        const int64_t i = row0 + r, sl = i * k + q;
+        int32_t j;
+        double w;
+        bool bd;
+        const bool ok = slot_edge(nbr, val, val_f64, n, i, sl, P, j, w, bd);
+        const int p = sm.roff[r] + q;
+        if (staged) {
+            sm.key[p] = ok ? (((uint64_t)(uint32_t)j << 32) | (uint32_t)e) : SENT;
+        } else {
+            col[gbase + p] = ok ? j : EMPTY;
+            wt[gbase + p] = w;
+        }
+    }
+    for (int64_t e = e0 + t; e < e1; e += BT) {
+        const int4 rc = rec[e];
+        const int p = sm.roff[rc.y] + k + atomicAdd(&sm.rfill[rc.y], 1);
+        if (staged) {
+            sm.key[p] = ((uint64_t)(uint32_t)rc.x << 32) | (uint32_t)(BR * k + (e - e0));
+        } else {
+            col[gbase + p] = rc.x;
+            wt[gbase + p] = __longlong_as_double(((long long)rc.w << 32) |
+                                                 (long long)(unsigned)rc.z);
+        }
+    }
+    __syncthreads();
+    auto raw_out = [&](int r) {  // the row's raw segment for the general path
+        const int o = sm.roff[r], mr = sm.roff[r + 1] - o;
+        for (int e = lane; e < mr; e += 64) {
+            const uint64_t x = sm.key[o + e];
+            col[gbase + o + e] = x == SENT ? EMPTY : (int)(x >> 32);
+            wt[gbase + o + e] = x == SENT ? 0.0
+                                          : bucket_w((uint32_t)x, row0, k, e0, nbr, val, val_f64,
+                                                     n, P, rec);
+        }
+    };
+    for (int r = wv; r < nr; r += BT / 64) {
+        const int64_t i = row0 + r;
+        const int o = sm.roff[r], mr = sm.roff[r + 1] - o;
+        if (!staged) {  // sorted from global memory by the list kernels
+            if (lane == 0) {
+                if (mr <= 256) wave_list[atomicAdd(wave_count, 1)] = (int32_t)i;
+                else mid_list[atomicAdd(mid_count, 1)] = (int32_t)i;
+            }
+            continue;
+        }
+        auto keyf = [&](int e) { return sm.key[o + e]; };
+        auto wf = [&](uint32_t e) {
+            return bucket_w(e, row0, k, e0, nbr, val, val_f64, n, P, rec);
+        };
+        const int rc = packed_row_any<4>(keyf, wf, mr, i, gbase + o, P.sym, col, wt, uniq, kept,
+                                         deg64, deg32);
+        if (rc != 1) {  // longer rows / duplicate ids: the wave kernel <16> from global
+            raw_out(r);
+            if (lane == 0) mid_list[atomicAdd(mid_count, 1)] = (int32_t)i;
+        }
+    }
+}
+
 // ---- MAX: kept counts; CSR write ------------------------------------------
 
 __device__ __forceinline__ float max_offdiag(float w, float di, float dj, int normalize) {
@@ -690,7 +1099,7 @@ static int laplacian_impl(const int32_t *nbr, const void *val, int32_t val_f64, 
                                                ((size_t)n / scan::SB + 2) * 8);
     char *g2 = (char *)scratch(kSlotGeneric2, (size_t)(2 * nk + 1) * 12 + 64);
     int *flags = (int *)scratch(kSlotFlags, 64);
-    int32_t *lists = (int32_t *)scratch(kSlotGeneric3, (size_t)n * 8 + 64);
+    int32_t *lists = (int32_t *)scratch(kSlotGeneric3, (size_t)n * 12 + 64);
     MN_REQUIRE(g1 && g2 && flags && lists, MN_ENOMEM,
                "mn_laplacian_from_knn: scratch allocation failed");
     int32_t *indeg = (int32_t *)g1;
@@ -703,7 +1112,7 @@ static int laplacian_impl(const int32_t *nbr, const void *val, int32_t val_f64, 
     const int64_t E2 = 2 * nk;
     int32_t *col = (int32_t *)g2;
     double *wt = (double *)(g2 + (((size_t)E2 * 4 + 15) & ~(size_t)15));
-    int32_t *big_list = lists, *huge_list = lists + n;
+    int32_t *big_list = lists, *huge_list = lists + n, *mid_list = lists + 2 * n;
     // degrees (into degrees_out when given, else scratch)
     void *degbuf = degrees_out;
     if (!degbuf) {
@@ -713,20 +1122,58 @@ static int laplacian_impl(const int32_t *nbr, const void *val, int32_t val_f64, 
     double *deg64 = P.sym == MN_SYM_UNION ? (double *)degbuf : nullptr;
     float *deg32 = P.sym == MN_SYM_UNION ? nullptr : (float *)degbuf;
 
+    // bucketed assembly (MN_LAP_V1=1: the atomic counting-sort path, A/B)
+    const int64_t NB = (n + BR - 1) / BR;
+    const int64_t nA = (nk + ACH - 1) / ACH;
+    const char *v1e = getenv("MN_LAP_V1");
+    const bool v2 = k > 0 && NB <= NBMAX && nk < INT_MAX && !(v1e && *v1e == '1');
+    char *g0 = nullptr;
+    if (v2) {
+        g0 = (char *)scratch(kSlotGeneric0, (size_t)nk * 16 + (size_t)nA * NB * 4 +
+                                                (size_t)NB * 4 + (size_t)(NB + 1) * 8 + 1024);
+        MN_REQUIRE(g0, MN_ENOMEM, "mn_laplacian_from_knn: scratch allocation failed");
+    }
+
     Timer tm;
     tm.start(true, s);
     MN_HIP_TRY(hipMemsetAsync(indeg, 0, (size_t)n * 4 * 5, s));
-    MN_HIP_TRY(hipMemsetAsync(flags, 0, 16, s));
-    if (k > 0)
-        hipLaunchKernelGGL(k_lap_slots, dim3(grid_for(nk)), dim3(256), 0, s, nbr, val, val_f64, n,
-                           k, P, indeg, flags);
-    hipLaunchKernelGGL(k_seg_len, dim3(grid_for(n)), dim3(256), 0, s, indeg, n, k, seg);
-    MN_HIP_TRY(scan::exclusive_scan(seg, n, offs, part, s));
-    if (k > 0)
-        hipLaunchKernelGGL(k_lap_scatter, dim3(grid_for(nk)), dim3(256), 0, s, nbr, val, val_f64,
-                           n, k, P, offs, fill, col, wt);
-    hipLaunchKernelGGL(k_row_sort_wave, dim3(grid_for(n * 64)), dim3(256), 0, s, offs, n, P.sym,
-                       col, wt, uniq, kept, deg64, deg32, big_list, flags + 1);
+    MN_HIP_TRY(hipMemsetAsync(flags, 0, 32, s));  // [1] big [2] hub [3] wave [4] mid lists
+    if (v2) {
+        int4 *rec = (int4 *)g0;
+        int32_t *cnt = (int32_t *)(g0 + (size_t)nk * 16);
+        int32_t *tot = cnt + (size_t)nA * NB;
+        int64_t *bstart = (int64_t *)(((uintptr_t)(tot + NB) + 15) & ~(uintptr_t)15);
+        int32_t *wave_list = huge_list;  // reused: the hub list is filled after the wave pass
+        hipLaunchKernelGGL(k_lap_bhist, dim3((unsigned)nA), dim3(ANT), 0, s, nbr, val, val_f64, n,
+                           k, P, (int)NB, cnt, flags);
+        hipLaunchKernelGGL(k_lap_bscan, dim3(grid_for(NB * 64)), dim3(256), 0, s, cnt, (int)nA,
+                           (int)NB, tot);
+        MN_HIP_TRY(scan::exclusive_scan(tot, NB, bstart, part, s));
+        hipLaunchKernelGGL(k_lap_bscatter, dim3((unsigned)nA), dim3(ANT), 0, s, nbr, val, val_f64,
+                           n, k, P, (int)NB, cnt, bstart, rec);
+        hipLaunchKernelGGL(k_lap_bucket, dim3((unsigned)NB), dim3(BT), 0, s, nbr, val, val_f64, n,
+                           k, P, bstart, rec, offs, col, wt, uniq, kept, deg64, deg32, wave_list,
+                           flags + 3, mid_list, flags + 4);
+        MN_KCHECK(s, "k_lap_bucket");
+        // rows of buckets too large for the LDS stage (hub buckets)
+        hipLaunchKernelGGL(k_row_sort_wave<4>, dim3(256), dim3(256), 0, s, offs, n, P.sym, col, wt,
+                           uniq, kept, deg64, deg32, mid_list, flags + 4, wave_list, flags + 3);
+    } else {
+        if (k > 0)
+            hipLaunchKernelGGL(k_lap_slots, dim3(grid_for(nk)), dim3(256), 0, s, nbr, val, val_f64,
+                               n, k, P, indeg, flags);
+        hipLaunchKernelGGL(k_seg_len, dim3(grid_for(n)), dim3(256), 0, s, indeg, n, k, seg);
+        MN_HIP_TRY(scan::exclusive_scan(seg, n, offs, part, s));
+        if (k > 0)
+            hipLaunchKernelGGL(k_lap_scatter, dim3(grid_for(nk)), dim3(256), 0, s, nbr, val,
+                               val_f64, n, k, P, offs, fill, col, wt);
+        hipLaunchKernelGGL(k_row_sort_wave<4>, dim3(grid_for(n * 64)), dim3(256), 0, s, offs, n,
+                           P.sym, col, wt, uniq, kept, deg64, deg32, mid_list, flags + 4,
+                           (const int32_t *)nullptr, (const int *)nullptr);
+    }
+    // rows of 257..1024 entries (one wave, 16 keys a lane), then longer ones
+    hipLaunchKernelGGL(k_row_sort_wave<16>, dim3(1024), dim3(256), 0, s, offs, n, P.sym, col, wt,
+                       uniq, kept, deg64, deg32, big_list, flags + 1, mid_list, flags + 4);
     hipLaunchKernelGGL(k_row_sort_block, dim3(256), dim3(1024), 0, s, offs, big_list, flags + 1,
                        P.sym, col, wt, uniq, kept, deg64, deg32, huge_list, flags + 2);
     hipLaunchKernelGGL(k_row_sort_hub, dim3(64), dim3(1024), 0, s, offs, huge_list, flags + 2,
@@ -757,11 +1204,11 @@ static int laplacian_impl(const int32_t *nbr, const void *val, int32_t val_f64, 
     MN_HIP_TRY(hipGetLastError());
     tm.mark();
     int64_t nnz = 0;
-    int hf[4] = {0, 0, 0, 0};
+    int hf[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     MN_HIP_TRY(hipMemcpyAsync(&nnz, indptr + n, 8, hipMemcpyDeviceToHost, s));
-    MN_HIP_TRY(hipMemcpyAsync(hf, flags, 16, hipMemcpyDeviceToHost, s));
+    MN_HIP_TRY(hipMemcpyAsync(hf, flags, 32, hipMemcpyDeviceToHost, s));
     MN_HIP_TRY(hipStreamSynchronize(s));
-    t_lap_stats.big_rows = hf[1];
+    t_lap_stats.big_rows = hf[4];  // rows past the one-wave 256-entry sort
     t_lap_stats.hub_rows = hf[2];
     if (hf[0] != 0) {  // out-of-range neighbour ids were skipped everywhere; outputs void
         if (!caller) { (void)hipFree(indptr); (void)hipFree(ocol); (void)hipFree(oval); }

@@ -31,6 +31,25 @@ hist = {f"<={edges[i + 1]}": int(((seg > edges[i]) & (seg <= edges[i + 1])).sum(
 big = seg[seg > 512]
 print(json.dumps({"seg_hist": hist, "entries_in_rows_gt512": int(big.sum()),
                   "max_seg": int(seg.max())}), flush=True)
+# A/B: the bucketed assembly (default) vs the atomic counting-sort path
+# (MN_LAP_V1=1): identical CSR and degrees, and both timings
+outs = {}
+for v in ("1", "0", "1", "0"):
+    os.environ["MN_LAP_V1"] = v
+    L, deg = S.build_laplacian_from_knn(r.idx, r.dist, weight_kernel="rational",
+                                        symmetrise="union", eps=float("inf"), sigma=1.0, p=2.0)
+    torch.cuda.synchronize()
+    st = S.laplacian.last_stats()
+    outs[v] = (L, deg)
+    print(json.dumps({"MN_LAP_V1": v, "lib_ms": round(st["ms_total"], 3), "nnz": L.nnz,
+                      "big_rows": st["big_rows"], "hub_rows": st["hub_rows"]}), flush=True)
+(a, da), (b, db) = outs["1"], outs["0"]
+same = (a.nnz == b.nnz and torch.equal(a.indptr, b.indptr) and torch.equal(a.indices, b.indices)
+        and torch.equal(a.values.view(torch.int64), b.values.view(torch.int64))
+        and torch.equal(da.view(torch.int64), db.view(torch.int64)))
+print(json.dumps({"v1_v2_identical": bool(same)}), flush=True)
+del outs, a, b, da, db
+os.environ.pop("MN_LAP_V1")
 for rep in range(6):
     t0 = time.perf_counter()
     L, _ = S.build_laplacian_from_knn(r.idx, r.dist, weight_kernel="rational", symmetrise="union",
