@@ -31,6 +31,7 @@
 //                       recomputed by an exact brute-force scan.
 #include <algorithm>
 #include <climits>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <vector>
@@ -1066,10 +1067,11 @@ __global__ __launch_bounds__(256) void k_tau_x1(int64_t nq, int S1, const float 
         float T = __builtin_inff();
         for (int s = 0; s < S1; ++s) T = fminf(T, btau1[q * S1 + s]);
         const float qn = nq_f[q];
+        const double Tf = __builtin_isfinite(T) ? __builtin_fabs((double)T) : 0.0;
+        const float dl = delta_x1(Tf, qn, hn_q[q], rn_q[q], cmax, d, dp);
         tau0[q] = T;
         tq[q] = (T - qn) * 0.5f;
-        const double Tf = __builtin_isfinite(T) ? __builtin_fabs((double)T) : 0.0;
-        delta[q] = delta_x1(Tf, qn, hn_q[q], rn_q[q], cmax, d, dp);
+        delta[q] = dl;
         if (__builtin_isfinite(T)) tb = __float_as_uint(__builtin_fabsf(T));
     }
     if (tmax) wave_atomic_umax(tmax, tb);  // every lane of the wave takes part
@@ -1133,7 +1135,8 @@ __global__ __launch_bounds__(64 * WPB) void k_rerank_x1(
     const int *__restrict__ qlist, const int *__restrict__ qlist_n, int *__restrict__ big_count,
     int *__restrict__ big_list, const int *__restrict__ perm, int64_t q_off, int excl,
     const int *__restrict__ qmap, float *__restrict__ ub, int32_t *__restrict__ out_idx,
-    float *__restrict__ out_dist, int *__restrict__ fb_count, int *__restrict__ fb_list) {
+    float *__restrict__ out_dist, int *__restrict__ fb_count, int *__restrict__ fb_list,
+    int *__restrict__ why = nullptr) {
     __shared__ int cand[WPB][64 * NR];
     __shared__ float candk[WPB][64 * NR];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -1144,6 +1147,7 @@ __global__ __launch_bounds__(64 * WPB) void k_rerank_x1(
     const int64_t qo = qmap ? (int64_t)qmap[q] : q;
     const float T = tau0[q];
     bool forced = T == -__builtin_inff();
+    int ovf = 0;  // diagnostics (why != NULL): a buffer overflowed
     int M = 0;
     // ids are positions in the visiting order: map them back (c_off +
     // perm[p]); the generators ran without exclusion, so the query's own row
@@ -1169,6 +1173,7 @@ __global__ __launch_bounds__(64 * WPB) void k_rerank_x1(
     for (int j = 0; j < S2; ++j) {
         int c = cnt2[q * S2 + j];
         forced |= c < 0 || c > cap2;  // -1: overflow; SW_SYM: a count past cap
+        ovf |= (c < 0 || c > cap2) ? 1 : 0;
         c = min(c, cap2);
         if (c > 0) gather(buf2 + (q * S2 + j) * (int64_t)cap2, c, false);
     }
@@ -1222,6 +1227,11 @@ __global__ __launch_bounds__(64 * WPB) void k_rerank_x1(
     const int kneed = (int)min((int64_t)k, nvalid_max);
     if (cert && T < __builtin_inff() && keff < kneed) cert = false;
     if (!cert) {
+        if (why && lane == 0) {  // reason counters (MN_X1_DEBUG)
+            const int rsn = ovf ? 0 : M > 64 * NR ? 1 : T == -__builtin_inff() ? 2
+                          : !(T < __builtin_inff()) ? 3 : keff < kneed ? 4 : 5;
+            atomicAdd(&why[rsn], 1);
+        }
         if (ub) {
             // any k exact candidate distances bound D_k from above (the refill)
             const float b = (kneed > 0 && keff >= kneed) ? wave_elem<NR>(dd, kneed - 1)
@@ -1422,10 +1432,11 @@ __global__ __launch_bounds__(FB_THREADS) void k_fallback(
 // the part's survivors — dist <= ub[row] (an exact upper bound of D_k from
 // the re-rank, +inf when none) — and writes the part's best keff by (dist,
 // id).  k_fb_merge then reduces groups of part lists to one list per row.
-constexpr int FSQ = 8;      // rows per launch
-constexpr int FSC = 1024;   // corpus rows per part (one sort of <= FSC survivors)
-constexpr int FST = 256;    // threads
+constexpr int FSQ = 16;     // rows per launch (LDS: FSQ d floats + the part's distances)
+constexpr int FSC = 1024;   // corpus rows per part (one per thread; one sort of <= FSC survivors)
+constexpr int FST = 1024;   // threads
 constexpr int FMG = 4096;   // merge: entries per group (sorted in LDS)
+constexpr int FMT = 256;    // merge threads
 
 __device__ __forceinline__ void lds_bitonic(float *kd, int *ki, int P) {
     for (int kk = 2; kk <= P; kk <<= 1)
@@ -1446,73 +1457,82 @@ __device__ __forceinline__ void lds_bitonic(float *kd, int *ki, int P) {
         }
 }
 
+// One corpus row per thread (FSC = FST, 16 waves): the row's 16-feature
+// pieces are loaded whole (4 float4, one 64-B segment) right before use, so
+// no lane relies on L1 keeping its row; the batch's query values are staged
+// feature-major in LDS (Qt [d][FSQ]: one broadcast ds_read_b128 per 4
+// queries and feature).  (Whole rows per lane with 4 waves per CU ran 13-20
+// ms per batch at 1M x 768; scalar-loaded queries spilled SGPRs, 9.7 ms.)
 template <bool VEC4, bool SQRT>
 __global__ __launch_bounds__(FST) void k_fb_part(
-    const float *__restrict__ Q, const float *__restrict__ C, int64_t nc, int d, int64_t q_off,
+    const float *__restrict__ Qt, const float *__restrict__ C, int64_t nc, int d, int64_t q_off,
     int64_t c_off, int excl, int keff_max, const int *__restrict__ rows, int nb,
     const float *__restrict__ ub, int64_t chunk, float2 *__restrict__ plist,
     int *__restrict__ pcnt) {
-    extern __shared__ float fsm[];
-    float *qs = fsm;                                // [nb][d]
-    float *dv = qs + (size_t)nb * d;                // [nb][FSC]
-    float *sd = dv + (size_t)nb * FSC;              // [FSC] sort keys
-    int *si = (int *)(sd + FSC);                    // [FSC] sort ids
-    int *scnt = si + FSC;
+    extern __shared__ float4 fsm4[];
+    float4 *qs = fsm4;                              // [d][FSQ / 4]: Qt staged
+    float *dv = (float *)(qs + (size_t)d * (FSQ / 4));  // [FSQ][FSC]
+    float *sd = dv + FSQ * FSC;                     // [FSC]
+    int *si = (int *)(sd + FSC);                    // [FSC]
+    int &scnt = si[FSC];
     const int P = gridDim.x, b = blockIdx.x, t = threadIdx.x;
     const int64_t c0 = (int64_t)b * chunk, c1 = min(nc, c0 + chunk);
-    for (int e = t; e < nb * d; e += FST) qs[e] = Q[(int64_t)rows[e / d] * d + (e % d)];
+    const int64_t c = c0 + t;
+    for (int e = t; e < d * (FSQ / 4); e += FST) qs[e] = reinterpret_cast<const float4 *>(Qt)[e];
     __syncthreads();
-    for (int64_t c = c0 + t; c < c1; c += FST) {
+    if (c < c1) {
         const float *crow = C + c * (int64_t)d;
         float acc[FSQ];
 #pragma unroll
         for (int r = 0; r < FSQ; ++r) acc[r] = -0.0f;
-        if (VEC4) {
-            for (int f = 0; f < d; f += 4) {
-                const float4 y = *reinterpret_cast<const float4 *>(crow + f);
+        auto step = [&](float y, int f) {
+            const float4 *qf = qs + (size_t)f * (FSQ / 4);  // LDS broadcast reads
 #pragma unroll
-                for (int r = 0; r < FSQ; ++r) {
-                    if (r < nb) {
-                        const float4 x = *reinterpret_cast<const float4 *>(qs + r * d + f);
-                        float df = x.x - y.x; acc[r] = acc[r] + df * df;
-                        df = x.y - y.y; acc[r] = acc[r] + df * df;
-                        df = x.z - y.z; acc[r] = acc[r] + df * df;
-                        df = x.w - y.w; acc[r] = acc[r] + df * df;
-                    }
-                }
+            for (int r4 = 0; r4 < FSQ / 4; ++r4) {
+                const float4 q4 = qf[r4];
+                float df = q4.x - y; acc[4 * r4 + 0] = acc[4 * r4 + 0] + df * df;
+                df = q4.y - y; acc[4 * r4 + 1] = acc[4 * r4 + 1] + df * df;
+                df = q4.z - y; acc[4 * r4 + 2] = acc[4 * r4 + 2] + df * df;
+                df = q4.w - y; acc[4 * r4 + 3] = acc[4 * r4 + 3] + df * df;
+            }
+        };
+        if (VEC4) {
+            int f = 0;
+            for (; f + 16 <= d; f += 16) {
+                const float4 *p4 = reinterpret_cast<const float4 *>(crow + f);
+                const float4 v0 = p4[0], v1 = p4[1], v2 = p4[2], v3 = p4[3];
+                step(v0.x, f); step(v0.y, f + 1); step(v0.z, f + 2); step(v0.w, f + 3);
+                step(v1.x, f + 4); step(v1.y, f + 5); step(v1.z, f + 6); step(v1.w, f + 7);
+                step(v2.x, f + 8); step(v2.y, f + 9); step(v2.z, f + 10); step(v2.w, f + 11);
+                step(v3.x, f + 12); step(v3.y, f + 13); step(v3.z, f + 14); step(v3.w, f + 15);
+            }
+            for (; f < d; f += 4) {
+                const float4 v = *reinterpret_cast<const float4 *>(crow + f);
+                step(v.x, f); step(v.y, f + 1); step(v.z, f + 2); step(v.w, f + 3);
             }
         } else {
-            for (int f = 0; f < d; ++f) {
-                const float y = crow[f];
-#pragma unroll
-                for (int r = 0; r < FSQ; ++r)
-                    if (r < nb) {
-                        const float df = qs[r * d + f] - y;
-                        acc[r] = acc[r] + df * df;
-                    }
-            }
+            for (int f = 0; f < d; ++f) step(crow[f], f);
         }
 #pragma unroll
-        for (int r = 0; r < FSQ; ++r)
-            if (r < nb) dv[r * FSC + (c - c0)] = SQRT ? sqrt_rn_f32(acc[r]) : acc[r];
+        for (int r = 0; r < FSQ; ++r) dv[r * FSC + t] = SQRT ? sqrt_rn_f32(acc[r]) : acc[r];
     }
     __syncthreads();
     for (int r = 0; r < nb; ++r) {
         const int64_t q = rows[r], gq = q_off + q;
         const float u = ub ? ub[q] : __builtin_inff();
-        if (t == 0) *scnt = 0;
+        if (t == 0) scnt = 0;
         __syncthreads();
-        for (int64_t c = c0 + t; c < c1; c += FST) {
-            const float dist = dv[r * FSC + (c - c0)];
+        if (c < c1) {
+            const float dist = dv[r * FSC + t];
             const int64_t gj = c_off + c;
             if (!(excl && gj == gq) && dist <= u) {
-                const int p = atomicAdd(scnt, 1);
+                const int p = atomicAdd(&scnt, 1);
                 sd[p] = dist;
                 si[p] = (int)gj;
             }
         }
         __syncthreads();
-        const int m = *scnt;
+        const int m = scnt;
         int keep = m;
         if (m > keff_max) {
             int Pw = 1;
@@ -1532,10 +1552,20 @@ __global__ __launch_bounds__(FST) void k_fb_part(
     }
 }
 
+// Qt [d][FSQ]: the batch's query rows feature-major (zero past nb)
+__global__ __launch_bounds__(256) void k_fb_qt(const float *__restrict__ Q, int d,
+                                               const int *__restrict__ rows, int nb,
+                                               float *__restrict__ Qt) {
+    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= (int64_t)d * FSQ) return;
+    const int f = (int)(e / FSQ), r = (int)(e % FSQ);
+    Qt[e] = r < nb ? Q[(int64_t)rows[r] * d + f] : 0.f;
+}
+
 // groups of gs part lists (<= FMG entries) of each row -> that group's best
 // keff; with one group left, the row's output (keff = min(k, valid), padded)
 template <bool FINAL>
-__global__ __launch_bounds__(FST) void k_fb_merge(
+__global__ __launch_bounds__(FMT) void k_fb_merge(
     const float2 *__restrict__ plist, const int *__restrict__ pcnt, int P, int keff_max, int gs,
     float2 *__restrict__ olist, int *__restrict__ ocnt, const int *__restrict__ rows,
     int64_t nc, int64_t q_off, int64_t c_off, int excl, int k, int32_t *__restrict__ out_idx,
@@ -1559,14 +1589,14 @@ __global__ __launch_bounds__(FST) void k_fb_merge(
     for (int p = p0; p < p1; ++p) {
         const int o = base[p - p0], n = base[p - p0 + 1] - o;
         const float2 *src = plist + ((int64_t)r * P + p) * keff_max;
-        for (int e = t; e < n; e += FST) {
+        for (int e = t; e < n; e += FMT) {
             sd[o + e] = src[e].x;
             si[o + e] = __float_as_int(src[e].y);
         }
     }
     int Pw = 1;
     while (Pw < m) Pw <<= 1;
-    for (int e = m + t; e < Pw; e += FST) {
+    for (int e = m + t; e < Pw; e += FMT) {
         sd[e] = __builtin_inff();
         si[e] = INT_MAX;
     }
@@ -1577,14 +1607,14 @@ __global__ __launch_bounds__(FST) void k_fb_merge(
         const int64_t q = rows[r], gq = q_off + q;
         const bool self_in = excl && gq >= c_off && gq < c_off + nc;
         const int keff = (int)min((int64_t)k, nc - (self_in ? 1 : 0));
-        for (int e = t; e < k; e += FST) {
+        for (int e = t; e < k; e += FMT) {
             const bool ok = e < keff && e < keep;
             out_idx[q * k + e] = ok ? si[e] : -1;
             out_dist[q * k + e] = ok ? sd[e] : __builtin_inff();
         }
     } else {
         float2 *out = olist + ((int64_t)r * G + g) * keff_max;
-        for (int e = t; e < keep; e += FST) out[e] = make_float2(sd[e], __int_as_float(si[e]));
+        for (int e = t; e < keep; e += FMT) out[e] = make_float2(sd[e], __int_as_float(si[e]));
         if (t == 0) ocnt[r * G + g] = keep;
     }
 }
@@ -1597,27 +1627,39 @@ static int fb_split_scan(const float *Q, const float *C, int64_t nc, int d, int6
                          const float *ub, bool sqrt_keys, int32_t *out_idx, float *out_dist,
                          hipStream_t s) {
     const int keff_max = k;
-    const size_t fixed = (size_t)FSC * 8 + 64;
-    const int nbm = (int)std::min<int64_t>(FSQ, (int64_t)((65536 - fixed) / ((size_t)(d + FSC) * 4)));
-    if (nbm < 1 || nc < 1 || k > KMAX) return 1;
+    const size_t ldsmax = 160 * 1024;
+    if (nc < 1 || k > KMAX || d < 1 ||
+        (size_t)d * FSQ * 4 + (size_t)FSQ * FSC * 4 + (size_t)FSC * 8 + 16 > ldsmax)
+        return 1;
+    static bool attr = false;  // dynamic LDS beyond 64 KB (once per process)
+    if (!attr) {
+        for (const void *f : {(const void *)k_fb_part<true, true>, (const void *)k_fb_part<true, false>,
+                              (const void *)k_fb_part<false, true>, (const void *)k_fb_part<false, false>})
+            MN_HIP_TRY(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ldsmax));
+        attr = true;
+    }
     const int64_t P = (nc + FSC - 1) / FSC;
-    const int64_t chunk = (nc + P - 1) / P;
+    const int64_t chunk = FSC;
     const int gs = FMG / keff_max;
-    // ping-pong part lists: [nb][P][keff] and the first merge level
-    const size_t l0 = (size_t)nbm * P * keff_max, l1 = (size_t)nbm * ((P + gs - 1) / gs) * keff_max;
+    // ping-pong part lists: [FSQ][P][keff] and the first merge level; Qt
+    const size_t l0 = (size_t)FSQ * P * keff_max, l1 = (size_t)FSQ * ((P + gs - 1) / gs) * keff_max;
     const size_t b0 = (l0 * 8 + 255) & ~(size_t)255, b1 = (l1 * 8 + 255) & ~(size_t)255;
-    const size_t c0b = ((size_t)nbm * P * 4 + 255) & ~(size_t)255;
-    char *g = (char *)scratch(kSlotX1Esc, b0 + b1 + 2 * c0b + 256);
+    const size_t c0b = ((size_t)FSQ * P * 4 + 255) & ~(size_t)255;
+    const size_t qtb = ((size_t)d * FSQ * 4 + 255) & ~(size_t)255;
+    char *g = (char *)scratch(kSlotX1Esc, b0 + b1 + 2 * c0b + qtb + 256);
     if (!g) return MN_ENOMEM;
     float2 *la = (float2 *)g, *lb = (float2 *)(g + b0);
     int *ca = (int *)(g + b0 + b1), *cb = (int *)(g + b0 + b1 + c0b);
+    float *Qt = (float *)(g + b0 + b1 + 2 * c0b);
     const bool vec4 = (d % 4 == 0) && (((uintptr_t)Q | (uintptr_t)C) % 16 == 0);
-    for (int r0 = 0; r0 < nfb; r0 += nbm) {
-        const int nb = std::min(nbm, nfb - r0);
-        const size_t lds = ((size_t)nb * (d + FSC)) * 4 + fixed;
+    for (int r0 = 0; r0 < nfb; r0 += FSQ) {
+        const int nb = std::min(FSQ, nfb - r0);
+        hipLaunchKernelGGL(k_fb_qt, dim3((unsigned)(((int64_t)d * FSQ + 255) / 256)), dim3(256), 0,
+                           s, Q, d, rows + r0, nb, Qt);
         auto kp = vec4 ? (sqrt_keys ? k_fb_part<true, true> : k_fb_part<true, false>)
                        : (sqrt_keys ? k_fb_part<false, true> : k_fb_part<false, false>);
-        hipLaunchKernelGGL(kp, dim3((unsigned)P), dim3(FST), lds, s, Q, C, nc, d, q_off, c_off,
+        const size_t lds = (size_t)d * FSQ * 4 + (size_t)FSQ * FSC * 4 + (size_t)FSC * 8 + 16;
+        hipLaunchKernelGGL(kp, dim3((unsigned)P), dim3(FST), lds, s, Qt, C, nc, d, q_off, c_off,
                            excl, keff_max, rows + r0, nb, ub, chunk, la, ca);
         MN_KCHECK(s, "k_fb_part");
         int Pl = (int)P;
@@ -1625,7 +1667,7 @@ static int fb_split_scan(const float *Q, const float *C, int64_t nc, int d, int6
         int *sc = ca, *dc = cb;
         while (Pl > gs) {
             const int G = (Pl + gs - 1) / gs;
-            hipLaunchKernelGGL(k_fb_merge<false>, dim3((unsigned)(nb * G)), dim3(FST), 0, s, src,
+            hipLaunchKernelGGL(k_fb_merge<false>, dim3((unsigned)(nb * G)), dim3(FMT), 0, s, src,
                                sc, Pl, keff_max, gs, dst, dc, rows + r0, nc, q_off, c_off, excl,
                                k, out_idx, out_dist);
             MN_KCHECK(s, "k_fb_merge");
@@ -1633,7 +1675,7 @@ static int fb_split_scan(const float *Q, const float *C, int64_t nc, int d, int6
             std::swap(sc, dc);
             Pl = G;
         }
-        hipLaunchKernelGGL(k_fb_merge<true>, dim3((unsigned)nb), dim3(FST), 0, s, src, sc, Pl,
+        hipLaunchKernelGGL(k_fb_merge<true>, dim3((unsigned)nb), dim3(FMT), 0, s, src, sc, Pl,
                            keff_max, gs, dst, dc, rows + r0, nc, q_off, c_off, excl, k, out_idx,
                            out_dist);
         MN_KCHECK(s, "k_fb_merge<final>");
@@ -2124,15 +2166,17 @@ static int knn_x1(const float *Q, int64_t nq, const float *C, int64_t nc, int32_
                                tqP, hcP, hcS, aoff, hoff, dltP);
             MN_KCHECK(s, "k_sym_pos");
             // block table: row block I against column tiles [J0, J1), J >= I,
-            // at most TPB tiles per block.  MN_SYM_ORDER 0: ranges from the
-            // diagonal, the longest first (co-resident blocks of an XCD share
-            // a row panel); 1: column ranges aligned to a TPB grid, ordered by
-            // range then row (co-resident blocks share the column stream)
+            // at most TPB tiles per block.  MN_SYM_ORDER 1 (default): column
+            // ranges aligned to a TPB grid, ordered by range then row, so the
+            // co-resident blocks of an XCD stream the same column tiles (one
+            // L2 fill serves them all; their row panels stay in the Infinity
+            // Cache): C2 sweep 775 ms; 0: ranges from the diagonal, the
+            // longest first: 984 ms (profiles/r03d_ab_sym_order.log)
             const int nbk = (int)((nc + ksw2::BC - 1) / ksw2::BC);
             const char *tpe2 = getenv("MN_SYM_TPB");
             const int TPB = (tpe2 && *tpe2) ? std::max(1, atoi(tpe2)) : 256;
             const char *ore = getenv("MN_SYM_ORDER");
-            const int order = (ore && *ore) ? atoi(ore) : 0;
+            const int order = (ore && *ore) ? atoi(ore) : 1;
             std::vector<int4> tab;
             tab.reserve((size_t)nbk * ((size_t)nbk / TPB + 2) / 2 + 16);
             if (order == 1) {
@@ -2254,11 +2298,27 @@ static int knn_x1(const float *Q, int64_t nq, const float *C, int64_t nc, int32_
     int *big_list = fb_list + nq;  // second half of the fallback-list slot
     // pass 1: up to 512 candidates per row, 4 rows per block; pass 2 (the rare
     // rows with more): up to 1024, one row per block
+    // MN_X1_DEBUG=1: why rows stay uncertified (stderr), per re-rank pass
+    const char *dbe = getenv("MN_X1_DEBUG");
+    int *why = (dbe && *dbe == '1') ? flags + 20 : nullptr;  // [20..25]
+    if (why) MN_HIP_TRY(hipMemsetAsync(why, 0, 24, s));
+    auto why_print = [&](const char *pass) {
+        if (!why) return;
+        int h[6] = {0};
+        if (hipMemcpyAsync(h, why, 24, hipMemcpyDeviceToHost, s) != hipSuccess ||
+            hipStreamSynchronize(s) != hipSuccess)
+            return;
+        fprintf(stderr,
+                "mn_knn x1 %s: uncertified by overflow %d, >1024 candidates %d, forced %d, "
+                "no threshold %d, < k candidates %d, bound %d\n",
+                pass, h[0], h[1], h[2], h[3], h[4], h[5]);
+        (void)hipMemsetAsync(why, 0, 24, s);
+    };
 #define MN_RRX(NRV, WPB, V, NB, QL, QN, BC, BL)                                                 \
     hipLaunchKernelGGL((k_rerank_x1<NRV, WPB, V>), dim3((unsigned)(NB)), dim3(64 * WPB), 0, s, \
                        Q, nq, C, d, c_off, S1r, pl.cap, cbuf1, bcnt1, tau_r, S2, cap2,          \
                        cbuf2, cnt2, dlt_r, k, nvalid, QL, QN, BC, BL, perm_r, q_off, excl,      \
-                       qmap_r, ubv, out_idx, out_dist, fb_count, fb_list)
+                       qmap_r, ubv, out_idx, out_dist, fb_count, fb_list, why)
     const int64_t nb1 = (nq + 3) / 4;
     if (vec4) MN_RRX(8, 4, true, nb1, (const int *)nullptr, (const int *)nullptr, big_count, big_list);
     else MN_RRX(8, 4, false, nb1, (const int *)nullptr, (const int *)nullptr, big_count, big_list);
@@ -2272,6 +2332,7 @@ static int knn_x1(const float *Q, int64_t nq, const float *C, int64_t nc, int32_
     }
 #undef MN_RRX
     MN_KCHECK(s, "k_rerank_x1");
+    why_print("re-rank");
     tm.mark();
     // statistics of the buffers now: an escalation below reuses (and may
     // reallocate) the scratch slots that hold them
@@ -2327,9 +2388,13 @@ static int knn_x1(const float *Q, int64_t nq, const float *C, int64_t nc, int32_
                            (int64_t)nfb, erows, ubv, qn3, qh3, ql3, q23, cmax3, d, dp, tq3, tau3,
                            dlt3);
         MN_KCHECK(s, "k_tau_x3");
-        // expected candidates per row: those within ~2 delta3 of D_k; a
-        // generous plan (an overflowing slice only costs that row's exact scan)
-        const ksw::SweepPlan p3 = ksw::plan_sweep(nfb, nc, 8.0 * (k + 16));
+        // expected candidates per row: those below ub + 1.125 delta3, where ub
+        // (the first pass's k-th exact distance) can sit up to its delta above
+        // D_k: in dense clusters several hundred rows (clustered C2: 8 (k + 16)
+        // overflowed 62.7k of 80k refilled rows); 32 (k + 16), the buffer kept
+        // within ~16 GB
+        const double ex3 = std::min(32.0 * (k + 16), 16e9 / (20.0 * (double)nfb));
+        const ksw::SweepPlan p3 = ksw::plan_sweep(nfb, nc, std::max(ex3, 8.0 * (k + 16)));
         const size_t nbuf3 = (size_t)nfb * p3.S * p3.cap;
         uint2 *cbuf3 = (uint2 *)scratch(kSlotX1Buf2, nbuf3 * sizeof(uint2) + 64);
         int *cnt3 = (int *)scratch(kSlotX1Meta2, (size_t)nfb * p3.S * 4 + 64);
@@ -2356,7 +2421,7 @@ static int knn_x1(const float *Q, int64_t nq, const float *C, int64_t nc, int32_
                        Q, (int64_t)nfb, C, d, c_off, 0, 0, (const uint2 *)nullptr,            \
                        (const int *)nullptr, tau3, (int)p3.S, p3.cap, cbuf3, cnt3, dlt3, k,    \
                        nvalid, QL, QN, BC, BL, perm_r, q_off, excl, erows, (float *)nullptr,     \
-                       out_idx, out_dist, fb_count, fb_list)
+                       out_idx, out_dist, fb_count, fb_list, why)
         const int64_t nb3 = (nfb + 3) / 4;
         if (vec4) MN_RR3(8, 4, true, nb3, (const int *)nullptr, (const int *)nullptr, big_count3, big_list3);
         else MN_RR3(8, 4, false, nb3, (const int *)nullptr, (const int *)nullptr, big_count3, big_list3);
@@ -2370,6 +2435,7 @@ static int knn_x1(const float *Q, int64_t nq, const float *C, int64_t nc, int32_
             MN_KCHECK(s, "k_rerank_x1<refill, wide>");
         }
 #undef MN_RR3
+        why_print("bf16x3 refill");
         te.mark();
         t_stats.n_escalated = nfb;
         t_stats.ms_escalate = te.ms(0, 1);
@@ -2385,10 +2451,10 @@ static int knn_x1(const float *Q, int64_t nq, const float *C, int64_t nc, int32_
     // a few rows: the split exact scan (every corpus part in parallel, pruned
     // by the rows' exact upper bounds of D_k), ~1 ms per 8 rows at C2
     int split = 1;
-    // MN_FB_SPLIT: the row limit of the split scan (default 256; 0 = always
+    // MN_FB_SPLIT: the row limit of the split scan (default 4096; 0 = always
     // the batched split-generator pass; A/B and tests)
     const char *fse = getenv("MN_FB_SPLIT");
-    const int fb_lim = (fse && *fse) ? std::max(0, atoi(fse)) : 256;
+    const int fb_lim = (fse && *fse) ? std::max(0, atoi(fse)) : 4096;
     if (nfb2 > 0 && nfb2 <= fb_lim && nc >= (1 << 16)) {
         split = fb_split_scan(Q, C, nc, d, q_off, c_off, excl, k, fb_list, nfb2, ubv, false,
                               out_idx, out_dist, s);

@@ -68,7 +68,7 @@ def test_c2_1m_uniform_sampled_rows_bit_exact(c2):
     assert st["n_uncertified"] <= 8 and st["n_escalated"] == 0
 
 
-def test_c2_1m_clustered_stress_bounded():
+def test_c2_1m_clustered_stress_bounded(c2):
     import surfface_hip as S
     t0 = time.time()
     Xh = datagen.clustered(N, D, seed=7)
@@ -85,10 +85,13 @@ def test_c2_1m_clustered_stress_bounded():
     rec = {"gen_s": round(t1 - t0, 1), "knn_wall_s": round(t2 - t1, 2),
            **{k: (round(v, 2) if isinstance(v, float) else v) for k, v in st.items()
              }}
+    uni = c2[1].stats["ms_total"]
+    rec["uniform_ms_total"] = round(uni, 1)
     print("C2-clustered stats", json.dumps(rec))
-    # bounded: the escalation / exact-scan cost stays within a small multiple
-    # of the uniform build (2 s)
-    assert t2 - t1 < 60.0, rec
+    # the clustered build within 2x the uniform one (the fp16
+    # symmetric sweep certifies ~92% of the rows, the bf16x3 refill the rest
+    # but the 1000 all-zero rows, which the split exact scan resolves)
+    assert st["ms_total"] <= 2.0 * uni, rec
 
 
 def _union_rows_oracle(idx, dist, rows, sigma=1.0):
