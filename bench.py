@@ -184,8 +184,12 @@ def main():
         sym = st0.get("sweep_slices") == -1
         nc_sw = n_loc if sym else n_loc - m0
         kname = "k_gram_sweep2" if os.environ.get("MN_X1_SWEEP", "2") != "1" else "k_gram_sweep"
+        # the exact instantiation (rocprofv3 name) the PMC reference must match
+        kfull = "k_gram_sweep2<0, 0, true>"
         if sym:
+            f16 = os.environ.get("MN_SYM_F16", "1") != "0"
             kname = "k_gram_sweep2<SW_SYM>"
+            kfull = "k_gram_sweep2<0, 2, true, %s>" % ("true" if f16 else "false")
         flops_launch = 2.0 * nq * nc_sw * d
         nbk = (n_loc + 255) // 256
         flops_exec = 2.0 * 256 * 256 * d * nbk * (nbk + 1) / 2 if sym else flops_launch
@@ -203,8 +207,11 @@ def main():
                              "tflops": round(flops_exec / (gms * 1e-3) / 1e12, 3),
                              "frac": round(flops_exec / (gms * 1e-3) / 1e12
                                            / BF16_MFMA_PEAK_TFLOPS, 4)},
-                "peak_basis": "dense bf16 MFMA 2500 TFLOP/s (one v_mfma_f32_16x16x32_bf16 product "
-                              "per f32 product: x ~ bf16(x), certified by the residual-norm bound)",
+                "peak_basis": ("dense fp16/bf16 MFMA 2500 TFLOP/s (one v_mfma_f32_16x16x32_f16 "
+                               "product per f32 product: x 2^e ~ fp16, certified by the residual-"
+                               "norm bound)" if sym else
+                               "dense bf16 MFMA 2500 TFLOP/s (one v_mfma_f32_16x16x32_bf16 product "
+                               "per f32 product: x ~ bf16(x), certified by the residual-norm bound)"),
                 "measured_mfma_ceiling": {"tflops": MEASURED_BF16_16X16X32_TFLOPS,
                                           "frac": round(achieved / MEASURED_BF16_16X16X32_TFLOPS, 4),
                                           "basis": "scripts/probes/probe_mfma_peak.hip "
@@ -217,7 +224,7 @@ def main():
                                "vs_f32_mfma_peak": round(2.0 * nq * n_loc * d / (ms_all * 1e-3) / 1e12
                                                          / FP32_MFMA_PEAK_TFLOPS, 3)}}
     elif algo == 2:
-        kname = "k_gram_bf16<GM_L2>"
+        kname = kfull = "k_gram_bf16<GM_L2>"
         flops_launch = 2.0 * nq * n_loc * d
         achieved = flops_launch / (gms * 1e-3) / 1e12
         peak = BF16_MFMA_PEAK_TFLOPS / 3.0
@@ -227,7 +234,7 @@ def main():
                 "peak_basis": ("dense bf16 MFMA 2500 TFLOP/s / 3 bf16 products per f32 product "
                                "(x = hi + lo; hi.hi + hi.lo + lo.hi)")}
     else:
-        kname = "k_gram_topk"
+        kname = kfull = "k_gram_topk"
         flops_launch = 2.0 * nq * n_loc * d
         achieved = flops_launch / (gms * 1e-3) / 1e12
         roof = {"bound": "mfma", "kernel": kname, "achieved": round(achieved, 3),
@@ -241,7 +248,7 @@ def main():
         try:
             pm = json.load(open(a.pmc_json))
             if (pm.get("rows_per_gpu") == n_loc and pm.get("dim") == d
-                    and pm.get("kernel", "").startswith(kname.split("<")[0])):
+                    and pm.get("kernel", "") == kfull):
                 roof["traffic"] = pm.get("hbm_bytes_per_launch")
                 roof["traffic_source"] = pm.get("source", os.path.relpath(a.pmc_json, ROOT))
         except (OSError, ValueError):
@@ -366,6 +373,17 @@ def c3_legs(S, X, idx, dist, k):
                                        "f64_tflops": round(f64_ops / (ms * 1e-3) / 1e12, 2),
                                        "f64_frac_of_78.6": round(f64_ops / (ms * 1e-3) / 1e12
                                                                  / FP64_VALU_PEAK_TFLOPS, 4)}}
+    # HBM bytes per launch of the energy kernel from the latest legs profile
+    # (bench_pmc_energy.json: separate FETCH_SIZE / WRITE_SIZE passes, FETCH x2),
+    # used when the kernel and shape match
+    try:
+        pe = json.load(open(os.path.join(ROOT, "bench_pmc_energy.json")))
+        if pe.get("rows") == n and pe.get("dim") == f:
+            out["energy_rows"]["roofline"]["traffic"] = pe.get("hbm_bytes_per_launch")
+            out["energy_rows"]["roofline"]["traffic_kernel"] = pe.get("kernel")
+            out["energy_rows"]["roofline"]["traffic_source"] = pe.get("source")
+    except (OSError, ValueError):
+        pass
     out["energy_rows_per_sec"] = n / (ms * 1e-3)
     out["_Lf"] = Lf
     # energymaps diffusion pre-pass (eta 0.1, 4 steps; energymaps.rs:518-546) on

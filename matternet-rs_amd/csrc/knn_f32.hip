@@ -2019,12 +2019,18 @@ static int knn_x1(const float *Q, int64_t nq, const float *C, int64_t nc, int32_
     unsigned long long *ncand = (unsigned long long *)(flags + 8);
 
     // phase-1 sample: the first m0 corpus rows, list length L1 (tau0 ~ the
-    // (L1 nc / m0)-th best key); small corpora run phase 1 alone (m0 = nc)
-    int L1 = std::min(std::max((k + 1) / 2, 16), 48);
+    // (L1 nc / m0)-th best key); small corpora run phase 1 alone (m0 = nc).
+    // The symmetric sweep (self kNN) takes half the sample with half the list
+    // (the same threshold rank, nc/32 x 8 vs nc/16 x 16: C2 964 vs 1044 ms,
+    // 157 rows left to the split exact scan; profiles/r03f_grid_sample_list.log)
+    const char *sye = getenv("MN_X1_SYM");  // 0: the query-major sweep (A/B)
+    const bool sym_pre = same && excl && tmaj && sweep_version() == 2 && !(sye && *sye == '0');
+    int L1 = sym_pre ? std::min(std::max((k + 1) / 4, 8), 48)
+                     : std::min(std::max((k + 1) / 2, 16), 48);
     const char *fl = getenv("MN_X1_L1");  // experiments: phase-1 list length
     if (fl && *fl) L1 = std::min(std::max(atoi(fl), 4), 48);
     const char *fs = getenv("MN_X1_SAMPLE_DIV");  // experiments: sample = nc / div
-    const int64_t div = (fs && *fs) ? std::max(2, atoi(fs)) : 16;
+    const int64_t div = (fs && *fs) ? std::max(2, atoi(fs)) : (sym_pre ? 32 : 16);
     int64_t m0 = std::max<int64_t>(nc / div, (int64_t)64 * L1);
     m0 = (m0 + 255) / 256 * 256;  // whole phase-1 tiles and whole sweep panels
     const bool two = m0 + 4 * ksw::BC <= nc;
@@ -2035,8 +2041,7 @@ static int knn_x1(const float *Q, int64_t nq, const float *C, int64_t nc, int32_
     // self kNN: the symmetric sweep (gram_sweep2.hpp SW_SYM: each unordered
     // pair once, rows in ascending-tau0 order; MN_X1_SYM=0 for the
     // query-major sweep of the rows outside the sample)
-    const char *sye = getenv("MN_X1_SYM");
-    bool sym = same && excl && two && tmaj && sweep_version() == 2 && !(sye && *sye == '0');
+    bool sym = sym_pre && two;
 
     // flags: [0..2] cmax, [3] non-finite input, [4] too large for bf16x1,
     // [5] fb_count, [6] big_count, [7] max |tau0|, [8..9] ncand, [10..13]

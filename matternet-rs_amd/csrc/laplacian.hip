@@ -48,7 +48,7 @@ struct Params {
 };
 
 constexpr int WAVE_CAP = 512;   // general (col, w) wave sort
-constexpr int BLOCK_CAP = 8192;
+constexpr int BLOCK_CAP = 16384;  // rows sorted in one block's LDS (packed 8-B keys)
 constexpr int EMPTY = INT_MAX;  // sentinel column of an invalid forward slot
 constexpr uint64_t SENT = ~0ull;  // sentinel packed key (column << 32 | entry)
 
@@ -431,11 +431,14 @@ __global__ __launch_bounds__(256) void k_row_sort_wave(const int64_t *__restrict
     }
 }
 
-// one 1024-thread block per row with WAVE_CAP < m <= BLOCK_CAP (bitonic in LDS)
+// one 1024-thread block per row of 1024 < m <= BLOCK_CAP entries (the rows
+// the wave kernels pass on): packed (column << 32 | entry) keys bitonic-sorted
+// in LDS, weights gathered only for the kept entries (the first of each
+// column run takes the run's largest weight, as (col asc, w desc) would),
+// every gather before the first store (the row is compacted in place), then
+// the kept weights in LDS for wave 0's ascending-column fold.
 struct alignas(16) BigSmem {
-    double w[BLOCK_CAP];
-    int c[BLOCK_CAP];
-    int flag[BLOCK_CAP];
+    uint64_t key[BLOCK_CAP];  // reused as the kept weights (double) for the fold
     int wsum[16];
 };
 
@@ -450,78 +453,97 @@ __global__ __launch_bounds__(1024) void k_row_sort_block(const int64_t *__restri
                                                          float *__restrict__ deg32,
                                                          int32_t *__restrict__ huge_list,
                                                          int *__restrict__ huge_count) {
+    constexpr int NQ = BLOCK_CAP / 1024;  // elements per thread
     __shared__ BigSmem sm;
+    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
     const int nb = *big_count;
+    auto colof = [](uint64_t v) { return v == SENT ? EMPTY : (int)(v >> 32); };
     for (int b = blockIdx.x; b < nb; b += gridDim.x) {
         const int64_t i = big_list[b];
         const int64_t o = offs[i];
         const int m = (int)(offs[i + 1] - o);
         if (m > BLOCK_CAP) {
-            if (threadIdx.x == 0) huge_list[atomicAdd(huge_count, 1)] = (int32_t)i;
+            if (t == 0) huge_list[atomicAdd(huge_count, 1)] = (int32_t)i;
             continue;
         }
         int P = 1;
         while (P < m) P <<= 1;
-        for (int e = threadIdx.x; e < P; e += blockDim.x) {
-            sm.c[e] = e < m ? col[o + e] : EMPTY;
-            sm.w[e] = e < m ? wt[o + e] : 0.0;
+        for (int e = t; e < P; e += 1024) {
+            const int c = e < m ? col[o + e] : EMPTY;
+            sm.key[e] = c == EMPTY ? SENT : (((uint64_t)(uint32_t)c << 32) | (uint32_t)e);
         }
         __syncthreads();
-        for (int kk = 2; kk <= P; kk <<= 1) {
+        for (int kk = 2; kk <= P; kk <<= 1)
             for (int j = kk >> 1; j > 0; j >>= 1) {
-                for (int e = threadIdx.x; e < P; e += blockDim.x) {
+                for (int e = t; e < P; e += 1024) {
                     const int pe = e ^ j;
                     if (pe > e) {
-                        const bool asc = (e & kk) == 0;
-                        const bool sw = asc ? cw_less(sm.c[pe], sm.w[pe], sm.c[e], sm.w[e])
-                                            : cw_less(sm.c[e], sm.w[e], sm.c[pe], sm.w[pe]);
-                        if (sw) {
-                            int tc = sm.c[e]; sm.c[e] = sm.c[pe]; sm.c[pe] = tc;
-                            double tw = sm.w[e]; sm.w[e] = sm.w[pe]; sm.w[pe] = tw;
+                        const uint64_t a = sm.key[e], c = sm.key[pe];
+                        if (((e & kk) == 0) ? c < a : a < c) {
+                            sm.key[e] = c;
+                            sm.key[pe] = a;
                         }
                     }
                 }
                 __syncthreads();
             }
-        }
-        // dedupe with a block scan over keep flags (chunks of 1024)
+        // dedupe: element e = 1024 q + t; kept entries' weights in registers,
+        // their positions from a block scan per chunk
+        int pr[NQ];
+        double wr[NQ];
         int base = 0;
-        for (int c0 = 0; c0 < m; c0 += 1024) {
-            const int e = c0 + threadIdx.x;
-            const bool keep =
-                e < m && sm.c[e] != EMPTY && (e == 0 || sm.c[e] != sm.c[e - 1]);
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+            const int e = 1024 * q + t;
+            pr[q] = -1;
+            wr[q] = 0.0;
+            if (1024 * q >= m) continue;  // block-uniform
+            const uint64_t x = e < m ? sm.key[e] : SENT;
+            const int c = colof(x);
+            const int cprev = (e > 0 && e < m) ? colof(sm.key[e - 1]) : INT_MIN;
+            const bool keep = e < m && c != EMPTY && c != cprev;
+            if (keep) {
+                double w = wt[o + (uint32_t)x];
+                for (int f = e + 1; f < m; ++f) {  // the column run (2 long at most in practice)
+                    const uint64_t y = sm.key[f];
+                    if (colof(y) != c) break;
+                    const double wp = wt[o + (uint32_t)y];
+                    if (wp > w) w = wp;
+                }
+                wr[q] = w;
+            }
             const uint64_t mk = __ballot(keep);
-            const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
             if (lane == 0) sm.wsum[wv] = (int)__popcll(mk);
             __syncthreads();
             int before = 0, tot = 0;
-            for (int q = 0; q < 16; ++q) {
-                if (q < wv) before += sm.wsum[q];
-                tot += sm.wsum[q];
+            for (int z = 0; z < 16; ++z) {
+                if (z < wv) before += sm.wsum[z];
+                tot += sm.wsum[z];
             }
-            if (keep) {
-                const int pos = base + before + (int)__popcll(mk & ((1ull << lane) - 1ull));
-                sm.flag[pos] = e;  // gather index (pos <= e: in-place safe via flag array)
-            }
+            if (keep) pr[q] = base + before + (int)__popcll(mk & ((1ull << lane) - 1ull));
             base += tot;
             __syncthreads();
         }
-        for (int q = threadIdx.x; q < base; q += blockDim.x) {
-            col[o + q] = sm.c[sm.flag[q]];
-            wt[o + q] = sm.w[sm.flag[q]];
-        }
-        // the ascending-column fold: wave 0 loads 64 kept weights at a time
-        // (parallel LDS gathers) and chains them through v_readlane, so the
-        // chain waits on the add latency, not on two dependent LDS reads
-        if (threadIdx.x < 64) {
-            const int lane = threadIdx.x;
+        // every gather from wt happened above: compact the row in place (the
+        // columns re-read from the keys), then stage the kept weights for the
+        // fold over the dead keys
+#pragma unroll
+        for (int q = 0; q < NQ; ++q)
+            if (pr[q] >= 0) {
+                col[o + pr[q]] = colof(sm.key[1024 * q + t]);
+                wt[o + pr[q]] = wr[q];
+            }
+        __syncthreads();
+        double *kw = reinterpret_cast<double *>(sm.key);
+#pragma unroll
+        for (int q = 0; q < NQ; ++q)
+            if (pr[q] >= 0) kw[pr[q]] = wr[q];
+        __syncthreads();
+        if (t < 64) {  // ascending-column fold: 64 weights a step, chained via v_readlane
             double s64 = -0.0;
             float s32 = 0.0f;
-            double nx = lane < base ? sm.w[sm.flag[lane]] : 0.0;
             for (int c0 = 0; c0 < base; c0 += 64) {
-                const double v = nx;
-                const int e = c0 + 64 + lane;
-                nx = e < base ? sm.w[sm.flag[e]] : 0.0;
+                const double v = c0 + lane < base ? kw[c0 + lane] : 0.0;
                 const int cnt = min(64, base - c0);
                 if (sym == MN_SYM_UNION)
                     for (int l = 0; l < cnt; ++l) s64 = s64 + readlane_f64(v, l);
@@ -548,7 +570,7 @@ __global__ __launch_bounds__(1024) void k_row_sort_block(const int64_t *__restri
 // +inf and are never touched; every step with partner distance < CH runs on
 // LDS-resident chunks of CH entries.  Between steps that exchange data through
 // HBM the block waits for its stores and invalidates its L1 (agent acquire).
-constexpr int CH = BLOCK_CAP;
+constexpr int CH = 8192;  // hub rows: LDS chunk of the HBM bitonic network
 
 __device__ __forceinline__ void hub_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");

@@ -31,6 +31,8 @@ res = {v: [] for v in VERS}
 probe = {v: [] for v in VERS}
 for r in range(rounds):
     for v in VERS:
+        for k_ in {kv.split("=")[0] for vv in VERS for kv in vv.split(",")}:
+            os.environ.pop(k_, None)  # a variant sets only its own keys
         for kv in v.split(","):
             k_, val = kv.split("=")
             os.environ[k_] = val

@@ -63,9 +63,10 @@ def test_c2_1m_uniform_sampled_rows_bit_exact(c2):
     _check_graph(X.cpu().numpy(), r.idx.cpu().numpy(), r.dist.cpu().numpy(), rows)
     st = r.stats
     print("C2 stats", json.dumps({k: v for k, v in st.items()}))
-    # an isolated uncertified row (its threshold sample fell close to D_k, or a
-    # full per-row buffer) is resolved exactly and checked like any other
-    assert st["n_uncertified"] <= 8 and st["n_escalated"] == 0
+    # rows no certificate settles (their threshold sample fell close to D_k,
+    # or a full per-row buffer: ~160 of 1M with the n/32 x 8 sample) go to the
+    # split exact scan (~12 ms) and are checked like any other; none escalates
+    assert st["n_uncertified"] <= 1024 and st["n_escalated"] == 0
 
 
 def test_c2_1m_clustered_stress_bounded(c2):
