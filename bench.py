@@ -452,7 +452,15 @@ def c5_leg(S, _lib, L, a, dev, stream):
     ms_sp, (sidx, sw, applied) = _timed(lambda: S.sparsify_rows(idx, w, 0.5))
     kept = int((sidx >= 0).sum().item())
     m0 = st.get("sample_rows", 0)
-    if m0 > 0:  # two-phase: the dominant kernel is the sweep over rows [m0, n)
+    exec_fl = None
+    if m0 > 0 and st.get("sweep_slices") == -1:
+        # SW_COS_SYM: the sweep decides all n^2 pairs, executing the upper-
+        # triangle 256 x 256 tiles (each unordered pair once)
+        kname, kms = "k_gram_sweep2<SW_COS_SYM, tile-major>", st["ms_sweep"]
+        flops = 2.0 * n * n * d
+        nbk = (n + 255) // 256
+        exec_fl = 2.0 * 256 * 256 * ((d + 31) // 32 * 32) * nbk * (nbk + 1) / 2
+    elif m0 > 0:  # two-phase: the dominant kernel is the sweep over rows [m0, n)
         kname, kms = "k_gram_sweep2<SW_COS, tile-major>", st["ms_sweep"]
         flops = 2.0 * n * (n - m0) * d
     else:
@@ -465,7 +473,12 @@ def c5_leg(S, _lib, L, a, dev, stream):
                         "peak": BF16_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                         "frac": round(ach / BF16_MFMA_PEAK_TFLOPS, 4), "flop_per_launch": flops,
                         "ms_per_launch": round(kms, 1),
-                        "frac_of_measured_ceiling": round(ach / MEASURED_BF16_16X16X32_TFLOPS, 4)},
+                        "frac_of_measured_ceiling": round(ach / MEASURED_BF16_16X16X32_TFLOPS, 4),
+                        **({"executed": {"flop_per_launch": exec_fl,
+                                         "tflops": round(exec_fl / (kms * 1e-3) / 1e12, 1),
+                                         "frac": round(exec_fl / (kms * 1e-3) / 1e12
+                                                       / BF16_MFMA_PEAK_TFLOPS, 4)}}
+                           if exec_fl else {})},
            "gram_all_phases": {"ms": round(st["ms_gram"], 1),
                                "tflops_equiv": round(2.0 * n * n * d / (st["ms_gram"] * 1e-3) / 1e12, 1),
                                "ms_sample": round(st.get("ms_sample", 0.0), 1),

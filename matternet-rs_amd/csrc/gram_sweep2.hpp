@@ -29,8 +29,10 @@
 //    rare candidate staging, the next tile's accumulator init) runs in the
 //    wave's READ window, beside its partner's MFMAs.
 #pragma once
+#include <algorithm>
 #include <climits>
 #include <type_traits>
+#include <vector>
 
 #include "common.hpp"
 
@@ -93,7 +95,18 @@ __device__ __forceinline__ int xcd_remap(int orig, int nwg) {
 // wave's read window (fusing the init into the first MFMA window, or one
 // ballot per 2 or 4 fragments before the per-fragment ones, measured equal
 // within noise at C2).
-enum SweepMode { SW_L2 = 0, SW_COS = 1, SW_SYM = 2 };
+enum SweepMode { SW_L2 = 0, SW_COS = 1, SW_SYM = 2, SW_COS_SYM = 3 };
+
+// SW_COS_SYM (the C5 self item graph, X both operands, rows in DESCENDING
+// cosine-threshold order t): SW_SYM's block table and per-row buffers with
+// SW_COS's product-form accumulator.  Diagonal tile: acc0 = tq(q) hc(c) with
+// tq = t(q)|q|, hc = -|c| (the row's own test, key = -acc / |c|, as SW_COS).
+// Off-diagonal tile (J > I, so t(c) <= t(q)): acc0 = ta(q) hoff(c) with ta =
+// |q|, hoff = -t(c)|c|: acc > 0 iff cos~ > t(c), the column's test; its key
+// -acc / |q| (the re-rank maps key / |c| - t(c) = -cos~); row q's own key
+// k_q = (-acc + hoff(c) ta(q)) / |c| + tq(q) (= -acc_q / |c|, acc_q = acc +
+// (t(c) - t(q)) |q||c|), buffered when k_q < 0.  tau0 carries |c| per
+// position (sm.tc).
 
 // SW_SYM (self kNN, X both operands, rows in ascending-tau0 order): the
 // sweep covers each unordered pair once.  Block b takes row block I = tab[b].x
@@ -132,7 +145,8 @@ __global__ __launch_bounds__(NT) void k_gram_sweep2(
     const float *__restrict__ tau0, const float *__restrict__ hc, int64_t c_begin, int S,
     int64_t chunk, int cap, uint2 *__restrict__ buf, int *__restrict__ cnt, int pst = 0,
     SymArgs sym = SymArgs{}) {
-    constexpr bool SYM = MODE == SW_SYM;
+    constexpr bool SYM = MODE == SW_SYM || MODE == SW_COS_SYM;
+    constexpr bool COSM = MODE == SW_COS || MODE == SW_COS_SYM;  // product-form acc0, NaN pads
     __shared__ Smem sm;
     const int tid = threadIdx.x, lane = tid & 63;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -155,15 +169,15 @@ __global__ __launch_bounds__(NT) void k_gram_sweep2(
     }
     const int ntile = cend > cbeg ? (cend - cbeg + BC - 1) / BC : 0;
     const int gtot = ntile * nkb;
-    const float pad = MODE == SW_COS ? __builtin_nanf("") : __builtin_inff();
+    const float pad = COSM ? __builtin_nanf("") : __builtin_inff();
     const bool diag0 = SYM && cbeg == q0;  // SW_SYM: the first tile is the diagonal one
 
     if (tid < NWAVES) sm.scnt[tid] = 0;
     if (tid < BQ) {
         // padded queries never qualify (COS: NaN, as -inf * -|c| would be +inf)
-        sm.tq[tid] = q0 + tid < nq ? tq[q0 + tid] : (MODE == SW_COS ? pad : -__builtin_inff());
+        sm.tq[tid] = q0 + tid < nq ? tq[q0 + tid] : (COSM ? pad : -__builtin_inff());
         sm.t0[tid] = q0 + tid < nq ? tau0[q0 + tid] : 0.f;
-        if constexpr (SYM) sm.ta[tid] = q0 + tid < nq ? sym.aoff[q0 + tid] : -__builtin_inff();
+        if constexpr (SYM) sm.ta[tid] = q0 + tid < nq ? sym.aoff[q0 + tid] : (COSM ? pad : -__builtin_inff());
         else sm.qcnt[tid] = 0;
     }
     if (ntile > 0 && tid < BC) {
@@ -248,7 +262,7 @@ __global__ __launch_bounds__(NT) void k_gram_sweep2(
 #pragma unroll
             for (int f = 0; f < WQF; ++f) {
                 // (hipcc packs these into v_pk_add_f32 / v_pk_mul_f32 pairs)
-                if constexpr (MODE == SW_COS) {
+                if constexpr (COSM) {
                     acc[f][g][0] = tql[f] * x.x;
                     acc[f][g][1] = tql[f] * x.y;
                     acc[f][g][2] = tql[f] * x.z;
@@ -333,6 +347,23 @@ __global__ __launch_bounds__(NT) void k_gram_sweep2(
         for (int r = 0; r < 4; ++r) pm |= a[r] > 0.f ? (1u << r) : 0u;
         if (excl && (unsigned)(qgl - c) < 4u) pm &= ~(1u << (qgl - c));
         if constexpr (SYM) {
+            if constexpr (MODE == SW_COS_SYM) {
+                const float tql = sm.tq[ql], tal = sm.ta[ql];
+                while (pm) {
+                    const int r = __builtin_ctz(pm);
+                    pm &= pm - 1;
+                    const int cl = 128 * wc + 16 * g + 4 * fk + r;
+                    const float hcl = sm.hc[hpar][cl];
+                    if (diag) {  // row q's test (SW_COS): key = -acc / |c|
+                        emit_sym((uint32_t)qgl, (uint32_t)(c + r), a[r] / hcl);
+                    } else {     // row c's test; row q's on these hits
+                        emit_sym((uint32_t)(c + r), (uint32_t)qgl, -a[r] / tal);
+                        const float kq = (hcl * tal - a[r]) / sm.tc[hpar][cl] + tql;
+                        if (kq < 0.f) emit_sym((uint32_t)qgl, (uint32_t)(c + r), kq);
+                    }
+                }
+                return;
+            }
             const float t0l = sm.t0[ql];
             while (pm) {
                 const int r = __builtin_ctz(pm);
@@ -485,6 +516,36 @@ __global__ __launch_bounds__(NT) void k_gram_sweep2(
 }
 
 #undef MN_VMCNT
+
+// SW_SYM / SW_COS_SYM block table: row block I against column tiles
+// [J0, J1), J >= I, at most TPB tiles per block.  order 1 (default): column
+// ranges aligned to a TPB grid, ordered by range then row, so the co-resident
+// blocks of an XCD stream the same column tiles (one L2 fill serves them all;
+// their row panels stay in the Infinity Cache); order 0: ranges from the
+// diagonal, the longest first.
+inline std::vector<int4> sym_block_table(int nbk, int TPB, int order) {
+    std::vector<int4> tab;
+    tab.reserve((size_t)nbk * ((size_t)nbk / TPB + 2) / 2 + 16);
+    if (order == 1) {
+        for (int I = 0; I < nbk; ++I)
+            for (int J0 = I; J0 < nbk;) {
+                const int J1 = std::min((J0 / TPB + 1) * TPB, nbk);
+                tab.push_back(make_int4(I, J0, J1, J0 / TPB));
+                J0 = J1;
+            }
+        std::stable_sort(tab.begin(), tab.end(), [](const int4 &a, const int4 &b) {
+            return a.w != b.w ? a.w < b.w : a.x < b.x;
+        });
+    } else {
+        for (int I = 0; I < nbk; ++I)
+            for (int J0 = I; J0 < nbk; J0 += TPB)
+                tab.push_back(make_int4(I, J0, std::min(J0 + TPB, nbk), 0));
+        std::stable_sort(tab.begin(), tab.end(), [](const int4 &a, const int4 &b) {
+            return (a.z - a.y) > (b.z - b.y);
+        });
+    }
+    return tab;
+}
 
 }  // namespace ksw2
 }  // namespace mn

@@ -367,9 +367,11 @@ inline Perm make_perm_ab(int64_t n) {
 // consecutive bytes of one k-block
 // tm > 0: the tile-major variant with panel stride tm k-blocks (gram_sweep2.hpp
 // TM; rows padded to 256 with zeros, n_pad = n rounded up)
+// pidx (may be NULL): position p holds row pidx[p] (the symmetric sweep's
+// threshold order), else Perm pm
 __global__ __launch_bounds__(256) void k_to_kb32(const uint16_t *__restrict__ X, int64_t n, int d,
                                                  int dp, Perm pm, uint16_t *__restrict__ XK,
-                                                 int tm) {
+                                                 int tm, const int *__restrict__ pidx = nullptr) {
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int nkb = dp / 32;
     const int64_t rows = tm ? (n + 255) / 256 * 256 : n;
@@ -396,7 +398,7 @@ __global__ __launch_bounds__(256) void k_to_kb32(const uint16_t *__restrict__ X,
         *reinterpret_cast<uint4 *>(XK + o) = make_uint4(0u, 0u, 0u, 0u);
         return;
     }
-    const int64_t src = pm.n ? pm(p) : p;
+    const int64_t src = pidx ? (int64_t)pidx[p] : (pm.n ? pm(p) : p);
     const int e0 = 32 * kb + 8 * cc;
     uint4 v = make_uint4(0u, 0u, 0u, 0u);
     if (e0 + 8 <= d) {
@@ -452,13 +454,53 @@ __global__ __launch_bounds__(256) void k_tau_cos(int64_t nq, int S1, const float
     tq_pos[pm.pos(q)] = ok ? (float)((double)t * qn[q]) : __builtin_inff();
 }
 
+// SW_COS_SYM: sort keys -t (descending thresholds), a non-finite flag
+__global__ __launch_bounds__(256) void k_cos_sym_keys(int64_t n, const float *__restrict__ tcos,
+                                                      float *__restrict__ key,
+                                                      int *__restrict__ iota,
+                                                      int *__restrict__ bad) {
+    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= n) return;
+    const float t = tcos[r];
+    key[r] = -t;
+    iota[r] = (int)r;
+    if (!__builtin_isfinite(t)) atomicOr(bad, 1);
+}
+
+// SW_COS_SYM per position p (row pi[p]): tq = t|x| (diagonal tiles: the
+// row's test, as k_tau_cos), ta = |x| and hoff = -t|x| (off-diagonal tiles),
+// hc = -|x| (diagonal columns), cn = |x| (the row keys)
+__global__ __launch_bounds__(256) void k_cos_sym_pos(int64_t n, const int *__restrict__ pi,
+                                                     const float *__restrict__ tcos,
+                                                     const double *__restrict__ xn,
+                                                     float *__restrict__ tq, float *__restrict__ ta,
+                                                     float *__restrict__ hc,
+                                                     float *__restrict__ hoff,
+                                                     float *__restrict__ cn) {
+    const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= n) return;
+    const int r = pi[p];
+    const double nr = xn[r];
+    const float t = tcos[r];
+    const float tqv = (float)((double)t * nr);
+    tq[p] = tqv;
+    ta[p] = (float)nr;
+    hc[p] = -(float)nr;
+    hoff[p] = -tqv;
+    cn[p] = (float)nr;
+}
+
 // One wave per query: both buffers' candidates in key = -cos~ order (sweep
 // keys mapped back: -cos~ = key / |q| - t), exact distances for the best kq
 // and every other candidate whose lower bound does not exceed the worst of
 // those, (dist, j) order, certification dist_min(never buffered) > D_k.
+// pidx != NULL (SW_COS_SYM): the work items are sweep POSITIONS p (row
+// pidx[p]; big_list holds positions), one per-position buffer (S2 = 1, counts
+// past cap2 = overflow), candidate ids are positions; no phase-1 lists.
 template <int NR>
 __global__ __launch_bounds__(256) void k_cos_rerank_x1(
-    const uint16_t *__restrict__ X, int64_t n, int d, Perm pm, const double *__restrict__ xn,
+    const uint16_t *__restrict__ X, int64_t n, int d, Perm pm, const int *__restrict__ pidx,
+    const double *__restrict__ xn,
     const float *__restrict__ xinv, int S1, int cap1, const uint2 *__restrict__ buf1,
     const int *__restrict__ cnt1, const float *__restrict__ btau1, int S2, int cap2,
     const uint2 *__restrict__ buf2, const int *__restrict__ cnt2, const float *__restrict__ tcos,
@@ -471,7 +513,8 @@ __global__ __launch_bounds__(256) void k_cos_rerank_x1(
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const int64_t wq = (int64_t)blockIdx.x * 4 + wid;
     if (qlist ? wq >= *qlist_n : wq >= n) return;
-    const int64_t q = qlist ? qlist[wq] : wq;
+    const int64_t item = qlist ? qlist[wq] : wq;  // a row, or (pidx) a position
+    const int64_t q = pidx ? (int64_t)pidx[item] : item;
     const float t = tcos[q];
     bool forced = !(t < __builtin_inff());
     int M = 0;
@@ -494,15 +537,16 @@ __global__ __launch_bounds__(256) void k_cos_rerank_x1(
             M += (int)__popcll(bm);
         }
     }
-    const int64_t qp = pm.pos(q);  // the sweep ran over positions
+    const int64_t qp = pidx ? item : pm.pos(q);  // the sweep ran over positions
     for (int s = 0; s < S2; ++s) {
-        const int cnt = cnt2[qp * S2 + s];
-        forced |= cnt < 0;
+        int cnt = cnt2[qp * S2 + s];
+        forced |= cnt < 0 || cnt > cap2;  // -1 / a count past cap (SW_COS_SYM): overflow
+        cnt = min(cnt, cap2);
         const uint2 *bp = buf2 + (qp * S2 + s) * (int64_t)cap2;
         for (int e0 = 0; e0 < cnt; e0 += 64) {
             const int e = e0 + lane;
             const uint2 v = e < cnt ? bp[e] : make_uint2(0u, 0u);
-            const int64_t gid = e < cnt ? pm((int64_t)v.y) : -1;
+            const int64_t gid = e < cnt ? (pidx ? (int64_t)pidx[v.y] : pm((int64_t)v.y)) : -1;
             const bool pass = e < cnt && gid != q;
             const uint64_t bm = __ballot(pass);
             const int pos = M + (int)__popcll(bm & ((1ull << lane) - 1ull));
@@ -514,7 +558,7 @@ __global__ __launch_bounds__(256) void k_cos_rerank_x1(
         }
     }
     if (!forced && M > 64 * NR && big_list) {
-        if (lane == 0) big_list[atomicAdd(big_count, 1)] = (int)q;
+        if (lane == 0) big_list[atomicAdd(big_count, 1)] = (int)item;
         return;
     }
     forced |= M > 64 * NR;
@@ -692,6 +736,9 @@ __global__ __launch_bounds__(FBT) void k_cos_fb_merge(
 
 }  // namespace kb16
 
+hipError_t sort_f32_pairs(const float *keys_in, float *keys_out, const int *vals_in,
+                          int *vals_out, int64_t n, hipStream_t s);  // sortkeys.hip
+
 static thread_local mn_knn_stats t_bf16_stats{};
 
 static int getenv_int(const char *name, int dflt) {
@@ -734,15 +781,12 @@ static int knn_cos_bf16_x1(const uint16_t *X, int64_t n, int32_t d, const mn_cos
     Timer tm;
     tm.start(o->timing != 0, s);
     {
-        const int64_t nt = nrows * 4 * nkb;
-        hipLaunchKernelGGL(k_to_kb32, dim3((unsigned)((nt + 255) / 256)), dim3(256), 0, s, X, n, d,
-                           dp, pm, XK, pst);
         const int64_t ns = m0 * (d / 8);
         hipLaunchKernelGGL(k_sample_rows, dim3((unsigned)((ns + 255) / 256)), dim3(256), 0, s, X, m0,
                            d, pm, XR);
         hipLaunchKernelGGL(k_perm_norms, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, xn,
                            xinv, n, pm, invp, negn);
-        MN_KCHECK(s, "k_to_kb32 / k_sample_rows / k_perm_norms");
+        MN_KCHECK(s, "k_sample_rows / k_perm_norms");
     }
     // phase 1: every query (rows, in place) against the sample (positions [0, m0))
     const GramPlan pl = plan_gram(n, m0, L1, 1, 1);
@@ -763,15 +807,98 @@ static int knn_cos_bf16_x1(const uint16_t *X, int64_t n, int32_t d, const mn_cos
         MN_KCHECK(s, "k_tau_cos");
     }
     tm.mark();
-    // phase 2: positions [m0, n) x all query positions
-    const double expect = (double)L1 * (double)(n - m0) / (double)m0;
-    const ksw::SweepPlan p2 = ksw::plan_sweep(n, n - m0, expect);
-    const int S2 = (int)p2.S, cap2 = p2.cap;
+    // phase 2, SW_COS_SYM (default, MN_BF16_SYM=0: the query-major sweep):
+    // positions in descending-threshold order, each unordered pair once; the
+    // query-major sweep when a threshold is not finite (a row without a full
+    // sample list) or the layout is k-block-major
+    const char *sye = getenv("MN_BF16_SYM");
+    bool sym = tmaj && !(sye && *sye == '0');
+    int *pi = nullptr;
+    float *tqS = nullptr, *taS = nullptr, *hcS = nullptr, *hoS = nullptr, *cnS = nullptr;
+    if (sym) {
+        const size_t an = ((size_t)n * 4 + 255) & ~(size_t)255;
+        char *so = (char *)scratch(kSlotSymOrd, an * 9 + 256);
+        MN_REQUIRE(so, MN_ENOMEM, "mn_knn_cos_bf16: symmetric-sweep scratch allocation failed");
+        float *key = (float *)so, *skey = (float *)(so + an);
+        int *iota = (int *)(so + 2 * an);
+        pi = (int *)(so + 3 * an);
+        tqS = (float *)(so + 4 * an);
+        taS = (float *)(so + 5 * an);
+        hcS = (float *)(so + 6 * an);
+        hoS = (float *)(so + 7 * an);
+        cnS = (float *)(so + 8 * an);
+        hipLaunchKernelGGL(k_cos_sym_keys, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, n,
+                           tcos, key, iota, flags + 4);
+        MN_KCHECK(s, "k_cos_sym_keys");
+        int bad = 0;
+        MN_HIP_TRY(hipMemcpyAsync(&bad, flags + 4, 4, hipMemcpyDeviceToHost, s));
+        MN_HIP_TRY(hipStreamSynchronize(s));
+        if (bad) {
+            sym = false;
+        } else {
+            MN_HIP_TRY(sort_f32_pairs(key, skey, iota, pi, n, s));
+        }
+    }
+    {
+        const int64_t nt = nrows * 4 * nkb;
+        hipLaunchKernelGGL(k_to_kb32, dim3((unsigned)((nt + 255) / 256)), dim3(256), 0, s, X, n, d,
+                           dp, pm, XK, pst, sym ? (const int *)pi : (const int *)nullptr);
+        MN_KCHECK(s, "k_to_kb32");
+        if (sym) {
+            hipLaunchKernelGGL(k_cos_sym_pos, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, n,
+                               pi, tcos, xn, tqS, taS, hcS, hoS, cnS);
+            MN_KCHECK(s, "k_cos_sym_pos");
+        }
+    }
+    tm.mark();  // the sweep copy (+ SW_COS_SYM order and per-position folds)
+    double expect;
+    int S2, cap2;
+    ksw::SweepPlan p2{};
+    if (sym) {
+        expect = (double)L1 * (double)n / (double)m0;
+        S2 = 1;
+        cap2 = std::max(256, (int)((2.5 * expect + 64.0 + 15.0) / 16.0) * 16);
+    } else {
+        expect = (double)L1 * (double)(n - m0) / (double)m0;
+        p2 = ksw::plan_sweep(n, n - m0, expect);
+        S2 = (int)p2.S;
+        cap2 = p2.cap;
+    }
     const size_t nbuf2 = (size_t)n * S2 * cap2;
     uint2 *buf2 = (uint2 *)scratch(kSlotX1Buf2, nbuf2 * sizeof(uint2) + 64);
     int *cnt2 = (int *)scratch(kSlotX1Meta2, (size_t)n * S2 * 4 + 64);
     MN_REQUIRE(buf2 && cnt2, MN_ENOMEM, "mn_knn_cos_bf16: sweep buffer allocation failed");
-    {
+    if (sym) {
+        const int nbk = (int)((n + ksw2::BC - 1) / ksw2::BC);
+        const std::vector<int4> tab = ksw2::sym_block_table(nbk, 256, 1);
+        int4 *dtab = (int4 *)scratch(kSlotSymTab, tab.size() * sizeof(int4) + 64);
+        MN_REQUIRE(dtab, MN_ENOMEM, "mn_knn_cos_bf16: block table allocation failed");
+        MN_HIP_TRY(hipMemcpyAsync(dtab, tab.data(), tab.size() * sizeof(int4),
+                                  hipMemcpyHostToDevice, s));
+        MN_HIP_TRY(hipMemsetAsync(cnt2, 0, (size_t)n * 4, s));
+        MN_REQUIRE(tab.size() < INT_MAX, MN_ENOTSUP, "mn_knn_cos_bf16: sweep grid too large");
+        const char *probe = getenv("MN_BF16_PROBE");
+        const bool noepi = probe && !strcmp(probe, "noepi");
+        auto kern = noepi ? ksw2::k_gram_sweep2<1, ksw2::SW_COS_SYM, true>
+                          : ksw2::k_gram_sweep2<0, ksw2::SW_COS_SYM, true>;
+        hipLaunchKernelGGL(kern, dim3((unsigned)tab.size()), dim3(ksw2::NT), 0, s, XK, n, XK, n, nkb,
+                           (int64_t)0, (int64_t)0, 1, tqS, cnS, hcS, (int64_t)0, 1, (int64_t)0,
+                           cap2, buf2, cnt2, pst, ksw2::SymArgs{dtab, taS, hoS, 0});
+        MN_KCHECK(s, "k_gram_sweep2<COS_SYM>");
+        if (probe && *probe) {  // timing probe: no outputs are produced
+            tm.mark();
+            MN_HIP_TRY(hipStreamSynchronize(s));
+            if (tm.on) {
+                t_bf16_stats.ms_sample = tm.ms(0, 1);
+                t_bf16_stats.ms_norms = tm.ms(1, 2);
+                t_bf16_stats.ms_sweep = tm.ms(2, 3);
+                t_bf16_stats.ms_gram = t_bf16_stats.ms_sample + t_bf16_stats.ms_sweep;
+            }
+            t_bf16_stats.sample_rows = m0;
+            t_bf16_stats.sweep_slices = -1;
+            return MN_OK;
+        }
+    } else {
         const int64_t grid = (n + ksw2::BQ - 1) / ksw2::BQ * p2.S;
         MN_REQUIRE(grid < INT_MAX, MN_ENOTSUP, "mn_knn_cos_bf16: sweep grid too large");
         const char *probe = getenv("MN_BF16_PROBE");
@@ -789,8 +916,9 @@ static int knn_cos_bf16_x1(const uint16_t *X, int64_t n, int32_t d, const mn_cos
             MN_HIP_TRY(hipStreamSynchronize(s));
             if (tm.on) {
                 t_bf16_stats.ms_sample = tm.ms(0, 1);
-                t_bf16_stats.ms_sweep = tm.ms(1, 2);
-                t_bf16_stats.ms_gram = tm.ms(0, 2);
+                t_bf16_stats.ms_norms = tm.ms(1, 2);
+                t_bf16_stats.ms_sweep = tm.ms(2, 3);
+                t_bf16_stats.ms_gram = t_bf16_stats.ms_sample + t_bf16_stats.ms_sweep;
             }
             t_bf16_stats.sample_rows = m0;
             t_bf16_stats.sweep_slices = S2;
@@ -805,12 +933,16 @@ static int knn_cos_bf16_x1(const uint16_t *X, int64_t n, int32_t d, const mn_cos
     // rounded up to the MFMA's 32: the all-zero k-blocks of the padding add
     // exactly 0 to the accumulator
     const int dk = (d + 31) / 32 * 32;
-    const double delta = 2.5 * ((double)dk + 16.0) * 0x1p-24;
+    // SW_COS_SYM: + 24 u for the off-diagonal row key k_q's four f32 roundings
+    // (terms |acc|/|q||c| <= 2, |t(c)|, |t(q)| <= 1 in cosine units)
+    const double delta = 2.5 * ((double)dk + 16.0) * 0x1p-24 + (sym ? 24.0 * 0x1p-24 : 0.0);
     int *fb_count = flags + 2, *big_count = flags + 3;
     int *big_list = fb_list + n;
+    const int *pix = sym ? (const int *)pi : (const int *)nullptr;
+    const int S1r = sym ? 0 : (int)pl.S;  // SW_COS_SYM decided the sample pairs too
 #define MN_RRC(NRV, NB, QL, QN, BC, BL)                                                          \
     hipLaunchKernelGGL(k_cos_rerank_x1<NRV>, dim3((unsigned)(NB)), dim3(256), 0, s, X, n, d, pm, \
-                       xn, xinv, (int)pl.S, pl.cap, buf1, cnt1, btau1, S2, cap2, buf2, cnt2,     \
+                       pix, xn, xinv, S1r, pl.cap, buf1, cnt1, btau1, S2, cap2, buf2, cnt2,     \
                        tcos, topk, delta, o->eps, o->sigma, o->p, QL, QN, BC, BL, out_idx,      \
                        out_dist, out_w, fb_count, fb_list)
     MN_RRC(8, (n + 3) / 4, (const int *)nullptr, (const int *)nullptr, big_count, big_list);
@@ -860,14 +992,15 @@ static int knn_cos_bf16_x1(const uint16_t *X, int64_t n, int32_t d, const mn_cos
     t_bf16_stats.slices = (int)pl.S;
     t_bf16_stats.list_len = L1;
     t_bf16_stats.sample_rows = m0;
-    t_bf16_stats.sweep_slices = S2;
+    t_bf16_stats.sweep_slices = sym ? -1 : S2;
     t_bf16_stats.sweep_cap = cap2;
     if (tm.on) {
         t_bf16_stats.ms_sample = tm.ms(0, 1);
-        t_bf16_stats.ms_sweep = tm.ms(1, 2);
-        t_bf16_stats.ms_gram = tm.ms(0, 2);
-        t_bf16_stats.ms_rerank = tm.ms(2, 3);
-        t_bf16_stats.ms_fallback = tm.ms(3, 4);
+        t_bf16_stats.ms_norms = tm.ms(1, 2);
+        t_bf16_stats.ms_sweep = tm.ms(2, 3);
+        t_bf16_stats.ms_gram = t_bf16_stats.ms_sample + t_bf16_stats.ms_sweep;
+        t_bf16_stats.ms_rerank = tm.ms(3, 4);
+        t_bf16_stats.ms_fallback = tm.ms(4, 5);
     }
     return MN_OK;
 }
@@ -954,9 +1087,9 @@ static int knn_cos_bf16_impl(const uint16_t *Q, int64_t nq, const uint16_t *C, i
             const int rc = knn_cos_bf16_x1(Q, nq, d, o, qn, qinv, flags, fb_list, out_idx, out_dist,
                                            out_w, s);
             if (rc != 1) {
-                if (tm.on) {
-                    t_bf16_stats.ms_norms = ms_norms;
-                    t_bf16_stats.ms_total = ms_norms + t_bf16_stats.ms_gram +
+                if (tm.on) {  // + the generator's own sweep-copy interval
+                    t_bf16_stats.ms_norms = ms_norms + t_bf16_stats.ms_norms;
+                    t_bf16_stats.ms_total = t_bf16_stats.ms_norms + t_bf16_stats.ms_gram +
                                             t_bf16_stats.ms_rerank + t_bf16_stats.ms_fallback;
                 }
                 return rc;

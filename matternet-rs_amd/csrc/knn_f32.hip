@@ -1467,8 +1467,8 @@ template <bool VEC4, bool SQRT>
 __global__ __launch_bounds__(FST) void k_fb_part(
     const float *__restrict__ Qt, const float *__restrict__ C, int64_t nc, int d, int64_t q_off,
     int64_t c_off, int excl, int keff_max, const int *__restrict__ rows, int nb,
-    const float *__restrict__ ub, int64_t chunk, float2 *__restrict__ plist,
-    int *__restrict__ pcnt) {
+    const float *__restrict__ ub, const float *__restrict__ ub2, int64_t chunk,
+    float2 *__restrict__ plist, int *__restrict__ pcnt) {
     extern __shared__ float4 fsm4[];
     float4 *qs = fsm4;                              // [d][FSQ / 4]: Qt staged
     float *dv = (float *)(qs + (size_t)d * (FSQ / 4));  // [FSQ][FSC]
@@ -1519,7 +1519,7 @@ __global__ __launch_bounds__(FST) void k_fb_part(
     __syncthreads();
     for (int r = 0; r < nb; ++r) {
         const int64_t q = rows[r], gq = q_off + q;
-        const float u = ub ? ub[q] : __builtin_inff();
+        const float u = fminf(ub ? ub[q] : __builtin_inff(), ub2 ? ub2[r] : __builtin_inff());
         if (t == 0) scnt = 0;
         __syncthreads();
         if (c < c1) {
@@ -1569,7 +1569,7 @@ __global__ __launch_bounds__(FMT) void k_fb_merge(
     const float2 *__restrict__ plist, const int *__restrict__ pcnt, int P, int keff_max, int gs,
     float2 *__restrict__ olist, int *__restrict__ ocnt, const int *__restrict__ rows,
     int64_t nc, int64_t q_off, int64_t c_off, int excl, int k, int32_t *__restrict__ out_idx,
-    float *__restrict__ out_dist) {
+    float *__restrict__ out_dist, float *__restrict__ ub_out = nullptr) {
     __shared__ float sd[FMG];
     __shared__ int si[FMG];
     __shared__ int base[FMG / 8 + 1];
@@ -1607,6 +1607,10 @@ __global__ __launch_bounds__(FMT) void k_fb_merge(
         const int64_t q = rows[r], gq = q_off + q;
         const bool self_in = excl && gq >= c_off && gq < c_off + nc;
         const int keff = (int)min((int64_t)k, nc - (self_in ? 1 : 0));
+        if (ub_out) {  // probe pass: the k-th exact distance seen (an upper bound of D_k)
+            if (t == 0) ub_out[r] = (keff > 0 && keep >= keff) ? sd[keff - 1] : __builtin_inff();
+            return;
+        }
         for (int e = t; e < k; e += FMT) {
             const bool ok = e < keff && e < keep;
             out_idx[q * k + e] = ok ? si[e] : -1;
@@ -1646,30 +1650,32 @@ static int fb_split_scan(const float *Q, const float *C, int64_t nc, int d, int6
     const size_t b0 = (l0 * 8 + 255) & ~(size_t)255, b1 = (l1 * 8 + 255) & ~(size_t)255;
     const size_t c0b = ((size_t)FSQ * P * 4 + 255) & ~(size_t)255;
     const size_t qtb = ((size_t)d * FSQ * 4 + 255) & ~(size_t)255;
-    char *g = (char *)scratch(kSlotX1Esc, b0 + b1 + 2 * c0b + qtb + 256);
+    char *g = (char *)scratch(kSlotX1Esc, b0 + b1 + 2 * c0b + qtb + FSQ * 4 + 256);
     if (!g) return MN_ENOMEM;
     float2 *la = (float2 *)g, *lb = (float2 *)(g + b0);
     int *ca = (int *)(g + b0 + b1), *cb = (int *)(g + b0 + b1 + c0b);
     float *Qt = (float *)(g + b0 + b1 + 2 * c0b);
     const bool vec4 = (d % 4 == 0) && (((uintptr_t)Q | (uintptr_t)C) % 16 == 0);
-    for (int r0 = 0; r0 < nfb; r0 += FSQ) {
-        const int nb = std::min(FSQ, nfb - r0);
-        hipLaunchKernelGGL(k_fb_qt, dim3((unsigned)(((int64_t)d * FSQ + 255) / 256)), dim3(256), 0,
-                           s, Q, d, rows + r0, nb, Qt);
+    float *ub2 = (float *)(g + b0 + b1 + 2 * c0b + qtb);  // [FSQ] probe bounds
+    // probe: the first PA parts give every row of the batch an exact upper
+    // bound of D_k (rows without one, e.g. exact ties at distance 0 beyond k
+    // with no candidates, would otherwise keep every part's full list)
+    const int64_t PA = std::min<int64_t>(P, 64);
+    auto pass = [&](int r0, int nb, int64_t Pn, const float *u2, float *uo) -> int {
         auto kp = vec4 ? (sqrt_keys ? k_fb_part<true, true> : k_fb_part<true, false>)
                        : (sqrt_keys ? k_fb_part<false, true> : k_fb_part<false, false>);
         const size_t lds = (size_t)d * FSQ * 4 + (size_t)FSQ * FSC * 4 + (size_t)FSC * 8 + 16;
-        hipLaunchKernelGGL(kp, dim3((unsigned)P), dim3(FST), lds, s, Qt, C, nc, d, q_off, c_off,
-                           excl, keff_max, rows + r0, nb, ub, chunk, la, ca);
+        hipLaunchKernelGGL(kp, dim3((unsigned)Pn), dim3(FST), lds, s, Qt, C, nc, d, q_off, c_off,
+                           excl, keff_max, rows + r0, nb, ub, u2, chunk, la, ca);
         MN_KCHECK(s, "k_fb_part");
-        int Pl = (int)P;
+        int Pl = (int)Pn;
         float2 *src = la, *dst = lb;
         int *sc = ca, *dc = cb;
         while (Pl > gs) {
             const int G = (Pl + gs - 1) / gs;
             hipLaunchKernelGGL(k_fb_merge<false>, dim3((unsigned)(nb * G)), dim3(FMT), 0, s, src,
                                sc, Pl, keff_max, gs, dst, dc, rows + r0, nc, q_off, c_off, excl,
-                               k, out_idx, out_dist);
+                               k, out_idx, out_dist, (float *)nullptr);
             MN_KCHECK(s, "k_fb_merge");
             std::swap(src, dst);
             std::swap(sc, dc);
@@ -1677,8 +1683,22 @@ static int fb_split_scan(const float *Q, const float *C, int64_t nc, int d, int6
         }
         hipLaunchKernelGGL(k_fb_merge<true>, dim3((unsigned)nb), dim3(FMT), 0, s, src, sc, Pl,
                            keff_max, gs, dst, dc, rows + r0, nc, q_off, c_off, excl, k, out_idx,
-                           out_dist);
+                           out_dist, uo);
         MN_KCHECK(s, "k_fb_merge<final>");
+        return MN_OK;
+    };
+    for (int r0 = 0; r0 < nfb; r0 += FSQ) {
+        const int nb = std::min(FSQ, nfb - r0);
+        hipLaunchKernelGGL(k_fb_qt, dim3((unsigned)(((int64_t)d * FSQ + 255) / 256)), dim3(256), 0,
+                           s, Q, d, rows + r0, nb, Qt);
+        const bool probe = P > 4 * PA;
+        if (probe) {
+            const int rc = pass(r0, nb, PA, (const float *)nullptr, ub2);
+            if (rc != MN_OK) return rc;
+        }
+        const int rc = pass(r0, nb, P, probe ? (const float *)ub2 : (const float *)nullptr,
+                            (float *)nullptr);
+        if (rc != MN_OK) return rc;
     }
     return MN_OK;
 }
@@ -2020,17 +2040,18 @@ static int knn_x1(const float *Q, int64_t nq, const float *C, int64_t nc, int32_
 
     // phase-1 sample: the first m0 corpus rows, list length L1 (tau0 ~ the
     // (L1 nc / m0)-th best key); small corpora run phase 1 alone (m0 = nc).
-    // The symmetric sweep (self kNN) takes half the sample with half the list
-    // (the same threshold rank, nc/32 x 8 vs nc/16 x 16: C2 964 vs 1044 ms,
-    // 157 rows left to the split exact scan; profiles/r03f_grid_sample_list.log)
+    // The symmetric sweep (self kNN) samples nc/24 with list 12 (same box,
+    // profiles/r03h_grid_*.log — uniform C2 / clustered C2 ms: nc/16 x 16
+    // 1025 / 1713, nc/24 x 12 978 / 1565, nc/32 x 8 946 / 1976 (its 155k
+    // refilled rows), nc/32 x 12 1004 / 1345)
     const char *sye = getenv("MN_X1_SYM");  // 0: the query-major sweep (A/B)
     const bool sym_pre = same && excl && tmaj && sweep_version() == 2 && !(sye && *sye == '0');
-    int L1 = sym_pre ? std::min(std::max((k + 1) / 4, 8), 48)
+    int L1 = sym_pre ? std::min(std::max((3 * k + 3) / 8, 12), 48)
                      : std::min(std::max((k + 1) / 2, 16), 48);
     const char *fl = getenv("MN_X1_L1");  // experiments: phase-1 list length
     if (fl && *fl) L1 = std::min(std::max(atoi(fl), 4), 48);
     const char *fs = getenv("MN_X1_SAMPLE_DIV");  // experiments: sample = nc / div
-    const int64_t div = (fs && *fs) ? std::max(2, atoi(fs)) : (sym_pre ? 32 : 16);
+    const int64_t div = (fs && *fs) ? std::max(2, atoi(fs)) : (sym_pre ? 24 : 16);
     int64_t m0 = std::max<int64_t>(nc / div, (int64_t)64 * L1);
     m0 = (m0 + 255) / 256 * 256;  // whole phase-1 tiles and whole sweep panels
     const bool two = m0 + 4 * ksw::BC <= nc;
@@ -2182,26 +2203,7 @@ static int knn_x1(const float *Q, int64_t nq, const float *C, int64_t nc, int32_
             const int TPB = (tpe2 && *tpe2) ? std::max(1, atoi(tpe2)) : 256;
             const char *ore = getenv("MN_SYM_ORDER");
             const int order = (ore && *ore) ? atoi(ore) : 1;
-            std::vector<int4> tab;
-            tab.reserve((size_t)nbk * ((size_t)nbk / TPB + 2) / 2 + 16);
-            if (order == 1) {
-                for (int I = 0; I < nbk; ++I)
-                    for (int J0 = I; J0 < nbk;) {
-                        const int J1 = std::min((J0 / TPB + 1) * TPB, nbk);
-                        tab.push_back(make_int4(I, J0, J1, J0 / TPB));
-                        J0 = J1;
-                    }
-                std::stable_sort(tab.begin(), tab.end(), [](const int4 &a, const int4 &b) {
-                    return a.w != b.w ? a.w < b.w : a.x < b.x;
-                });
-            } else {
-                for (int I = 0; I < nbk; ++I)
-                    for (int J0 = I; J0 < nbk; J0 += TPB)
-                        tab.push_back(make_int4(I, J0, std::min(J0 + TPB, nbk), 0));
-                std::stable_sort(tab.begin(), tab.end(), [](const int4 &a, const int4 &b) {
-                    return (a.z - a.y) > (b.z - b.y);
-                });
-            }
+            const std::vector<int4> tab = ksw2::sym_block_table(nbk, TPB, order);
             int4 *dtab = (int4 *)scratch(kSlotSymTab, tab.size() * sizeof(int4) + 64);
             MN_REQUIRE(dtab, MN_ENOMEM, "mn_knn: block table allocation failed");
             MN_HIP_TRY(hipMemcpyAsync(dtab, tab.data(), tab.size() * sizeof(int4),

@@ -29,6 +29,7 @@ for r0 in range(0, n, ch):
 del tmp
 torch.cuda.synchronize()
 variants = os.environ.get("C5P_VARIANTS", "default").split(";")
+ref = None
 for rep in range(int(os.environ.get("C5P_REPS", 1))):
     for v in variants:
         env = {}
@@ -47,12 +48,19 @@ for rep in range(int(os.environ.get("C5P_REPS", 1))):
                 os.environ.pop(k_, None)
             else:
                 os.environ[k_] = val
-        sweep_rows = n - stt.get("sample_rows", 0)
+        same = None
+        if ref is None:
+            ref = (idx.clone(), dist.clone())
+        else:
+            same = bool(torch.equal(ref[0], idx) and torch.equal(ref[1], dist))
+        # the pairs the sweep decides: all n^2 for SW_COS_SYM (sweep_slices -1)
+        sweep_rows = n if stt.get("sweep_slices") == -1 else n - stt.get("sample_rows", 0)
         tf = 2.0 * n * sweep_rows * d / (stt["ms_sweep"] * 1e-3) / 1e12 if stt.get("ms_sweep") else None
         print(json.dumps({"rep": rep, "variant": v, "ms": round(ms, 1),
                           "ms_sample": round(stt.get("ms_sample", 0), 1),
                           "ms_sweep": round(stt.get("ms_sweep", 0), 1),
                           "sweep_tflops": tf and round(tf, 1),
                           "ms_rerank": round(stt["ms_rerank"], 1),
-                          "uncert": stt["n_uncertified"], "S2": stt.get("sweep_slices")}), flush=True)
+                          "uncert": stt["n_uncertified"], "S2": stt.get("sweep_slices"),
+                          "same_as_first": same}), flush=True)
         del idx, dist, w

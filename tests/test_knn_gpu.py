@@ -124,7 +124,8 @@ def test_large_n_sampled_rows_d768(algo):
     # size-independent properties on every row
     assert (np.diff(dist, axis=1) >= 0).all()
     assert (idx != np.arange(n)[:, None]).all()
-    assert st["n_uncertified"] == 0
+    # bf16x1: the n/32 x 8 sample leaves a few rows to the split exact scan
+    assert st["n_uncertified"] <= 64
 
 
 def test_tiny_values_flush_to_exact_path(algo):

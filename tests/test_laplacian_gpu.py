@@ -61,14 +61,16 @@ def test_union_eps_filter_and_hub_rows():
     n, k = 12000, 4
     rng = np.random.default_rng(0)
     idx = rng.integers(0, n, size=(n, k)).astype(np.int32)
-    idx[:, 0] = 0        # node 0 is everybody's neighbour: in-degree ~ n (> 8192: dense path)
-    idx[:700, 1] = 1     # node 1: in-degree ~ 500 valid (block path)
+    idx[:, 0] = 0        # node 0 is everybody's neighbour: in-degree ~ n (one block's LDS sort)
+    idx[:700, 1] = 1     # node 1: in-degree ~ 500 valid (the 16-keys-a-lane wave sort)
     idx[5, 2] = 5        # self loop dropped
     idx[7, 3] = -1       # empty slot
     dist = rng.uniform(0, 2.0, size=(n, k)).astype(np.float64)
     ip, ix, iv, deg = lap(idx, dist, weight_kernel="rational", eps=1.5, sigma=0.7, p=3.0)
     st = S.laplacian.last_stats()
-    assert st["hub_rows"] >= 1 and st["big_rows"] >= 2
+    # rows past the one-wave sort (> 256 entries); hub rows (> 16384: the HBM
+    # network) are covered by test_large_hub_rows_device_sort
+    assert st["big_rows"] >= 2
     d = dist
     w = 1.0 / (1.0 + np.power(d / 0.7, 3.0))
     valid = (d <= 1.5) & (w > 1e-12) & (idx >= 0)
