@@ -178,3 +178,27 @@ def test_two_phase_sorted_rows_stay_certified(kind):
     exact((i, dd, w), O.knn_cos(Xf, 10))
     if kind == "projection":
         assert st["n_uncertified"] <= n // 100, st
+
+
+@pytest.mark.parametrize("kind", ["uniform", "clustered"])
+def test_two_phase_symmetric_sweep_matches_query_major(kind, monkeypatch):
+    """The self item graph's symmetric sweep (gram_sweep2.hpp SW_COS_SYM: rows
+    in descending-threshold order, each unordered pair once, the column's
+    test in the accumulator and the row's key from the same hit; the default)
+    and the query-major SW_COS sweep (MN_BF16_SYM=0): both bit-exact vs the
+    oracle, so identical to each other."""
+    import json
+    X = (datagen.uniform(12_000, 192, seed=17) if kind == "uniform"
+         else datagen.clustered(12_000, 192, seed=18, blobs=16, dup_frac=0.01, zero_frac=0.002))
+    Xt, Xf = bf16_rows(X)
+    kw = dict(eps=0.9, sigma=0.7, p=2.0)
+    i, d, w, st = hip(Xt, 24, timing=True, **kw)
+    print(f"COS_SYM {kind}", json.dumps({k: (round(v, 2) if isinstance(v, float) else v)
+                                         for k, v in st.items()}))
+    assert st["sweep_slices"] == -1  # the symmetric sweep ran
+    monkeypatch.setenv("MN_BF16_SYM", "0")
+    i0, d0, w0, st0 = hip(Xt, 24, **kw)
+    assert st0["sweep_slices"] > 0
+    ref = O.knn_cos(Xf, 24, **kw)
+    exact((i, d, w), ref)
+    exact((i0, d0, w0), ref)
