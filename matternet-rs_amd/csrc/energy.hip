@@ -42,7 +42,6 @@ namespace mn {
 namespace energy {
 
 constexpr int FMAX = 4096;             // row length limit (registers: FMAX/64 per lane)
-constexpr int ROWS = 2;                // item rows per wave per pass (interleaved in LDS)
 constexpr size_t LDS_BUDGET = 160 * 1024;
 constexpr size_t EDGE_LDS_MAX = 96 * 1024;  // entry lists kept in LDS up to this size
 
@@ -109,21 +108,24 @@ __global__ __launch_bounds__(256) void k_check_sym(const int64_t *__restrict__ i
 // taumode = ordered pairs i != j (taumode.rs:366-408), energymaps = j > i
 // (energymaps.rs:990-1030), spectral = ordered pairs with W = max(0, -L)
 // (spectral/mod.rs:115-140: the diagonal's (x_f - x_f)^2 term is 0).
-__device__ __forceinline__ int entry_class(int i, int j, double v, int sym, int g_mode) {
+//   D (2)  the diagonal, when split_diag (k_energy_rows2): summed per feature
+//          into dg[i] and applied from the lane's own row registers.
+__device__ __forceinline__ int entry_class(int i, int j, double v, int sym, int g_mode,
+                                           int split_diag = 0) {
     if (sym && j < i) return -1;  // covered by (j, i)
-    if (i == j) return 1;
+    if (i == j) return split_diag ? 2 : 1;
     const bool counts = (g_mode != MN_G_ENERGYMAPS) || sym || j > i;
     return (counts && -v > 0.0) ? 0 : 1;
 }
 
 __global__ void k_count_entries(const int64_t *__restrict__ ip, const int32_t *__restrict__ ix,
-                                Vals v, int f, int sym, int g_mode,
+                                Vals v, int f, int sym, int g_mode, int split_diag,
                                 int32_t *__restrict__ cnt) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= f) return;
     int ca = 0, cb = 0;
     for (int64_t p = ip[i]; p < ip[i + 1]; ++p) {
-        const int c = entry_class(i, ix[p], v[p], sym, g_mode);
+        const int c = entry_class(i, ix[p], v[p], sym, g_mode, split_diag);
         ca += c == 0;
         cb += c == 1;
     }
@@ -132,20 +134,26 @@ __global__ void k_count_entries(const int64_t *__restrict__ ip, const int32_t *_
 }
 
 __global__ void k_fill_entries(const int64_t *__restrict__ ip, const int32_t *__restrict__ ix,
-                               Vals v, int f, int sym, int g_mode,
+                               Vals v, int f, int sym, int g_mode, int split_diag,
                                const int64_t *__restrict__ off, uint32_t *__restrict__ eij,
-                               double *__restrict__ ev) {
+                               double *__restrict__ ev, double *__restrict__ dg) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= f) return;
     int64_t qa = off[i], qb = off[f + i];
+    double di = 0.0;  // the row's diagonal entries in CSR order (one thread: deterministic)
     for (int64_t p = ip[i]; p < ip[i + 1]; ++p) {
         const int j = ix[p];
-        const int c = entry_class(i, j, v[p], sym, g_mode);
+        const int c = entry_class(i, j, v[p], sym, g_mode, split_diag);
+        if (c == 2) {
+            di += v[p];
+            continue;
+        }
         if (c < 0) continue;
         const int64_t q = c == 0 ? qa++ : qb++;
         eij[q] = (uint32_t)i | ((uint32_t)j << 16);
         ev[q] = c == 0 ? -v[p] : ((sym && i != j) ? 2.0 * v[p] : v[p]);
     }
+    if (split_diag) dg[i] = di;
 }
 
 // ---- wave-level exact order statistic on f32 keys -------------------------
@@ -315,7 +323,7 @@ __device__ double row_tau(const uint32_t (&keys)[NR], int f, double msum, int ta
     const int lane = threadIdx.x & 63;
     const int rank = (tau_mode == MN_TAU_PERCENTILE) ? pct_rank : ((f % 2 == 1) ? f / 2 : f / 2 - 1);
     // sel 1: value-linear buckets (wave_select_lin), else the radix select
-    const uint32_t ka = sel == 1 ? wave_select_lin<NR>(keys, f, rank, hist)
+    const uint32_t ka = (sel & 1) ? wave_select_lin<NR>(keys, f, rank, hist)
                                  : wave_select<NR>(keys, NR, rank, hist);
     double med = (double)key2f(ka);
     if (tau_mode == MN_TAU_MEDIAN && f % 2 == 0) {
@@ -377,7 +385,8 @@ __global__ __launch_bounds__(NR <= 16 ? 1024 : 256) void k_energy_rows(
 #pragma unroll
         for (int t = 0; t < ROWS; ++t) {
             // a missing last row repeats the previous one (computed, not written)
-            const float *xr = X + min(r0 + t, n - 1) * (int64_t)f;
+            // (sel & 16: timing probe, every pass re-reads row 0)
+            const float *xr = X + ((sel & 16) ? 0 : min(r0 + t, n - 1)) * (int64_t)f;
             double dn = 0.0, ms = 0.0;
             bool nz = false;
 #pragma unroll
@@ -414,7 +423,9 @@ __global__ __launch_bounds__(NR <= 16 ? 1024 : 256) void k_energy_rows(
         for (int64_t p = lane; p < na; p += 64) {
             const uint32_t ij = EIJ[p];
             const double wv = EV[p];
-            const int i = (int)(ij & 0xFFFFu), j = (int)(ij >> 16);
+            // (sel & 32: timing probe, conflict-free gathers of fixed features)
+            const int i = (sel & 32) ? lane : (int)(ij & 0xFFFFu);
+            const int j = (sel & 32) ? lane + 64 : (int)(ij >> 16);
             const gat_t gi = *reinterpret_cast<const gat_t *>(&xs[i * ROWS]);
             const gat_t gj = *reinterpret_cast<const gat_t *>(&xs[j * ROWS]);
             float ai[ROWS], aj[ROWS];
@@ -435,7 +446,8 @@ __global__ __launch_bounds__(NR <= 16 ? 1024 : 256) void k_energy_rows(
         for (int64_t p = na + lane; p < ne; p += 64) {
             const uint32_t ij = EIJ[p];
             const double v = EV[p];
-            const int i = (int)(ij & 0xFFFFu), j = (int)(ij >> 16);
+            const int i = (sel & 32) ? lane : (int)(ij & 0xFFFFu);
+            const int j = (sel & 32) ? lane + 64 : (int)(ij >> 16);
             const gat_t gi = *reinterpret_cast<const gat_t *>(&xs[i * ROWS]);
             const gat_t gj = *reinterpret_cast<const gat_t *>(&xs[j * ROWS]);
             float ai[ROWS], aj[ROWS];
@@ -471,6 +483,413 @@ __global__ __launch_bounds__(NR <= 16 ? 1024 : 256) void k_energy_rows(
                                                    pct_rank, hist, sel);
                     const double ebv = e_raw / (e_raw + tau);
                     lam = tau * ebv + (1.0 - tau) * g_raw;
+                } else {
+                    lam = e_raw;
+                }
+            }
+            if (lane == 0 && r0 + t < n) {
+                if (Eo) Eo[r0 + t] = e_raw;
+                if (Go) Go[r0 + t] = g_raw;
+                if (Lo) Lo[r0 + t] = lam;
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+    }
+}
+
+// ---- K3 v2: counted order statistics, diagonal from registers, prefetch ----
+// Column c of one row through a buffer resource sized to the row: columns
+// >= f read 0 without a branch (a guarded `c < f ? x[c] : 0` compiles to a
+// branch with its own vmcnt(0) wait — one serial HBM trip per register).
+// `row` must be wave-uniform.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t row_rsrc(const float *row, int f) {
+    return __builtin_amdgcn_make_buffer_rsrc((void *)row, (short)0, f * 4, 0x00020000);
+}
+__device__ __forceinline__ float row_at(__amdgpu_buffer_rsrc_t rs, int c) {
+    return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, c * 4, 0, 0));
+}
+
+// Wave reductions through DPP (quad_perm xor 1 / xor 2, row half-mirror, row
+// mirror, row_bcast15 / row_bcast31): six VALU steps with no LDS round trip
+// (a __shfl_xor is a ds_bpermute each).  The total lands in lane 63 and is
+// read out wave-uniform.
+template <int CTRL, int RM>
+__device__ __forceinline__ uint32_t dpp32(uint32_t old, uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp((int)old, (int)v, CTRL, RM, 0xF, false);
+}
+template <int CTRL, int RM>
+__device__ __forceinline__ double dpp64(double old, double v) {
+    const uint64_t o = __double_as_longlong(old), u = __double_as_longlong(v);
+    const uint32_t lo = dpp32<CTRL, RM>((uint32_t)o, (uint32_t)u);
+    const uint32_t hi = dpp32<CTRL, RM>((uint32_t)(o >> 32), (uint32_t)(u >> 32));
+    return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+__device__ __forceinline__ uint32_t lane63_u32(uint32_t x) {
+    return (uint32_t)__builtin_amdgcn_readlane((int)x, 63);
+}
+__device__ __forceinline__ uint32_t wave_umin_dpp(uint32_t x) {
+    x = min(x, dpp32<0xB1, 0xF>(x, x));
+    x = min(x, dpp32<0x4E, 0xF>(x, x));
+    x = min(x, dpp32<0x141, 0xF>(x, x));
+    x = min(x, dpp32<0x140, 0xF>(x, x));
+    x = min(x, dpp32<0x142, 0xA>(x, x));
+    x = min(x, dpp32<0x143, 0xC>(x, x));
+    return lane63_u32(x);
+}
+__device__ __forceinline__ uint32_t wave_umax_dpp(uint32_t x) {
+    x = max(x, dpp32<0xB1, 0xF>(x, x));
+    x = max(x, dpp32<0x4E, 0xF>(x, x));
+    x = max(x, dpp32<0x141, 0xF>(x, x));
+    x = max(x, dpp32<0x140, 0xF>(x, x));
+    x = max(x, dpp32<0x142, 0xA>(x, x));
+    x = max(x, dpp32<0x143, 0xC>(x, x));
+    return lane63_u32(x);
+}
+// (`old` = x: lanes a row mask leaves out keep garbage that never reaches
+// lane 63 — rows 1 and 3 are written by the bcast15 step, row 3 by bcast31)
+__device__ __forceinline__ double wave_sum_dpp(double x) {
+    x += dpp64<0xB1, 0xF>(x, x);
+    x += dpp64<0x4E, 0xF>(x, x);
+    x += dpp64<0x141, 0xF>(x, x);
+    x += dpp64<0x140, 0xF>(x, x);
+    x += dpp64<0x142, 0xA>(x, x);
+    x += dpp64<0x143, 0xC>(x, x);
+    const uint64_t u = __double_as_longlong(x);
+    const uint32_t lo = lane63_u32((uint32_t)u), hi = lane63_u32((uint32_t)(u >> 32));
+    return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+
+// keys <= k over the wave's row (pads 0xFFFFFFFF never count: k < 0xFFFFFFFF)
+template <int NR>
+__device__ __forceinline__ int wave_cle(const uint32_t (&keys)[NR], uint32_t k) {
+    int c = 0;
+#pragma unroll
+    for (int r = 0; r < NR; ++r) c += (int)__popcll(__ballot(keys[r] <= k));
+    return c;
+}
+
+// Exact order statistic `rank` (and rank + 1 when need == 2) of a row's f keys
+// (pads 0xFFFFFFFF) without a histogram: a bracket (kA, kB] with
+// cle(kA) <= rank and cle(kB) >= rank + need is narrowed by pairs of
+// value-interpolated probes (+-hw keys at the bracket's mean density; a probe
+// is NR compares + ballot popcounts, no LDS) until it holds <= 20 keys (<= 64
+// after 8 rounds); those are compacted into LDS and each lane ranks its own
+// candidate by counting over broadcast reads (sorted position t holds the u
+// with #(< u) <= t < #(<= u)).  false: the row did not settle (non-finite
+// values, > 64 tied keys, skewed rows) — the caller runs the radix select.
+template <int NR>
+__device__ bool wave_select_cnt(const uint32_t (&keys)[NR], int f, int rank, int need,
+                                uint32_t *cand, uint32_t &out0, uint32_t &out1) {
+    const int lane = threadIdx.x & 63;
+    uint32_t kmin = 0xFFFFFFFFu, kmax = 0u;
+#pragma unroll
+    for (int r = 0; r < NR; ++r) {
+        if (lane + 64 * r < f) {
+            kmin = keys[r] < kmin ? keys[r] : kmin;
+            kmax = keys[r] > kmax ? keys[r] : kmax;
+        }
+    }
+    kmin = wave_umin_dpp(kmin);
+    kmax = wave_umax_dpp(kmax);
+    if (kmin == kmax) {
+        out0 = out1 = kmin;
+        return true;
+    }
+    if (!__builtin_isfinite(key2f(kmin)) || !__builtin_isfinite(key2f(kmax))) return false;
+    uint32_t kA = kmin - 1u, kB = kmax;  // finite keys are >= f2key(-FLT_MAX) > 0
+    int cA = 0, cB = f;
+    for (int it = 0; it < 8 && cB - cA > 20; ++it) {
+        const float vlo = key2f(kA + 1u), vhi = key2f(kB);
+        const int m = cB - cA;
+        const float span = vhi - vlo;
+        if (!(span > 0.f)) break;  // one value left (ties): compact or fall back
+        const int hw = m / 6 < 6 ? 6 : (m / 6 > 24 ? 24 : m / 6);
+        const float est = vlo + span * (((float)(rank - cA) + 0.5f * (float)need) / (float)m);
+        const float half = span * ((float)hw / (float)m);
+        const float p1 = fmaxf(est - half, vlo), p2 = fminf(est + half, vhi);
+        const uint32_t k1 = f2key(p1), k2 = f2key(p2);
+        const int c1 = wave_cle<NR>(keys, k1), c2 = wave_cle<NR>(keys, k2);
+        if (c1 <= rank) {
+            if (k1 > kA) { kA = k1; cA = c1; }
+        } else if (c1 >= rank + need && k1 < kB) {
+            kB = k1; cB = c1;
+        }
+        if (c2 <= rank) {
+            if (k2 > kA) { kA = k2; cA = c2; }
+        } else if (c2 >= rank + need && k2 < kB) {
+            kB = k2; cB = c2;
+        }
+    }
+    const int m = cB - cA;
+    if (m > 64) return false;
+    int base = 0;
+#pragma unroll
+    for (int r = 0; r < NR; ++r) {
+        const bool in = keys[r] > kA && keys[r] <= kB;  // pads exceed kB (finite)
+        const uint64_t mk = __ballot(in);
+        if (in) cand[base + (int)__popcll(mk & ((1ull << lane) - 1ull))] = keys[r];
+        base += (int)__popcll(mk);
+    }
+    if (lane >= m) cand[lane] = 0xFFFFFFFFu;
+    __builtin_amdgcn_wave_barrier();
+    const uint32_t u = cand[lane];
+    int lt = 0, le = 0;
+    for (int q = 0; q < m; q += 4) {
+        const uint4 v = *reinterpret_cast<const uint4 *>(&cand[q]);
+        lt += (v.x < u) + (v.y < u) + (v.z < u) + (v.w < u);
+        le += (v.x <= u) + (v.y <= u) + (v.z <= u) + (v.w <= u);
+    }
+    const int t0 = rank - cA;
+    const uint64_t h0 = __ballot(lane < m && lt <= t0 && t0 < le);
+    out0 = (uint32_t)__builtin_amdgcn_readlane((int)u, (int)__builtin_ctzll(h0));
+    if (need == 2) {
+        const uint64_t h1 = __ballot(lane < m && lt <= t0 + 1 && t0 + 1 < le);
+        out1 = (uint32_t)__builtin_amdgcn_readlane((int)u, (int)__builtin_ctzll(h1));
+    } else {
+        out1 = out0;
+    }
+    __builtin_amdgcn_wave_barrier();  // cand is reused by the next row
+    return true;
+}
+
+// Median / Percentile tau of every row, one wave per row (grid-stride), for
+// k_energy_rows2: a lean kernel (keys in registers, 1 KB LDS per wave) at
+// high occupancy re-reads X instead of holding the select's registers and
+// latency inside the entry-loop kernel (which keeps Fixed / Mean inline).
+template <int NR>
+__global__ __launch_bounds__(256) void k_row_tau(const float *__restrict__ X, int64_t n, int f,
+                                                 int tau_mode, double tau_param, int pct_rank,
+                                                 double *__restrict__ tau) {
+    __shared__ __attribute__((aligned(16))) int hist_all[4][256];
+    const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    int *hist = hist_all[w];
+    const bool med = tau_mode == MN_TAU_MEDIAN;
+    const int rank = med ? ((f % 2 == 1) ? f / 2 : f / 2 - 1) : pct_rank;
+    const int need = (med && f % 2 == 0) ? 2 : 1;
+    const int64_t rstride = (int64_t)gridDim.x * 4;
+    int64_t row = (int64_t)blockIdx.x * 4 + w;
+    float xv[NR];
+    auto load_row = [&](int64_t rw) {
+        const __amdgpu_buffer_rsrc_t rs = row_rsrc(X + rw * (int64_t)f, f);
+#pragma unroll
+        for (int r = 0; r < NR; ++r) xv[r] = row_at(rs, lane + 64 * r);
+        __builtin_amdgcn_sched_barrier(0);  // all loads issue before any use
+    };
+    if (row < n) load_row(row);
+    for (; row < n; row += rstride) {
+        uint32_t keys[NR];
+#pragma unroll
+        for (int r = 0; r < NR; ++r) keys[r] = lane + 64 * r < f ? f2key(xv[r]) : 0xFFFFFFFFu;
+        if (row + rstride < n) load_row(row + rstride);  // next row in flight during the select
+        uint32_t k0, k1;
+        double v;
+        if (wave_select_cnt<NR>(keys, f, rank, need, (uint32_t *)hist, k0, k1)) {
+            v = (double)key2f(k0);
+            if (need == 2) v = 0.5 * (v + (double)key2f(k1));
+            v = fmax(v, 1e-10);
+        } else {
+            v = row_tau<NR>(keys, f, 0.0, tau_mode, tau_param, pct_rank, hist);
+        }
+        if (lane == 0) tau[row] = v;
+    }
+}
+
+// Two item rows per wave pass (as k_energy_rows), reorganised:
+//  - the Laplacian diagonal (class D) is applied from the rows' registers
+//    while they are staged (sum dg_c x_c^2): no gathers for it;
+//  - the entry lists hold byte offsets of x_i / x_j in the wave's stage
+//    (i*8 | j*8 << 16) and are padded to whole 4-entry-per-lane chunks with
+//    entries at a zero slot past the row (exact no-ops), so the loop has no
+//    tail and issues 4 entry reads, then 8 gathers, per lane at a time;
+//  - the next pass's rows are loaded into registers while this pass runs
+//    (the HBM latency hides behind the entry loop);
+//  - Median / Percentile tau come from k_row_tau (counted selection).
+// LDS: eij u32 [neP] | ev f64 [neP] | dg f64 [fpad] | per wave: xs f32
+// [fpad + 1][2] (slot fpad = 0).
+constexpr int E2_CH = 256;  // entries per chunk (4 per lane)
+constexpr int E2_MIN_WAVES = 4;
+// k_energy_rows2's LDS: the padded lists + dg, plus `waves` wave stages
+static inline size_t e2_lds_bytes(int64_t na, int64_t nb, int f, int waves, bool tk = false) {
+    const int64_t neP = (na + E2_CH - 1) / E2_CH * E2_CH + (nb + E2_CH - 1) / E2_CH * E2_CH;
+    const size_t fpad = (size_t)((f + 3) & ~3);
+    return (((size_t)neP * 4 + 15) & ~(size_t)15) + (size_t)neP * 8 + fpad * 8 +
+           (size_t)waves * ((fpad + 4) * 8 + (tk ? 1024 : 0));
+}
+template <int NR, bool TK>
+__global__ __launch_bounds__(1024) void k_energy_rows2(
+    const float *__restrict__ X, int64_t n, int f, int64_t na, int64_t naP, int64_t nb,
+    int64_t nbP, const uint32_t *__restrict__ geij, const double *__restrict__ gev,
+    const double *__restrict__ gdg, double mA_num, double mA_g, int g_mode, int tau_mode,
+    double tau_param, int pct_rank, const double *__restrict__ tau_in, double *__restrict__ Eo,
+    double *__restrict__ Go, double *__restrict__ Lo) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char dsm[];
+    const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int nw = blockDim.x >> 6;
+    const int fpad = (f + 3) & ~3;
+    const int64_t neP = naP + nbP;
+    uint32_t *seij = (uint32_t *)dsm;
+    double *sev = (double *)(dsm + (((size_t)neP * 4 + 15) & ~(size_t)15));
+    double *sdg = sev + neP;
+    const size_t wbytes = (size_t)(fpad + 4) * 8 + (TK ? 1024 : 0);
+    float *xs = (float *)((unsigned char *)(sdg + fpad) + (size_t)w * wbytes);
+    int *hist = (int *)(xs + 2 * (fpad + 4));  // TK: the select's scratch
+    const uint32_t zoff = (uint32_t)fpad * 8u;  // the zero slot
+    const uint32_t zpair = zoff | (zoff << 16);
+    for (int64_t p = threadIdx.x; p < neP; p += blockDim.x) {
+        const int64_t q = p < naP ? p : na + (p - naP);  // source index
+        const bool real = p < naP ? p < na : (p - naP) < nb;
+        uint32_t e = zpair;
+        double v = 0.0;
+        if (real) {
+            const uint32_t ij = geij[q];
+            e = ((ij & 0xFFFFu) * 8u) | (((ij >> 16) * 8u) << 16);
+            v = gev[q];
+        }
+        seij[p] = e;
+        sev[p] = v;
+    }
+    for (int c = threadIdx.x; c < fpad; c += blockDim.x) sdg[c] = c < f ? gdg[c] : 0.0;
+    if (lane < 8) xs[2 * fpad + lane] = 0.f;
+    __syncthreads();
+    const unsigned char *xsb = (const unsigned char *)xs;
+    const bool mean_tau = g_mode == MN_G_TAUMODE && tau_mode == MN_TAU_MEAN;
+    const int64_t npass = (n + 1) / 2;
+    const int64_t pstride = (int64_t)gridDim.x * nw;
+    int64_t ps = (int64_t)blockIdx.x * nw + w;
+    float cur[2][NR];
+    auto load_rows = [&](int64_t pq, float (&dst)[2][NR]) {
+        const int64_t r0 = pq * 2;
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+            // a missing last row repeats (computed, not written)
+            const __amdgpu_buffer_rsrc_t rs = row_rsrc(X + min(r0 + t, n - 1) * (int64_t)f, f);
+#pragma unroll
+            for (int r = 0; r < NR; ++r) dst[t][r] = row_at(rs, lane + 64 * r);
+        }
+        __builtin_amdgcn_sched_barrier(0);  // all loads issue before any use
+    };
+    if (ps < npass) load_rows(ps, cur);
+    for (; ps < npass; ps += pstride) {
+        const int64_t r0 = ps * 2;
+        double den[2] = {0.0, 0.0}, msum[2] = {0.0, 0.0}, numD[2] = {0.0, 0.0};
+        bool nzr[2] = {false, false};
+#pragma unroll
+        for (int r = 0; r < NR; ++r) {
+            const int c = lane + 64 * r;
+            if (c < f) {
+                const double dgc = sdg[c];
+                *reinterpret_cast<float2 *>(&xs[2 * c]) = make_float2(cur[0][r], cur[1][r]);
+#pragma unroll
+                for (int t = 0; t < 2; ++t) {
+                    const double xd = (double)cur[t][r];
+                    const double x2 = xd * xd;
+                    den[t] += x2;
+                    if (mean_tau) msum[t] += xd;
+                    numD[t] = __builtin_fma(dgc, x2, numD[t]);
+                    nzr[t] |= !(fabs(xd) <= 1e-10);
+                }
+            }
+        }
+        // tau: per-row Median / Percentile from k_row_tau (tau_in), in this
+        // kernel (TK, MN_ENERGY_TAU=1 A/B), else Fixed / Mean inline
+        double tau[2] = {0.0, 0.0};
+        uint32_t keys[TK ? 2 : 1][NR];
+        if (TK) {
+#pragma unroll
+            for (int t = 0; t < (TK ? 2 : 1); ++t)
+#pragma unroll
+                for (int r = 0; r < NR; ++r)
+                    keys[t][r] = lane + 64 * r < f ? f2key(cur[t][r]) : 0xFFFFFFFFu;
+        }
+        // the next pass's rows: in flight during this pass's select + entry loop
+        if (ps + pstride < npass) load_rows(ps + pstride, cur);
+        if (g_mode == MN_G_TAUMODE) {
+#pragma unroll
+            for (int t = 0; t < 2; ++t) {
+                if (TK && (tau_mode == MN_TAU_MEDIAN || tau_mode == MN_TAU_PERCENTILE)) {
+                    const bool med = tau_mode == MN_TAU_MEDIAN;
+                    const int rank = med ? ((f % 2 == 1) ? f / 2 : f / 2 - 1) : pct_rank;
+                    const int need = (med && f % 2 == 0) ? 2 : 1;
+                    uint32_t k0, k1;
+                    if (wave_select_cnt<NR>(keys[TK ? t : 0], f, rank, need, (uint32_t *)hist, k0,
+                                            k1)) {
+                        double v = (double)key2f(k0);
+                        if (need == 2) v = 0.5 * (v + (double)key2f(k1));
+                        tau[t] = fmax(v, 1e-10);
+                    } else {
+                        tau[t] = row_tau<NR>(keys[TK ? t : 0], f, msum[t], tau_mode, tau_param,
+                                             pct_rank, hist);
+                    }
+                } else if (tau_in) {
+                    tau[t] = tau_in[min(r0 + t, n - 1)];
+                } else if (tau_mode == MN_TAU_MEAN) {
+                    tau[t] = fmax(wave_sum_dpp(msum[t]) / (double)f, 1e-10);
+                } else {
+                    tau[t] = (isfinite(tau_param) && tau_param > 0.0) ? tau_param : 1e-10;
+                }
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+        double nA0 = 0.0, nA1 = 0.0, S0 = 0.0, S1 = 0.0, Q0 = 0.0, Q1 = 0.0;
+        for (int64_t p0 = lane; p0 < naP; p0 += E2_CH) {
+            uint32_t ij[4];
+            double wv[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                ij[u] = seij[p0 + 64 * u];
+                wv[u] = sev[p0 + 64 * u];
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const float2 gi = *reinterpret_cast<const float2 *>(xsb + (ij[u] & 0xFFFFu));
+                const float2 gj = *reinterpret_cast<const float2 *>(xsb + (ij[u] >> 16));
+                const double xi0 = (double)gi.x, xj0 = (double)gj.x;
+                const double xi1 = (double)gi.y, xj1 = (double)gj.y;
+                nA0 = __builtin_fma(-wv[u], xi0 * xj0, nA0);
+                nA1 = __builtin_fma(-wv[u], xi1 * xj1, nA1);
+                const double d0 = xi0 - xj0, d1 = xi1 - xj1;
+                const double e0 = (d0 * d0) * wv[u], e1 = (d1 * d1) * wv[u];
+                S0 += e0;
+                S1 += e1;
+                Q0 = __builtin_fma(e0, e0, Q0);
+                Q1 = __builtin_fma(e1, e1, Q1);
+            }
+        }
+        double nB0 = 0.0, nB1 = 0.0;
+        for (int64_t p0 = naP + lane; p0 < neP; p0 += E2_CH) {
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const uint32_t ij = seij[p0 + 64 * u];
+                const double v = sev[p0 + 64 * u];
+                const float2 gi = *reinterpret_cast<const float2 *>(xsb + (ij & 0xFFFFu));
+                const float2 gj = *reinterpret_cast<const float2 *>(xsb + (ij >> 16));
+                nB0 = __builtin_fma(v, (double)gi.x * (double)gj.x, nB0);
+                nB1 = __builtin_fma(v, (double)gi.y * (double)gj.y, nB1);
+            }
+        }
+        const double nAs[2] = {nA0, nA1}, nBs[2] = {nB0, nB1}, Sv[2] = {S0, S1}, Qv[2] = {Q0, Q1};
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+            const double num = wave_sum_dpp(mA_num * nAs[t] + nBs[t] + numD[t]);
+            const double Ss = mA_g * wave_sum_dpp(Sv[t]);
+            const double Qs = mA_g * wave_sum_dpp(Qv[t]);
+            const double dn = wave_sum_dpp(den[t]);
+            const bool nonzero = __any(nzr[t]) != 0;
+            double e_raw = 0.0, g_raw = 0.0, lam = 0.0;
+            if (g_mode == MN_G_SPECTRAL) {
+                const double rr = num / (dn + 1e-9);
+                e_raw = rr < -1e6 ? -1e6 : (rr > 1e6 ? 1e6 : rr);
+                g_raw = Ss;
+                lam = e_raw;
+            } else if (!(g_mode == MN_G_TAUMODE && !nonzero)) {  // zero vector: lambda 0
+                e_raw = dn > 1e-12 ? fmax(num / dn, 0.0) : 0.0;
+                if (Ss > 1e-12) {
+                    const double g = Qs / (Ss * Ss);
+                    g_raw = g < 0.0 ? 0.0 : (g > 1.0 ? 1.0 : g);
+                }
+                if (g_mode == MN_G_TAUMODE) {
+                    const double ebv = e_raw / (e_raw + tau[t]);
+                    lam = tau[t] * ebv + (1.0 - tau[t]) * g_raw;
                 } else {
                     lam = e_raw;
                 }
@@ -898,7 +1317,7 @@ static int energy_impl(const mn_csr *L, const float *X, int64_t n, int32_t f,
     const bool spec = opts->g_mode == MN_G_SPECTRAL;
     const Vals vals{L->values, L->value_type == MN_F32 ? 1 : 0};
     char *g = (char *)scratch(kSlotGeneric0, (size_t)nnz * 12 + (size_t)f * 8 +
-                                                 (size_t)(2 * f + 1) * 8 + 256);
+                                                 (size_t)(2 * f + 1) * 8 + (size_t)f * 8 + 256);
     if (spec) {  // E and the raw row energies are needed for the global pass
         double *sc = (double *)scratch(kSlotNorms2, (size_t)n * 16 + 8 * SUM_BLOCKS + 64);
         MN_REQUIRE(sc, MN_ENOMEM, "mn_energy_rows: scratch allocation failed");
@@ -910,7 +1329,8 @@ static int energy_impl(const mn_csr *L, const float *X, int64_t n, int32_t f,
     int32_t *cnt = (int32_t *)(eij + nnz);
     double *ev = (double *)(((uintptr_t)(cnt + 2 * f) + 15) & ~(uintptr_t)15);
     int64_t *off = (int64_t *)(ev + nnz);
-    int *flag = (int *)(off + 2 * f);
+    double *dg = (double *)(off + 2 * f);
+    int *flag = (int *)(dg + f);
 
     Timer tm;
     tm.start(opts->timing != 0, s);
@@ -924,11 +1344,18 @@ static int energy_impl(const mn_csr *L, const float *X, int64_t n, int32_t f,
     MN_HIP_TRY(hipStreamSynchronize(s));
     MN_REQUIRE(!(hflag & 2), MN_EINVAL, "mn_energy_rows: Laplacian column index out of range");
     const int sym = (hflag & 1) ? 0 : 1;
-    hipLaunchKernelGGL(k_count_entries, dim3(fb), dim3(256), 0, s, L->indptr, L->indices, vals,
-                       f, sym, opts->g_mode, cnt);
-    // tiny scan on the host side of the stream (f <= 4096): list A, then B
+    // k_energy_rows2 (default for f <= 1024; MN_ENERGY_V1=1: the round-2
+    // kernels) takes the diagonal apart from the entry lists
+    const char *v1e = getenv("MN_ENERGY_V1");
+    const int nr = (f + 63) / 64;
+    int split = (nr <= 16 && !(v1e && *v1e == '1')) ? 1 : 0;
+    int64_t na = 0, ne = 0;
     std::vector<int32_t> hc(2 * (size_t)f);
     std::vector<int64_t> ho(2 * (size_t)f);
+    for (int attempt = 0; attempt < 2; ++attempt) {
+    hipLaunchKernelGGL(k_count_entries, dim3(fb), dim3(256), 0, s, L->indptr, L->indices, vals,
+                       f, sym, opts->g_mode, split, cnt);
+    // tiny scan on the host side of the stream (f <= 4096): list A, then B
     MN_HIP_TRY(hipMemcpyAsync(hc.data(), cnt, 8 * (size_t)f, hipMemcpyDeviceToHost, s));
     MN_HIP_TRY(hipStreamSynchronize(s));
     int64_t acc = 0;
@@ -936,10 +1363,17 @@ static int energy_impl(const mn_csr *L, const float *X, int64_t n, int32_t f,
         ho[i] = acc;
         acc += hc[i];
     }
-    const int64_t na = ho[f], ne = acc;
+    na = ho[f];
+    ne = acc;
+    if (split && e2_lds_bytes(na, ne - na, f, E2_MIN_WAVES) > LDS_BUDGET) {
+        split = 0;  // lists too long for the v2 LDS plan: rebuild them whole
+        continue;
+    }
+    break;
+    }
     MN_HIP_TRY(hipMemcpyAsync(off, ho.data(), 16 * (size_t)f, hipMemcpyHostToDevice, s));
     hipLaunchKernelGGL(k_fill_entries, dim3(fb), dim3(256), 0, s, L->indptr, L->indices, vals, f,
-                       sym, opts->g_mode, off, eij, ev);
+                       sym, opts->g_mode, split, off, eij, ev, dg);
     int pct_rank = 0;
     if (opts->tau_mode == MN_TAU_PERCENTILE) {
         double pp = opts->tau_param;
@@ -952,7 +1386,62 @@ static int energy_impl(const mn_csr *L, const float *X, int64_t n, int32_t f,
     const double mA_num = sym ? 2.0 : 1.0;
     const double mA_g = (sym && opts->g_mode != MN_G_ENERGYMAPS) ? 2.0 : 1.0;
     tm.mark();
-    const int nr = (f + 63) / 64;
+    if (split) {
+        const int64_t naP = (na + E2_CH - 1) / E2_CH * E2_CH;
+        const int64_t nbP = (ne - na + E2_CH - 1) / E2_CH * E2_CH;
+        const char *tke = getenv("MN_ENERGY_TAU");  // 1: the select inside the entry-loop kernel
+        const bool tk = tke && *tke == '1';
+        const size_t fixed = e2_lds_bytes(na, ne - na, f, 0);
+        const size_t wbytes = e2_lds_bytes(na, ne - na, f, 1, tk) - fixed;
+        const int nw2 = (int)std::min<size_t>(16, (LDS_BUDGET - fixed) / wbytes);
+        const size_t sh2 = fixed + (size_t)nw2 * wbytes;
+        const int64_t npass2 = (n + 1) / 2;
+        const int64_t blocks2 = std::min<int64_t>((npass2 + nw2 - 1) / nw2, 1024);
+        double *tau_d = nullptr;
+        if (!tk && opts->g_mode == MN_G_TAUMODE &&
+            (opts->tau_mode == MN_TAU_MEDIAN || opts->tau_mode == MN_TAU_PERCENTILE)) {
+            tau_d = (double *)scratch(kSlotGeneric1, (size_t)n * 8 + 64);
+            MN_REQUIRE(tau_d, MN_ENOMEM, "mn_energy_rows: tau scratch allocation failed");
+            // one resident wave set, no second round: blocks = occupancy x CUs
+            int dev = 0, ncu = 256;
+            MN_HIP_TRY(hipGetDevice(&dev));
+            MN_HIP_TRY(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+#define MN_TAU(NRV)                                                                             \
+    do {                                                                                        \
+        int occ = 1;                                                                            \
+        MN_HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_row_tau<NRV>, 256, 0));   \
+        const unsigned tb = (unsigned)std::min<int64_t>((n + 3) / 4, (int64_t)std::max(occ, 1) * ncu); \
+        hipLaunchKernelGGL((k_row_tau<NRV>), dim3(tb), dim3(256), 0, s, X, n, f, opts->tau_mode, \
+                           opts->tau_param, pct_rank, tau_d);                                   \
+    } while (0)
+            if (nr <= 4) MN_TAU(4);
+            else if (nr <= 8) MN_TAU(8);
+            else if (nr <= 12) MN_TAU(12);
+            else MN_TAU(16);
+#undef MN_TAU
+            MN_KCHECK(s, "k_row_tau");
+        }
+#define MN_E2T(NRV, TKV)                                                                        \
+    do {                                                                                        \
+        MN_HIP_TRY(hipFuncSetAttribute((const void *)k_energy_rows2<NRV, TKV>,                  \
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)sh2));  \
+        hipLaunchKernelGGL((k_energy_rows2<NRV, TKV>), dim3((unsigned)blocks2), dim3(64 * nw2),  \
+                           sh2, s, X, n, f, na, naP, ne - na, nbP, eij, ev, dg, mA_num, mA_g,    \
+                           opts->g_mode, opts->tau_mode, opts->tau_param, pct_rank, tau_d, E, G, \
+                           lam);                                                                \
+    } while (0)
+#define MN_E2(NRV)                                                                              \
+    do {                                                                                        \
+        if (tk) MN_E2T(NRV, true); else MN_E2T(NRV, false);                                     \
+    } while (0)
+        if (nr <= 4) MN_E2(4);
+        else if (nr <= 8) MN_E2(8);
+        else if (nr <= 12) MN_E2(12);
+        else MN_E2(16);
+#undef MN_E2
+#undef MN_E2T
+        MN_KCHECK(s, "k_energy_rows2");
+    } else {
     const int fpad = (f + 3) & ~3;
     const size_t ebytes = (((size_t)ne * 12) + 15) & ~(size_t)15;
     const int in_lds = ebytes <= EDGE_LDS_MAX ? 1 : 0;
@@ -961,7 +1450,9 @@ static int energy_impl(const mn_csr *L, const float *X, int64_t n, int32_t f,
     const char *rwe = getenv("MN_ENERGY_ROWS");
     const int rows = (rwe && *rwe == '4' && nr <= 16) ? 4 : 2;
     const char *sle = getenv("MN_TAU_SEL");
-    const int sel = (sle && *sle == '1') ? 1 : 0;
+    // (MN_ENERGY_PROBE: timing-probe bits 16 / 32, see k_energy_rows)
+    const char *epe = getenv("MN_ENERGY_PROBE");
+    const int sel = ((sle && *sle == '1') ? 1 : 0) | ((epe && *epe) ? (atoi(epe) & 48) : 0);
     const size_t per_wave = (size_t)rows * fpad * 4 + 256 * 4;
     const size_t avail = LDS_BUDGET - (in_lds ? ebytes : 0);
     const int wmax = nr <= 16 ? 16 : 4;  // = launch bounds / 64
@@ -1022,6 +1513,7 @@ static int energy_impl(const mn_csr *L, const float *X, int64_t n, int32_t f,
 #undef MN_ER
 #undef MN_ER2
     MN_KCHECK(s, "k_energy_rows");
+    }
     if (spec) {
         double *part = (double *)scratch(kSlotNorms2, (size_t)n * 16 + 8 * SUM_BLOCKS + 64) + 2 * n;
         hipLaunchKernelGGL(k_sum_partials, dim3(SUM_BLOCKS), dim3(256), 0, s, G, n, part);

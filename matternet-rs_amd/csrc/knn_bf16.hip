@@ -758,8 +758,13 @@ static int knn_cos_bf16_x1(const uint16_t *X, int64_t n, int32_t d, const mn_cos
     int L1 = std::min(std::max((topk + 1) / 2, 16), 48);
     const char *fl = getenv("MN_BF16_L1");  // experiments: phase-1 list length
     if (fl && *fl) L1 = std::min(std::max(atoi(fl), 4), 48);
+    // sample = n / div rows: n/24 under the symmetric sweep (its cost does not
+    // follow the threshold; C5 1M x 3072: phase 1 726 -> 497 ms, 0 uncertified,
+    // profiles/r03k_c5_grid.log), n/16 for the query-major sweep (round 2 grid)
+    const char *te0 = getenv("MN_BF16_TM"), *sy0 = getenv("MN_BF16_SYM");
+    const bool sym_planned = !(te0 && *te0 == '0') && !(sy0 && *sy0 == '0');
     const char *fs = getenv("MN_BF16_SAMPLE_DIV");  // experiments: sample = n / div
-    const int64_t div = (fs && *fs) ? std::max(2, atoi(fs)) : 16;
+    const int64_t div = (fs && *fs) ? std::max(2, atoi(fs)) : (sym_planned ? 24 : 16);
     int64_t m0 = std::max<int64_t>(n / div, (int64_t)64 * L1);
     m0 = (m0 + 255) / 256 * 256;  // whole sweep tiles (TM) and phase-1 tiles
     if (m0 + 4 * ksw2::BC > n || n * 32 >= INT_MAX || n >= INT_MAX) return 1;

@@ -257,6 +257,14 @@ def test_tau_order_statistic_adversarial_rows(tau):
     X[7] = np.float32(3.0)
     X[7, 100] = np.float32(3.0000002)
     X[8:64] = (rng.standard_normal((56, f)) ** 3).astype(np.float32)
+    X[64] = np.where(rng.random(f) < 0.9, 0.0, X[64]).astype(np.float32)  # sparse: tied zeros
+    X[65] = np.where(rng.random(f) < 0.5, np.float32(-0.0), np.float32(0.0))
+    X[65, :40] = rng.random(40).astype(np.float32)                # -0 / +0 around the middle
+    X[66] = np.float32(-2.0)
+    X[66, 384:] = np.float32(7.0)                                 # the two middle keys differ
+    X[67] = np.sort(X[67])                                        # sorted along the row
+    X[68] = np.float32(-np.float32(3.4e38))
+    X[68, ::2] = np.float32(3.4e38)                               # the span overflows f32
     tm = {"median": (S.TauMode.Median, O.TAU_MEDIAN, 0.0),
           "pct": (S.TauMode.Percentile(0.77), O.TAU_PERCENTILE, 0.77)}[tau]
     E, G, lam = run(X, ip, ix, iv, 0, tm[0])
@@ -264,3 +272,24 @@ def test_tau_order_statistic_adversarial_rows(tau):
     np.testing.assert_allclose(E, rE, rtol=RTOL, atol=ATOL)
     np.testing.assert_allclose(G, rG, rtol=RTOL, atol=ATOL)
     np.testing.assert_allclose(lam, rl, rtol=RTOL, atol=ATOL)
+
+
+@pytest.mark.parametrize("tau", ["median", "pct", "mean"])
+def test_v2_kernel_matches_v1(tau, monkeypatch):
+    """k_energy_rows2 (diagonal from registers, counted tau select, prefetched
+    rows) against the round-2 kernel (MN_ENERGY_V1=1) and the oracle on the
+    C3 feature Laplacian with an odd row count."""
+    import surfface_hip as S
+    ip, ix, iv = feature_laplacian()
+    X = datagen.uniform(3001, 768, seed=41)
+    X[10] = (np.random.default_rng(3).standard_normal(768) ** 3).astype(np.float32)
+    tm = {"median": (S.TauMode.Median, O.TAU_MEDIAN, 0.0),
+          "pct": (S.TauMode.Percentile(0.1), O.TAU_PERCENTILE, 0.1),
+          "mean": (S.TauMode.Mean, O.TAU_MEAN, 0.0)}[tau]
+    E2, G2, l2 = run(X, ip, ix, iv, 0, tm[0])
+    monkeypatch.setenv("MN_ENERGY_V1", "1")
+    E1, G1, l1 = run(X, ip, ix, iv, 0, tm[0])
+    rE, rG, rl = O.energy_rows(X, ip, ix, iv, O.G_TAUMODE, tm[1], tm[2])
+    for a, b, r in ((E2, E1, rE), (G2, G1, rG), (l2, l1, rl)):
+        np.testing.assert_allclose(a, b, rtol=RTOL, atol=ATOL)
+        np.testing.assert_allclose(a, r, rtol=RTOL, atol=ATOL)
