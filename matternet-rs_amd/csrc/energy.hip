@@ -583,11 +583,9 @@ __device__ bool wave_select_cnt(const uint32_t (&keys)[NR], int f, int rank, int
     const int lane = threadIdx.x & 63;
     uint32_t kmin = 0xFFFFFFFFu, kmax = 0u;
 #pragma unroll
-    for (int r = 0; r < NR; ++r) {
-        if (lane + 64 * r < f) {
-            kmin = keys[r] < kmin ? keys[r] : kmin;
-            kmax = keys[r] > kmax ? keys[r] : kmax;
-        }
+    for (int r = 0; r < NR; ++r) {  // pads (0xFFFFFFFF) never lower kmin; kept out of kmax
+        kmin = min(kmin, keys[r]);
+        kmax = max(kmax, lane + 64 * r < f ? keys[r] : 0u);
     }
     kmin = wave_umin_dpp(kmin);
     kmax = wave_umax_dpp(kmax);
@@ -604,8 +602,10 @@ __device__ bool wave_select_cnt(const uint32_t (&keys)[NR], int f, int rank, int
         const float span = vhi - vlo;
         if (!(span > 0.f)) break;  // one value left (ties): compact or fall back
         const int hw = m / 6 < 6 ? 6 : (m / 6 > 24 ? 24 : m / 6);
-        const float est = vlo + span * (((float)(rank - cA) + 0.5f * (float)need) / (float)m);
-        const float half = span * ((float)hw / (float)m);
+        // estimates only (any probe is exact): approximate reciprocal
+        const float rm = __builtin_amdgcn_rcpf((float)m);
+        const float est = vlo + span * (((float)(rank - cA) + 0.5f * (float)need) * rm);
+        const float half = span * ((float)hw * rm);
         const float p1 = fmaxf(est - half, vlo), p2 = fminf(est + half, vhi);
         const uint32_t k1 = f2key(p1), k2 = f2key(p2);
         const int c1 = wave_cle<NR>(keys, k1), c2 = wave_cle<NR>(keys, k2);
@@ -657,7 +657,7 @@ __device__ bool wave_select_cnt(const uint32_t (&keys)[NR], int f, int rank, int
 // high occupancy re-reads X instead of holding the select's registers and
 // latency inside the entry-loop kernel (which keeps Fixed / Mean inline).
 template <int NR>
-__global__ __launch_bounds__(256) void k_row_tau(const float *__restrict__ X, int64_t n, int f,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 8))) void k_row_tau(const float *__restrict__ X, int64_t n, int f,
                                                  int tau_mode, double tau_param, int pct_rank,
                                                  double *__restrict__ tau) {
     __shared__ __attribute__((aligned(16))) int hist_all[4][256];
@@ -679,7 +679,12 @@ __global__ __launch_bounds__(256) void k_row_tau(const float *__restrict__ X, in
     for (; row < n; row += rstride) {
         uint32_t keys[NR];
 #pragma unroll
-        for (int r = 0; r < NR; ++r) keys[r] = lane + 64 * r < f ? f2key(xv[r]) : 0xFFFFFFFFu;
+        for (int r = 0; r < NR; ++r) {
+            // sortable key (as f2key, branch-free) | all-ones for columns >= f
+            const uint32_t u = __float_as_uint(xv[r]);
+            const uint32_t k = u ^ ((uint32_t)((int32_t)u >> 31) | 0x80000000u);
+            keys[r] = k | (uint32_t)-(int32_t)(lane + 64 * r >= f);
+        }
         if (row + rstride < n) load_row(row + rstride);  // next row in flight during the select
         uint32_t k0, k1;
         double v;
