@@ -24,16 +24,19 @@ def pick(prefix):
     return max(c, key=lambda k: ks[k]["total_ms"]) if c else None
 
 
-for fname, prefix, extra in (("bench_pmc_gram.json", "k_gram_sweep2<0, 2, true", {"rows_per_gpu": n}),
-                             ("bench_pmc_energy.json", "k_energy_rows", {"rows": n})):
-    k = pick(prefix)
-    if not k or "fetch_bytes" not in ks[k] or "write_bytes" not in ks[k]:
-        print("no PMC data for", prefix)
+# the energy pass is two kernels since round 3 (k_row_tau: Median tau, then
+# k_energy_rows2): their bytes per call are summed
+for fname, prefixes, extra in (("bench_pmc_gram.json", ("k_gram_sweep2<0, 2, true",), {"rows_per_gpu": n}),
+                               ("bench_pmc_energy.json", ("k_row_tau", "k_energy_rows2"), {"rows": n})):
+    kk = [pick(p) for p in prefixes]
+    if not all(kk) or any("fetch_bytes" not in ks[k] or "write_bytes" not in ks[k] for k in kk):
+        print("no PMC data for", prefixes)
         continue
-    v = ks[k]
-    out = {"tag": tag, "dim": d, "kernel": k.split("::")[-1], "kernel_full": k,
-           "avg_ms": v["avg_ms"], "fetch_bytes_per_launch": v["fetch_bytes"],
-           "write_bytes_per_launch": v["write_bytes"],
-           "hbm_bytes_per_launch": v["fetch_bytes"] + v["write_bytes"], "source": src, **extra}
+    fb = sum(ks[k]["fetch_bytes"] for k in kk)
+    wb = sum(ks[k]["write_bytes"] for k in kk)
+    out = {"tag": tag, "dim": d, "kernel": " + ".join(k.split("::")[-1] for k in kk),
+           "kernel_full": " + ".join(kk), "avg_ms": sum(ks[k]["avg_ms"] for k in kk),
+           "fetch_bytes_per_launch": fb, "write_bytes_per_launch": wb,
+           "hbm_bytes_per_launch": fb + wb, "source": src, **extra}
     json.dump(out, open(os.path.join(ROOT, fname), "w"), indent=1)
     print(fname, json.dumps({kk: out[kk] for kk in ("kernel", "avg_ms", "hbm_bytes_per_launch")}))
