@@ -1136,14 +1136,20 @@ template <bool XF64>
 __global__ __launch_bounds__(512) void k_diffuse_rows(
     const void *__restrict__ Xin, int64_t n, int f, const int64_t *__restrict__ gip,
     const int32_t *__restrict__ gix, const double *__restrict__ gv, int64_t nnz, int l_in_lds,
-    double eta, int steps, int matvec, double *__restrict__ Xout) {
+    const int32_t *__restrict__ gperm, double eta, int steps, int matvec,
+    double *__restrict__ Xout) {
     extern __shared__ __attribute__((aligned(16))) unsigned char dsm[];
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
-    // LDS: [val f64 x nnz | col i32 x nnz | ptr i32 x (f+1)] | x [waves][2][f] f64
+    const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int nw = blockDim.x >> 6;
+    // LDS: [val f64 x nnz | col i32 x nnz | ptr i32 x (f+1) | perm i32 x f]
+    //      | x [waves][2][f] f64
+    // Lane l of sweep g folds feature row perm[64 g + l]: rows ordered by
+    // length (host), so a sweep's 64 chains are about equally long
     double *lv = (double *)dsm;
     int32_t *lc = (int32_t *)(dsm + (size_t)nnz * 8);
     int32_t *lp = lc + nnz;
-    const size_t lb = l_in_lds ? ((((size_t)nnz * 12 + (size_t)(f + 1) * 4) + 15) & ~(size_t)15) : 0;
+    int32_t *lperm = lp + f + 1;
+    const size_t lb = l_in_lds ? ((((size_t)nnz * 12 + (size_t)(2 * f + 1) * 4) + 15) & ~(size_t)15) : 0;
     double *xb = (double *)(dsm + lb) + (size_t)w * 2 * f;
     if (l_in_lds) {
         for (int64_t p = threadIdx.x; p < nnz; p += blockDim.x) {
@@ -1151,17 +1157,32 @@ __global__ __launch_bounds__(512) void k_diffuse_rows(
             lc[p] = gix[p];
         }
         for (int i = threadIdx.x; i <= f; i += blockDim.x) lp[i] = (int32_t)gip[i];
+        for (int i = threadIdx.x; i < f; i += blockDim.x) lperm[i] = gperm[i];
     }
     __syncthreads();
     for (int64_t row = (int64_t)blockIdx.x * nw + w; row < n; row += (int64_t)gridDim.x * nw) {
         double *x = xb, *y = xb + f;
-        for (int i = lane; i < f; i += 64)
-            x[i] = XF64 ? ((const double *)Xin)[row * f + i]
-                        : (double)((const float *)Xin)[row * f + i];
+        if (!XF64 && f <= 1024) {
+            // f32 rows: all 16 loads in flight at once (buffer loads, columns
+            // >= f read 0; a guarded strided loop waits on each load in turn)
+            const __amdgpu_buffer_rsrc_t rs = row_rsrc((const float *)Xin + row * f, f);
+            float v[16];
+#pragma unroll
+            for (int r = 0; r < 16; ++r) v[r] = row_at(rs, lane + 64 * r);
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int r = 0; r < 16; ++r)
+                if (lane + 64 * r < f) x[lane + 64 * r] = (double)v[r];
+        } else {
+            for (int i = lane; i < f; i += 64)
+                x[i] = XF64 ? ((const double *)Xin)[row * f + i]
+                            : (double)((const float *)Xin)[row * f + i];
+        }
         __builtin_amdgcn_wave_barrier();
         const int ns = matvec ? 1 : steps;
         for (int st = 0; st < ns; ++st) {
-            for (int i = lane; i < f; i += 64) {
+            for (int q = lane; q < f; q += 64) {
+                const int i = l_in_lds ? lperm[q] : gperm[q];
                 const int64_t p0 = l_in_lds ? lp[i] : gip[i], p1 = l_in_lds ? lp[i + 1] : gip[i + 1];
                 double sum = 0.0;
                 for (int64_t p = p0; p < p1; ++p) {
@@ -1595,7 +1616,20 @@ static int diffuse_impl(const mn_csr *L, const void *X, int32_t x_is_f64, int64_
     hipStream_t s = (hipStream_t)stream;
     if (n == 0) return MN_OK;
     const int64_t nnz = L->nnz;
-    const size_t lbytes = ((size_t)nnz * 12 + (size_t)(f + 1) * 4 + 15) & ~(size_t)15;
+    // feature rows by length (descending, stable): the lanes of one sweep fold
+    // rows of about equal length (per-row order unchanged: bit-exact)
+    std::vector<int64_t> hip_(f + 1);
+    MN_HIP_TRY(hipMemcpyAsync(hip_.data(), L->indptr, 8 * ((size_t)f + 1), hipMemcpyDeviceToHost, s));
+    MN_HIP_TRY(hipStreamSynchronize(s));
+    std::vector<int32_t> hperm(f);
+    for (int i = 0; i < f; ++i) hperm[i] = i;
+    std::stable_sort(hperm.begin(), hperm.end(), [&](int a, int b) {
+        return hip_[a + 1] - hip_[a] > hip_[b + 1] - hip_[b];
+    });
+    int32_t *perm = (int32_t *)scratch(kSlotGeneric2, (size_t)f * 4 + 64);
+    MN_REQUIRE(perm, MN_ENOMEM, "mn_diffuse_rows: scratch allocation failed");
+    MN_HIP_TRY(hipMemcpyAsync(perm, hperm.data(), 4 * (size_t)f, hipMemcpyHostToDevice, s));
+    const size_t lbytes = ((size_t)nnz * 12 + (size_t)(2 * f + 1) * 4 + 15) & ~(size_t)15;
     const size_t per_wave = (size_t)2 * f * 8;
     const int l_in_lds = lbytes + per_wave <= LDS_BUDGET ? 1 : 0;
     const size_t avail = LDS_BUDGET - (l_in_lds ? lbytes : 0);
@@ -1608,13 +1642,13 @@ static int diffuse_impl(const mn_csr *L, const void *X, int32_t x_is_f64, int64_
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)shmem));
         hipLaunchKernelGGL(k_diffuse_rows<true>, dim3((unsigned)blocks), dim3(64 * nw), shmem, s,
                            X, n, f, L->indptr, L->indices, (const double *)L->values, nnz, l_in_lds,
-                           eta, steps, matvec, out);
+                           perm, eta, steps, matvec, out);
     } else {
         MN_HIP_TRY(hipFuncSetAttribute((const void *)k_diffuse_rows<false>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)shmem));
         hipLaunchKernelGGL(k_diffuse_rows<false>, dim3((unsigned)blocks), dim3(64 * nw), shmem, s,
                            X, n, f, L->indptr, L->indices, (const double *)L->values, nnz, l_in_lds,
-                           eta, steps, matvec, out);
+                           perm, eta, steps, matvec, out);
     }
     MN_KCHECK(s, "k_diffuse_rows");
     MN_HIP_TRY(hipStreamSynchronize(s));
