@@ -1132,6 +1132,7 @@ __global__ __launch_bounds__(256) void k_normalise(double *__restrict__ lam, int
 // matvec mode, y = L x once.  One wave per row, the row double-buffered in
 // LDS; L (CSR) in LDS when it fits.  Lane-parallel over features i: every
 // fold is its own sequential chain, so the result is bit-exact.
+constexpr int DF_SW = 16;  // feature sweeps held in registers (f <= 1024)
 template <bool XF64>
 __global__ __launch_bounds__(512) void k_diffuse_rows(
     const void *__restrict__ Xin, int64_t n, int f, const int64_t *__restrict__ gip,
@@ -1160,6 +1161,15 @@ __global__ __launch_bounds__(512) void k_diffuse_rows(
         for (int i = threadIdx.x; i < f; i += blockDim.x) lperm[i] = gperm[i];
     }
     __syncthreads();
+    // lane l of sweep g: feature row si[g] = perm[64 g + l], entries [sp0, sp1)
+    int si[DF_SW], sp0[DF_SW], sp1[DF_SW];
+#pragma unroll
+    for (int g = 0; g < DF_SW; ++g) {
+        const int q = min(lane + 64 * g, f - 1);
+        si[g] = l_in_lds ? lperm[q] : 0;
+        sp0[g] = l_in_lds ? lp[si[g]] : 0;
+        sp1[g] = l_in_lds && lane + 64 * g < f ? lp[si[g] + 1] : sp0[g];
+    }
     for (int64_t row = (int64_t)blockIdx.x * nw + w; row < n; row += (int64_t)gridDim.x * nw) {
         double *x = xb, *y = xb + f;
         if (!XF64 && f <= 1024) {
@@ -1181,6 +1191,21 @@ __global__ __launch_bounds__(512) void k_diffuse_rows(
         __builtin_amdgcn_wave_barrier();
         const int ns = matvec ? 1 : steps;
         for (int st = 0; st < ns; ++st) {
+            if (l_in_lds && f <= 64 * DF_SW) {
+                // row-independent sweep metadata from registers (loaded once)
+#pragma unroll
+                for (int g = 0; g < DF_SW; ++g) {
+                    if (64 * g >= f) break;
+                    if (lane + 64 * g < f) {
+                        double sum = 0.0;
+                        for (int p = sp0[g]; p < sp1[g]; ++p) sum = sum + lv[p] * x[lc[p]];
+                        y[si[g]] = matvec ? sum : x[si[g]] - eta * sum;
+                    }
+                }
+                __builtin_amdgcn_wave_barrier();
+                double *t = x; x = y; y = t;
+                continue;
+            }
             for (int q = lane; q < f; q += 64) {
                 const int i = l_in_lds ? lperm[q] : gperm[q];
                 const int64_t p0 = l_in_lds ? lp[i] : gip[i], p1 = l_in_lds ? lp[i + 1] : gip[i + 1];
