@@ -352,7 +352,25 @@ __device__ __forceinline__ float exact_l2sq(const float *__restrict__ a,
     if (VEC4) {
         const float4 *a4 = reinterpret_cast<const float4 *>(a);
         const float4 *b4 = reinterpret_cast<const float4 *>(b);
-        for (int t = 0; t < (d >> 2); ++t) {
+        const int d4 = d >> 2;
+        int t = 0;
+        // 4 float4 of the (random) candidate row in flight per lane ahead of
+        // the ordered adds (a one-at-a-time loop waits on each gather)
+        for (; t + 4 <= d4; t += 4) {
+            float4 y[4], x[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) y[u] = b4[t + u];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) x[u] = a4[t + u];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                float df = x[u].x - y[u].x; acc = acc + df * df;
+                df = x[u].y - y[u].y; acc = acc + df * df;
+                df = x[u].z - y[u].z; acc = acc + df * df;
+                df = x[u].w - y[u].w; acc = acc + df * df;
+            }
+        }
+        for (; t < d4; ++t) {
             const float4 x = a4[t], y = b4[t];
             float df = x.x - y.x; acc = acc + df * df;
             df = x.y - y.y; acc = acc + df * df;

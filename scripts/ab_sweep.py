@@ -42,6 +42,7 @@ for r in range(rounds):
         torch.cuda.synchronize()
         st = out.stats
         res[v].append({"ms_sweep": round(st["ms_sweep"], 2), "ms_total": round(st["ms_total"], 2),
+                       "ms_rerank": round(st["ms_rerank"], 2),
                        "n_cand": st["n_candidates"], "unc": st["n_uncertified"],
                        "esc": st["n_escalated"], "wall": round(time.time() - t, 3)})
         if ref is None:
