@@ -345,6 +345,7 @@ __global__ __launch_bounds__(NT) void k_gram_topk(
 
 // The reference fold (distance.rs:206-213): acc starts at -0.0 and adds each
 // (a-b)^2 in feature order; -ffp-contract=off keeps mul and add separate.
+constexpr int EXU = 4;  // (8: 47 vs 43 ms at C2, profiles/r03n_rerank_unroll.log)
 template <bool VEC4>
 __device__ __forceinline__ float exact_l2sq(const float *__restrict__ a,
                                             const float *__restrict__ b, int d) {
@@ -354,16 +355,16 @@ __device__ __forceinline__ float exact_l2sq(const float *__restrict__ a,
         const float4 *b4 = reinterpret_cast<const float4 *>(b);
         const int d4 = d >> 2;
         int t = 0;
-        // 4 float4 of the (random) candidate row in flight per lane ahead of
+        // EXU float4 of the (random) candidate row in flight per lane ahead of
         // the ordered adds (a one-at-a-time loop waits on each gather)
-        for (; t + 4 <= d4; t += 4) {
-            float4 y[4], x[4];
+        for (; t + EXU <= d4; t += EXU) {
+            float4 y[EXU], x[EXU];
 #pragma unroll
-            for (int u = 0; u < 4; ++u) y[u] = b4[t + u];
+            for (int u = 0; u < EXU; ++u) y[u] = b4[t + u];
 #pragma unroll
-            for (int u = 0; u < 4; ++u) x[u] = a4[t + u];
+            for (int u = 0; u < EXU; ++u) x[u] = a4[t + u];
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
+            for (int u = 0; u < EXU; ++u) {
                 float df = x[u].x - y[u].x; acc = acc + df * df;
                 df = x[u].y - y[u].y; acc = acc + df * df;
                 df = x[u].z - y[u].z; acc = acc + df * df;
