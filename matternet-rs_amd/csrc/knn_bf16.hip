@@ -110,9 +110,7 @@ __device__ __forceinline__ double exact_dot(const uint16_t *__restrict__ a,
                                             const uint16_t *__restrict__ b, int d) {
     double acc = -0.0;
     if ((d & 7) == 0) {
-        for (int t = 0; t < d; t += 8) {
-            const uint4 va = *reinterpret_cast<const uint4 *>(a + t);
-            const uint4 vb = *reinterpret_cast<const uint4 *>(b + t);
+        auto fold8 = [&](const uint4 va, const uint4 vb) {
             const uint32_t wa[4] = {va.x, va.y, va.z, va.w}, wb[4] = {vb.x, vb.y, vb.z, vb.w};
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
@@ -121,7 +119,21 @@ __device__ __forceinline__ double exact_dot(const uint16_t *__restrict__ a,
                 acc = __builtin_fma(bf2d((uint16_t)(wa[u] >> 16)), bf2d((uint16_t)(wb[u] >> 16)),
                                     acc);
             }
+        };
+        int t = 0;
+        // 4 16-B pieces of the (random) candidate row in flight per lane ahead
+        // of the ordered FMAs (one at a time, each waits on its gather)
+        for (; t + 32 <= d; t += 32) {
+            uint4 va[4], vb[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) vb[u] = *reinterpret_cast<const uint4 *>(b + t + 8 * u);
+#pragma unroll
+            for (int u = 0; u < 4; ++u) va[u] = *reinterpret_cast<const uint4 *>(a + t + 8 * u);
+#pragma unroll
+            for (int u = 0; u < 4; ++u) fold8(va[u], vb[u]);
         }
+        for (; t < d; t += 8)
+            fold8(*reinterpret_cast<const uint4 *>(a + t), *reinterpret_cast<const uint4 *>(b + t));
     } else {
         for (int t = 0; t < d; ++t) acc = __builtin_fma(bf2d(a[t]), bf2d(b[t]), acc);
     }
