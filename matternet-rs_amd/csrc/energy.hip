@@ -1247,29 +1247,50 @@ __global__ __launch_bounds__(256) void k_energy_signals(
     const double mg = (sym && g_mode == MN_G_TAUMODE) ? 2.0 : 1.0;
     for (int64_t i = r0; i < r1; ++i) {
         double xi[FPT];
-#pragma unroll
-        for (int u = 0; u < FPT; ++u) {
-            const int c = t + 256 * u;
-            xi[u] = c < f ? (double)X[i * f + c] : 0.0;
-            den[u] += xi[u] * xi[u];
-        }
-        const int64_t p0 = ip[i], p1 = ip[i + 1];
-        for (int64_t p = p0; p < p1; ++p) {
-            const int j = ix[p];
-            if (sym && j < i) continue;  // covered by (j, i)
-            const double vv = v[p];
-            const bool g = j != i && -vv > 0.0 && (g_mode == MN_G_TAUMODE || sym || j > i);
-            const double m = (j != i) ? mnum : 1.0;
+        {
+            const __amdgpu_buffer_rsrc_t rs = row_rsrc(X + i * f, f);  // columns >= f read 0
 #pragma unroll
             for (int u = 0; u < FPT; ++u) {
-                const int c = t + 256 * u;
-                const double xj = c < f ? (double)X[(int64_t)j * f + c] : 0.0;
-                num[u] += m * (vv * (xi[u] * xj));
-                if (g) {
-                    const double dd = xi[u] - xj;
-                    const double e = (dd * dd) * (-vv);
-                    S[u] += mg * e;
-                    Q[u] += mg * (e * e);
+                xi[u] = (double)row_at(rs, t + 256 * u);
+                den[u] += xi[u] * xi[u];
+            }
+        }
+        const int64_t p0 = ip[i], p1 = ip[i + 1];
+        // 4 entries at a time: their x_j rows are gathered together (an entry
+        // skipped by the symmetric walk gets a zero-length resource: no
+        // traffic), then folded in entry order (same arithmetic as one by one)
+        for (int64_t p = p0; p < p1; p += 4) {
+            int jj[4];
+            double vv[4];
+            bool ok[4];
+            float xjf[4][FPT];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const bool in = p + u < p1;
+                jj[u] = in ? ix[p + u] : 0;
+                vv[u] = in ? v[p + u] : 0.0;
+                ok[u] = in && !(sym && jj[u] < i);  // (j, i) covers j < i
+                const __amdgpu_buffer_rsrc_t rs = row_rsrc(X + (int64_t)jj[u] * f, ok[u] ? f : 0);
+#pragma unroll
+                for (int w = 0; w < FPT; ++w) xjf[u][w] = row_at(rs, t + 256 * w);
+            }
+            __builtin_amdgcn_sched_barrier(0);  // the gathers issue before the folds
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                if (!ok[u]) continue;
+                const int j = jj[u];
+                const bool g = j != i && -vv[u] > 0.0 && (g_mode == MN_G_TAUMODE || sym || j > i);
+                const double m = (j != i) ? mnum : 1.0;
+#pragma unroll
+                for (int w = 0; w < FPT; ++w) {
+                    const double xj = (double)xjf[u][w];
+                    num[w] += m * (vv[u] * (xi[w] * xj));
+                    if (g) {
+                        const double dd = xi[w] - xj;
+                        const double e = (dd * dd) * (-vv[u]);
+                        S[w] += mg * e;
+                        Q[w] += mg * (e * e);
+                    }
                 }
             }
         }

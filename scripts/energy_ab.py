@@ -70,3 +70,22 @@ for rep in range(3):
     best = e0.elapsed_time(e1) if best is None else min(best, e0.elapsed_time(e1))
 print(json.dumps({"diffusion_4_steps_ms": round(best, 3), "GB_per_s": round(n * d * 12 / best / 1e6, 1)}),
       flush=True)
+# EAB_SIGNALS=1: the item-graph orientation leg (bench.py c3_legs.item_graph_signals):
+# the F feature signals against the C2 item Laplacian
+if os.environ.get("EAB_SIGNALS") == "1":
+    del Xd
+    g = S.knn_l2sq(X, 32, algo="bf16x1")
+    Lit, _ = S.build_laplacian_from_knn(g.idx, g.dist, weight_kernel="rational", symmetrise="union",
+                                        eps=float("inf"), sigma=1.0, p=2.0)
+    del g
+    S.signal_energy_and_dispersion(X, Lit)
+    best = None
+    for rep in range(3):
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        S.signal_energy_and_dispersion(X, Lit)
+        e1.record()
+        torch.cuda.synchronize()
+        best = e0.elapsed_time(e1) if best is None else min(best, e0.elapsed_time(e1))
+    print(json.dumps({"item_graph_signals_ms": round(best, 3), "nnz": Lit.nnz}), flush=True)
