@@ -183,13 +183,12 @@ def main():
         m0 = int(st0.get("sample_rows") or 0)
         sym = st0.get("sweep_slices") == -1
         nc_sw = n_loc if sym else n_loc - m0
-        kname = "k_gram_sweep2" if os.environ.get("MN_X1_SWEEP", "2") != "1" else "k_gram_sweep"
+        kname = "k_gram_sweep2"
         # the exact instantiation (rocprofv3 name) the PMC reference must match
         kfull = "k_gram_sweep2<0, 0, true>"
-        if sym:
-            f16 = os.environ.get("MN_SYM_F16", "1") != "0"
+        if sym:  # fp16 operands (x 2^e): the release library's only SW_SYM form
             kname = "k_gram_sweep2<SW_SYM>"
-            kfull = "k_gram_sweep2<0, 2, true, %s>" % ("true" if f16 else "false")
+            kfull = "k_gram_sweep2<0, 2, true, true>"
         flops_launch = 2.0 * nq * nc_sw * d
         nbk = (n_loc + 255) // 256
         flops_exec = 2.0 * 256 * 256 * d * nbk * (nbk + 1) / 2 if sym else flops_launch

@@ -5,6 +5,7 @@
 #include <cstdarg>
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
 
 #include "matternet_hip.h"
 
@@ -16,6 +17,17 @@ void clear_error();
 
 // MN_DEBUG_SYNC=1: synchronise after every launch so a fault names its kernel.
 bool debug_sync();
+
+// Tuning knobs (A/B experiments, timing probes whose outputs are invalid):
+// read from the environment ONLY in the tuning build (-DMN_TUNING,
+// libmatternet_hip_tuning.so, loaded by scripts/ on request).  The release
+// library ignores every MN_* variable except the diagnostics MN_DEBUG_SYNC
+// and MN_X1_DEBUG, which never change an output.
+#ifdef MN_TUNING
+inline const char *knob(const char *name) { return getenv(name); }
+#else
+inline const char *knob(const char *) { return nullptr; }
+#endif
 
 // Grow-only device scratch, one set of slots per (thread, device).  Growing
 // frees the old block (hipFree synchronises), so never call it while kernels
@@ -239,6 +251,24 @@ __device__ __forceinline__ T wave_elem(const T (&d)[NR], int pos) {
 #pragma unroll
     for (int q = 1; q < NR; ++q) if (q == r) v = d[q];
     return __shfl(v, l);
+}
+
+// Store a wave's sorted (key, idx) list (element e = lane + 64 r) as the k
+// entries out[0..k): the first keff, then (-1, +inf) padding.  k <= 64 NR.
+template <int NR, typename T>
+__device__ __forceinline__ void wave_store_list(const T (&d)[NR], const int (&ix)[NR], int k,
+                                                int keff, int32_t *__restrict__ oi,
+                                                T *__restrict__ od) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int r = 0; r < NR; ++r) {
+        const int e = lane + 64 * r;
+        if (e < k) {
+            const bool ok = e < keff;
+            oi[e] = ok ? ix[r] : -1;
+            od[e] = ok ? d[r] : (T)__builtin_inf();
+        }
+    }
 }
 
 // Keys-only ascending bitonic sort of 64*NR floats (element e = lane + 64*r),

@@ -1418,7 +1418,7 @@ static int energy_impl(const mn_csr *L, const float *X, int64_t n, int32_t f,
     const int sym = (hflag & 1) ? 0 : 1;
     // k_energy_rows2 (default for f <= 1024; MN_ENERGY_V1=1: the round-2
     // kernels) takes the diagonal apart from the entry lists
-    const char *v1e = getenv("MN_ENERGY_V1");
+    const char *v1e = knob("MN_ENERGY_V1");
     const int nr = (f + 63) / 64;
     int split = (nr <= 16 && !(v1e && *v1e == '1')) ? 1 : 0;
     int64_t na = 0, ne = 0;
@@ -1461,7 +1461,7 @@ static int energy_impl(const mn_csr *L, const float *X, int64_t n, int32_t f,
     if (split) {
         const int64_t naP = (na + E2_CH - 1) / E2_CH * E2_CH;
         const int64_t nbP = (ne - na + E2_CH - 1) / E2_CH * E2_CH;
-        const char *tke = getenv("MN_ENERGY_TAU");  // 1: the select inside the entry-loop kernel
+        const char *tke = knob("MN_ENERGY_TAU");  // 1: the select inside the entry-loop kernel
         const bool tk = tke && *tke == '1';
         const size_t fixed = e2_lds_bytes(na, ne - na, f, 0);
         const size_t wbytes = e2_lds_bytes(na, ne - na, f, 1, tk) - fixed;
@@ -1519,11 +1519,11 @@ static int energy_impl(const mn_csr *L, const float *X, int64_t n, int32_t f,
     const int in_lds = ebytes <= EDGE_LDS_MAX ? 1 : 0;
     // rows per wave pass: MN_ENERGY_ROWS (2 or 4; 4 halves the entry-list
     // reads per row, 16-B gathers, half the waves); tau select MN_TAU_SEL
-    const char *rwe = getenv("MN_ENERGY_ROWS");
+    const char *rwe = knob("MN_ENERGY_ROWS");
     const int rows = (rwe && *rwe == '4' && nr <= 16) ? 4 : 2;
-    const char *sle = getenv("MN_TAU_SEL");
+    const char *sle = knob("MN_TAU_SEL");
     // (MN_ENERGY_PROBE: timing-probe bits 16 / 32, see k_energy_rows)
-    const char *epe = getenv("MN_ENERGY_PROBE");
+    const char *epe = knob("MN_ENERGY_PROBE");
     const int sel = ((sle && *sle == '1') ? 1 : 0) | ((epe && *epe) ? (atoi(epe) & 48) : 0);
     const size_t per_wave = (size_t)rows * fpad * 4 + 256 * 4;
     const size_t avail = LDS_BUDGET - (in_lds ? ebytes : 0);
@@ -1536,7 +1536,7 @@ static int energy_impl(const mn_csr *L, const float *X, int64_t n, int32_t f,
     // register-resident entry lists (k_energy_rows_reg): the lists fit 48
     // slots a lane (list A padded to whole slots), rows of <= 1024 features
     const int64_t slots = (na + 63) / 64 + (ne - na + 63) / 64;
-    const char *rge = getenv("MN_ENERGY_REG");  // 1: register lists (A/B; slower so far)
+    const char *rge = knob("MN_ENERGY_REG");  // 1: register lists (A/B; slower so far)
     const bool reg = slots <= 48 && nr <= 16 && (rge && *rge == '1');
     if (reg) {
         const int nwr = slots <= 16 ? 8 : 4;  // = launch bounds / 64

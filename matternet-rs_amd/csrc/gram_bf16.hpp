@@ -494,7 +494,7 @@ inline GramPlan plan_gram(int64_t nq, int64_t nc, int L, int64_t min_slices,
     int64_t S = std::max<int64_t>(min_slices, (512 + blocks_q - 1) / blocks_q);
     // S * L bounds the re-rank width (8 registers x 64 lanes); 256 leaves room
     // for 2x (ties, queue lag); MN_GRAM_MAX_SL overrides it (experiments)
-    const char *msl = getenv("MN_GRAM_MAX_SL");
+    const char *msl = knob("MN_GRAM_MAX_SL");
     const int64_t max_sl = (msl && *msl) ? std::min(480, std::max(64, atoi(msl))) : 256;
     S = std::min<int64_t>(S, std::max<int64_t>(1, max_sl / L));
     S = std::min<int64_t>(S, std::max<int64_t>(1, (nc + BN - 1) / BN));

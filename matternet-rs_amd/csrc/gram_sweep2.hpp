@@ -517,6 +517,32 @@ __global__ __launch_bounds__(NT) void k_gram_sweep2(
 
 #undef MN_VMCNT
 
+// Slicing + buffer sizing of the query-major sweep: nc2 = corpus rows of the
+// sweep, expect = expected candidates per query.
+struct SweepPlan {
+    int64_t S, chunk;
+    int cap;
+};
+
+inline SweepPlan plan_sweep(int64_t nq, int64_t nc2, double expect) {
+    SweepPlan p;
+    const int64_t nqb = (nq + BQ - 1) / BQ;
+    int64_t S = std::max<int64_t>(8, (2048 + nqb - 1) / nqb);
+    const char *es = knob("MN_SWEEP_S");  // tuning build: corpus slices
+    if (es && *es) S = std::max(1, atoi(es));
+    S = std::min<int64_t>(S, std::max<int64_t>(1, nc2 / (4 * BC)));
+    S = std::max<int64_t>(S, 1);
+    int64_t chunk = (nc2 + S - 1) / S;
+    chunk = std::max<int64_t>(BC, (chunk + BC - 1) / BC * BC);
+    S = std::max<int64_t>(1, (nc2 + chunk - 1) / chunk);
+    p.S = S;
+    p.chunk = chunk;
+    const double per = expect / (double)S;
+    const int cap = (int)((2.5 * per + 64.0 + 15.0) / 16.0) * 16;
+    p.cap = std::max(cap, 64);
+    return p;
+}
+
 // SW_SYM / SW_COS_SYM block table: row block I against column tiles
 // [J0, J1), J >= I, at most TPB tiles per block.  order 1 (default): column
 // ranges aligned to a TPB grid, ordered by range then row, so the co-resident

@@ -44,7 +44,6 @@
 
 #include "common.hpp"
 #include "gram_bf16.hpp"
-#include "gram_sweep.hpp"
 #include "gram_sweep2.hpp"
 
 namespace mn {
@@ -753,8 +752,8 @@ hipError_t sort_f32_pairs(const float *keys_in, float *keys_out, const int *vals
 
 static thread_local mn_knn_stats t_bf16_stats{};
 
-static int getenv_int(const char *name, int dflt) {
-    const char *e = getenv(name);
+static int knob_int(const char *name, int dflt) {
+    const char *e = knob(name);
     return (e && *e) ? atoi(e) : dflt;
 }
 
@@ -768,14 +767,14 @@ static int knn_cos_bf16_x1(const uint16_t *X, int64_t n, int32_t d, const mn_cos
     using namespace kb16;
     const int topk = o->topk;
     int L1 = std::min(std::max((topk + 1) / 2, 16), 48);
-    const char *fl = getenv("MN_BF16_L1");  // experiments: phase-1 list length
+    const char *fl = knob("MN_BF16_L1");  // experiments: phase-1 list length
     if (fl && *fl) L1 = std::min(std::max(atoi(fl), 4), 48);
     // sample = n / div rows: n/24 under the symmetric sweep (its cost does not
     // follow the threshold; C5 1M x 3072: phase 1 726 -> 497 ms, 0 uncertified,
     // profiles/r03k_c5_grid.log), n/16 for the query-major sweep (round 2 grid)
-    const char *te0 = getenv("MN_BF16_TM"), *sy0 = getenv("MN_BF16_SYM");
+    const char *te0 = knob("MN_BF16_TM"), *sy0 = knob("MN_BF16_SYM");
     const bool sym_planned = !(te0 && *te0 == '0') && !(sy0 && *sy0 == '0');
-    const char *fs = getenv("MN_BF16_SAMPLE_DIV");  // experiments: sample = n / div
+    const char *fs = knob("MN_BF16_SAMPLE_DIV");  // experiments: sample = n / div
     const int64_t div = (fs && *fs) ? std::max(2, atoi(fs)) : (sym_planned ? 24 : 16);
     int64_t m0 = std::max<int64_t>(n / div, (int64_t)64 * L1);
     m0 = (m0 + 255) / 256 * 256;  // whole sweep tiles (TM) and phase-1 tiles
@@ -784,9 +783,9 @@ static int knn_cos_bf16_x1(const uint16_t *X, int64_t n, int32_t d, const mn_cos
     const int nkb = dp / 32;
     const Perm pm = make_perm_ab(n);
 
-    const char *te = getenv("MN_BF16_TM");  // layout A/B: 0 = k-block-major KB32
+    const char *te = knob("MN_BF16_TM");  // layout A/B: 0 = k-block-major KB32
     const int tmaj = (te && *te == '0') ? 0 : 1;
-    const char *tpe = getenv("MN_TM_PAD");  // panel stride nkb + pad k-blocks (default 1)
+    const char *tpe = knob("MN_TM_PAD");  // panel stride nkb + pad k-blocks (default 1)
     const int pst = tmaj ? nkb + ((tpe && *tpe) ? std::max(0, atoi(tpe)) : 1) : 0;
     const int64_t nrows = tmaj ? (n + 255) / 256 * 256 : n;
     uint16_t *XK = (uint16_t *)scratch(kSlotX1CK, (size_t)nrows * (tmaj ? pst * 32 : dp) * 2 + 64);
@@ -828,7 +827,7 @@ static int knn_cos_bf16_x1(const uint16_t *X, int64_t n, int32_t d, const mn_cos
     // positions in descending-threshold order, each unordered pair once; the
     // query-major sweep when a threshold is not finite (a row without a full
     // sample list) or the layout is k-block-major
-    const char *sye = getenv("MN_BF16_SYM");
+    const char *sye = knob("MN_BF16_SYM");
     bool sym = tmaj && !(sye && *sye == '0');
     int *pi = nullptr;
     float *tqS = nullptr, *taS = nullptr, *hcS = nullptr, *hoS = nullptr, *cnS = nullptr;
@@ -870,14 +869,14 @@ static int knn_cos_bf16_x1(const uint16_t *X, int64_t n, int32_t d, const mn_cos
     tm.mark();  // the sweep copy (+ SW_COS_SYM order and per-position folds)
     double expect;
     int S2, cap2;
-    ksw::SweepPlan p2{};
+    ksw2::SweepPlan p2{};
     if (sym) {
         expect = (double)L1 * (double)n / (double)m0;
         S2 = 1;
         cap2 = std::max(256, (int)((2.5 * expect + 64.0 + 15.0) / 16.0) * 16);
     } else {
         expect = (double)L1 * (double)(n - m0) / (double)m0;
-        p2 = ksw::plan_sweep(n, n - m0, expect);
+        p2 = ksw2::plan_sweep(n, n - m0, expect);
         S2 = (int)p2.S;
         cap2 = p2.cap;
     }
@@ -894,10 +893,11 @@ static int knn_cos_bf16_x1(const uint16_t *X, int64_t n, int32_t d, const mn_cos
                                   hipMemcpyHostToDevice, s));
         MN_HIP_TRY(hipMemsetAsync(cnt2, 0, (size_t)n * 4, s));
         MN_REQUIRE(tab.size() < INT_MAX, MN_ENOTSUP, "mn_knn_cos_bf16: sweep grid too large");
-        const char *probe = getenv("MN_BF16_PROBE");
-        const bool noepi = probe && !strcmp(probe, "noepi");
-        auto kern = noepi ? ksw2::k_gram_sweep2<1, ksw2::SW_COS_SYM, true>
-                          : ksw2::k_gram_sweep2<0, ksw2::SW_COS_SYM, true>;
+        auto kern = ksw2::k_gram_sweep2<0, ksw2::SW_COS_SYM, true>;
+        const char *probe = knob("MN_BF16_PROBE");  // tuning build: noepi = K loop only
+#ifdef MN_TUNING
+        if (probe && !strcmp(probe, "noepi")) kern = ksw2::k_gram_sweep2<1, ksw2::SW_COS_SYM, true>;
+#endif
         hipLaunchKernelGGL(kern, dim3((unsigned)tab.size()), dim3(ksw2::NT), 0, s, XK, n, XK, n, nkb,
                            (int64_t)0, (int64_t)0, 1, tqS, cnS, hcS, (int64_t)0, 1, (int64_t)0,
                            cap2, buf2, cnt2, pst, ksw2::SymArgs{dtab, taS, hoS, 0});
@@ -918,12 +918,14 @@ static int knn_cos_bf16_x1(const uint16_t *X, int64_t n, int32_t d, const mn_cos
     } else {
         const int64_t grid = (n + ksw2::BQ - 1) / ksw2::BQ * p2.S;
         MN_REQUIRE(grid < INT_MAX, MN_ENOTSUP, "mn_knn_cos_bf16: sweep grid too large");
-        const char *probe = getenv("MN_BF16_PROBE");
-        const bool noepi = probe && !strcmp(probe, "noepi");
-        auto kern = tmaj ? (noepi ? ksw2::k_gram_sweep2<1, ksw2::SW_COS, true>
-                                  : ksw2::k_gram_sweep2<0, ksw2::SW_COS, true>)
-                         : (noepi ? ksw2::k_gram_sweep2<1, ksw2::SW_COS, false>
-                                  : ksw2::k_gram_sweep2<0, ksw2::SW_COS, false>);
+        auto kern = tmaj ? ksw2::k_gram_sweep2<0, ksw2::SW_COS, true>
+                         : ksw2::k_gram_sweep2<0, ksw2::SW_COS, false>;
+        const char *probe = knob("MN_BF16_PROBE");  // tuning build: noepi = K loop only
+#ifdef MN_TUNING
+        if (probe && !strcmp(probe, "noepi"))
+            kern = tmaj ? ksw2::k_gram_sweep2<1, ksw2::SW_COS, true>
+                        : ksw2::k_gram_sweep2<1, ksw2::SW_COS, false>;
+#endif
         hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(ksw2::NT), 0, s, XK, n, XK, n, nkb,
                            (int64_t)0, (int64_t)0, 0, tq_pos, tq_pos, negn, m0, S2, p2.chunk,
                            cap2, buf2, cnt2, pst, ksw2::SymArgs{});
@@ -981,19 +983,19 @@ static int knn_cos_bf16_x1(const uint16_t *X, int64_t n, int32_t d, const mn_cos
     // per row would leave the chip idle); many rows: one block per row
     // (k_cos_fb_merge loads the P part lists one per thread: P <= FBT)
     const int P = (int)std::min<int64_t>(FBT, std::max<int64_t>(1, (2048 + nfb - 1) / std::max(nfb, 1)));
-    const char *fse = getenv("MN_BF16_FB_SPLIT");  // 0: always one block per row (A/B)
+    const char *fse = knob("MN_BF16_FB_SPLIT");  // 0: always one block per row (A/B)
     if (nfb > 0 && P >= 4 && !(fse && *fse == '0')) {
         const int64_t cs = (n + P - 1) / P;
         const size_t np = (size_t)nfb * P;
         char *fbp = (char *)scratch(kSlotGeneric3, np * KMAX * 12 + np * 4 + 256);
         MN_REQUIRE(fbp, MN_ENOMEM, "mn_knn_cos_bf16: split-scan scratch allocation failed");
         double *pd = (double *)fbp;
-        int *pi = (int *)(pd + np * KMAX), *pc = pi + np * KMAX;
+        int *pix2 = (int *)(pd + np * KMAX), *pc = pix2 + np * KMAX;
         hipLaunchKernelGGL(k_cos_fb_part, dim3((unsigned)np), dim3(FBT), 0, s, X, n, d, xn, topk, P,
-                           cs, fb_list, pd, pi, pc);
+                           cs, fb_list, pd, pix2, pc);
         MN_KCHECK(s, "k_cos_fb_part");
         hipLaunchKernelGGL(k_cos_fb_merge, dim3((unsigned)nfb), dim3(FBT), 0, s, n, topk, P, o->eps,
-                           o->sigma, o->p, fb_list, pd, pi, pc, out_idx, out_dist, out_w);
+                           o->sigma, o->p, fb_list, pd, pix2, pc, out_idx, out_dist, out_w);
         MN_KCHECK(s, "k_cos_fb_merge");
     } else {
         hipLaunchKernelGGL(k_cos_fallback, dim3((unsigned)std::min<int64_t>(n, 1024)), dim3(FBT), 0,
@@ -1043,7 +1045,7 @@ static int knn_cos_bf16_impl(const uint16_t *Q, int64_t nq, const uint16_t *C, i
     if (nq == 0) return MN_OK;
     const bool same = (Q == C) && nq == nc && q_off == c_off;
     const int excl = 1;
-    const GramPlan pl = plan_gram(nq, nc, L, (int64_t)getenv_int("MN_BF16_MIN_SLICES", 2));
+    const GramPlan pl = plan_gram(nq, nc, L, (int64_t)knob_int("MN_BF16_MIN_SLICES", 2));
     const int64_t S = pl.S, chunk = pl.chunk;
     const int cap = pl.cap, NR = pl.NR;
     const int64_t blocks_q = (nq + BM - 1) / BM;
@@ -1098,7 +1100,7 @@ static int knn_cos_bf16_impl(const uint16_t *Q, int64_t nq, const uint16_t *C, i
     tm.mark();
     {
         // self graphs at scale: the two-phase generator (MN_BF16_X1=0: one phase)
-        const char *xe = getenv("MN_BF16_X1");
+        const char *xe = knob("MN_BF16_X1");
         if (same && !(xe && *xe == '0')) {
             const float ms_norms = tm.on ? tm.ms(0, 1) : 0.f;
             const int rc = knn_cos_bf16_x1(Q, nq, d, o, qn, qinv, flags, fb_list, out_idx, out_dist,
@@ -1114,11 +1116,16 @@ static int knn_cos_bf16_impl(const uint16_t *Q, int64_t nq, const uint16_t *C, i
         }
     }
     if (nc > 0) {
-        const char *probe = getenv("MN_BF16_PROBE");
-        auto kern = !probe ? k_gram_bf16<GM_COS, 0>
-                    : !strcmp(probe, "noepi") ? k_gram_bf16<GM_COS, 1>
-                    : !strcmp(probe, "filteronly") ? k_gram_bf16<GM_COS, 2>
-                    : !strcmp(probe, "nomerge") ? k_gram_bf16<GM_COS, 3> : k_gram_bf16<GM_COS, 0>;
+        auto kern = k_gram_bf16<GM_COS, 0>;
+#ifdef MN_TUNING
+        // timing probes (results invalid): noepi = K loop only, filteronly /
+        // nomerge = the epilogue without its list updates
+        const char *probe = knob("MN_BF16_PROBE");
+        if (probe && *probe)
+            kern = !strcmp(probe, "noepi") ? k_gram_bf16<GM_COS, 1>
+                   : !strcmp(probe, "filteronly") ? k_gram_bf16<GM_COS, 2>
+                   : !strcmp(probe, "nomerge") ? k_gram_bf16<GM_COS, 3> : k_gram_bf16<GM_COS, 0>;
+#endif
         hipLaunchKernelGGL(kern, dim3((unsigned)(blocks_q * S)), dim3(NT), 0, s, Q, nq,
                            C, nc, d, q_off, c_off, excl, qinv, cinv, L, (int)S, chunk, cap, cbuf,
                            bcnt, btau);

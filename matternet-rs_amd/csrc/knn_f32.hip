@@ -38,7 +38,6 @@
 
 #include "common.hpp"
 #include "gram_bf16.hpp"
-#include "gram_sweep.hpp"
 #include "gram_sweep2.hpp"
 
 namespace mn {
@@ -61,7 +60,9 @@ constexpr int NCT = BN / 16;        // column tiles per corpus tile
 constexpr int QCAP = 48;            // LDS candidate queue per query
 constexpr int QPRE = QCAP - 16;     // merge before a column tile if cnt > QPRE
 constexpr int LMAX = 128 - QCAP;    // L + QCAP <= 128 (two elements per lane)
-constexpr int KMAX = 64;            // k limit (fallback keeps k per thread in LDS)
+constexpr int KMAX = 64;            // k limit of the C ABI
+constexpr int KLIST = KMAX + 8;     // internal list limit (MN_L2's extended L2^2 list;
+                                    // the fallback keeps it per thread in LDS)
 constexpr int FB_THREADS = 128;
 
 struct alignas(16) GramSmem {
@@ -445,11 +446,7 @@ __global__ __launch_bounds__(256) void k_rerank(
             fb_list[pos] = (int)q;
         }
     }
-    if (lane < k) {
-        const bool ok = lane < keff;
-        out_idx[q * k + lane] = ok ? ix[0] : -1;
-        out_dist[q * k + lane] = ok ? dd[0] : __builtin_inff();
-    }
+    wave_store_list<NR>(dd, ix, k, keff, out_idx + q * k, out_dist + q * k);
 }
 
 // ---------------------------------------------------------------------------
@@ -651,11 +648,7 @@ __global__ __launch_bounds__(256) void k_rerank_buf(
         if (lane == 0) fb_list[atomicAdd(fb_count, 1)] = (int)q;
         return;
     }
-    if (lane < k) {
-        const bool ok = lane < keff;
-        out_idx[q * k + lane] = ok ? ix[0] : -1;
-        out_dist[q * k + lane] = ok ? dd[0] : __builtin_inff();
-    }
+    wave_store_list<NR>(dd, ix, k, keff, out_idx + q * k, out_dist + q * k);
 }
 
 
@@ -671,7 +664,7 @@ __global__ __launch_bounds__(256) void k_rerank_buf(
 //                best key.
 //   k_tau_x1     tau0, tq = (tau0 - |q|^2)/2 and the certification bound
 //                delta(q) (below).
-//   phase 2      gram_sweep.hpp over rows m0..nc-1: every pair with
+//   phase 2      gram_sweep2.hpp over rows m0..nc-1: every pair with
 //                key < tau0(q) is buffered.
 //   k_rerank_x1  exact re-rank + certification over both buffers.
 //
@@ -1260,11 +1253,7 @@ __global__ __launch_bounds__(64 * WPB) void k_rerank_x1(
         if (lane == 0) fb_list[atomicAdd(fb_count, 1)] = (int)qo;
         return;
     }
-    if (lane < k) {
-        const bool ok = lane < keff;
-        out_idx[qo * k + lane] = ok ? ix[0] : -1;
-        out_dist[qo * k + lane] = ok ? dd[0] : __builtin_inff();
-    }
+    wave_store_list<NR>(dd, ix, k, keff, out_idx + qo * k, out_dist + qo * k);
 }
 
 // sum of buffered entries (statistics only; timing mode)
@@ -1287,12 +1276,13 @@ __global__ __launch_bounds__(256) void k_count_cands(const int *__restrict__ c, 
 // MN_L2 (distance.rs:195-203; mst.rs:344 stable sort of the ROOTED f32
 // distances): two different L2^2 values can round to the same f32 root, and
 // then the reference orders them by index, not by the squared value.  The
-// L2^2 list is computed k2 = k + 8 long; one wave per row takes the correctly
-// rounded roots (Rust f32::sqrt; gfx950 sqrtf is not correctly rounded,
-// common.hpp), re-sorts by (root, idx) — which only permutes runs of equal
-// roots — and keeps k.  Entries beyond the list have roots >= the last one,
-// so the result is exact unless the run of roots equal to the k-th one
-// reaches the end of a full list: those rows go to the exact root-keyed scan.
+// L2^2 list is computed k2 = k + 8 long (k2 <= KLIST: two entries a lane); one
+// wave per row takes the correctly rounded roots (Rust f32::sqrt; gfx950
+// sqrtf is not correctly rounded, common.hpp), re-sorts by (root, idx) —
+// which only permutes runs of equal roots — and keeps k.  Entries beyond the
+// list have roots >= the last one, so the result is exact unless the run of
+// roots equal to the k-th one reaches the end of a full list: those rows go to
+// the exact root-keyed scan.
 __global__ __launch_bounds__(256) void k_l2_order(const int32_t *__restrict__ idx2,
                                                   const float *__restrict__ d2, int64_t nq, int k2,
                                                   int k, int64_t nc, int64_t q_off, int64_t c_off,
@@ -1303,26 +1293,29 @@ __global__ __launch_bounds__(256) void k_l2_order(const int32_t *__restrict__ id
     const int lane = threadIdx.x & 63;
     const int64_t q = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     if (q >= nq) return;
-    const int id = lane < k2 ? idx2[q * k2 + lane] : -1;
-    const float sq = lane < k2 ? d2[q * k2 + lane] : __builtin_inff();
-    float key[1] = {id >= 0 ? sqrt_rn_f32(sq) : __builtin_inff()};
-    int ix[1] = {id >= 0 ? id : INT_MAX};
-    const int m = (int)__popcll(__ballot(id >= 0));
-    wave_bitonic_sort<1>(key, ix);
+    float key[2];
+    int ix[2], m = 0;
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+        const int e = lane + 64 * r;
+        const int id = e < k2 ? idx2[q * k2 + e] : -1;
+        const float sq = e < k2 ? d2[q * k2 + e] : __builtin_inff();
+        key[r] = id >= 0 ? sqrt_rn_f32(sq) : __builtin_inff();
+        ix[r] = id >= 0 ? id : INT_MAX;
+        m += (int)__popcll(__ballot(id >= 0));
+    }
+    wave_bitonic_sort<2>(key, ix);
     const int64_t gq = q_off + q;
     const int64_t valid = nc - ((excl && gq >= c_off && gq < c_off + nc) ? 1 : 0);
-    const float rk = __shfl(key[0], min(k, m) - 1 < 0 ? 0 : min(k, m) - 1);
-    const float rl = __shfl(key[0], k2 - 1);
+    const float rk = wave_elem<2>(key, min(k, m) - 1 < 0 ? 0 : min(k, m) - 1);
+    const float rl = wave_elem<2>(key, k2 - 1);
+    // k2 > k always (k <= KMAX, k2 = k + 8): the list extends past rank k
     const bool more = m == k2 && (int64_t)k2 < valid;
     if (more && k <= m && rl == rk) {
         if (lane == 0) fb_list[atomicAdd(fb_count, 1)] = (int)q;
         return;
     }
-    if (lane < k) {
-        const bool ok = lane < m;
-        out_idx[q * k + lane] = ok ? ix[0] : -1;
-        out_dist[q * k + lane] = ok ? key[0] : __builtin_inff();
-    }
+    wave_store_list<2>(key, ix, k, m, out_idx + q * k, out_dist + q * k);
 }
 
 // Rows the bf16x1 path leaves uncertified (after its bf16x3 refill) against a
@@ -1366,8 +1359,8 @@ __global__ __launch_bounds__(256) void k_scatter_escalated(
 // 4. exact fallback scan for uncertified rows
 // ---------------------------------------------------------------------------
 struct alignas(16) FallbackSmem {
-    float ld[FB_THREADS][KMAX];
-    int li[FB_THREADS][KMAX];
+    float ld[FB_THREADS][KLIST];
+    int li[FB_THREADS][KLIST];
     float rd[2];
     int ri[2];
     int rt[2];
@@ -1651,7 +1644,7 @@ static int fb_split_scan(const float *Q, const float *C, int64_t nc, int d, int6
                          hipStream_t s) {
     const int keff_max = k;
     const size_t ldsmax = 160 * 1024;
-    if (nc < 1 || k > KMAX || d < 1 ||
+    if (nc < 1 || k > KLIST || d < 1 ||
         (size_t)d * FSQ * 4 + (size_t)FSQ * FSC * 4 + (size_t)FSC * 8 + 16 > ldsmax)
         return 1;
     static bool attr = false;  // dynamic LDS beyond 64 KB (once per process)
@@ -1663,7 +1656,9 @@ static int fb_split_scan(const float *Q, const float *C, int64_t nc, int d, int6
     }
     const int64_t P = (nc + FSC - 1) / FSC;
     const int64_t chunk = FSC;
-    const int gs = FMG / keff_max;
+    // parts per merge group: their entries fit FMG, their prefix k_fb_merge's
+    // base[FMG / 8 + 1] (k < 8 would otherwise put > 512 parts in a group)
+    const int gs = std::min(FMG / keff_max, FMG / 8);
     // ping-pong part lists: [FSQ][P][keff] and the first merge level; Qt
     const size_t l0 = (size_t)FSQ * P * keff_max, l1 = (size_t)FSQ * ((P + gs - 1) / gs) * keff_max;
     const size_t b0 = (l0 * 8 + 255) & ~(size_t)255, b1 = (l1 * 8 + 255) & ~(size_t)255;
@@ -1790,8 +1785,9 @@ static int knn_f32_core(const float *Q, int64_t nq, const float *C, int64_t nc, 
                         int32_t *out_idx, float *out_dist, int algo) {
     using namespace knn;
     const int k = opts->k;
-    MN_REQUIRE(k >= 1 && k <= KMAX, MN_ENOTSUP, "mn_knn: k=%d outside [1,%d]", k, KMAX);
-    const int margin = opts->margin > 0 ? opts->margin : 16;
+    MN_REQUIRE(k >= 1 && k <= KLIST, MN_ENOTSUP, "mn_knn: k=%d outside [1,%d]", k, KLIST);
+    // margin clipped so that L = k + margin <= LMAX (MN_L2's extended lists)
+    const int margin = std::min(opts->margin > 0 ? opts->margin : 16, LMAX - k);
     const int L = k + margin;
     MN_REQUIRE(L <= LMAX, MN_ENOTSUP, "mn_knn: k+margin=%d exceeds %d", L, LMAX);
     // candidate generator: bf16-split MFMA or f32 MFMA; both are followed by
@@ -1893,7 +1889,7 @@ static int knn_f32_core(const float *Q, int64_t nq, const float *C, int64_t nc, 
                                perm, nc, cnp);
         MN_KCHECK(s, "k_split_bf16");
         tm.mark();
-        const char *ms = getenv("MN_L2_MIN_SLICES");
+        const char *ms = knob("MN_L2_MIN_SLICES");
         const kb16::GramPlan pl = kb16::plan_gram(nq, nc, L, (ms && *ms) ? atoi(ms) : 2);
         t_stats.slices = (int)pl.S;
         const size_t nbuf = (size_t)nq * pl.S * pl.cap;
@@ -1905,10 +1901,12 @@ static int knn_f32_core(const float *Q, int64_t nq, const float *C, int64_t nc, 
         float *btau = (float *)(bmeta + (size_t)nq * pl.S * 4);
         if (nc > 0) {
             const int64_t bq = (nq + kb16::BM - 1) / kb16::BM;
+            auto kern = kb16::k_gram_bf16<kb16::GM_L2, 0>;
+#ifdef MN_TUNING
             // MN_L2_PROBE=noepi: timing probe (K loop only; results invalid)
-            const char *probe = getenv("MN_L2_PROBE");
-            auto kern = (probe && !strcmp(probe, "noepi")) ? kb16::k_gram_bf16<kb16::GM_L2, 1>
-                                                            : kb16::k_gram_bf16<kb16::GM_L2, 0>;
+            const char *probe = knob("MN_L2_PROBE");
+            if (probe && !strcmp(probe, "noepi")) kern = kb16::k_gram_bf16<kb16::GM_L2, 1>;
+#endif
             hipLaunchKernelGGL(kern, dim3((unsigned)(bq * pl.S)),
                                dim3(kb16::NT), 0, s, XSq, nq, XSc, nc, 2 * dp, q_off, c_off, 0, qn,
                                cnp, L, (int)pl.S, pl.chunk, pl.cap, cbuf, bcnt, btau);
@@ -2001,13 +1999,6 @@ static int knn_f32_core(const float *Q, int64_t nq, const float *C, int64_t nc, 
                         int64_t q_off, int64_t c_off, const mn_knn_opts *opts,
                         int32_t *out_idx, float *out_dist, int algo);
 
-// Phase-2 sweep kernel: 2 = gram_sweep2.hpp (ping-pong, 16x16x32 MFMA; the
-// default), 1 = gram_sweep.hpp (MN_X1_SWEEP=1, kept for A/B measurements).
-static int sweep_version() {
-    const char *e = getenv("MN_X1_SWEEP");
-    return (e && *e == '1') ? 1 : 2;
-}
-
 // Host driver of MN_KNN_BF16X1 (section 2c).  Returns 1 (nothing written)
 // when some row is too large for the single-bf16 bound: the caller then runs
 // the split generator.
@@ -2032,10 +2023,10 @@ static int knn_x1(const float *Q, int64_t nq, const float *C, int64_t nc, int32_
     uint16_t *QR = (uint16_t *)scratch(kSlotX1QR, (size_t)nq * dp * 2 + 64);
     // sweep2 reads tile-major KB32 (rows padded to whole 256-row panels; the
     // pad rows are never candidates); the legacy sweep the k-block-major form
-    const char *tme = getenv("MN_X1_TM");  // layout A/B: 0 = k-block-major for sweep2 too
-    const int tmaj = (sweep_version() == 1 || (tme && *tme == '0')) ? 0 : 1;
+    const char *tme = knob("MN_X1_TM");  // tuning build: 0 = k-block-major layout (A/B)
+    const int tmaj = (tme && *tme == '0') ? 0 : 1;
     // tile-major panel stride: nkb + TM_PAD k-blocks (MN_TM_PAD, default 1)
-    const char *tpe = getenv("MN_TM_PAD");
+    const char *tpe = knob("MN_TM_PAD");
     const int tpad = (tpe && *tpe) ? std::max(0, atoi(tpe)) : 1;
     const int pst1 = tmaj ? nkb + tpad : 0, pst3 = tmaj ? 3 * nkb + tpad : 0;
     auto pad256 = [&](int64_t r) { return tmaj ? (r + 255) / 256 * 256 : r; };
@@ -2063,17 +2054,17 @@ static int knn_x1(const float *Q, int64_t nq, const float *C, int64_t nc, int32_
     // profiles/r03h_grid_*.log — uniform C2 / clustered C2 ms: nc/16 x 16
     // 1025 / 1713, nc/24 x 12 978 / 1565, nc/32 x 8 946 / 1976 (its 155k
     // refilled rows), nc/32 x 12 1004 / 1345)
-    const char *sye = getenv("MN_X1_SYM");  // 0: the query-major sweep (A/B)
-    const bool sym_pre = same && excl && tmaj && sweep_version() == 2 && !(sye && *sye == '0');
+    const char *sye = knob("MN_X1_SYM");  // tuning build: 0 = the query-major sweep (A/B)
+    const bool sym_pre = same && excl && tmaj && !(sye && *sye == '0');
     int L1 = sym_pre ? std::min(std::max((3 * k + 3) / 8, 12), 48)
                      : std::min(std::max((k + 1) / 2, 16), 48);
-    const char *fl = getenv("MN_X1_L1");  // experiments: phase-1 list length
+    const char *fl = knob("MN_X1_L1");  // experiments: phase-1 list length
     if (fl && *fl) L1 = std::min(std::max(atoi(fl), 4), 48);
-    const char *fs = getenv("MN_X1_SAMPLE_DIV");  // experiments: sample = nc / div
+    const char *fs = knob("MN_X1_SAMPLE_DIV");  // experiments: sample = nc / div
     const int64_t div = (fs && *fs) ? std::max(2, atoi(fs)) : (sym_pre ? 24 : 16);
     int64_t m0 = std::max<int64_t>(nc / div, (int64_t)64 * L1);
     m0 = (m0 + 255) / 256 * 256;  // whole phase-1 tiles and whole sweep panels
-    const bool two = m0 + 4 * ksw::BC <= nc;
+    const bool two = m0 + 4 * ksw2::BC <= nc;
     if (!two) {
         m0 = nc;
         L1 = std::min(k + margin, kb16::LMAX);
@@ -2152,7 +2143,9 @@ static int knn_x1(const float *Q, int64_t nq, const float *C, int64_t nc, int32_
     const float *tau_r = tau0, *dlt_r = dlt;
     const int *perm_r = perm, *qmap_r = nullptr;
     const float *chc_r = chc;
-    const char *probe = getenv("MN_X1_PROBE");  // noepi: sweep K loop only, no results
+    // tuning build only: timing probes (noepi = sweep K loop only; nodma /
+    // noread = also without the DMA issue / fragment reads): NO outputs
+    const char *probe = knob("MN_X1_PROBE");
     if (sym) {
         // rows in ascending tau0 (position p holds row pi[p]); rows with a
         // non-finite threshold at the top end would break the column fold
@@ -2175,7 +2168,7 @@ static int knn_x1(const float *Q, int64_t nq, const float *C, int64_t nc, int32_
         MN_HIP_TRY(hipMemcpyAsync(&amaxb, flags + 14, 4, hipMemcpyDeviceToHost, s));
         MN_HIP_TRY(hipStreamSynchronize(s));
         // fp16 operands (MN_SYM_F16=0: bf16): x 2^e with max |x 2^e| < 2^14
-        const char *f16e = getenv("MN_SYM_F16");
+        const char *f16e = knob("MN_SYM_F16");
         const bool f16 = !(f16e && *f16e == '0');
         int e16 = 0;
         if (f16) {
@@ -2218,9 +2211,9 @@ static int knn_x1(const float *Q, int64_t nq, const float *C, int64_t nc, int32_
             // Cache): C2 sweep 775 ms; 0: ranges from the diagonal, the
             // longest first: 984 ms (profiles/r03d_ab_sym_order.log)
             const int nbk = (int)((nc + ksw2::BC - 1) / ksw2::BC);
-            const char *tpe2 = getenv("MN_SYM_TPB");
+            const char *tpe2 = knob("MN_SYM_TPB");
             const int TPB = (tpe2 && *tpe2) ? std::max(1, atoi(tpe2)) : 256;
-            const char *ore = getenv("MN_SYM_ORDER");
+            const char *ore = knob("MN_SYM_ORDER");
             const int order = (ore && *ore) ? atoi(ore) : 1;
             const std::vector<int4> tab = ksw2::sym_block_table(nbk, TPB, order);
             int4 *dtab = (int4 *)scratch(kSlotSymTab, tab.size() * sizeof(int4) + 64);
@@ -2229,7 +2222,7 @@ static int knn_x1(const float *Q, int64_t nq, const float *C, int64_t nc, int32_
                                       hipMemcpyHostToDevice, s));
             // per-row buffers: expect ~ L1 nc / m0 candidates a row
             const double expect = (double)L1 * (double)nc / (double)m0;
-            const char *cpe = getenv("MN_SYM_CAP");
+            const char *cpe = knob("MN_SYM_CAP");
             cap2 = (cpe && *cpe) ? std::max(64, atoi(cpe))
                                  : std::max(256, (int)((2.5 * expect + 64.0 + 15.0) / 16.0) * 16);
             S2 = 1;
@@ -2246,15 +2239,16 @@ static int knn_x1(const float *Q, int64_t nq, const float *C, int64_t nc, int32_
             tm.mark();  // SW_SYM: sort / fp16 copy / table -> ms_norms
             sym_mark = 1;
             ksw2::SymArgs sa{dtab, aoff, hoff, -2 * e16};
+            auto sk = f16 ? ksw2::k_gram_sweep2<0, ksw2::SW_SYM, true, true>
+                          : ksw2::k_gram_sweep2<0, ksw2::SW_SYM, true, false>;
+#ifdef MN_TUNING
             // timing probes (results invalid): noepi = K loop only, nodma /
             // noread = also without the DMA issue / fragment reads
-            const int pk = !probe || !*probe ? 0 : !strcmp(probe, "nodma") ? 2
-                           : !strcmp(probe, "noread") ? 3 : 1;
-            auto sk = f16 ? (pk == 0 ? ksw2::k_gram_sweep2<0, ksw2::SW_SYM, true, true>
-                             : pk == 1 ? ksw2::k_gram_sweep2<1, ksw2::SW_SYM, true, true>
-                             : pk == 2 ? ksw2::k_gram_sweep2<2, ksw2::SW_SYM, true, true>
-                                       : ksw2::k_gram_sweep2<3, ksw2::SW_SYM, true, true>)
-                          : ksw2::k_gram_sweep2<0, ksw2::SW_SYM, true, false>;
+            if (f16 && probe && *probe)
+                sk = !strcmp(probe, "nodma") ? ksw2::k_gram_sweep2<2, ksw2::SW_SYM, true, true>
+                     : !strcmp(probe, "noread") ? ksw2::k_gram_sweep2<3, ksw2::SW_SYM, true, true>
+                                                : ksw2::k_gram_sweep2<1, ksw2::SW_SYM, true, true>;
+#endif
             hipLaunchKernelGGL(sk, dim3((unsigned)tab.size()), dim3(ksw2::NT), 0, s, XK, nc, XK,
                                nc, nkb, (int64_t)0, (int64_t)0, 1, tqP, tauP, hcS, (int64_t)0, 1,
                                (int64_t)0, cap2, cbuf2, cnt2, pst1, sa);
@@ -2269,7 +2263,7 @@ static int knn_x1(const float *Q, int64_t nq, const float *C, int64_t nc, int32_
     }
     if (two && !sym) {
         const double expect = (double)L1 * (double)(nc - m0) / (double)m0;
-        const ksw::SweepPlan p2 = ksw::plan_sweep(nq, nc - m0, expect);
+        const ksw2::SweepPlan p2 = ksw2::plan_sweep(nq, nc - m0, expect);
         S2 = (int)p2.S;
         cap2 = p2.cap;
         t_stats.sweep_slices = S2;
@@ -2279,31 +2273,24 @@ static int knn_x1(const float *Q, int64_t nq, const float *C, int64_t nc, int32_
         cnt2 = (int *)scratch(kSlotX1Meta2, (size_t)nq * S2 * 4 + 64);
         MN_REQUIRE(cbuf2 && cnt2, MN_ENOMEM, "mn_knn: sweep buffer allocation failed (%zu MB)",
                    (nbuf2 * sizeof(uint2)) >> 20);
-        const int64_t nqb = (nq + ksw::BQ - 1) / ksw::BQ;
+        const int64_t nqb = (nq + ksw2::BQ - 1) / ksw2::BQ;
         const int64_t grid = nqb * p2.S;
         MN_REQUIRE(grid < INT_MAX && nq * 32 < INT_MAX && nc * 32 < INT_MAX, MN_ENOTSUP,
                    "mn_knn: sweep grid too large (split the queries / corpus)");
+        using ksw2::SW_L2;
+        auto kern = tmaj ? ksw2::k_gram_sweep2<0, SW_L2, true> : ksw2::k_gram_sweep2<0, SW_L2, false>;
+#ifdef MN_TUNING
         // timing probes: noepi = K loop only; nodma / noread = also without the
-        // in-loop DMA issue / fragment reads (diagnostics, results invalid)
-        const bool noepi = probe && (!strcmp(probe, "noepi") || !strcmp(probe, "nodma") ||
-                                     !strcmp(probe, "noread") || !strcmp(probe, "nowait"));
-        if (sweep_version() == 1) {
-            auto kern = noepi ? ksw::k_gram_sweep<1> : ksw::k_gram_sweep<0>;
-            hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(ksw::NT), 0, s, QK, nq, CK, nc,
-                               nkb, q_off, (int64_t)0, 0, tq, tau0, chc, m0, S2, p2.chunk, cap2,
-                               cbuf2, cnt2);
-        } else {
-            using ksw2::SW_L2;
-            auto kern = !noepi ? (tmaj ? ksw2::k_gram_sweep2<0, SW_L2, true>
-                                     : ksw2::k_gram_sweep2<0, SW_L2, false>)
-                        : !strcmp(probe, "nodma") ? ksw2::k_gram_sweep2<2, SW_L2, true>
-                        : !strcmp(probe, "noread") ? ksw2::k_gram_sweep2<3, SW_L2, true>
-                        : !strcmp(probe, "nowait") ? ksw2::k_gram_sweep2<4, SW_L2, true>
-                                                   : ksw2::k_gram_sweep2<1, SW_L2, true>;
-            hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(ksw2::NT), 0, s, QK, nq, CK, nc,
-                               nkb, q_off, (int64_t)0, 0, tq, tau0, chc, m0, S2, p2.chunk, cap2,
-                               cbuf2, cnt2, pst1, ksw2::SymArgs{});
-        }
+        // in-loop DMA issue / fragment reads; nowait = DMA never waited for
+        if (probe && *probe)
+            kern = !strcmp(probe, "nodma") ? ksw2::k_gram_sweep2<2, SW_L2, true>
+                   : !strcmp(probe, "noread") ? ksw2::k_gram_sweep2<3, SW_L2, true>
+                   : !strcmp(probe, "nowait") ? ksw2::k_gram_sweep2<4, SW_L2, true>
+                                              : ksw2::k_gram_sweep2<1, SW_L2, true>;
+#endif
+        hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(ksw2::NT), 0, s, QK, nq, CK, nc,
+                           nkb, q_off, (int64_t)0, 0, tq, tau0, chc, m0, S2, p2.chunk, cap2,
+                           cbuf2, cnt2, pst1, ksw2::SymArgs{});
         MN_KCHECK(s, "k_gram_sweep");
     }
     tm.mark();
@@ -2420,25 +2407,19 @@ static int knn_x1(const float *Q, int64_t nq, const float *C, int64_t nc, int32_
         // overflowed 62.7k of 80k refilled rows); 32 (k + 16), the buffer kept
         // within ~16 GB
         const double ex3 = std::min(32.0 * (k + 16), 16e9 / (20.0 * (double)nfb));
-        const ksw::SweepPlan p3 = ksw::plan_sweep(nfb, nc, std::max(ex3, 8.0 * (k + 16)));
+        const ksw2::SweepPlan p3 = ksw2::plan_sweep(nfb, nc, std::max(ex3, 8.0 * (k + 16)));
         const size_t nbuf3 = (size_t)nfb * p3.S * p3.cap;
         uint2 *cbuf3 = (uint2 *)scratch(kSlotX1Buf2, nbuf3 * sizeof(uint2) + 64);
         int *cnt3 = (int *)scratch(kSlotX1Meta2, (size_t)nfb * p3.S * 4 + 64);
         MN_REQUIRE(cbuf3 && cnt3, MN_ENOMEM, "mn_knn: refill buffer allocation failed (%zu MB)",
                    (nbuf3 * sizeof(uint2)) >> 20);
-        const int64_t grid3 = ((nfb + ksw::BQ - 1) / ksw::BQ) * p3.S;
+        const int64_t grid3 = ((nfb + ksw2::BQ - 1) / ksw2::BQ) * p3.S;
         MN_REQUIRE(grid3 < INT_MAX, MN_ENOTSUP, "mn_knn: refill grid too large");
-        if (sweep_version() == 1)
-            hipLaunchKernelGGL(ksw::k_gram_sweep<0>, dim3((unsigned)grid3), dim3(ksw::NT), 0, s,
-                               QK3, (int64_t)nfb, CK3, nc, nkb3, (int64_t)0, (int64_t)0, 0, tq3,
-                               tau3, chc_r, (int64_t)0, (int)p3.S, p3.chunk, p3.cap, cbuf3, cnt3);
-        else
-            hipLaunchKernelGGL((tmaj ? ksw2::k_gram_sweep2<0, ksw2::SW_L2, true>
-                                   : ksw2::k_gram_sweep2<0, ksw2::SW_L2, false>),
-                               dim3((unsigned)grid3), dim3(ksw2::NT), 0, s,
-                               QK3, (int64_t)nfb, CK3, nc, nkb3, (int64_t)0, (int64_t)0, 0, tq3,
-                               tau3, chc_r, (int64_t)0, (int)p3.S, p3.chunk, p3.cap, cbuf3, cnt3,
-                               pst3, ksw2::SymArgs{});
+        hipLaunchKernelGGL((tmaj ? ksw2::k_gram_sweep2<0, ksw2::SW_L2, true>
+                                 : ksw2::k_gram_sweep2<0, ksw2::SW_L2, false>),
+                           dim3((unsigned)grid3), dim3(ksw2::NT), 0, s, QK3, (int64_t)nfb, CK3,
+                           nc, nkb3, (int64_t)0, (int64_t)0, 0, tq3, tau3, chc_r, (int64_t)0,
+                           (int)p3.S, p3.chunk, p3.cap, cbuf3, cnt3, pst3, ksw2::SymArgs{});
         MN_KCHECK(s, "k_gram_sweep<x3>");
         int *big_count3 = flags + 6;
         int *big_list3 = fb_list + nq;
@@ -2479,7 +2460,7 @@ static int knn_x1(const float *Q, int64_t nq, const float *C, int64_t nc, int32_
     int split = 1;
     // MN_FB_SPLIT: the row limit of the split scan (default 4096; 0 = always
     // the batched split-generator pass; A/B and tests)
-    const char *fse = getenv("MN_FB_SPLIT");
+    const char *fse = knob("MN_FB_SPLIT");
     const int fb_lim = (fse && *fse) ? std::max(0, atoi(fse)) : 4096;
     if (nfb2 > 0 && nfb2 <= fb_lim && nc >= (1 << 16)) {
         split = fb_split_scan(Q, C, nc, d, q_off, c_off, excl, k, fb_list, nfb2, ubv, false,
@@ -2488,7 +2469,7 @@ static int knn_x1(const float *Q, int64_t nq, const float *C, int64_t nc, int32_
     }
     if (split == MN_OK) {
         // done
-    } else if (nfb2 > 0 && nc >= (1 << 16) && k + 1 <= KMAX) {
+    } else if (nfb2 > 0 && nc >= (1 << 16) && k + 1 <= KLIST) {
         // the refill slot is dead here (knn_f32_core below does not use it):
         // rows, the gathered queries and the (k + 1)-lists, 16-B aligned parts
         auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
@@ -2573,7 +2554,7 @@ static int knn_f32_impl(const float *Q, int64_t nq, const float *C, int64_t nc, 
     t_stats.n_queries = nq;
     // MN_L2: the L2^2 graph k2 = k + 8 long, then k_l2_order (root order)
     const bool l2 = opts->metric == MN_L2 && nq > 0;
-    const int k2 = l2 ? std::min(k + 8, KMAX) : k;
+    const int k2 = l2 ? k + 8 : k;  // <= KLIST
     mn_knn_opts o2 = *opts;
     o2.k = k2;
     o2.metric = MN_L2SQ;

@@ -1144,10 +1144,11 @@ static int laplacian_impl(const int32_t *nbr, const void *val, int32_t val_f64, 
     double *deg64 = P.sym == MN_SYM_UNION ? (double *)degbuf : nullptr;
     float *deg32 = P.sym == MN_SYM_UNION ? nullptr : (float *)degbuf;
 
-    // bucketed assembly (MN_LAP_V1=1: the atomic counting-sort path, A/B)
+    // bucketed assembly (the atomic counting-sort path for shapes outside its
+    // limits; tuning build: MN_LAP_V1=1 forces it, A/B)
     const int64_t NB = (n + BR - 1) / BR;
     const int64_t nA = (nk + ACH - 1) / ACH;
-    const char *v1e = getenv("MN_LAP_V1");
+    const char *v1e = knob("MN_LAP_V1");
     const bool v2 = k > 0 && NB <= NBMAX && nk < INT_MAX && !(v1e && *v1e == '1');
     char *g0 = nullptr;
     if (v2) {

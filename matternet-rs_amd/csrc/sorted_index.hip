@@ -472,7 +472,7 @@ static int sorted_index_impl(const double *lam, int64_t n, int64_t *order, doubl
         MN_HIP_TRY(stream_wait(side, s));
         // pass-1 certificate partials (the sequential pass 1 runs only if it
         // fails); MN_STD_SEQ=1 forces the sequential pass (tests)
-        const char *fs = getenv("MN_STD_SEQ");
+        const char *fs = knob("MN_STD_SEQ");
         const bool force_seq = fs && *fs == '1';
         double *part1 = force_seq ? nullptr : (double *)scratch(kSlotNorms2, sizeof(double) * 3 * SUM_BLOCKS + 64);
         if (part1) {

@@ -189,10 +189,13 @@ constexpr int SF_LDS_CAP = 8192;
 
 __global__ __launch_bounds__(256) void k_sf_keep(const int64_t *__restrict__ indptr, int64_t n,
                                                  double ratio, int active,
-                                                 int32_t *__restrict__ keep) {
+                                                 int32_t *__restrict__ keep,
+                                                 int *__restrict__ too_long) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const int64_t len = indptr[i + 1] - indptr[i];
+    // the row sorts index a row with int positions and a power-of-two pad
+    if (len > ((int64_t)1 << 30)) atomicOr(too_long, 1);
     int64_t kc = len;
     if (active && len > 0) {
         // ((len as f64 * ratio).ceil() as usize).max(1).min(len)
@@ -401,16 +404,26 @@ static int sfgrass_impl(const mn_csr *in, int64_t n_nodes, double ratio, mn_csr 
     // output row pointers first (their last entry is the output nnz)
     int64_t *optr = caller ? given.indptr : nullptr;
     if (!caller) MN_HIP_TRY(hipMalloc(&optr, sizeof(int64_t) * (n + 1)));
-    hipLaunchKernelGGL(k_sf_keep, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, in->indptr,
-                       n, r, active, keep);
-    hipError_t e = scan::exclusive_scan(keep, n, optr, part, s);
+    hipError_t e = hipMemsetAsync(flags + 4, 0, 4, s);
+    if (e == hipSuccess) {
+        hipLaunchKernelGGL(k_sf_keep, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s,
+                           in->indptr, n, r, active, keep, flags + 4);
+        e = scan::exclusive_scan(keep, n, optr, part, s);
+    }
     int64_t nnz = 0;
+    int too_long = 0;
     if (e == hipSuccess) e = hipMemcpyAsync(&nnz, optr + n, 8, hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipMemcpyAsync(&too_long, flags + 4, 4, hipMemcpyDeviceToHost, s);
     if (e == hipSuccess) e = hipStreamSynchronize(s);
     if (e != hipSuccess) {
         if (!caller) (void)hipFree(optr);
         set_error("mn_sparsify_sfgrass: %s", hipGetErrorString(e));
         return MN_EHIP;
+    }
+    if (too_long) {
+        if (!caller) (void)hipFree(optr);
+        set_error("mn_sparsify_sfgrass: a row longer than 2^30 entries");
+        return MN_ENOTSUP;
     }
     if (caller && nnz > given.nnz) {
         out->nnz = nnz;

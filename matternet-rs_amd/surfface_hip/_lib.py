@@ -6,11 +6,16 @@ to load, every op raises.  Build it with `make -C matternet-rs_amd/csrc` (or
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes as C
 import os
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(os.path.dirname(PKG_DIR), "libmatternet_hip.so")
+# The tuning build (-DMN_TUNING: reads the MN_* A/B knobs, carries the timing
+# probes) for scripts/ and the tests of alternative generator paths; the
+# release library above ignores every MN_* tuning variable.
+TUNING_LIB_PATH = os.path.join(os.path.dirname(PKG_DIR), "libmatternet_hip_tuning.so")
 
 MN_OK, MN_EINVAL, MN_ENOMEM, MN_ENONFINITE, MN_ECAP, MN_EHIP, MN_ENOTSUP = 0, -1, -2, -3, -4, -5, -6
 _NAMES = {-1: "MN_EINVAL", -2: "MN_ENOMEM", -3: "MN_ENONFINITE", -4: "MN_ECAP", -5: "MN_EHIP",
@@ -156,22 +161,49 @@ SIGNATURES = {
 MN_SPARSIFY_SFGRASS, MN_SPARSIFY_INLINE = 0, 1
 
 _LIB = None
+_LOADED = {}
+
+
+def _load(path: str) -> C.CDLL:
+    if path not in _LOADED:
+        if not os.path.exists(path):
+            raise ImportError(f"{os.path.basename(path)} not built at {path}; "
+                              "run `make -C matternet-rs_amd/csrc`")
+        L = C.CDLL(path)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _LOADED[path] = L
+    return _LOADED[path]
 
 
 def lib() -> C.CDLL:
     """Load the HIP library (raises loudly if it is missing: no fallback path)."""
     global _LIB
     if _LIB is None:
-        if not os.path.exists(LIB_PATH):
-            raise ImportError(f"libmatternet_hip.so not built at {LIB_PATH}; "
-                              "run `make -C matternet-rs_amd/csrc`")
-        L = C.CDLL(LIB_PATH)
-        for name, (res, args) in SIGNATURES.items():
-            fn = getattr(L, name)
-            fn.restype = res
-            fn.argtypes = args
-        _LIB = L
+        _LIB = _load(LIB_PATH)
     return _LIB
+
+
+def select_tuning_library() -> None:
+    """Scripts: make every op of this process use the tuning build (MN_* knobs
+    and timing probes honoured).  Call before the first op."""
+    global _LIB
+    _LIB = _load(TUNING_LIB_PATH)
+
+
+@contextlib.contextmanager
+def use_tuning():
+    """Tests of alternative paths: the ops inside the block run on the tuning
+    build (same sources, MN_* knobs honoured); the release library after."""
+    global _LIB
+    prev = lib()
+    _LIB = _load(TUNING_LIB_PATH)
+    try:
+        yield _LIB
+    finally:
+        _LIB = prev
 
 
 def check(rc: int) -> None:

@@ -39,6 +39,7 @@ import math
 from dataclasses import dataclass, field
 from typing import Optional
 
+import numpy as np
 import torch
 
 from . import _lib
@@ -125,16 +126,14 @@ def _weight_can_drop(eps: float, sigma: float, p: float) -> bool:
         return False
 
     def w(d):
-        x = d / sigma
-        if x == 0.0:
-            t = 0.0 if p > 0 else (1.0 if p == 0 else math.inf)
-        else:
-            try:
-                t = math.pow(x, p)
-            except OverflowError:
-                t = math.inf
-        return 1.0 / (1.0 + t)
-    return not (min(w(0.0), w(dmax)) > 1e-12)
+        # the reference's f64 arithmetic (laplacian.rs:256 `(d / sigma).powf(p)`):
+        # sigma = 0 or a negative base with a fractional p give inf / NaN, the
+        # weight then fails the `> 1e-12` filter (no Python raise)
+        with np.errstate(all="ignore"):
+            t = np.power(np.float64(d) / np.float64(sigma), np.float64(p))
+            return np.float64(1.0) / (np.float64(1.0) + t)
+    # NaN-safe: a NaN weight can drop (it fails the filter)
+    return not (min(w(0.0), w(dmax)) > 1e-12) or bool(np.isnan(w(0.0)) or np.isnan(w(dmax)))
 
 
 @on_device

@@ -1,8 +1,7 @@
-"""A/B of the two phase-2 sweep kernels (MN_X1_SWEEP=1 gram_sweep.hpp vs 2
-gram_sweep2.hpp) in ONE process on the same device and data (guide rule 24):
-C2 shape by default, interleaved rounds, outputs compared bit for bit.
-  python scripts/ab_sweep.py [n] [d] [rounds]
-AB_ENVS="MN_X1_TM=1;MN_X1_TM=0" compares environment variants instead
+"""A/B of sweep variants (tuning-build knobs) in ONE process on the same device
+and data (guide rule 24): C2 shape by default, interleaved rounds, outputs
+compared bit for bit; AB_PROBES times the K-loop probes of each variant.
+  AB_ENVS="MN_X1_SYM=1;MN_X1_SYM=0" python scripts/ab_sweep.py [n] [d] [rounds]
 (';' between variants, ',' between assignments)."""
 import json
 import os
@@ -14,6 +13,7 @@ sys.path[:0] = [ROOT, os.path.join(ROOT, "matternet-rs_amd")]
 import torch  # noqa: E402
 
 import surfface_hip as S  # noqa: E402
+S._lib.select_tuning_library()  # MN_* knobs / timing probes: the tuning build
 from surfface_hip import _lib  # noqa: E402
 
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 1_000_000
@@ -23,10 +23,7 @@ X = torch.empty((n, d), dtype=torch.float32, device="cuda")
 _lib.check(_lib.lib().mn_fill_uniform_f32(X.data_ptr(), n, d, 42, 0, None))
 torch.cuda.synchronize()
 ref = None
-if os.environ.get("AB_ENVS"):
-    VERS = os.environ["AB_ENVS"].split(";")
-else:
-    VERS = ["MN_X1_SWEEP=" + v for v in os.environ.get("AB_VERSIONS", "1,2").split(",")]
+VERS = os.environ.get("AB_ENVS", "MN_X1_SYM=1").split(";")
 res = {v: [] for v in VERS}
 probe = {v: [] for v in VERS}
 for r in range(rounds):

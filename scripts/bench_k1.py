@@ -6,6 +6,7 @@ _R = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(_R, "matternet-rs_amd"))
 import torch
 import surfface_hip as S
+S._lib.select_tuning_library()  # MN_* knobs / timing probes: the tuning build
 from surfface_hip import _lib
 
 ap = argparse.ArgumentParser()

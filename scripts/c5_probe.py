@@ -12,6 +12,7 @@ import torch
 ROOT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..")
 sys.path[:0] = [ROOT, os.path.join(ROOT, "matternet-rs_amd")]
 import surfface_hip as S  # noqa: E402
+S._lib.select_tuning_library()  # MN_* knobs / timing probes: the tuning build
 from surfface_hip import _lib  # noqa: E402
 
 n = int(os.environ.get("C5P_N", 1 << 20))

@@ -13,6 +13,7 @@ import torch  # noqa: E402
 
 import datagen  # noqa: E402
 import surfface_hip as S  # noqa: E402
+S._lib.select_tuning_library()  # MN_* knobs / timing probes: the tuning build
 
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 1_000_000
 variants = (sys.argv[2] if len(sys.argv) > 2 else "default").split(";")

@@ -3,6 +3,7 @@ import numpy as np, torch
 ROOT = os.environ.get("GRAFT_REPO_ROOT", ".")
 sys.path[:0] = [ROOT, os.path.join(ROOT, "matternet-rs_amd"), os.path.join(ROOT, "tests")]
 import surfface_hip as S
+S._lib.select_tuning_library()  # MN_* knobs / timing probes: the tuning build
 import datagen
 rng = np.random.default_rng(3)
 n, d = 20_000, 64

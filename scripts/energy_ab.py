@@ -11,6 +11,7 @@ sys.path[:0] = [ROOT, os.path.join(ROOT, "matternet-rs_amd")]
 import torch  # noqa: E402
 
 import surfface_hip as S  # noqa: E402
+S._lib.select_tuning_library()  # MN_* knobs / timing probes: the tuning build
 from surfface_hip import _lib  # noqa: E402
 
 n = int(os.environ.get("EAB_N", 1_000_000))

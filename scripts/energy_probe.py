@@ -9,6 +9,7 @@ sys.path[:0] = [ROOT, os.path.join(ROOT, "matternet-rs_amd")]
 import torch  # noqa: E402
 
 import surfface_hip as S  # noqa: E402
+S._lib.select_tuning_library()  # MN_* knobs / timing probes: the tuning build
 from surfface_hip import _lib  # noqa: E402
 
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 1_000_000

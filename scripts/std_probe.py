@@ -10,6 +10,7 @@ import torch
 
 sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "matternet-rs_amd"))
 import surfface_hip as S  # noqa: E402
+S._lib.select_tuning_library()  # MN_* knobs / timing probes: the tuning build
 
 rng = np.random.default_rng(0)
 lam = torch.from_numpy(rng.uniform(0, 1, 1_000_000)).cuda()

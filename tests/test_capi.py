@@ -61,6 +61,31 @@ def test_no_cpu_fallback_in_product_path():
         assert not re.search(r"import\s+oracle|from\s+oracle|liboracle|\bor_[a-z0-9_]+\(", text), path
 
 
+def test_release_library_has_no_probes_or_tuning_knobs():
+    """the release .so cannot be switched into a timing
+    probe (results invalid, MN_OK) or an A/B path by a stray environment
+    variable.  The probe kernel instantiations (PROBE != 0 template argument)
+    and the MN_* tuning variable names exist only in the tuning build; the
+    release library reads only the diagnostics MN_DEBUG_SYNC / MN_X1_DEBUG."""
+    blob = open(_lib.LIB_PATH, "rb").read()
+    # k_gram_sweep2<PROBE, ...> / k_gram_bf16<MODE, PROBE>: only PROBE = 0
+    assert re.search(rb"k_gram_sweep2ILi0E", blob)
+    assert not re.search(rb"k_gram_sweep2ILi[1-9]E", blob)
+    assert not re.search(rb"k_gram_bf16ILi\d+ELi[1-9]E", blob)
+    # the legacy sweep of gram_sweep.hpp is gone
+    assert not re.search(rb"k_gram_sweepILi", blob)
+    # MN_* names in the binary: the header's own constants (error texts) and
+    # the two diagnostics only
+    consts = set(re.findall(rb"\b(MN_[A-Z0-9_]+)\b",
+                            open(os.path.join(ROOT, "include", "matternet_hip.h"), "rb").read()))
+    names = set(re.findall(rb"MN_[A-Z0-9_]{3,}", blob)) - consts
+    assert names <= {b"MN_DEBUG_SYNC", b"MN_X1_DEBUG"}, names
+    # the tuning build carries them (scripts/ and alternative-path tests)
+    if os.path.exists(_lib.TUNING_LIB_PATH):
+        tb = open(_lib.TUNING_LIB_PATH, "rb").read()
+        assert b"MN_X1_PROBE" in tb and re.search(rb"k_gram_sweep2ILi1E", tb)
+
+
 def test_lexicographic_rank_formula_matches_string_sort():
     """The closed-form rank used by k_make_keys (sorted_index.hip), restated."""
     def cwp(v, N):

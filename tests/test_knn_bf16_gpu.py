@@ -10,6 +10,7 @@ import pytest
 import torch
 
 import datagen
+from surfface_hip import _lib
 from oracle import oracle as O
 
 pytestmark = pytest.mark.gpu
@@ -140,11 +141,12 @@ def test_two_phase_edge_rows_and_one_phase_agree(monkeypatch):
     assert st["algo"] == 3 and st["sample_rows"] > 0  # MN_KNN_BF16X1
     assert st["n_uncertified"] >= 150
     exact((i, d, w), O.knn_cos(Xf, 16, **kw))
-    monkeypatch.setenv("MN_BF16_TM", "0")  # k-block-major sweep layout
-    exact((i, d, w), hip(Xt, 16, **kw)[:3])
-    monkeypatch.delenv("MN_BF16_TM")
-    monkeypatch.setenv("MN_BF16_X1", "0")
-    i1, d1, w1, st1 = hip(Xt, 16, **kw)
+    with _lib.use_tuning():  # the alternative paths: tuning build knobs
+        monkeypatch.setenv("MN_BF16_TM", "0")  # k-block-major sweep layout
+        exact((i, d, w), hip(Xt, 16, **kw)[:3])
+        monkeypatch.delenv("MN_BF16_TM")
+        monkeypatch.setenv("MN_BF16_X1", "0")
+        i1, d1, w1, st1 = hip(Xt, 16, **kw)
     assert st1["sample_rows"] == 0
     exact((i, d, w), (i1, d1, w1))
 
@@ -197,7 +199,8 @@ def test_two_phase_symmetric_sweep_matches_query_major(kind, monkeypatch):
                                          for k, v in st.items()}))
     assert st["sweep_slices"] == -1  # the symmetric sweep ran
     monkeypatch.setenv("MN_BF16_SYM", "0")
-    i0, d0, w0, st0 = hip(Xt, 24, **kw)
+    with _lib.use_tuning():
+        i0, d0, w0, st0 = hip(Xt, 24, **kw)
     assert st0["sweep_slices"] > 0
     ref = O.knn_cos(Xf, 24, **kw)
     exact((i, d, w), ref)

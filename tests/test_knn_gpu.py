@@ -10,6 +10,7 @@ import pytest
 import torch
 
 import datagen
+from surfface_hip import _lib
 from oracle import oracle as O
 
 pytestmark = pytest.mark.gpu
@@ -270,12 +271,13 @@ def test_bf16x1_symmetric_sweep_matches_query_major(kind, f16, monkeypatch):
     X = (datagen.uniform(n, d, seed=8) if kind == "uniform"
          else datagen.clustered(n, d, seed=9, blobs=12, dup_frac=0.01, zero_frac=0.002))
     monkeypatch.setenv("MN_SYM_F16", f16)
-    idx, dist, st = hip_knn(X, k, algo="bf16x1", timing=True)
-    print(f"SYM {kind} f16={f16}", json.dumps({kk: (round(v, 2) if isinstance(v, float) else v)
-                                               for kk, v in st.items()}))
-    assert st["sweep_slices"] == -1  # the symmetric sweep ran
-    monkeypatch.setenv("MN_X1_SYM", "0")
-    idx0, dist0, st0 = hip_knn(X, k, algo="bf16x1", timing=True)
+    with _lib.use_tuning():  # the tuning build honours the knobs
+        idx, dist, st = hip_knn(X, k, algo="bf16x1", timing=True)
+        print(f"SYM {kind} f16={f16}", json.dumps({kk: (round(v, 2) if isinstance(v, float) else v)
+                                                   for kk, v in st.items()}))
+        assert st["sweep_slices"] == -1  # the symmetric sweep ran
+        monkeypatch.setenv("MN_X1_SYM", "0")
+        idx0, dist0, st0 = hip_knn(X, k, algo="bf16x1", timing=True)
     assert st0["sweep_slices"] > 0
     ridx, rdist = O.knn_l2sq(X, k)
     assert_exact(idx, dist, ridx, rdist)
@@ -314,7 +316,8 @@ def test_uncertified_rows_split_scan(split, monkeypatch):
     dup = np.setdiff1d(np.arange(1, 12), zero)
     X[dup + 20000] = X[dup]
     monkeypatch.setenv("MN_FB_SPLIT", split)
-    idx, dist, st = hip_knn(X, k, algo="bf16x1", timing=True)
+    with _lib.use_tuning():  # the tuning build honours MN_FB_SPLIT
+        idx, dist, st = hip_knn(X, k, algo="bf16x1", timing=True)
     print(f"uncertified split={split}", json.dumps(
         {kk: (round(v, 3) if isinstance(v, float) else v) for kk, v in st.items()}))
     assert st["n_uncertified"] > 0, st
@@ -359,3 +362,81 @@ def test_euclidean_root_ties_rescan_large_corpus():
     np.testing.assert_array_equal(r.idx.cpu().numpy()[rows], ridx)
     np.testing.assert_array_equal(r.dist.cpu().numpy()[rows].view(np.uint32), rdist.view(np.uint32))
     assert r.stats["n_root_rescan"] >= 1
+
+
+def _wide_range_rows(case, n, d, seed):
+    """data the fp16 symmetric sweep's single global
+    exponent and corpus-maximum bounds handle worst.
+      log_scales  every row scaled by 10^U(-6, 6): the largest rows set the
+                  fp16 exponent, rows below ~1e-2 flush to all-zero fp16;
+      tiny_mixed  10 % of the rows scaled by 1e-30 among O(1) rows (their
+                  squared differences underflow: exact ties at 0);
+      fp16_edge   O(1) rows plus rows at the fp16 range limit (65504 and
+                  65520, which rounds to fp16 inf unscaled)."""
+    rng = np.random.default_rng(seed)
+    X = datagen.uniform(n, d, seed=seed)
+    if case == "log_scales":
+        X = (X * (10.0 ** rng.uniform(-6, 6, n))[:, None]).astype(np.float32)
+    elif case == "tiny_mixed":
+        rows = rng.choice(n, n // 10, replace=False)
+        X[rows] *= np.float32(1e-30)
+    else:
+        X[123] *= np.float32(65504.0)
+        X[4567, 7] = np.float32(65520.0)
+        X[8901] = np.float32(65504.0)
+    return np.ascontiguousarray(X)
+
+
+@pytest.mark.parametrize("case", ["log_scales", "tiny_mixed", "fp16_edge"])
+def test_symmetric_fp16_sweep_wide_dynamic_range(case):
+    """The headline fp16 symmetric sweep (SW_SYM ran: sweep_slices == -1) on
+    wide-dynamic-range rows at a size where it is selected: every row
+    bit-exact vs the oracle; the rows the certification leaves to the
+    refill / exact scan and the time they take are printed and bounded."""
+    import json
+    n, d, k = 40_000, 64, 16
+    X = _wide_range_rows(case, n, d, seed={"log_scales": 31, "tiny_mixed": 32, "fp16_edge": 33}[case])
+    idx, dist, st = hip_knn(X, k, algo="bf16x1", timing=True)
+    print(f"wide-range {case}", json.dumps({kk: (round(v, 2) if isinstance(v, float) else v)
+                                            for kk, v in st.items()}))
+    assert st["sweep_slices"] == -1  # SW_SYM ran
+    ridx, rdist = O.knn_l2sq(X, k)
+    assert_exact(idx, dist, ridx, rdist)
+    assert st["ms_total"] < 20_000, st
+    if case == "fp16_edge":
+        assert st["n_uncertified"] <= n // 100, st
+
+
+def test_split_scan_small_k_many_parts():
+    """the split exact scan's final merge with k < 8 over
+    more than 512 corpus parts (nc > 600K: 684 parts of 1024 rows) — the
+    merge groups are capped at FMG / 8 parts.  Zero rows (exact ties at 0
+    far beyond k) are the uncertified rows; bit-exact vs the oracle."""
+    n, d, k = 700_000, 16, 3
+    X = datagen.uniform(n, d, seed=17)
+    zero = np.random.default_rng(4).choice(n, 200, replace=False)
+    X[zero] = 0.0
+    idx, dist, st = hip_knn(X, k, algo="bf16x1", timing=True)
+    assert 0 < st["n_uncertified"] <= 4096, st  # the split scan's row range
+    rows = np.unique(np.concatenate([zero[:48], np.random.default_rng(5).choice(n, 16, replace=False)]))
+    ridx, rdist = O.knn_l2sq_rows(X, k, rows)
+    np.testing.assert_array_equal(idx[rows], ridx)
+    np.testing.assert_array_equal(dist[rows].view(np.uint32), rdist.view(np.uint32))
+
+
+@pytest.mark.parametrize("algo_e", ["auto", "bf16x1"])
+def test_euclidean_k64_extended_list(algo_e):
+    """MN_L2 at k = 64 computes the L2^2 list k + 8 = 72
+    long (two entries a lane), so a row is sent to the root-keyed rescan only
+    when its equal-root run really reaches past the list: on random data
+    (almost) none; sampled rows bit-exact vs the reference root order."""
+    import surfface_hip as S
+    n, d, k = 20_000, 32, 64
+    X = datagen.uniform(n, d, seed=23)
+    r = S.knn_l2sq(torch.from_numpy(X).cuda(), k, euclidean=True, algo=algo_e, timing=True)
+    torch.cuda.synchronize()
+    assert r.stats["n_root_rescan"] <= 16, r.stats
+    rows = np.random.default_rng(7).choice(n, 24, replace=False)
+    ridx, rdist = _euclid_rows_np(X, rows, k)
+    np.testing.assert_array_equal(r.idx.cpu().numpy()[rows], ridx)
+    np.testing.assert_array_equal(r.dist.cpu().numpy()[rows].view(np.uint32), rdist.view(np.uint32))

@@ -8,6 +8,7 @@ import pytest
 import torch
 
 from oracle import oracle as O
+from surfface_hip import _lib
 
 pytestmark = pytest.mark.gpu
 
@@ -102,7 +103,8 @@ def _std_both(lam, monkeypatch):
     sequential pass 1 (MN_STD_SEQ=1)."""
     _, _, sd = hip_sort(lam)
     monkeypatch.setenv("MN_STD_SEQ", "1")
-    _, _, sd_seq = hip_sort(lam)
+    with _lib.use_tuning():  # the tuning build honours MN_STD_SEQ
+        _, _, sd_seq = hip_sort(lam)
     monkeypatch.delenv("MN_STD_SEQ")
     return sd, sd_seq
 
