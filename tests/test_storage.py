@@ -1,5 +1,6 @@
 """§8(f) rank 4: parquet interchange in the reference's layouts
 (src_legacy/storage/parquet.rs:412-583, 728-880) — CPU only."""
+import json
 import os
 import sys
 
@@ -60,3 +61,73 @@ def test_lambda_roundtrip(tmp_path):
     np.testing.assert_array_equal(ST.load_lambda(fp), lam)
     with pytest.raises(ValueError):
         ST.save_lambda(np.zeros(0), str(tmp_path), "empty")
+
+
+def test_dense_roundtrip_schema_and_metadata(tmp_path):
+    """parquet.rs:233-400: name_id / n_rows / n_cols + col_0..col_{c-1}, all
+    non-null Float64 columns, Snappy; the metadata JSON (parquet.rs:131-165,
+    312-330) when a builder config is given; bit-exact round trip."""
+    M = np.random.default_rng(4).standard_normal((257, 9))
+    M[3, 4] = -0.0
+    M[5] = np.array([np.inf, -np.inf, 1e-310, 2.0 ** -1074, 1e308, 0.0, 1.0, -1.0, 3.0])
+    cfg = {"lambda_eps": ST.config_value("F64", 0.25), "lambda_k": ST.config_value("Usize", 7),
+           "synthesis": ST.config_value("TauMode", "Median"),
+           "sparsity_eps": ST.config_value("OptionF64", None),
+           "tau": ST.config_value("TauMode", {"Fixed": 0.3})}
+    fp = ST.save_dense_matrix(M, str(tmp_path), "emb", builder_config=cfg)
+    assert os.path.basename(fp) == "emb.parquet"
+    t = pq.read_table(fp)
+    assert t.schema.names == ["name_id", "n_rows", "n_cols"] + [f"col_{i}" for i in range(9)]
+    assert [f.type for f in t.schema] == [pa.utf8(), pa.uint64(), pa.uint64()] + [pa.float64()] * 9
+    assert all(not f.nullable for f in t.schema)
+    assert t.num_rows == 257 and t.column("n_cols")[0].as_py() == 9
+    assert pq.ParquetFile(fp).metadata.row_group(0).column(3).compression == "SNAPPY"
+    M2 = ST.load_dense_matrix(fp)
+    assert M2.shape == (257, 9)
+    np.testing.assert_array_equal(M2.view(np.uint64), M.view(np.uint64))
+    md = ST.load_metadata(str(tmp_path), "emb")
+    assert (md.name_id, md.n_rows, md.n_cols) == ("emb", 257, 9)
+    assert md.lambda_eps() == 0.25 and md.lambda_k() == 7 and md.synthesis() == "Median"
+    f = md.files["matrix"]
+    assert (f.filename, f.file_type, f.rows, f.cols, f.nnz) == ("emb.parquet", "dense", 257, 9, None)
+    assert f.size_bytes == os.path.getsize(fp)
+    raw = json.load(open(tmp_path / "emb_metadata.json"))
+    assert list(raw) == ["name_id", "timestamp", "n_rows", "n_cols", "builder_config", "files"]
+    assert raw["builder_config"]["tau"] == {"TauMode": {"Fixed": 0.3}}
+    assert raw["builder_config"]["sparsity_eps"] == {"OptionF64": None}
+
+
+def test_dense_without_config_writes_no_metadata_and_load_errors(tmp_path):
+    ST.save_dense_matrix(np.ones((3, 2)), str(tmp_path), "m")
+    assert not os.path.exists(tmp_path / "m_metadata.json")
+    with pytest.raises(ST.StorageError, match="Failed to read metadata"):
+        ST.load_metadata(str(tmp_path), "m")
+    # a column missing / the row count disagreeing with n_rows / no rows
+    t = pa.Table.from_arrays([pa.array(["x"] * 2), pa.array(np.full(2, 2, np.uint64)),
+                              pa.array(np.full(2, 2, np.uint64)), pa.array([1.0, 2.0])],
+                             names=["name_id", "n_rows", "n_cols", "col_0"])
+    pq.write_table(t, str(tmp_path / "bad.parquet"))
+    with pytest.raises(ST.StorageError, match="Column col_1 missing"):
+        ST.load_dense_matrix(str(tmp_path / "bad.parquet"))
+    t = pa.Table.from_arrays([pa.array(["x"] * 2), pa.array(np.full(2, 5, np.uint64)),
+                              pa.array(np.full(2, 1, np.uint64)), pa.array([1.0, 2.0])],
+                             names=["name_id", "n_rows", "n_cols", "col_0"])
+    pq.write_table(t, str(tmp_path / "short.parquet"))
+    with pytest.raises(ST.StorageError, match="contained 2 rows, but metadata claimed 5"):
+        ST.load_dense_matrix(str(tmp_path / "short.parquet"))
+    (tmp_path / "bad_metadata.json").write_text('{"name_id": "bad"}')
+    with pytest.raises(ST.StorageError, match="Failed to parse metadata"):
+        ST.load_metadata(str(tmp_path), "bad")
+
+
+def test_sparse_with_builder_config_writes_metadata(tmp_path):
+    ip = np.array([0, 2, 3], np.int64)
+    ix = np.array([0, 1, 1], np.int32)
+    iv = np.array([2.0, -1.0, 1.0])
+    fp = ST.save_sparse_matrix((ip, ix, iv, (2, 2)), str(tmp_path), "L",
+                               builder_config={"lambda_k": ST.config_value("Usize", 3)})
+    md = ST.load_metadata(str(tmp_path), "L")
+    f = md.files["matrix"]
+    assert (f.file_type, f.rows, f.cols, f.nnz, f.size_bytes) == ("sparse", 2, 2, 3, os.path.getsize(fp))
+    with pytest.raises(ST.StorageError):
+        ST.config_value("F32", 1.0)
