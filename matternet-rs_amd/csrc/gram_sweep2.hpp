@@ -110,7 +110,8 @@ enum SweepMode { SW_L2 = 0, SW_COS = 1, SW_SYM = 2, SW_COS_SYM = 3 };
 
 // SW_SYM (self kNN, X both operands, rows in ascending-tau0 order): the
 // sweep covers each unordered pair once.  Block b takes row block I = tab[b].x
-// against column tiles [tab[b].y, tab[b].z) with every tile J >= I.  The
+// against the tab[b].z column tiles J = tab[b].y + t tab[b].w (t = 0, 1, ..),
+// every J >= I (sym_block_table).  The
 // diagonal tile (J == I, only ever a block's first tile) runs as SW_L2: acc0 =
 // tq(q) - hc(c), a pair is row q's candidate iff acc > 0, key = tau0(q) -
 // 2 acc.  An off-diagonal tile (J > I, so tau0(c) >= tau0(q): sorted order)
@@ -121,7 +122,7 @@ enum SweepMode { SW_L2 = 0, SW_COS = 1, SW_SYM = 2, SW_COS_SYM = 3 };
 // buffers buf[row][cap] through global counters cnt[row] (returned atomics at
 // the flush of the per-wave LDS staging area; counts past cap mean overflow).
 struct SymArgs {
-    const int4 *tab;    // per block: (I, Jbeg, Jend) in 256-row blocks
+    const int4 *tab;    // per block: (I, Jfirst, tiles, tile stride) in 256-row blocks
     const float *aoff;  // [n] -|x|^2 / 2
     const float *hoff;  // [n] (|x|^2 - tau0) / 2
     int kexp;           // F16: operands hold x 2^e, the folds (tq, hc, aoff, hoff)
@@ -154,20 +155,25 @@ __global__ __launch_bounds__(NT) void k_gram_sweep2(
     const int fr = lane & 15, fk = lane >> 4;
     const int v = xcd_remap((int)blockIdx.x, (int)gridDim.x);
     // (32-bit row / step counters: nq * 32, nc * 32 < 2^31 is checked by the driver)
-    int q0, sl, cbeg, cend;
+    // Tiles start at cbeg, cbeg + cstr, ... (ntile of them); rows >= cend are
+    // padding (the slice end; SW_SYM: the corpus end)
+    int q0, sl, cbeg, cend, cstr, ntile;
     if constexpr (SYM) {
         const int4 e = sym.tab[v];
         q0 = e.x * BQ;
         sl = 0;
         cbeg = e.y * BC;
-        cend = (int)min(nc, (int64_t)e.z * BC);
+        cend = (int)nc;
+        ntile = e.z;
+        cstr = e.w * BC;
     } else {
         q0 = (v / S) * BQ;
         sl = v % S;
         cbeg = (int)(c_begin + (int64_t)sl * chunk);
         cend = (int)min(nc, (int64_t)cbeg + chunk);
+        ntile = cend > cbeg ? (cend - cbeg + BC - 1) / BC : 0;
+        cstr = BC;
     }
-    const int ntile = cend > cbeg ? (cend - cbeg + BC - 1) / BC : 0;
     const int gtot = ntile * nkb;
     const float pad = COSM ? __builtin_nanf("") : __builtin_inff();
     const bool diag0 = SYM && cbeg == q0;  // SW_SYM: the first tile is the diagonal one
@@ -193,7 +199,7 @@ __global__ __launch_bounds__(NT) void k_gram_sweep2(
     // ---- LDS-DMA issue state: the next k-step gi to stage (tile row bt0,
     // k-block bkb).  Each wave stages rows [32w, 32w+32) of both operands:
     // two 16-row pieces each, lane l -> row +(l>>2), physical chunk l&3.
-    int bt0 = cbeg;
+    int bt0 = cbeg, bti = 0;  // tile start row / index being staged
     int bkb = 0, bslot = 0;
     const int prow0 = 32 * w + (lane >> 2), prow1 = prow0 + 16;
     const int pch = 8 * ((lane & 3) ^ (((lane >> 5) & 1) << 1));  // source chunk (swizzle)
@@ -222,7 +228,7 @@ __global__ __launch_bounds__(NT) void k_gram_sweep2(
                                                  16, voff, 0, 0, 0);
     };
     auto issue = [&]() {
-        if (bt0 < cend) {
+        if (bti < ntile) {
             const __amdgpu_buffer_rsrc_t rc =
                 __builtin_amdgcn_make_buffer_rsrc((void *)cbk, (short)0, cbytes, 0x00020000);
             const __amdgpu_buffer_rsrc_t rq =
@@ -236,7 +242,8 @@ __global__ __launch_bounds__(NT) void k_gram_sweep2(
             qbk += qstep;
             if (++bkb == nkb) {
                 bkb = 0;
-                bt0 += BC;
+                bt0 += cstr;
+                ++bti;
                 cbk = cpan(bt0);
                 qbk = qpan;
                 if constexpr (!TM) {
@@ -437,18 +444,18 @@ __global__ __launch_bounds__(NT) void k_gram_sweep2(
     if (gtot > 0) init_acc(0, diag0);
     if (wc == 1) __builtin_amdgcn_s_barrier();  // the trailing group starts one window late
 
-    int c0 = cbeg;  // first corpus row of the current tile
+    int c0 = cbeg, ti = 0;  // first corpus row / index of the current tile
     int kb = 0, par = 0;
     float hcn = 0.f, tcn = 0.f;  // next tile's hc (and SW_SYM tau0), waves 0-3
     for (int g = 0; g < gtot; ++g) {
         // ================= READ window of k-step g =================
-        const bool more = c0 + BC < cend;
+        const bool more = ti + 1 < ntile;
         if (wc == 0 && kb == nkb - 4 && more) {
             // the next tile's |c|^2 / 2: waves 0-3 load one value per lane
             // (asm loads: the compiler's own waits would drain the DMA queue);
             // older than the DMA issued just below, so the counted waits
             // retire them.  SW_SYM: the next tile is off-diagonal: hoff, tau0
-            const int cn = min(c0 + BC + 64 * wq + lane, (int)nc - 1);
+            const int cn = min(c0 + cstr + 64 * wq + lane, (int)nc - 1);
             const float *p = SYM ? sym.hoff + cn : hc + cn;
             asm volatile("global_load_dword %0, %1, off" : "=v"(hcn) : "v"(p) : "memory");
             if constexpr (SYM) {
@@ -460,13 +467,13 @@ __global__ __launch_bounds__(NT) void k_gram_sweep2(
         if (kb == 0 && g > 0) {
             // the previous tile's candidates, then this tile's accumulator
             // init (before the fragment reads: the fragments are dead here)
-            check(c0 - BC, par ^ 1, diag0 && c0 - BC == cbeg);
+            check(c0 - cstr, par ^ 1, diag0 && ti == 1);
             init_acc(par, false);
         }
         if constexpr (PROBE < 3 || PROBE == 4) read_frags((int)(g & (NSLOT - 1)));
         if (kb == nkb - 2 && more && wc == 0) {
             // written 2 k-steps (>= 2 barriers) before init_acc reads it
-            const int cb = c0 + BC + 64 * wq + lane;
+            const int cb = c0 + cstr + 64 * wq + lane;
             sm.hc[par ^ 1][64 * wq + lane] = cb < cend ? hcn : pad;
             if constexpr (SYM) sm.tc[par ^ 1][64 * wq + lane] = cb < cend ? tcn : pad;
         }
@@ -500,12 +507,13 @@ __global__ __launch_bounds__(NT) void k_gram_sweep2(
         __builtin_amdgcn_sched_barrier(0);
         if (++kb == nkb) {
             kb = 0;
-            c0 += BC;
+            c0 += cstr;
+            ++ti;
             par ^= 1;
         }
     }
     if (wc == 0) __builtin_amdgcn_s_barrier();  // match the trailing group's extra window
-    if (gtot > 0) check(c0 - BC, par ^ 1, diag0 && c0 - BC == cbeg);
+    if (gtot > 0) check(c0 - cstr, par ^ 1, diag0 && ti == 1);
     if (sm.scnt[w] > 0) flush();
     if constexpr (SYM) return;  // the per-row counters are final
     __syncthreads();
@@ -543,33 +551,94 @@ inline SweepPlan plan_sweep(int64_t nq, int64_t nc2, double expect) {
     return p;
 }
 
-// SW_SYM / SW_COS_SYM block table: row block I against column tiles
-// [J0, J1), J >= I, at most TPB tiles per block.  order 1 (default): column
-// ranges aligned to a TPB grid, ordered by range then row, so the co-resident
-// blocks of an XCD stream the same column tiles (one L2 fill serves them all;
-// their row panels stay in the Infinity Cache); order 0: ranges from the
-// diagonal, the longest first.
+// SW_SYM / SW_COS_SYM block table: entries (I, Jfirst, tiles, stride) = row
+// block I against column tiles Jfirst + t stride, all J >= I.
+//   order 1: ranges of TPB consecutive tiles aligned to a TPB grid, ordered by
+//     range then row, so the co-resident blocks of an XCD stream the same
+//     column tiles while their row panels come from the Infinity Cache;
+//   order 0: ranges from the diagonal, the longest first;
+//   order 2 (XCD groups): the 32 co-resident blocks of an XCD form a 4 x 8
+//     group — row blocks I0..I0+3 x column phases c = 0..7 over a range of
+//     8 TPB8 tiles (block (r, c) takes J = J0 + c + 8 t) — so in every tile
+//     step the group reads 4 row panels (each shared by 8 blocks) and 8 column
+//     tiles (each shared by 4) instead of 32 row panels and one column tile:
+//     2.75x fewer panel reads beyond L2.  The diagonal tiles run as one-tile
+//     blocks.  Groups are dealt to the XCDs so that concurrent groups on
+//     different XCDs share a column range (one Infinity-Cache fill); each
+//     XCD's list is padded with empty entries to a common length (the
+//     kernel's xcd_remap gives XCD x the contiguous range x L .. x L + L - 1).
 inline std::vector<int4> sym_block_table(int nbk, int TPB, int order) {
     std::vector<int4> tab;
+    if (order == 2) {
+        constexpr int GR = 4, GC = 8, NX = 8;
+        const int T8 = std::max(1, TPB / GC);  // tiles per block
+        const int W = GC * T8;                 // column range of a group
+        // groups in time order: column range outer (shared across XCDs), row
+        // band inner; the full groups (every block T8 tiles: they finish
+        // together, so the next group starts in step) first, then the ragged
+        // ones near the diagonal; group g goes to XCD g % 8
+        std::vector<std::vector<int4>> full, part;
+        for (int J0 = 0; J0 < nbk; J0 += W) {
+            for (int I0 = 0; I0 < nbk && I0 < J0 + W - 1; I0 += GR) {
+                std::vector<int4> grp;
+                bool all = true;
+                for (int r = 0; r < GR; ++r)
+                    for (int c = 0; c < GC; ++c) {
+                        const int I = I0 + r;
+                        if (I >= nbk) { all = false; continue; }
+                        // J = J0 + c + GC t with I < J < min(nbk, J0 + W)
+                        const int Jend = std::min(nbk, J0 + W);
+                        const int t0 = (J0 + c <= I) ? (I - (J0 + c)) / GC + 1 : 0;
+                        const int Jf = J0 + c + GC * t0;
+                        if (Jf >= Jend) { all = false; continue; }
+                        const int cnt = (Jend - 1 - Jf) / GC + 1;
+                        all = all && cnt == T8;
+                        grp.push_back(make_int4(I, Jf, cnt, GC));
+                    }
+                if (!grp.empty()) (all ? full : part).push_back(grp);
+            }
+        }
+        std::vector<std::vector<int4>> xl(NX);
+        size_t g = 0;
+        for (auto *list : {&full, &part})
+            for (auto &grp : *list) {
+                auto &dst = xl[g++ % NX];
+                dst.insert(dst.end(), grp.begin(), grp.end());
+            }
+        // the diagonal tiles: one-tile blocks, spread over the XCDs
+        for (int I = 0; I < nbk; ++I) xl[I % NX].push_back(make_int4(I, I, 1, 1));
+        size_t L = 0;
+        for (auto &x : xl) L = std::max(L, x.size());
+        tab.reserve(L * NX);
+        for (auto &x : xl) {
+            tab.insert(tab.end(), x.begin(), x.end());
+            tab.insert(tab.end(), L - x.size(), make_int4(0, 0, 0, 1));
+        }
+        return tab;
+    }
     tab.reserve((size_t)nbk * ((size_t)nbk / TPB + 2) / 2 + 16);
     if (order == 1) {
+        std::vector<int> key;
         for (int I = 0; I < nbk; ++I)
             for (int J0 = I; J0 < nbk;) {
                 const int J1 = std::min((J0 / TPB + 1) * TPB, nbk);
-                tab.push_back(make_int4(I, J0, J1, J0 / TPB));
+                tab.push_back(make_int4(I, J0, J1 - J0, 1));
+                key.push_back(J0 / TPB);
                 J0 = J1;
             }
-        std::stable_sort(tab.begin(), tab.end(), [](const int4 &a, const int4 &b) {
-            return a.w != b.w ? a.w < b.w : a.x < b.x;
+        std::vector<size_t> ord(tab.size());
+        for (size_t i = 0; i < ord.size(); ++i) ord[i] = i;
+        std::stable_sort(ord.begin(), ord.end(), [&](size_t a, size_t b) {
+            return key[a] != key[b] ? key[a] < key[b] : tab[a].x < tab[b].x;
         });
-    } else {
-        for (int I = 0; I < nbk; ++I)
-            for (int J0 = I; J0 < nbk; J0 += TPB)
-                tab.push_back(make_int4(I, J0, std::min(J0 + TPB, nbk), 0));
-        std::stable_sort(tab.begin(), tab.end(), [](const int4 &a, const int4 &b) {
-            return (a.z - a.y) > (b.z - b.y);
-        });
+        std::vector<int4> out(tab.size());
+        for (size_t i = 0; i < ord.size(); ++i) out[i] = tab[ord[i]];
+        return out;
     }
+    for (int I = 0; I < nbk; ++I)
+        for (int J0 = I; J0 < nbk; J0 += TPB)
+            tab.push_back(make_int4(I, J0, std::min(J0 + TPB, nbk) - J0, 1));
+    std::stable_sort(tab.begin(), tab.end(), [](const int4 &a, const int4 &b) { return a.z > b.z; });
     return tab;
 }
 
