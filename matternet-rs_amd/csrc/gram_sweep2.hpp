@@ -51,7 +51,7 @@ constexpr int NT = 64 * NWAVES;
 constexpr int NSLOT = 4;     // LDS ring of k-steps
 constexpr int WQF = 4;       // 16-query fragments per wave
 constexpr int WCF = 8;       // 16-row corpus fragments per wave
-constexpr int SCAP = 256;    // staged candidates per wave
+constexpr int SCAP = 224;    // staged candidates per wave
 
 struct alignas(16) Smem {
     uint16_t C[NSLOT][BC][KB];   // corpus k-step, 16 KB per slot
@@ -64,6 +64,8 @@ struct alignas(16) Smem {
     };
     float t0[BQ];                // tau0 of the block's queries
     float tq[BQ];                // (tau0 - |q|^2) / 2 of the block's queries
+    float sq[BQ];                // F16: the queries' scales 2^e
+    float sc[2][BC];             // F16: a tile's rows' scales 2^e
     int scnt[NWAVES];            // staged entries per wave
     uint2 stk[NWAVES][SCAP];     // staged candidates per wave: (key bits, global id)
     uint32_t stp[NWAVES][SCAP];  //   and (query in block | buffer position << 8)
@@ -122,12 +124,16 @@ enum SweepMode { SW_L2 = 0, SW_COS = 1, SW_SYM = 2, SW_COS_SYM = 3 };
 // buffers buf[row][cap] through global counters cnt[row] (returned atomics at
 // the flush of the per-wave LDS staging area; counts past cap mean overflow).
 struct SymArgs {
-    const int4 *tab;    // per block: (I, Jfirst, tiles, tile stride) in 256-row blocks
-    const float *aoff;  // [n] -|x|^2 / 2
-    const float *hoff;  // [n] (|x|^2 - tau0) / 2
-    int kexp;           // F16: operands hold x 2^e, the folds (tq, hc, aoff, hoff)
-                        // are scaled by 2^2e; keys = tau0 - 2 acc 2^kexp, kexp = -2e
+    const int4 *tab;     // per block: (I, Jfirst, tiles, tile stride) in 256-row blocks
+    const float *aoff;   // [n] off-diagonal fold, row side
+    const float *hoff;   // [n] off-diagonal fold, column side
+    const float *scale;  // F16: [n] 2^e of each row's fp16 copy (x 2^e, per-row e)
 };
+// F16 (fp16 operands with per-row exponents, knn_f32.hip k_prep_f16r /
+// k_sym_pos): the folds carry the per-pair certification bound and are
+// scaled by the row's own 2^e, so acc0 = A(q) s_c + B(c) s_q (diagonal: A = tq,
+// B = hc; off-diagonal: A = aoff, B = hoff) and a hit's key is
+// Teff - 2 acc / (s_q s_c) (tau0 carries Teff); padding folds are -inf.
 
 // TM (tile-major layout): element (row r, feature e) of Qk / Ck at
 // ((r / 256) pst + e / 32) * 8192 + (r % 256) * 32 + e % 32 (pst >= nkb: the
@@ -175,7 +181,9 @@ __global__ __launch_bounds__(NT) void k_gram_sweep2(
         cstr = BC;
     }
     const int gtot = ntile * nkb;
-    const float pad = COSM ? __builtin_nanf("") : __builtin_inff();
+    // padding rows never qualify: acc0 = -inf (COS: NaN, as -inf * -|c| = +inf;
+    // F16 adds the column fold: -inf)
+    const float pad = COSM ? __builtin_nanf("") : (F16 ? -__builtin_inff() : __builtin_inff());
     const bool diag0 = SYM && cbeg == q0;  // SW_SYM: the first tile is the diagonal one
 
     if (tid < NWAVES) sm.scnt[tid] = 0;
@@ -185,12 +193,14 @@ __global__ __launch_bounds__(NT) void k_gram_sweep2(
         sm.t0[tid] = q0 + tid < nq ? tau0[q0 + tid] : 0.f;
         if constexpr (SYM) sm.ta[tid] = q0 + tid < nq ? sym.aoff[q0 + tid] : (COSM ? pad : -__builtin_inff());
         else sm.qcnt[tid] = 0;
+        if constexpr (F16) sm.sq[tid] = q0 + tid < nq ? sym.scale[q0 + tid] : 1.f;
     }
     if (ntile > 0 && tid < BC) {
         const int c = cbeg + tid;
         if constexpr (SYM) {
             sm.hc[0][tid] = (c < cend) ? (diag0 ? hc[c] : sym.hoff[c]) : pad;
             sm.tc[0][tid] = (c < cend) ? tau0[c] : pad;
+            if constexpr (F16) sm.sc[0][tid] = (c < cend) ? sym.scale[c] : 1.f;
         } else {
             sm.hc[0][tid] = (c < cend) ? hc[c] : pad;
         }
@@ -262,14 +272,29 @@ __global__ __launch_bounds__(NT) void k_gram_sweep2(
         const float *qa = (SYM && !diag) ? sm.ta : sm.tq;
 #pragma unroll
         for (int f = 0; f < WQF; ++f) tql[f] = qa[64 * wq + 16 * f + fr];
+        float sql[WQF];
+        if constexpr (F16) {
+#pragma unroll
+            for (int f = 0; f < WQF; ++f) sql[f] = sm.sq[64 * wq + 16 * f + fr];
+        }
 #pragma unroll
         for (int g = 0; g < WCF; ++g) {
             const float4 x =
                 *reinterpret_cast<const float4 *>(&sm.hc[par][128 * wc + 16 * g + 4 * fk]);
+            float4 sc4 = make_float4(1.f, 1.f, 1.f, 1.f);
+            if constexpr (F16)
+                sc4 = *reinterpret_cast<const float4 *>(&sm.sc[par][128 * wc + 16 * g + 4 * fk]);
 #pragma unroll
             for (int f = 0; f < WQF; ++f) {
                 // (hipcc packs these into v_pk_add_f32 / v_pk_mul_f32 pairs)
-                if constexpr (COSM) {
+                if constexpr (F16) {
+                    // A(q) s_c + B(c) s_q: both products exact (powers of 2),
+                    // one rounding
+                    acc[f][g][0] = __builtin_fmaf(tql[f], sc4.x, x.x * sql[f]);
+                    acc[f][g][1] = __builtin_fmaf(tql[f], sc4.y, x.y * sql[f]);
+                    acc[f][g][2] = __builtin_fmaf(tql[f], sc4.z, x.z * sql[f]);
+                    acc[f][g][3] = __builtin_fmaf(tql[f], sc4.w, x.w * sql[f]);
+                } else if constexpr (COSM) {
                     acc[f][g][0] = tql[f] * x.x;
                     acc[f][g][1] = tql[f] * x.y;
                     acc[f][g][2] = tql[f] * x.z;
@@ -375,7 +400,10 @@ __global__ __launch_bounds__(NT) void k_gram_sweep2(
             while (pm) {
                 const int r = __builtin_ctz(pm);
                 pm &= pm - 1;
-                const float a2 = 2.f * (F16 ? __builtin_ldexpf(a[r], sym.kexp) : a[r]);
+                // F16: 2 acc / (s_q s_c), exact (powers of 2)
+                const float a2 = 2.f * (F16 ? a[r] / sm.sq[ql] /
+                                                  sm.sc[hpar][128 * wc + 16 * g + 4 * fk + r]
+                                            : a[r]);
                 if (diag) {  // row q's test, as SW_L2
                     emit_sym((uint32_t)qgl, (uint32_t)(c + r), t0l - a2);
                 } else {     // row c's test (acc > 0); row q's only on these hits
@@ -446,7 +474,7 @@ __global__ __launch_bounds__(NT) void k_gram_sweep2(
 
     int c0 = cbeg, ti = 0;  // first corpus row / index of the current tile
     int kb = 0, par = 0;
-    float hcn = 0.f, tcn = 0.f;  // next tile's hc (and SW_SYM tau0), waves 0-3
+    float hcn = 0.f, tcn = 0.f, scn = 1.f;  // next tile's hc (SW_SYM tau0, F16 scale), waves 0-3
     for (int g = 0; g < gtot; ++g) {
         // ================= READ window of k-step g =================
         const bool more = ti + 1 < ntile;
@@ -462,6 +490,10 @@ __global__ __launch_bounds__(NT) void k_gram_sweep2(
                 const float *pt = tau0 + cn;
                 asm volatile("global_load_dword %0, %1, off" : "=v"(tcn) : "v"(pt) : "memory");
             }
+            if constexpr (F16) {
+                const float *ps = sym.scale + cn;
+                asm volatile("global_load_dword %0, %1, off" : "=v"(scn) : "v"(ps) : "memory");
+            }
         }
         if constexpr (PROBE < 2 || PROBE == 4) issue();  // k-step g + 3
         if (kb == 0 && g > 0) {
@@ -476,6 +508,7 @@ __global__ __launch_bounds__(NT) void k_gram_sweep2(
             const int cb = c0 + cstr + 64 * wq + lane;
             sm.hc[par ^ 1][64 * wq + lane] = cb < cend ? hcn : pad;
             if constexpr (SYM) sm.tc[par ^ 1][64 * wq + lane] = cb < cend ? tcn : pad;
+            if constexpr (F16) sm.sc[par ^ 1][64 * wq + lane] = cb < cend ? scn : 1.f;
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         if (PROBE != 4 && wc == 1) {

@@ -796,30 +796,30 @@ __global__ __launch_bounds__(256) void k_prep_x1(const float *__restrict__ X, in
     }
 }
 
-// fp16 copy for the symmetric sweep (gram_sweep2.hpp F16): h = fp16(x 2^e)
-// (round to nearest even; |x 2^e| < 2^-14 flushed to 0, so the MFMA never
-// sees a subnormal), stored tile-major KB32 like k_prep_x1; in UNSCALED units
-// |h 2^-e| and |x - h 2^-e| per row (the residual is exact) and their maxima
-// over all rows (maxbits[0..1]).  Position `row` holds source row perm[row].
+// fp16 copy for the symmetric sweep (gram_sweep2.hpp F16) with a PER-ROW
+// exponent: h = fp16(x 2^e) with e = 14 - E, max|x| < 2^E (the row's largest
+// value lands in [2^13, 2^14); |e| <= 100), round to nearest even, |x 2^e| <
+// 2^-14 flushed to 0 (the MFMA never sees a subnormal), stored tile-major KB32
+// like k_prep_x1.  Per position, in UNSCALED units: |h 2^-e| and |x - h 2^-e|
+// (the residual is exact), rounded up, and the scale s = 2^e.  A row's own
+// exponent keeps its relative precision whatever the other rows' magnitudes
+// (one global exponent let a single huge row flush every small one).
+// Position `row` holds source row perm[row].
 template <bool VEC4>
-__global__ __launch_bounds__(256) void k_prep_f16(const float *__restrict__ X, int64_t n, int d,
-                                                  int dp, const int *__restrict__ perm,
-                                                  uint16_t *__restrict__ XK, int e,
-                                                  float *__restrict__ hn, float *__restrict__ rn,
-                                                  unsigned *__restrict__ maxbits, int tm) {
+__global__ __launch_bounds__(256) void k_prep_f16r(const float *__restrict__ X, int64_t n, int d,
+                                                   int dp, const int *__restrict__ perm,
+                                                   uint16_t *__restrict__ XK,
+                                                   float *__restrict__ hn, float *__restrict__ rn,
+                                                   float *__restrict__ sc, int tm) {
     const int lane = threadIdx.x & 63, hl = lane >> 5, ll = lane & 31;
     const int64_t wave0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
-    unsigned mx0 = 0u, mx1 = 0u;  // maxima (one atomic per wave)
     for (int64_t r2 = 2 * wave0; r2 < n; r2 += 2 * nwaves) {
         const int64_t row = r2 + hl;
         const bool live = row < n;
         const int64_t srow = perm ? (int64_t)perm[min(row, n - 1)] : min(row, n - 1);
         const float *p = X + srow * (int64_t)d;
-        double sh = 0.0, sr = 0.0;
-        for (int t0 = 8 * ll; t0 < dp; t0 += 256) {
-            uint32_t wv[4];
-            float xv[8];
+        auto load8 = [&](int t0, float (&xv)[8]) {
             if (VEC4 && t0 + 8 <= d) {
                 const float4 a = *reinterpret_cast<const float4 *>(p + t0);
                 const float4 b = *reinterpret_cast<const float4 *>(p + t0 + 4);
@@ -829,20 +829,39 @@ __global__ __launch_bounds__(256) void k_prep_f16(const float *__restrict__ X, i
 #pragma unroll
                 for (int u = 0; u < 8; ++u) xv[u] = t0 + u < d ? p[t0 + u] : 0.f;
             }
+        };
+        // the row's exponent (half-wave max over its 32 lanes)
+        float am = 0.f;
+        for (int t0 = 8 * ll; t0 < dp; t0 += 256) {
+            float xv[8];
+            load8(t0, xv);
+#pragma unroll
+            for (int u = 0; u < 8; ++u) am = fmaxf(am, __builtin_fabsf(xv[u]));
+        }
+#pragma unroll
+        for (int o = 16; o > 0; o >>= 1) am = fmaxf(am, __shfl_xor(am, o));
+        int E = 0;
+        if (am > 0.f) frexpf(am, &E);  // am < 2^E
+        const int e = am > 0.f ? min(max(14 - E, -100), 100) : 0;
+        double sh = 0.0, sr = 0.0;
+        for (int t0 = 8 * ll; t0 < dp; t0 += 256) {
+            uint32_t wv[4];
+            float xv[8];
+            load8(t0, xv);
 #pragma unroll
             for (int u = 0; u < 8; u += 2) {
                 uint32_t hb2[2];
 #pragma unroll
                 for (int v = 0; v < 2; ++v) {
                     const float x = xv[u + v];
-                    const float xs = __builtin_ldexpf(x, e);  // exact (|x 2^e| < 2^14)
+                    const float xs = __builtin_ldexpf(x, e);  // exact: |x 2^e| < 2^14
                     _Float16 h = __builtin_fabsf(xs) >= 0x1p-14f ? (_Float16)xs : (_Float16)0.f;
                     uint16_t hbits;
                     __builtin_memcpy(&hbits, &h, 2);
-                    const float hf = __builtin_ldexpf((float)h, -e);
-                    const float r = x - hf;  // exact
-                    sh += (double)hf * (double)hf;
-                    sr += (double)r * (double)r;
+                    const double hf = __builtin_ldexp((double)(float)h, -e);  // exact in f64
+                    const double r = (double)x - hf;                          // exact in f64
+                    sh += hf * hf;
+                    sr += r * r;
                     hb2[v] = hbits;
                 }
                 wv[u >> 1] = hb2[0] | (hb2[1] << 16);
@@ -858,16 +877,13 @@ __global__ __launch_bounds__(256) void k_prep_f16(const float *__restrict__ X, i
             sr += __shfl_xor(sr, o);
         }
         if (ll == 0 && live) {
-            const float hf = f32_up(__builtin_sqrt(sh) * (1.0 + 0x1p-50));
-            const float rf = f32_up(__builtin_sqrt(sr) * (1.0 + 0x1p-50));
-            hn[row] = hf;
-            rn[row] = rf;
-            mx0 = max(mx0, __float_as_uint(hf));
-            mx1 = max(mx1, __float_as_uint(rf));
+            // f64 sums of squares: relative error <= (dp + 1) 2^-53, covered by
+            // the 2^-40 margin (dp <= 2^12)
+            hn[row] = f32_up(__builtin_sqrt(sh * (1.0 + 0x1p-40)) * (1.0 + 0x1p-50));
+            rn[row] = f32_up(__builtin_sqrt(sr * (1.0 + 0x1p-40)) * (1.0 + 0x1p-50));
+            sc[row] = __builtin_ldexpf(1.f, e);
         }
     }
-    wave_atomic_umax(maxbits + 0, mx0);
-    wave_atomic_umax(maxbits + 1, mx1);
 }
 
 // ---------------------------------------------------------------------------
@@ -1089,41 +1105,75 @@ __global__ __launch_bounds__(256) void k_tau_x1(int64_t nq, int S1, const float 
     if (tmax) wave_atomic_umax(tmax, tb);  // every lane of the wave takes part
 }
 
-// SW_SYM per-position arrays (position p holds row pi[p]): the threshold,
-// both accumulator folds (gram_sweep2.hpp SW_SYM), scaled by 2^(2e) for the
-// fp16 operands (e = 0: bf16), and the certification bound with the
-// accumulator magnitude of any column's threshold (max |T|).  hq / rq: the
-// operand copy's |h| and |x - h| per POSITION (fp16) or per row (pos_hr = 0);
-// cmh: their maxima.
+// f64 -> f32 rounded toward +inf (any sign)
+__device__ __forceinline__ float f32_ceil(double v) {
+    float f = (float)v;
+    if ((double)f < v) {  // one ulp toward +inf (f is finite here)
+        const uint32_t b = __float_as_uint(f);
+        f = (b & 0x80000000u) ? (b == 0x80000000u ? __uint_as_float(1u) : __uint_as_float(b - 1u))
+                              : __uint_as_float(b + 1u);
+    }
+    return f;
+}
+
+// SW_SYM per-position folds (position p holds row pi[p]) with a PER-PAIR,
+// separable certification bound (round 4; the round-3 bound used corpus
+// maxima of |h| and |x - h|, so one huge row left every row uncertified).
+//
+// For a pair (q, c): keỹ = qn_q + qn_c - 2 P, P = h̄_q . h̄_c (h̄ = h 2^-e, r =
+// x - h̄ exact), and the sweep's f32 accumulator acc = s_q s_c (a + b + P) +
+// rounding, s = 2^e.  Every term of |d_exact - keỹ| and of the accumulator's
+// rounding splits into a per-row part (AM-GM on the cross terms, lambda =
+// 2^-12 ~ the fp16 relative precision):
+//   |q|^2 - qn_q          <= u qn (1 + 2u)                    (f64 sum -> f32)
+//   2|q.c - P|            <= 2(|h̄_q||r_c| + |r_q||h̄_c| + |r_q||r_c|)
+//                          <= sum over x in {q, c} of lambda |h̄_x|^2 + |r_x|^2 (1/lambda + 1)
+//   2 |acc error| / s_q s_c <= gamma (|a| + |b| + |h̄_q||h̄_c|) 2, gamma = 2 (dp + 33) u
+//                          (any-order accumulation of acc0 and dp exact products,
+//                          <= 2u per addition, + acc0's rounding), |a| + |b| <=
+//                          sum over x of (|T_x| + qn_x + alpha_x) / 2
+// so alpha_x = [u' qn + lambda hn^2 + rn^2 (1/lambda + 1) + gamma (|T| + qn + hn^2)]
+//              / (1 - gamma)   bounds x's share, and Delta(q, c) = alpha_q + alpha_c.
+// The folds put the bound into the test: with Teff = T + |T| (d + 6) u (the
+// reference fold's own relative error (d + 3) u + roundings), the row test is
+//   acc0 = U_q s_c + V_c s_q,  U = (Teff + alpha - qn) / 2 s,  V = -(qn - alpha) / 2 s
+// (the off-diagonal column test swaps the roles: V_q s_c + U_c s_q).  acc <= 0
+// => keỹ - Delta >= Teff => d_exact >= Teff => d_ref >= T.  So every pair never
+// buffered has d_ref >= T and the certificate is T > D_k; a buffered pair's
+// key kl = Teff - 2 acc / (s_q s_c) is a lower bound of d_exact up to f32
+// roundings (the re-rank's relative slack).  U, V are rounded up (larger =
+// more candidates = safe).  Per-position outputs: tauP = T (certificate),
+// teffP = Teff (the kernel's keys), U, V (scaled), hcP = qn / 2 (unscaled,
+// the bf16x3 refill's corpus term).
 __global__ __launch_bounds__(256) void k_sym_pos(int64_t n, const int *__restrict__ pi,
                                                  const float *__restrict__ tau0,
                                                  const float *__restrict__ nq_f,
-                                                 const float *__restrict__ hq,
-                                                 const float *__restrict__ rq, int pos_hr,
-                                                 const unsigned *__restrict__ cmax,
-                                                 const unsigned *__restrict__ cmh,
-                                                 const unsigned *__restrict__ tmax, int d, int dp,
-                                                 int e, int tight, float *__restrict__ tauP,
-                                                 float *__restrict__ tqP, float *__restrict__ hcP,
-                                                 float *__restrict__ hcS, float *__restrict__ aoff,
-                                                 float *__restrict__ hoff,
-                                                 float *__restrict__ dltP) {
+                                                 const float *__restrict__ hn,
+                                                 const float *__restrict__ rn,
+                                                 const float *__restrict__ sc, int d, int dp,
+                                                 float *__restrict__ tauP,
+                                                 float *__restrict__ teffP,
+                                                 float *__restrict__ Uo, float *__restrict__ Vo,
+                                                 float *__restrict__ hcP) {
     const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (p >= n) return;
     const int r = pi[p];
-    const float T = tau0[r], qn = nq_f[r];
-    const float tq = (T - qn) * 0.5f, hc = 0.5f * qn;
-    tauP[p] = T;
-    tqP[p] = __builtin_ldexpf(tq, 2 * e);     // diagonal tile: row fold (as k_tau_x1)
-    hcS[p] = __builtin_ldexpf(hc, 2 * e);     //   and its column term
-    hcP[p] = hc;                              // (unscaled: the bf16x3 refill's corpus term)
-    aoff[p] = __builtin_ldexpf(-hc, 2 * e);   // off-diagonal tiles: acc0 = aoff(q) - hoff(c)
-    hoff[p] = __builtin_ldexpf(-tq, 2 * e);   //   = -|q|^2/2 + (tau0(c) - |c|^2)/2
-    const double Tf = __builtin_isfinite(T) ? __builtin_fabs((double)T) : 0.0;
-    const double Tm = fmax(Tf, (double)__uint_as_float(*tmax));
-    const int64_t hr = pos_hr ? p : r;
-    dltP[p] = delta_x1(Tm, qn, hq[hr], rq[hr], __uint_as_float(cmax[0]),
-                       __uint_as_float(cmh[0]), __uint_as_float(cmh[1]), d, dp, tight);
+    const double u = 0x1p-24, lam = 0x1p-12;
+    const double T = tau0[r], qn = nq_f[r], h = hn[p], rr = rn[p], s = sc[p];
+    const double gam = 2.0 * (dp + 33.0) * u + u;
+    const double Ta = __builtin_isfinite(T) ? __builtin_fabs(T) : 0.0;
+    // (|Teff| <= 1.001 |T|: the (d + 4) u margin)
+    const double base = 1.0000001 * u * qn + lam * h * h + rr * rr * (1.0 / lam + 1.0) +
+                        gam * (1.001 * Ta + qn + h * h);
+    const double alpha = base / (1.0 - gam) * (1.0 + 0x1p-20);
+    // (d + 6) u: the reference fold's (d + 3) u, the key's own f32 rounding
+    // and the second-order terms (a pair with d_ref < T keeps key < Teff)
+    const float Teff = f32_ceil(T + Ta * (d + 6.0) * u);
+    tauP[p] = (float)T;
+    teffP[p] = Teff;
+    Uo[p] = f32_ceil(((double)Teff + alpha - qn) * 0.5 * s);
+    Vo[p] = f32_ceil(-(qn - alpha) * 0.5 * s);
+    hcP[p] = 0.5f * (float)qn;
 }
 
 __global__ __launch_bounds__(256) void k_iota(int *__restrict__ v, int64_t n) {
@@ -1148,7 +1198,7 @@ __global__ __launch_bounds__(64 * WPB) void k_rerank_x1(
     int *__restrict__ big_list, const int *__restrict__ perm, int64_t q_off, int excl,
     const int *__restrict__ qmap, float *__restrict__ ub, int32_t *__restrict__ out_idx,
     float *__restrict__ out_dist, int *__restrict__ fb_count, int *__restrict__ fb_list,
-    int *__restrict__ why = nullptr) {
+    float rel, int *__restrict__ why = nullptr) {
     __shared__ int cand[WPB][64 * NR];
     __shared__ float candk[WPB][64 * NR];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -1159,6 +1209,10 @@ __global__ __launch_bounds__(64 * WPB) void k_rerank_x1(
     const int64_t qo = qmap ? (int64_t)qmap[q] : q;
     const float T = tau0[q];
     bool forced = T == -__builtin_inff();
+    // rel > 0 (SW_SYM): buffered keys are per-pair LOWER bounds (k_sym_pos),
+    // buffered below Teff <= T + rel |T|; a candidate's exact distance is >=
+    // key - rel (|key| + |T|), and the certificate is T > D_k (delta = 0)
+    const float Tg = (rel > 0.f && __builtin_isfinite(T)) ? T + rel * __builtin_fabsf(T) : T;
     int ovf = 0;  // diagnostics (why != NULL): a buffer overflowed
     int M = 0;
     // ids are positions in the visiting order: map them back (c_off +
@@ -1170,7 +1224,7 @@ __global__ __launch_bounds__(64 * WPB) void k_rerank_x1(
             const uint2 v = e < cnt ? bp[e] : make_uint2(0x7f800000u, 0u);
             int64_t gid = (int64_t)v.y;
             if (e < cnt) gid = c_off + perm[gid];
-            const bool pass = e < cnt && __uint_as_float(v.x) < T && !(excl && gid == q_off + qo);
+            const bool pass = e < cnt && __uint_as_float(v.x) < Tg && !(excl && gid == q_off + qo);
             const uint64_t pm = __ballot(pass);
             const int pos = M + (int)__popcll(pm & ((1ull << lane) - 1ull));
             if (pass && pos < 64 * NR) {
@@ -1223,7 +1277,8 @@ __global__ __launch_bounds__(64 * WPB) void k_rerank_x1(
 #pragma unroll
     for (int r = 0; r < NR; ++r) {
         const int e = lane + 64 * r;
-        if (e >= kq && e < M && !(kk[r] - dlt > Dp))
+        const float lb = kk[r] - dlt - rel * (__builtin_fabsf(kk[r]) + __builtin_fabsf(T));
+        if (e >= kq && e < M && !(lb > Dp))
             dd[r] = exact_l2sq<VEC4>(qrow, C + ((int64_t)ix[r] - c_off) * d, d);
     }
 #pragma unroll
@@ -2094,7 +2149,7 @@ static int knn_x1(const float *Q, int64_t nq, const float *C, int64_t nc, int32_
     if (sym) {
         // phase 1 only: the rows (maxima over them: Q == C) and the sample;
         // the sweep copy is built in tau0 order below
-        prep(Q, nq, nullptr, QR, nullptr, qn, nullptr, qhn, qrn, 1, (unsigned *)(flags + 14));
+        prep(Q, nq, nullptr, QR, nullptr, qn, nullptr, qhn, qrn, 1);
         prep(C, m0, perm, CR, nullptr, cnv, chc, nullptr, nullptr, 0);
     } else {
         prep(Q, nq, nullptr, QR, QK, qn, nullptr, qhn, qrn, 0);
@@ -2141,6 +2196,7 @@ static int knn_x1(const float *Q, int64_t nq, const float *C, int64_t nc, int32_
     int S1r = (int)pl.S;
     int sym_mark = 0;  // 1: an extra timer mark before the SW_SYM sweep
     const float *tau_r = tau0, *dlt_r = dlt;
+    float rel_r = 0.f;  // > 0: keys are per-pair lower bounds (SW_SYM), see k_rerank_x1
     const int *perm_r = perm, *qmap_r = nullptr;
     const float *chc_r = chc;
     // tuning build only: timing probes (noepi = sweep K loop only; nodma /
@@ -2156,28 +2212,14 @@ static int knn_x1(const float *Q, int64_t nq, const float *C, int64_t nc, int32_
         auto arr = [&](int i) { return so + (size_t)i * (((nn * 4) + 255) & ~(size_t)255); };
         float *skey = (float *)arr(0);
         int *pi = (int *)arr(1), *iota = (int *)arr(2);
-        float *tauP = (float *)arr(3), *tqP = (float *)arr(4), *hcP = (float *)arr(5),
-              *aoff = (float *)arr(6), *hoff = (float *)arr(7), *dltP = (float *)arr(8),
-              *nrmP = (float *)arr(9), *hcS = (float *)arr(10), *h16 = (float *)arr(11),
-              *r16 = (float *)arr(12);
+        float *tauP = (float *)arr(3), *teffP = (float *)arr(4), *hcP = (float *)arr(5),
+              *Up = (float *)arr(6), *Vp = (float *)arr(7), *zdlt = (float *)arr(8),
+              *scP = (float *)arr(9), *h16 = (float *)arr(10), *r16 = (float *)arr(11);
         hipLaunchKernelGGL(k_iota, dim3((unsigned)((nc + 255) / 256)), dim3(256), 0, s, iota, nc);
         MN_HIP_TRY(sort_f32_pairs(tau0, skey, iota, pi, nc, s));
         float kmax = 0.f;
-        unsigned amaxb = 0;
         MN_HIP_TRY(hipMemcpyAsync(&kmax, skey + nc - 1, 4, hipMemcpyDeviceToHost, s));
-        MN_HIP_TRY(hipMemcpyAsync(&amaxb, flags + 14, 4, hipMemcpyDeviceToHost, s));
         MN_HIP_TRY(hipStreamSynchronize(s));
-        // fp16 operands (MN_SYM_F16=0: bf16): x 2^e with max |x 2^e| < 2^14
-        const char *f16e = knob("MN_SYM_F16");
-        const bool f16 = !(f16e && *f16e == '0');
-        int e16 = 0;
-        if (f16) {
-            float am;
-            memcpy(&am, &amaxb, 4);
-            int E = 0;
-            if (am > 0.f) frexpf(am, &E);  // am < 2^E
-            e16 = 14 - E;
-        }
         if (!(kmax < __builtin_inff())) {
             // fall back to the query-major sweep: its copies were skipped
             sym = false;
@@ -2185,36 +2227,31 @@ static int knn_x1(const float *Q, int64_t nq, const float *C, int64_t nc, int32_
             prep(C, nc, perm, nullptr, CK, cnv, chc, nullptr, nullptr, 1);
             MN_KCHECK(s, "k_prep_x1");
         } else {
-            unsigned *cm16 = (unsigned *)(flags + 16);
-            if (f16) {
-                const int64_t blocks = std::min<int64_t>((nc + 7) / 8, 16384);
-                if (vec4)
-                    hipLaunchKernelGGL(k_prep_f16<true>, dim3((unsigned)blocks), dim3(256), 0, s,
-                                       C, nc, d, dp, pi, XK, e16, h16, r16, cm16, pst1);
-                else
-                    hipLaunchKernelGGL(k_prep_f16<false>, dim3((unsigned)blocks), dim3(256), 0, s,
-                                       C, nc, d, dp, pi, XK, e16, h16, r16, cm16, pst1);
-                MN_KCHECK(s, "k_prep_f16");
-            } else {
-                prep(C, nc, pi, nullptr, XK, nrmP, nullptr, nullptr, nullptr, 0);
-            }
+            // fp16 operands x 2^e with a per-row e, the per-pair bound folded
+            // into the thresholds (k_prep_f16r, k_sym_pos)
+            const int64_t blocks = std::min<int64_t>((nc + 7) / 8, 16384);
+            if (vec4)
+                hipLaunchKernelGGL(k_prep_f16r<true>, dim3((unsigned)blocks), dim3(256), 0, s, C,
+                                   nc, d, dp, pi, XK, h16, r16, scP, pst1);
+            else
+                hipLaunchKernelGGL(k_prep_f16r<false>, dim3((unsigned)blocks), dim3(256), 0, s, C,
+                                   nc, d, dp, pi, XK, h16, r16, scP, pst1);
+            MN_KCHECK(s, "k_prep_f16r");
             hipLaunchKernelGGL(k_sym_pos, dim3((unsigned)((nc + 255) / 256)), dim3(256), 0, s,
-                               nc, pi, tau0, qn, f16 ? h16 : qhn, f16 ? r16 : qrn, f16 ? 1 : 0,
-                               cmax, f16 ? cm16 : cmax + 1, tmaxb, d, dp, e16, f16 ? 1 : 0, tauP,
-                               tqP, hcP, hcS, aoff, hoff, dltP);
+                               nc, pi, tau0, qn, h16, r16, scP, d, dp, tauP, teffP, Up, Vp, hcP);
+            MN_HIP_TRY(hipMemsetAsync(zdlt, 0, nn * 4, s));
             MN_KCHECK(s, "k_sym_pos");
-            // block table: row block I against column tiles [J0, J1), J >= I,
-            // at most TPB tiles per block.  MN_SYM_ORDER 1 (default): column
-            // ranges aligned to a TPB grid, ordered by range then row, so the
-            // co-resident blocks of an XCD stream the same column tiles (one
-            // L2 fill serves them all; their row panels stay in the Infinity
-            // Cache): C2 sweep 775 ms; 0: ranges from the diagonal, the
-            // longest first: 984 ms (profiles/r03d_ab_sym_order.log)
+            // block table (gram_sweep2.hpp sym_block_table): order 2 (default,
+            // round 4), XCD groups of 4 row blocks x 8 column phases — each
+            // XCD's 32 co-resident blocks read 12 panels per tile step instead
+            // of 33: C2 sweep 788 -> 720 ms, same process (profiles/
+            // r04/r04b_ab_order.log); order 1: column ranges of TPB tiles ordered by
+            // range then row (round 3); order 0: ranges from the diagonal
             const int nbk = (int)((nc + ksw2::BC - 1) / ksw2::BC);
             const char *tpe2 = knob("MN_SYM_TPB");
             const int TPB = (tpe2 && *tpe2) ? std::max(1, atoi(tpe2)) : 256;
             const char *ore = knob("MN_SYM_ORDER");
-            const int order = (ore && *ore) ? atoi(ore) : 1;
+            const int order = (ore && *ore) ? atoi(ore) : 2;
             const std::vector<int4> tab = ksw2::sym_block_table(nbk, TPB, order);
             int4 *dtab = (int4 *)scratch(kSlotSymTab, tab.size() * sizeof(int4) + 64);
             MN_REQUIRE(dtab, MN_ENOMEM, "mn_knn: block table allocation failed");
@@ -2238,24 +2275,26 @@ static int knn_x1(const float *Q, int64_t nq, const float *C, int64_t nc, int32_
                        "mn_knn: sweep grid too large (split the queries / corpus)");
             tm.mark();  // SW_SYM: sort / fp16 copy / table -> ms_norms
             sym_mark = 1;
-            ksw2::SymArgs sa{dtab, aoff, hoff, -2 * e16};
-            auto sk = f16 ? ksw2::k_gram_sweep2<0, ksw2::SW_SYM, true, true>
-                          : ksw2::k_gram_sweep2<0, ksw2::SW_SYM, true, false>;
+            // diagonal tile: acc0 = U_q s_c + V_c s_q (tq = U, hc = V);
+            // off-diagonal: V_q s_c + U_c s_q (aoff = V, hoff = U); keys from Teff
+            ksw2::SymArgs sa{dtab, Vp, Up, scP};
+            auto sk = ksw2::k_gram_sweep2<0, ksw2::SW_SYM, true, true>;
 #ifdef MN_TUNING
             // timing probes (results invalid): noepi = K loop only, nodma /
             // noread = also without the DMA issue / fragment reads
-            if (f16 && probe && *probe)
+            if (probe && *probe)
                 sk = !strcmp(probe, "nodma") ? ksw2::k_gram_sweep2<2, ksw2::SW_SYM, true, true>
                      : !strcmp(probe, "noread") ? ksw2::k_gram_sweep2<3, ksw2::SW_SYM, true, true>
                                                 : ksw2::k_gram_sweep2<1, ksw2::SW_SYM, true, true>;
 #endif
             hipLaunchKernelGGL(sk, dim3((unsigned)tab.size()), dim3(ksw2::NT), 0, s, XK, nc, XK,
-                               nc, nkb, (int64_t)0, (int64_t)0, 1, tqP, tauP, hcS, (int64_t)0, 1,
+                               nc, nkb, (int64_t)0, (int64_t)0, 1, Up, teffP, Vp, (int64_t)0, 1,
                                (int64_t)0, cap2, cbuf2, cnt2, pst1, sa);
             MN_KCHECK(s, "k_gram_sweep2<SYM>");
             S1r = 0;
-            tau_r = tauP;
-            dlt_r = dltP;
+            tau_r = tauP;   // the certificate: T > D_k (the bound is in the folds)
+            dlt_r = zdlt;
+            rel_r = (d + 8.0f) * 0x1p-24f;  // keys are lower bounds up to f32 roundings
             perm_r = pi;
             qmap_r = pi;
             chc_r = hcP;
@@ -2331,7 +2370,7 @@ static int knn_x1(const float *Q, int64_t nq, const float *C, int64_t nc, int32_
     hipLaunchKernelGGL((k_rerank_x1<NRV, WPB, V>), dim3((unsigned)(NB)), dim3(64 * WPB), 0, s, \
                        Q, nq, C, d, c_off, S1r, pl.cap, cbuf1, bcnt1, tau_r, S2, cap2,          \
                        cbuf2, cnt2, dlt_r, k, nvalid, QL, QN, BC, BL, perm_r, q_off, excl,      \
-                       qmap_r, ubv, out_idx, out_dist, fb_count, fb_list, why)
+                       qmap_r, ubv, out_idx, out_dist, fb_count, fb_list, rel_r, why)
     const int64_t nb1 = (nq + 3) / 4;
     if (vec4) MN_RRX(8, 4, true, nb1, (const int *)nullptr, (const int *)nullptr, big_count, big_list);
     else MN_RRX(8, 4, false, nb1, (const int *)nullptr, (const int *)nullptr, big_count, big_list);
@@ -2428,7 +2467,7 @@ static int knn_x1(const float *Q, int64_t nq, const float *C, int64_t nc, int32_
                        Q, (int64_t)nfb, C, d, c_off, 0, 0, (const uint2 *)nullptr,            \
                        (const int *)nullptr, tau3, (int)p3.S, p3.cap, cbuf3, cnt3, dlt3, k,    \
                        nvalid, QL, QN, BC, BL, perm_r, q_off, excl, erows, (float *)nullptr,     \
-                       out_idx, out_dist, fb_count, fb_list, why)
+                       out_idx, out_dist, fb_count, fb_list, 0.f, why)
         const int64_t nb3 = (nfb + 3) / 4;
         if (vec4) MN_RR3(8, 4, true, nb3, (const int *)nullptr, (const int *)nullptr, big_count3, big_list3);
         else MN_RR3(8, 4, false, nb3, (const int *)nullptr, (const int *)nullptr, big_count3, big_list3);

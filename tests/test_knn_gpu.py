@@ -258,23 +258,21 @@ def test_bf16x1_two_phase_sorted_rows(kind):
     assert_exact(idx, dist, ridx, rdist)
 
 
-@pytest.mark.parametrize("f16", ["1", "0"], ids=["fp16", "bf16"])
 @pytest.mark.parametrize("kind", ["uniform", "clustered"])
-def test_bf16x1_symmetric_sweep_matches_query_major(kind, f16, monkeypatch):
+def test_bf16x1_symmetric_sweep_matches_query_major(kind, monkeypatch):
     """The self-kNN sweep covers each unordered pair once (gram_sweep2.hpp
     SW_SYM: rows in ascending-threshold order, a tile's hits feed both rows'
-    buffers), on fp16 operands (x 2^e, the default) or bf16 (MN_SYM_F16=0);
-    the query-major sweep (MN_X1_SYM=0) covers every ordered pair.  All
-    bit-exact vs the oracle, so identical to each other."""
+    buffers, fp16 operands x 2^e with per-row e, the per-pair bound in the
+    folds); the query-major sweep (MN_X1_SYM=0) covers every ordered pair.
+    All bit-exact vs the oracle, so identical to each other."""
     import json
     n, d, k = 30_000, 96, 16
     X = (datagen.uniform(n, d, seed=8) if kind == "uniform"
          else datagen.clustered(n, d, seed=9, blobs=12, dup_frac=0.01, zero_frac=0.002))
-    monkeypatch.setenv("MN_SYM_F16", f16)
     with _lib.use_tuning():  # the tuning build honours the knobs
         idx, dist, st = hip_knn(X, k, algo="bf16x1", timing=True)
-        print(f"SYM {kind} f16={f16}", json.dumps({kk: (round(v, 2) if isinstance(v, float) else v)
-                                                   for kk, v in st.items()}))
+        print(f"SYM {kind}", json.dumps({kk: (round(v, 2) if isinstance(v, float) else v)
+                                         for kk, v in st.items()}))
         assert st["sweep_slices"] == -1  # the symmetric sweep ran
         monkeypatch.setenv("MN_X1_SYM", "0")
         idx0, dist0, st0 = hip_knn(X, k, algo="bf16x1", timing=True)
