@@ -7,10 +7,13 @@ configs[3]) on MI355X through the HIP C ABI.
 
 One step = one exact kNN graph build (k=32, squared L2, self excluded) over all
 rows: at N=1 the C2 workload (1M x 768 f32), at N GPUs N x 1M rows row-sharded
-(C4 at N=8): every rank keeps its 1M-row corpus shard resident, receives all
-query rows (all-gather over RCCL/xGMI), computes the exact per-shard top-k of
-every query, and the per-shard lists are exchanged (all-to-all) and merged on
-each query's owner rank.  Inputs are generated on device before timing.
+(C4 at N=8) through the library's C entry mn_knn_sharded_f32 on an RCCL
+communicator it creates (mn_rccl_comm_init; the 128-byte id broadcast over the
+torch process group): every rank keeps its 1M-row corpus shard resident,
+receives all query rows (ncclAllGather over xGMI), computes the exact
+per-shard top-k of every query, and the per-shard lists are exchanged
+(grouped ncclSend/ncclRecv) and merged on each query's owner rank.  Inputs
+are generated on device before timing.
 value = N_total^2 vector pairs / max-over-ranks step time.
 """
 from __future__ import annotations
@@ -93,30 +96,17 @@ def main():
     stream = torch.cuda.current_stream(dev)
     _lib.check(L.mn_fill_uniform_f32(X.data_ptr(), n_loc, d, a.seed, rank * n_loc,
                                      stream.cuda_stream))
+    comm = None
     if world > 1:
-        from surfface_hip.dist import sharded_knn
+        from surfface_hip.dist import RcclComm, knn_sharded_capi
+        uid = [RcclComm.unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        comm = RcclComm(uid[0], world, rank)
     torch.cuda.synchronize()
 
     gram_ms = []
 
     last = {}
-
-    def knn_fn(Q, C, kk, c_off):
-        # per-shard exact top-k of all queries, in query chunks (the candidate
-        # buffers scale with the queries of one call)
-        nq_all = Q.shape[0]
-        idx = torch.empty((nq_all, kk), dtype=torch.int32, device=Q.device)
-        dd = torch.empty((nq_all, kk), dtype=torch.float32, device=Q.device)
-        g = 0.0
-        for a0 in range(0, nq_all, a.query_chunk):
-            b0 = min(nq_all, a0 + a.query_chunk)
-            r = S.knn_l2sq_qc(Q[a0:b0], C, kk, q_offset=a0, c_offset=c_off, timing=True)
-            idx[a0:b0].copy_(r.idx)
-            dd[a0:b0].copy_(r.dist)
-            g += r.stats.get("ms_sweep") or r.stats["ms_gram"]
-            last["stats"] = r.stats
-        gram_ms.append(g)
-        return idx, dd
 
     def step():
         if world == 1:
@@ -125,10 +115,15 @@ def main():
             gram_ms.append(r.stats.get("ms_sweep") or r.stats["ms_gram"])
             last["stats"] = r.stats
             return r.idx, r.dist, r.stats
-        # all-gather queries, exact per-shard top-k vs the resident shard,
-        # all-to-all of the lists, merge on the owner (surfface_hip/dist.py)
-        idx, dd = sharded_knn(X, k, knn_fn=knn_fn, merge_fn=S.merge_parts)
-        return idx, dd, last["stats"]
+        # the C entry: all-gather of the shards, exact per-shard top-k of every
+        # query in query chunks, list exchange, merge (csrc/shard.hip)
+        idx, dd = knn_sharded_capi(X, k, comm, query_chunk=a.query_chunk, timing=True,
+                                   stream=stream)
+        st = S.knn.last_stats()  # the last query chunk's generator stats
+        chunks = (n_tot + a.query_chunk - 1) // a.query_chunk
+        gram_ms.append((st.get("ms_sweep") or st["ms_gram"]) * chunks)
+        last["stats"] = st
+        return idx, dd, st
 
     steps_req, warm_req = a.steps, a.warmup
     t_w = time.perf_counter()
@@ -296,8 +291,9 @@ def main():
                        "n_rows": n_tot, "dim": d, "k": k, "rows_per_gpu": n_loc,
                        "metric_space": "squared L2 (reference sequential f32 fold)",
                        "parallelism": ("single GPU (no collective)" if world == 1 else
-                                       f"corpus row-shard x{world}: RCCL all-gather of queries, "
-                                       "exact per-shard top-k, all-to-all + merge")},
+                                       f"corpus row-shard x{world} (mn_knn_sharded_f32): RCCL "
+                                       "all-gather of queries, exact per-shard top-k, grouped "
+                                       "send/recv of the lists + merge")},
             "roofline": roof,
             "cpu_baseline": cpu,
             "parity_sample": parity,
@@ -314,6 +310,8 @@ def main():
                                    "warmup_run": a.warmup,
                                    "query_chunk": a.query_chunk}
         print(json.dumps(line), flush=True)
+    if comm is not None:
+        comm.close()
     if dist:
         dist.barrier()
         dist.destroy_process_group()

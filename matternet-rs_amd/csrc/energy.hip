@@ -133,16 +133,21 @@ __global__ void k_count_entries(const int64_t *__restrict__ ip, const int32_t *_
     cnt[f + i] = cb;
 }
 
+// ident (k_energy_rows3, symmetric L): dg[i] = L_ii - dgA_i with dgA_i = the
+// row's list-A weight sum over BOTH triangles (sum of -L_ij > 0, j != i), so
+// that the list-A part of x^T L x needs no x_i x_j products (see rows3).
 __global__ void k_fill_entries(const int64_t *__restrict__ ip, const int32_t *__restrict__ ix,
                                Vals v, int f, int sym, int g_mode, int split_diag,
                                const int64_t *__restrict__ off, uint32_t *__restrict__ eij,
-                               double *__restrict__ ev, double *__restrict__ dg) {
+                               double *__restrict__ ev, double *__restrict__ dg, int ident = 0) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= f) return;
     int64_t qa = off[i], qb = off[f + i];
     double di = 0.0;  // the row's diagonal entries in CSR order (one thread: deterministic)
+    double da = 0.0;  // ident: the row's list-A weights, both triangles, CSR order
     for (int64_t p = ip[i]; p < ip[i + 1]; ++p) {
         const int j = ix[p];
+        if (ident && j != i && -v[p] > 0.0) da += -v[p];
         const int c = entry_class(i, j, v[p], sym, g_mode, split_diag);
         if (c == 2) {
             di += v[p];
@@ -153,7 +158,7 @@ __global__ void k_fill_entries(const int64_t *__restrict__ ip, const int32_t *__
         eij[q] = (uint32_t)i | ((uint32_t)j << 16);
         ev[q] = c == 0 ? -v[p] : ((sym && i != j) ? 2.0 * v[p] : v[p]);
     }
-    if (split_diag) dg[i] = di;
+    if (split_diag) dg[i] = ident ? di - da : di;
 }
 
 // ---- wave-level exact order statistic on f32 keys -------------------------
@@ -909,6 +914,224 @@ __global__ __launch_bounds__(1024) void k_energy_rows2(
     }
 }
 
+// ---- K3 v3: one pass over X (round 4) -------------------------------------
+// k_row_tau + k_energy_rows2 read X twice (PMC 6.2 GB per call for 3.1 GB of
+// rows).  rows3 streams each row once: a wave takes two rows per pass, selects
+// their tau (counted selection, registers), stages them in LDS as f64 pairs
+// (no f32 -> f64 converts in the entry loop) and folds the entry lists, while
+// the next pass's rows are in flight.  For a symmetric L the list-A part of
+// the Rayleigh numerator uses the identity (w = -L_ij > 0, the upper list A)
+//     2 sum_A L_ij x_i x_j = sum_A w (x_i - x_j)^2 - sum_c dgA_c x_c^2
+// (dgA_c = the A weights at c, both triangles), so
+//     x^T L x = sum_c (L_cc - dgA_c) x_c^2 + S_A + sum_B v x_i x_j
+// with S_A = sum_A w (x_i - x_j)^2 — the dispersion's own sum: per entry and
+// row d = x_i - x_j, e = w d^2, S += e, Q += e^2 (5 f64 ops instead of 7).
+// Exact identity; its rounding differs from the reference's fold by O(u) of
+// the terms (the 1e-9 contract; tests/test_energy_gpu.py).
+// LDS: eij u32 [neP] | ev f64 [neP] | dgm f64 [fpad] | per wave: xs double2
+// [fpad + 1] (slot fpad = 0) | 256 ints (select scratch).
+constexpr int E3_WAVES = 8;
+static inline size_t e3_lds_bytes(int64_t neP, int f, int waves) {
+    const size_t fpad = (size_t)((f + 3) & ~3);
+    return (((size_t)neP * 4 + 15) & ~(size_t)15) + (size_t)neP * 8 + fpad * 8 +
+           (size_t)waves * ((fpad + 1) * 16 + 1024);
+}
+template <int NR>
+__global__ __launch_bounds__(64 * E3_WAVES) void k_energy_rows3(
+    const float *__restrict__ X, int64_t n, int f, int64_t na, int64_t naP, int64_t nb,
+    int64_t nbP, const uint32_t *__restrict__ geij, const double *__restrict__ gev,
+    const double *__restrict__ gdgm, double mA_g, int g_mode, int tau_mode, double tau_param,
+    int pct_rank, double *__restrict__ Eo, double *__restrict__ Go, double *__restrict__ Lo) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char dsm[];
+    const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int fpad = (f + 3) & ~3;
+    const int64_t neP = naP + nbP;
+    uint32_t *seij = (uint32_t *)dsm;
+    double *sev = (double *)(dsm + (((size_t)neP * 4 + 15) & ~(size_t)15));
+    double *sdg = sev + neP;
+    unsigned char *wbase = (unsigned char *)(sdg + fpad) + (size_t)w * ((fpad + 1) * 16 + 1024);
+    double2 *xs = (double2 *)wbase;                       // [fpad + 1]
+    int *hist = (int *)(wbase + (size_t)(fpad + 1) * 16);  // 256 ints
+    // entry offsets: byte offsets of x_i / x_j in the stage (16 B per column),
+    // packed (i * 16) | (j * 16) << 16 (fpad * 16 < 2^16); padding -> zero slot
+    const uint32_t zoff = (uint32_t)fpad * 16u;
+    const uint32_t zpair = zoff | (zoff << 16);
+    for (int64_t p = threadIdx.x; p < neP; p += blockDim.x) {
+        const int64_t q = p < naP ? p : na + (p - naP);
+        const bool real = p < naP ? p < na : (p - naP) < nb;
+        uint32_t e = zpair;
+        double v = 0.0;
+        if (real) {
+            const uint32_t ij = geij[q];
+            e = ((ij & 0xFFFFu) * 16u) | (((ij >> 16) * 16u) << 16);
+            v = gev[q];
+        }
+        seij[p] = e;
+        sev[p] = v;
+    }
+    for (int c = threadIdx.x; c < fpad; c += blockDim.x) sdg[c] = c < f ? gdgm[c] : 0.0;
+    if (lane == 0) xs[fpad] = make_double2(0.0, 0.0);
+    __syncthreads();
+    const unsigned char *xsb = (const unsigned char *)xs;
+    const bool mean_tau = g_mode == MN_G_TAUMODE && tau_mode == MN_TAU_MEAN;
+    const bool sel_tau = g_mode == MN_G_TAUMODE &&
+                         (tau_mode == MN_TAU_MEDIAN || tau_mode == MN_TAU_PERCENTILE);
+    const bool med = tau_mode == MN_TAU_MEDIAN;
+    const int rank = med ? ((f % 2 == 1) ? f / 2 : f / 2 - 1) : pct_rank;
+    const int need = (med && f % 2 == 0) ? 2 : 1;
+    const int64_t npass = (n + 1) / 2;
+    const int64_t pstride = (int64_t)gridDim.x * E3_WAVES;
+    int64_t ps = (int64_t)blockIdx.x * E3_WAVES + w;
+    float cur[2][NR];
+    auto load_rows = [&](int64_t pq, float (&dst)[2][NR]) {
+        const int64_t r0 = pq * 2;
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+            // a missing last row repeats (computed, not written)
+            const __amdgpu_buffer_rsrc_t rs = row_rsrc(X + min(r0 + t, n - 1) * (int64_t)f, f);
+#pragma unroll
+            for (int r = 0; r < NR; ++r) dst[t][r] = row_at(rs, lane + 64 * r);
+        }
+        __builtin_amdgcn_sched_barrier(0);  // all loads issue before any use
+    };
+    if (ps < npass) load_rows(ps, cur);
+    for (; ps < npass; ps += pstride) {
+        const int64_t r0 = ps * 2;
+        // stage the pair (f64) and the diagonal part from registers
+        double den[2] = {0.0, 0.0}, msum[2] = {0.0, 0.0}, numD[2] = {0.0, 0.0};
+        bool nzr[2] = {false, false};
+#pragma unroll
+        for (int r = 0; r < NR; ++r) {
+            const int c = lane + 64 * r;
+            if (c < f) {
+                const double x0 = (double)cur[0][r], x1 = (double)cur[1][r];
+                xs[c] = make_double2(x0, x1);
+                const double dgc = sdg[c];
+                const double q0 = x0 * x0, q1 = x1 * x1;
+                den[0] += q0;
+                den[1] += q1;
+                numD[0] = __builtin_fma(dgc, q0, numD[0]);
+                numD[1] = __builtin_fma(dgc, q1, numD[1]);
+                if (mean_tau) {
+                    msum[0] += x0;
+                    msum[1] += x1;
+                }
+                nzr[0] |= !(fabs(x0) <= 1e-10);
+                nzr[1] |= !(fabs(x1) <= 1e-10);
+            }
+        }
+        double tau[2] = {0.0, 0.0};
+        if (sel_tau) {
+#pragma unroll
+            for (int t = 0; t < 2; ++t) {
+                uint32_t keys[NR];
+#pragma unroll
+                for (int r = 0; r < NR; ++r) {
+                    const uint32_t u = __float_as_uint(cur[t][r]);
+                    const uint32_t k = u ^ ((uint32_t)((int32_t)u >> 31) | 0x80000000u);
+                    keys[r] = k | (uint32_t)-(int32_t)(lane + 64 * r >= f);
+                }
+                uint32_t k0, k1;
+                if (wave_select_cnt<NR>(keys, f, rank, need, (uint32_t *)hist, k0, k1)) {
+                    double v = (double)key2f(k0);
+                    if (need == 2) v = 0.5 * (v + (double)key2f(k1));
+                    tau[t] = fmax(v, 1e-10);
+                } else {
+                    tau[t] = row_tau<NR>(keys, f, 0.0, tau_mode, tau_param, pct_rank, hist);
+                }
+            }
+        } else if (g_mode == MN_G_TAUMODE) {
+#pragma unroll
+            for (int t = 0; t < 2; ++t)
+                tau[t] = tau_mode == MN_TAU_MEAN
+                             ? fmax(wave_sum_dpp(msum[t]) / (double)f, 1e-10)
+                             : ((isfinite(tau_param) && tau_param > 0.0) ? tau_param : 1e-10);
+        }
+        // the next pass's rows: in flight during this pass's entry loop
+        if (ps + pstride < npass) load_rows(ps + pstride, cur);
+        __builtin_amdgcn_wave_barrier();
+        // list A: S, Q (two accumulator sets: shorter add chains)
+        double S0a = 0.0, S1a = 0.0, Q0a = 0.0, Q1a = 0.0;
+        double S0b = 0.0, S1b = 0.0, Q0b = 0.0, Q1b = 0.0;
+        for (int64_t p0 = lane; p0 < naP; p0 += E2_CH) {
+            uint32_t ij[4];
+            double wv[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                ij[u] = seij[p0 + 64 * u];
+                wv[u] = sev[p0 + 64 * u];
+            }
+            double2 gi[4], gj[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                gi[u] = *reinterpret_cast<const double2 *>(xsb + (ij[u] & 0xFFFFu));
+                gj[u] = *reinterpret_cast<const double2 *>(xsb + (ij[u] >> 16));
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const double d0 = gi[u].x - gj[u].x, d1 = gi[u].y - gj[u].y;
+                const double e0 = wv[u] * (d0 * d0), e1 = wv[u] * (d1 * d1);
+                if (u & 1) {
+                    S0b += e0; S1b += e1;
+                    Q0b = __builtin_fma(e0, e0, Q0b); Q1b = __builtin_fma(e1, e1, Q1b);
+                } else {
+                    S0a += e0; S1a += e1;
+                    Q0a = __builtin_fma(e0, e0, Q0a); Q1a = __builtin_fma(e1, e1, Q1a);
+                }
+            }
+        }
+        // list B: numerator-only entries (v x_i x_j, multiplicity in v)
+        double nB0 = 0.0, nB1 = 0.0;
+        for (int64_t p0 = naP + lane; p0 < neP; p0 += E2_CH) {
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const uint32_t ij = seij[p0 + 64 * u];
+                const double v = sev[p0 + 64 * u];
+                const double2 gi = *reinterpret_cast<const double2 *>(xsb + (ij & 0xFFFFu));
+                const double2 gj = *reinterpret_cast<const double2 *>(xsb + (ij >> 16));
+                nB0 = __builtin_fma(v, gi.x * gj.x, nB0);
+                nB1 = __builtin_fma(v, gi.y * gj.y, nB1);
+            }
+        }
+        const double SA[2] = {S0a + S0b, S1a + S1b}, QA[2] = {Q0a + Q0b, Q1a + Q1b};
+        const double nBs[2] = {nB0, nB1};
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+            const double SAs = wave_sum_dpp(SA[t]);
+            const double num = wave_sum_dpp(numD[t] + nBs[t]) + SAs;
+            const double Ss = mA_g * SAs;
+            const double Qs = mA_g * wave_sum_dpp(QA[t]);
+            const double dn = wave_sum_dpp(den[t]);
+            const bool nonzero = __any(nzr[t]) != 0;
+            double e_raw = 0.0, g_raw = 0.0, lam = 0.0;
+            if (g_mode == MN_G_SPECTRAL) {
+                const double rr = num / (dn + 1e-9);
+                e_raw = rr < -1e6 ? -1e6 : (rr > 1e6 ? 1e6 : rr);
+                g_raw = Ss;
+                lam = e_raw;
+            } else if (!(g_mode == MN_G_TAUMODE && !nonzero)) {  // zero vector: lambda 0
+                e_raw = dn > 1e-12 ? fmax(num / dn, 0.0) : 0.0;
+                if (Ss > 1e-12) {
+                    const double g = Qs / (Ss * Ss);
+                    g_raw = g < 0.0 ? 0.0 : (g > 1.0 ? 1.0 : g);
+                }
+                if (g_mode == MN_G_TAUMODE) {
+                    const double ebv = e_raw / (e_raw + tau[t]);
+                    lam = tau[t] * ebv + (1.0 - tau[t]) * g_raw;
+                } else {
+                    lam = e_raw;
+                }
+            }
+            if (lane == 0 && r0 + t < n) {
+                if (Eo) Eo[r0 + t] = e_raw;
+                if (Go) Go[r0 + t] = g_raw;
+                if (Lo) Lo[r0 + t] = lam;
+            }
+        }
+        __builtin_amdgcn_wave_barrier();  // the stage is rewritten next pass
+    }
+}
+
 // ---- register-resident entry lists (the C3 shape: ne <= 64 NE) -------------
 // The entry lists are the same for every row, so each lane keeps its slots
 // p = lane + 64 t in registers for the whole launch (list A padded to whole
@@ -1444,8 +1667,15 @@ static int energy_impl(const mn_csr *L, const float *X, int64_t n, int32_t f,
     break;
     }
     MN_HIP_TRY(hipMemcpyAsync(off, ho.data(), 16 * (size_t)f, hipMemcpyHostToDevice, s));
+    // K3 v3 (one pass over X, the list-A identity) for a symmetric L whose
+    // lists fit its LDS plan; else k_row_tau + k_energy_rows2
+    const int64_t naP3 = (na + E2_CH - 1) / E2_CH * E2_CH;
+    const int64_t nbP3 = (ne - na + E2_CH - 1) / E2_CH * E2_CH;
+    const char *v3e = knob("MN_ENERGY_V3");  // tuning build: 0 = the two-kernel path (A/B)
+    const bool v3 = split && sym && nr <= 16 && !(v3e && *v3e == '0') &&
+                    e3_lds_bytes(naP3 + nbP3, f, E3_WAVES) <= LDS_BUDGET;
     hipLaunchKernelGGL(k_fill_entries, dim3(fb), dim3(256), 0, s, L->indptr, L->indices, vals, f,
-                       sym, opts->g_mode, split, off, eij, ev, dg);
+                       sym, opts->g_mode, split, off, eij, ev, dg, v3 ? 1 : 0);
     int pct_rank = 0;
     if (opts->tau_mode == MN_TAU_PERCENTILE) {
         double pp = opts->tau_param;
@@ -1458,7 +1688,28 @@ static int energy_impl(const mn_csr *L, const float *X, int64_t n, int32_t f,
     const double mA_num = sym ? 2.0 : 1.0;
     const double mA_g = (sym && opts->g_mode != MN_G_ENERGYMAPS) ? 2.0 : 1.0;
     tm.mark();
-    if (split) {
+    if (v3) {
+        const size_t sh3 = e3_lds_bytes(naP3 + nbP3, f, E3_WAVES);
+        int dev = 0, ncu = 256;
+        MN_HIP_TRY(hipGetDevice(&dev));
+        MN_HIP_TRY(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+        const int64_t npass3 = (n + 1) / 2;
+        const int64_t blocks3 = std::min<int64_t>((npass3 + E3_WAVES - 1) / E3_WAVES, ncu);
+#define MN_E3(NRV)                                                                              \
+    do {                                                                                        \
+        MN_HIP_TRY(hipFuncSetAttribute((const void *)k_energy_rows3<NRV>,                       \
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)sh3));  \
+        hipLaunchKernelGGL((k_energy_rows3<NRV>), dim3((unsigned)blocks3), dim3(64 * E3_WAVES), \
+                           sh3, s, X, n, f, na, naP3, ne - na, nbP3, eij, ev, dg, mA_g,         \
+                           opts->g_mode, opts->tau_mode, opts->tau_param, pct_rank, E, G, lam); \
+    } while (0)
+        if (nr <= 4) MN_E3(4);
+        else if (nr <= 8) MN_E3(8);
+        else if (nr <= 12) MN_E3(12);
+        else MN_E3(16);
+#undef MN_E3
+        MN_KCHECK(s, "k_energy_rows3");
+    } else if (split) {
         const int64_t naP = (na + E2_CH - 1) / E2_CH * E2_CH;
         const int64_t nbP = (ne - na + E2_CH - 1) / E2_CH * E2_CH;
         const char *tke = knob("MN_ENERGY_TAU");  // 1: the select inside the entry-loop kernel

@@ -294,3 +294,39 @@ def test_v2_kernel_matches_v1(tau, monkeypatch):
     for a, b, r in ((E2, E1, rE), (G2, G1, rG), (l2, l1, rl)):
         np.testing.assert_allclose(a, b, rtol=RTOL, atol=ATOL)
         np.testing.assert_allclose(a, r, rtol=RTOL, atol=ATOL)
+
+
+@pytest.mark.parametrize("gm,tau", [(0, "median"), (0, "pct"), (0, "mean"), (0, "fixed"), (1, "median"),
+                                    (2, "median")])
+def test_v3_single_pass_matches_two_kernel_path(gm, tau, monkeypatch):
+    """k_energy_rows3 (round 4: X streamed once, tau selected inline, rows
+    staged as f64 pairs, the list-A identity x^T L x = sum (L_cc - dgA_c) x_c^2
+    + sum_A w (x_i - x_j)^2 + list B) against the two-kernel path
+    (k_row_tau + k_energy_rows2, MN_ENERGY_V3=0) and the oracle: taumode with
+    every tau mode, energymaps and Stage D, an odd row count, the heavy-tail /
+    constant / zero / tied rows."""
+    import surfface_hip as S
+    ip, ix, iv = feature_laplacian()
+    X = datagen.uniform(4097, 768, seed=43)
+    rng = np.random.default_rng(8)
+    X[1] = 0.0
+    X[2] = np.float32(2.5)
+    X[3] = (rng.standard_normal(768) ** 5).astype(np.float32)
+    X[4, ::2] = np.float32(0.125)
+    X[5] = np.where(rng.random(768) < 0.9, 0.0, X[5]).astype(np.float32)
+    tm = {"median": (S.TauMode.Median, O.TAU_MEDIAN, 0.0),
+          "pct": (S.TauMode.Percentile(0.3), O.TAU_PERCENTILE, 0.3),
+          "mean": (S.TauMode.Mean, O.TAU_MEAN, 0.0),
+          "fixed": (S.TauMode.Fixed(0.2), O.TAU_FIXED, 0.2)}[tau]
+    E3, G3, l3 = run(X, ip, ix, iv, gm, tm[0])
+    monkeypatch.setenv("MN_ENERGY_V3", "0")
+    with S._lib.use_tuning():
+        E2, G2, l2 = run(X, ip, ix, iv, gm, tm[0])
+    if gm == 2:  # Stage D: f32 Burn reference, the oracle within 1e-4 (test_stage_d_*)
+        for a, b in ((E3, E2), (G3, G2), (l3, l2)):
+            np.testing.assert_allclose(a, b, rtol=RTOL, atol=ATOL)
+        return
+    rE, rG, rl = O.energy_rows(X, ip, ix, iv, gm, tm[1], tm[2])
+    for a, b, r in ((E3, E2, rE), (G3, G2, rG), (l3, l2, rl)):
+        np.testing.assert_allclose(a, b, rtol=RTOL, atol=ATOL)
+        np.testing.assert_allclose(a, r, rtol=RTOL, atol=ATOL)
