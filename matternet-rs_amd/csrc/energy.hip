@@ -928,33 +928,39 @@ __global__ __launch_bounds__(1024) void k_energy_rows2(
 // row d = x_i - x_j, e = w d^2, S += e, Q += e^2 (5 f64 ops instead of 7).
 // Exact identity; its rounding differs from the reference's fold by O(u) of
 // the terms (the 1e-9 contract; tests/test_energy_gpu.py).
-// LDS: eij u32 [neP] | ev f64 [neP] | dgm f64 [fpad] | per wave: xs double2
-// [fpad + 1] (slot fpad = 0) | 256 ints (select scratch).
-constexpr int E3_WAVES = 8;
-static inline size_t e3_lds_bytes(int64_t neP, int f, int waves) {
+// LDS: eij u32 [neP] | ev f64 [neP] | dgm f64 [fpad] | per wave: xs [fpad + 1]
+// (slot fpad = 0) of double2 (S64: 8 waves a block) or float2 (16 waves, the
+// converts in the loop) | 256 ints (select scratch).
+template <bool S64> struct E3 {
+    static constexpr int WAVES = S64 ? 8 : 16;
+    static constexpr int XB = S64 ? 16 : 8;  // stage bytes per column (two rows)
+};
+static inline size_t e3_lds_bytes(int64_t neP, int f, int waves, int xb) {
     const size_t fpad = (size_t)((f + 3) & ~3);
     return (((size_t)neP * 4 + 15) & ~(size_t)15) + (size_t)neP * 8 + fpad * 8 +
-           (size_t)waves * ((fpad + 1) * 16 + 1024);
+           (size_t)waves * ((fpad + 1) * xb + 1024);
 }
-template <int NR>
-__global__ __launch_bounds__(64 * E3_WAVES) void k_energy_rows3(
+template <int NR, bool S64>
+__global__ __launch_bounds__(64 * E3<S64>::WAVES) void k_energy_rows3(
     const float *__restrict__ X, int64_t n, int f, int64_t na, int64_t naP, int64_t nb,
     int64_t nbP, const uint32_t *__restrict__ geij, const double *__restrict__ gev,
     const double *__restrict__ gdgm, double mA_g, int g_mode, int tau_mode, double tau_param,
     int pct_rank, double *__restrict__ Eo, double *__restrict__ Go, double *__restrict__ Lo) {
     extern __shared__ __attribute__((aligned(16))) unsigned char dsm[];
+    constexpr int NW = E3<S64>::WAVES, XB = E3<S64>::XB;
+    typedef typename std::conditional<S64, double2, float2>::type stage_t;
     const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int fpad = (f + 3) & ~3;
     const int64_t neP = naP + nbP;
     uint32_t *seij = (uint32_t *)dsm;
     double *sev = (double *)(dsm + (((size_t)neP * 4 + 15) & ~(size_t)15));
     double *sdg = sev + neP;
-    unsigned char *wbase = (unsigned char *)(sdg + fpad) + (size_t)w * ((fpad + 1) * 16 + 1024);
-    double2 *xs = (double2 *)wbase;                       // [fpad + 1]
-    int *hist = (int *)(wbase + (size_t)(fpad + 1) * 16);  // 256 ints
-    // entry offsets: byte offsets of x_i / x_j in the stage (16 B per column),
-    // packed (i * 16) | (j * 16) << 16 (fpad * 16 < 2^16); padding -> zero slot
-    const uint32_t zoff = (uint32_t)fpad * 16u;
+    unsigned char *wbase = (unsigned char *)(sdg + fpad) + (size_t)w * ((fpad + 1) * XB + 1024);
+    stage_t *xs = (stage_t *)wbase;                       // [fpad + 1]
+    int *hist = (int *)(wbase + (size_t)(fpad + 1) * XB);  // 256 ints
+    // entry offsets: byte offsets of x_i / x_j in the stage (XB B per column),
+    // packed (i XB) | (j XB) << 16 (fpad XB < 2^16); padding -> zero slot
+    const uint32_t zoff = (uint32_t)fpad * XB;
     const uint32_t zpair = zoff | (zoff << 16);
     for (int64_t p = threadIdx.x; p < neP; p += blockDim.x) {
         const int64_t q = p < naP ? p : na + (p - naP);
@@ -963,14 +969,14 @@ __global__ __launch_bounds__(64 * E3_WAVES) void k_energy_rows3(
         double v = 0.0;
         if (real) {
             const uint32_t ij = geij[q];
-            e = ((ij & 0xFFFFu) * 16u) | (((ij >> 16) * 16u) << 16);
+            e = ((ij & 0xFFFFu) * XB) | (((ij >> 16) * XB) << 16);
             v = gev[q];
         }
         seij[p] = e;
         sev[p] = v;
     }
     for (int c = threadIdx.x; c < fpad; c += blockDim.x) sdg[c] = c < f ? gdgm[c] : 0.0;
-    if (lane == 0) xs[fpad] = make_double2(0.0, 0.0);
+    if (lane == 0) xs[fpad] = stage_t{0, 0};
     __syncthreads();
     const unsigned char *xsb = (const unsigned char *)xs;
     const bool mean_tau = g_mode == MN_G_TAUMODE && tau_mode == MN_TAU_MEAN;
@@ -980,8 +986,8 @@ __global__ __launch_bounds__(64 * E3_WAVES) void k_energy_rows3(
     const int rank = med ? ((f % 2 == 1) ? f / 2 : f / 2 - 1) : pct_rank;
     const int need = (med && f % 2 == 0) ? 2 : 1;
     const int64_t npass = (n + 1) / 2;
-    const int64_t pstride = (int64_t)gridDim.x * E3_WAVES;
-    int64_t ps = (int64_t)blockIdx.x * E3_WAVES + w;
+    const int64_t pstride = (int64_t)gridDim.x * NW;
+    int64_t ps = (int64_t)blockIdx.x * NW + w;
     float cur[2][NR];
     auto load_rows = [&](int64_t pq, float (&dst)[2][NR]) {
         const int64_t r0 = pq * 2;
@@ -1005,7 +1011,8 @@ __global__ __launch_bounds__(64 * E3_WAVES) void k_energy_rows3(
             const int c = lane + 64 * r;
             if (c < f) {
                 const double x0 = (double)cur[0][r], x1 = (double)cur[1][r];
-                xs[c] = make_double2(x0, x1);
+                if constexpr (S64) xs[c] = make_double2(x0, x1);
+                else xs[c] = make_float2(cur[0][r], cur[1][r]);
                 const double dgc = sdg[c];
                 const double q0 = x0 * x0, q1 = x1 * x1;
                 den[0] += q0;
@@ -1061,15 +1068,16 @@ __global__ __launch_bounds__(64 * E3_WAVES) void k_energy_rows3(
                 ij[u] = seij[p0 + 64 * u];
                 wv[u] = sev[p0 + 64 * u];
             }
-            double2 gi[4], gj[4];
+            stage_t gi[4], gj[4];
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
-                gi[u] = *reinterpret_cast<const double2 *>(xsb + (ij[u] & 0xFFFFu));
-                gj[u] = *reinterpret_cast<const double2 *>(xsb + (ij[u] >> 16));
+                gi[u] = *reinterpret_cast<const stage_t *>(xsb + (ij[u] & 0xFFFFu));
+                gj[u] = *reinterpret_cast<const stage_t *>(xsb + (ij[u] >> 16));
             }
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
-                const double d0 = gi[u].x - gj[u].x, d1 = gi[u].y - gj[u].y;
+                const double d0 = (double)gi[u].x - (double)gj[u].x;
+                const double d1 = (double)gi[u].y - (double)gj[u].y;
                 const double e0 = wv[u] * (d0 * d0), e1 = wv[u] * (d1 * d1);
                 if (u & 1) {
                     S0b += e0; S1b += e1;
@@ -1087,10 +1095,10 @@ __global__ __launch_bounds__(64 * E3_WAVES) void k_energy_rows3(
             for (int u = 0; u < 4; ++u) {
                 const uint32_t ij = seij[p0 + 64 * u];
                 const double v = sev[p0 + 64 * u];
-                const double2 gi = *reinterpret_cast<const double2 *>(xsb + (ij & 0xFFFFu));
-                const double2 gj = *reinterpret_cast<const double2 *>(xsb + (ij >> 16));
-                nB0 = __builtin_fma(v, gi.x * gj.x, nB0);
-                nB1 = __builtin_fma(v, gi.y * gj.y, nB1);
+                const stage_t gi = *reinterpret_cast<const stage_t *>(xsb + (ij & 0xFFFFu));
+                const stage_t gj = *reinterpret_cast<const stage_t *>(xsb + (ij >> 16));
+                nB0 = __builtin_fma(v, (double)gi.x * (double)gj.x, nB0);
+                nB1 = __builtin_fma(v, (double)gi.y * (double)gj.y, nB1);
             }
         }
         const double SA[2] = {S0a + S0b, S1a + S1b}, QA[2] = {Q0a + Q0b, Q1a + Q1b};
@@ -1671,9 +1679,14 @@ static int energy_impl(const mn_csr *L, const float *X, int64_t n, int32_t f,
     // lists fit its LDS plan; else k_row_tau + k_energy_rows2
     const int64_t naP3 = (na + E2_CH - 1) / E2_CH * E2_CH;
     const int64_t nbP3 = (ne - na + E2_CH - 1) / E2_CH * E2_CH;
-    const char *v3e = knob("MN_ENERGY_V3");  // tuning build: 0 = the two-kernel path (A/B)
-    const bool v3 = split && sym && nr <= 16 && !(v3e && *v3e == '0') &&
-                    e3_lds_bytes(naP3 + nbP3, f, E3_WAVES) <= LDS_BUDGET;
+    // tuning build: MN_ENERGY_V3 = 0 the two-kernel path, 2 the float2 stage
+    // at 16 waves a block (A/B); default 1: the double2 stage at 8 waves
+    const char *v3e = knob("MN_ENERGY_V3");
+    const int v3k = (v3e && *v3e) ? atoi(v3e) : 1;
+    const bool s64 = v3k != 2;
+    const bool v3 = split && sym && nr <= 16 && v3k != 0 &&
+                    e3_lds_bytes(naP3 + nbP3, f, s64 ? E3<true>::WAVES : E3<false>::WAVES,
+                                 s64 ? E3<true>::XB : E3<false>::XB) <= LDS_BUDGET;
     hipLaunchKernelGGL(k_fill_entries, dim3(fb), dim3(256), 0, s, L->indptr, L->indices, vals, f,
                        sym, opts->g_mode, split, off, eij, ev, dg, v3 ? 1 : 0);
     int pct_rank = 0;
@@ -1689,24 +1702,27 @@ static int energy_impl(const mn_csr *L, const float *X, int64_t n, int32_t f,
     const double mA_g = (sym && opts->g_mode != MN_G_ENERGYMAPS) ? 2.0 : 1.0;
     tm.mark();
     if (v3) {
-        const size_t sh3 = e3_lds_bytes(naP3 + nbP3, f, E3_WAVES);
+        const int nw3 = s64 ? E3<true>::WAVES : E3<false>::WAVES;
+        const size_t sh3 = e3_lds_bytes(naP3 + nbP3, f, nw3, s64 ? E3<true>::XB : E3<false>::XB);
         int dev = 0, ncu = 256;
         MN_HIP_TRY(hipGetDevice(&dev));
         MN_HIP_TRY(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
         const int64_t npass3 = (n + 1) / 2;
-        const int64_t blocks3 = std::min<int64_t>((npass3 + E3_WAVES - 1) / E3_WAVES, ncu);
-#define MN_E3(NRV)                                                                              \
+        const int64_t blocks3 = std::min<int64_t>((npass3 + nw3 - 1) / nw3, ncu);
+#define MN_E3(NRV, S6)                                                                          \
     do {                                                                                        \
-        MN_HIP_TRY(hipFuncSetAttribute((const void *)k_energy_rows3<NRV>,                       \
+        MN_HIP_TRY(hipFuncSetAttribute((const void *)k_energy_rows3<NRV, S6>,                   \
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)sh3));  \
-        hipLaunchKernelGGL((k_energy_rows3<NRV>), dim3((unsigned)blocks3), dim3(64 * E3_WAVES), \
+        hipLaunchKernelGGL((k_energy_rows3<NRV, S6>), dim3((unsigned)blocks3), dim3(64 * nw3),  \
                            sh3, s, X, n, f, na, naP3, ne - na, nbP3, eij, ev, dg, mA_g,         \
                            opts->g_mode, opts->tau_mode, opts->tau_param, pct_rank, E, G, lam); \
     } while (0)
-        if (nr <= 4) MN_E3(4);
-        else if (nr <= 8) MN_E3(8);
-        else if (nr <= 12) MN_E3(12);
-        else MN_E3(16);
+#define MN_E3S(NRV) do { if (s64) MN_E3(NRV, true); else MN_E3(NRV, false); } while (0)
+        if (nr <= 4) MN_E3S(4);
+        else if (nr <= 8) MN_E3S(8);
+        else if (nr <= 12) MN_E3S(12);
+        else MN_E3S(16);
+#undef MN_E3S
 #undef MN_E3
         MN_KCHECK(s, "k_energy_rows3");
     } else if (split) {

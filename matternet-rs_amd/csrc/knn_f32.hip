@@ -800,8 +800,9 @@ __global__ __launch_bounds__(256) void k_prep_x1(const float *__restrict__ X, in
 // exponent: h = fp16(x 2^e) with e = 14 - E, max|x| < 2^E (the row's largest
 // value lands in [2^13, 2^14); |e| <= 100), round to nearest even, |x 2^e| <
 // 2^-14 flushed to 0 (the MFMA never sees a subnormal), stored tile-major KB32
-// like k_prep_x1.  Per position, in UNSCALED units: |h 2^-e| and |x - h 2^-e|
-// (the residual is exact), rounded up, and the scale s = 2^e.  A row's own
+// like k_prep_x1 (XK may be NULL: the statistics pass).  Per position, in
+// UNSCALED units: |h 2^-e| and |x - h 2^-e| (the residual is exact), rounded
+// up, and the scale s = 2^e (hn may be NULL: no statistics).  A row's own
 // exponent keeps its relative precision whatever the other rows' magnitudes
 // (one global exponent let a single huge row flush every small one).
 // Position `row` holds source row perm[row].
@@ -866,7 +867,7 @@ __global__ __launch_bounds__(256) void k_prep_f16r(const float *__restrict__ X, 
                 }
                 wv[u >> 1] = hb2[0] | (hb2[1] << 16);
             }
-            if (live) {
+            if (live && XK) {
                 const uint4 pk = make_uint4(wv[0], wv[1], wv[2], wv[3]);
                 *reinterpret_cast<uint4 *>(XK + kb32_at(row, t0 >> 5, n, tm) + (t0 & 31)) = pk;
             }
@@ -876,7 +877,7 @@ __global__ __launch_bounds__(256) void k_prep_f16r(const float *__restrict__ X, 
             sh += __shfl_xor(sh, o);
             sr += __shfl_xor(sr, o);
         }
-        if (ll == 0 && live) {
+        if (ll == 0 && live && hn) {
             // f64 sums of squares: relative error <= (dp + 1) 2^-53, covered by
             // the 2^-40 margin (dp <= 2^12)
             hn[row] = f32_up(__builtin_sqrt(sh * (1.0 + 0x1p-40)) * (1.0 + 0x1p-50));
@@ -1116,64 +1117,92 @@ __device__ __forceinline__ float f32_ceil(double v) {
     return f;
 }
 
-// SW_SYM per-position folds (position p holds row pi[p]) with a PER-PAIR,
-// separable certification bound (round 4; the round-3 bound used corpus
-// maxima of |h| and |x - h|, so one huge row left every row uncertified).
+// f64 -> f32 rounded toward -inf (any sign)
+__device__ __forceinline__ float f32_floor(double v) { return -f32_ceil(-v); }
+
+// SW_SYM folds with a PER-PAIR, separable certification bound (round 4; the
+// round-3 bound used corpus maxima of |h| and |x - h|, so one huge row left
+// every row uncertified).
 //
 // For a pair (q, c): keỹ = qn_q + qn_c - 2 P, P = h̄_q . h̄_c (h̄ = h 2^-e, r =
 // x - h̄ exact), and the sweep's f32 accumulator acc = s_q s_c (a + b + P) +
-// rounding, s = 2^e.  Every term of |d_exact - keỹ| and of the accumulator's
-// rounding splits into a per-row part (AM-GM on the cross terms, lambda =
-// 2^-12 ~ the fp16 relative precision):
+// rounding, s = 2^e (per row).  Every term of |d_exact - keỹ| and of the
+// accumulator's rounding splits into a per-row part (AM-GM on the cross
+// terms, lambda = 2^-12 ~ the fp16 relative precision):
 //   |q|^2 - qn_q          <= u qn (1 + 2u)                    (f64 sum -> f32)
 //   2|q.c - P|            <= 2(|h̄_q||r_c| + |r_q||h̄_c| + |r_q||r_c|)
 //                          <= sum over x in {q, c} of lambda |h̄_x|^2 + |r_x|^2 (1/lambda + 1)
-//   2 |acc error| / s_q s_c <= gamma (|a| + |b| + |h̄_q||h̄_c|) 2, gamma = 2 (dp + 33) u
+//   2 |acc error| / s_q s_c <= 2 gamma (|a| + |b| + |h̄_q||h̄_c|), gamma = 2 (dp + 33) u + u
 //                          (any-order accumulation of acc0 and dp exact products,
 //                          <= 2u per addition, + acc0's rounding), |a| + |b| <=
-//                          sum over x of (|T_x| + qn_x + alpha_x) / 2
+//                          sum over x of (|T_x| + qn_x + 3 alpha_x) / 2
 // so alpha_x = [u' qn + lambda hn^2 + rn^2 (1/lambda + 1) + gamma (|T| + qn + hn^2)]
-//              / (1 - gamma)   bounds x's share, and Delta(q, c) = alpha_q + alpha_c.
-// The folds put the bound into the test: with Teff = T + |T| (d + 6) u (the
-// reference fold's own relative error (d + 3) u + roundings), the row test is
-//   acc0 = U_q s_c + V_c s_q,  U = (Teff + alpha - qn) / 2 s,  V = -(qn - alpha) / 2 s
-// (the off-diagonal column test swaps the roles: V_q s_c + U_c s_q).  acc <= 0
-// => keỹ - Delta >= Teff => d_exact >= Teff => d_ref >= T.  So every pair never
-// buffered has d_ref >= T and the certificate is T > D_k; a buffered pair's
-// key kl = Teff - 2 acc / (s_q s_c) is a lower bound of d_exact up to f32
-// roundings (the re-rank's relative slack).  U, V are rounded up (larger =
-// more candidates = safe).  Per-position outputs: tauP = T (certificate),
-// teffP = Teff (the kernel's keys), U, V (scaled), hcP = qn / 2 (unscaled,
-// the bf16x3 refill's corpus term).
-__global__ __launch_bounds__(256) void k_sym_pos(int64_t n, const int *__restrict__ pi,
-                                                 const float *__restrict__ tau0,
+//              / (1 - 3 gamma)   bounds x's share: |d_exact - keỹ| + 2|acc err| <=
+// Delta(q, c) = alpha_q + alpha_c.
+// Certificate threshold Tc = T - 2 alpha (so the candidates are about those
+// with keỹ < T, as with one shared bound: keỹ - alpha_q - alpha_c < Tc_q ~
+// keỹ < T + alpha_c - alpha_q), fold threshold Tf = Tc + |Tc| (d + 6) u (the
+// reference fold's own (d + 3) u, the key's roundings); the row test is
+//   acc0 = U_q s_c + V_c s_q,  U = (Tf + alpha - qn) / 2 s,  V = -(qn - alpha) / 2 s
+// (the off-diagonal column test swaps the roles: V_q s_c + U_c s_q; rows are
+// sorted by Tf, so Tf(c) >= Tf(q) there).  acc <= 0 => keỹ - Delta >= Tf =>
+// d_exact >= Tf => d_ref >= Tc.  So every pair never buffered has d_ref >= Tc
+// and the certificate is Tc > D_k; a buffered pair's key kl = Tf - 2 acc /
+// (s_q s_c) is a lower bound of d_exact up to f32 roundings (the re-rank's
+// relative slack).  U, V, Tf are rounded up (more candidates = safe), Tc down.
+// An outlier column's alpha_c only widens its own pairs (their keys ~ |c|^2
+// >> alpha_c are still rejected); an outlier row fails its own certificate.
+
+// per row r: alpha, the fold threshold tf (also the sort key) and the
+// certificate tc; hn / rn from the statistics pass of k_prep_f16r
+__global__ __launch_bounds__(256) void k_sym_row(int64_t n, const float *__restrict__ tau0,
                                                  const float *__restrict__ nq_f,
                                                  const float *__restrict__ hn,
-                                                 const float *__restrict__ rn,
-                                                 const float *__restrict__ sc, int d, int dp,
+                                                 const float *__restrict__ rn, int d, int dp,
+                                                 float *__restrict__ alpha_o,
+                                                 float *__restrict__ tf_o,
+                                                 float *__restrict__ tc_o) {
+    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= n) return;
+    const double u = 0x1p-24, lam = 0x1p-12;
+    const double T = tau0[r], qn = nq_f[r], h = hn[r], rr = rn[r];
+    const double gam = 2.0 * (dp + 33.0) * u + u;
+    const double Ta = __builtin_isfinite(T) ? __builtin_fabs(T) : 0.0;
+    const double base = 1.0000001 * u * qn + lam * h * h + rr * rr * (1.0 / lam + 1.0) +
+                        gam * (Ta + qn + h * h);
+    const float alpha = f32_up(base / (1.0 - 3.0 * gam) * (1.0 + 0x1p-20));
+    const double Tc = T - 2.0 * (double)alpha;  // +inf stays +inf
+    const double Tca = __builtin_isfinite(Tc) ? __builtin_fabs(Tc) : 0.0;
+    alpha_o[r] = alpha;
+    tc_o[r] = __builtin_isfinite(Tc) ? f32_floor(Tc) : (float)Tc;
+    tf_o[r] = __builtin_isfinite(Tc) ? f32_ceil(Tc + Tca * (d + 6.0) * u) : (float)Tc;
+}
+
+// per position p (row pi[p], sorted by tf): the kernel's folds and keys, the
+// re-rank's certificate, hcP = qn / 2 (unscaled: the bf16x3 refill's corpus
+// term), the scale by position
+__global__ __launch_bounds__(256) void k_sym_pos(int64_t n, const int *__restrict__ pi,
+                                                 const float *__restrict__ nq_f,
+                                                 const float *__restrict__ alpha,
+                                                 const float *__restrict__ tf,
+                                                 const float *__restrict__ tc,
+                                                 const float *__restrict__ sc_row,
                                                  float *__restrict__ tauP,
                                                  float *__restrict__ teffP,
                                                  float *__restrict__ Uo, float *__restrict__ Vo,
-                                                 float *__restrict__ hcP) {
+                                                 float *__restrict__ hcP,
+                                                 float *__restrict__ scP) {
     const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (p >= n) return;
     const int r = pi[p];
-    const double u = 0x1p-24, lam = 0x1p-12;
-    const double T = tau0[r], qn = nq_f[r], h = hn[p], rr = rn[p], s = sc[p];
-    const double gam = 2.0 * (dp + 33.0) * u + u;
-    const double Ta = __builtin_isfinite(T) ? __builtin_fabs(T) : 0.0;
-    // (|Teff| <= 1.001 |T|: the (d + 4) u margin)
-    const double base = 1.0000001 * u * qn + lam * h * h + rr * rr * (1.0 / lam + 1.0) +
-                        gam * (1.001 * Ta + qn + h * h);
-    const double alpha = base / (1.0 - gam) * (1.0 + 0x1p-20);
-    // (d + 6) u: the reference fold's (d + 3) u, the key's own f32 rounding
-    // and the second-order terms (a pair with d_ref < T keeps key < Teff)
-    const float Teff = f32_ceil(T + Ta * (d + 6.0) * u);
-    tauP[p] = (float)T;
-    teffP[p] = Teff;
-    Uo[p] = f32_ceil(((double)Teff + alpha - qn) * 0.5 * s);
-    Vo[p] = f32_ceil(-(qn - alpha) * 0.5 * s);
+    const double qn = nq_f[r], a = alpha[r], s = sc_row[r];
+    const float Tf = tf[r];
+    tauP[p] = tc[r];
+    teffP[p] = Tf;
+    Uo[p] = f32_ceil(((double)Tf + a - qn) * 0.5 * s);
+    Vo[p] = f32_ceil(-(qn - a) * 0.5 * s);
     hcP[p] = 0.5f * (float)qn;
+    scP[p] = (float)s;
 }
 
 __global__ __launch_bounds__(256) void k_iota(int *__restrict__ v, int64_t n) {
@@ -2203,10 +2232,10 @@ static int knn_x1(const float *Q, int64_t nq, const float *C, int64_t nc, int32_
     // noread = also without the DMA issue / fragment reads): NO outputs
     const char *probe = knob("MN_X1_PROBE");
     if (sym) {
-        // rows in ascending tau0 (position p holds row pi[p]); rows with a
-        // non-finite threshold at the top end would break the column fold
+        // rows in ascending fold threshold Tf (position p holds row pi[p],
+        // k_sym_row); a non-finite threshold would break the column fold
         const size_t nn = (size_t)nc;
-        char *so = (char *)scratch(kSlotSymOrd, nn * 4 * 14 + 4096);
+        char *so = (char *)scratch(kSlotSymOrd, nn * 4 * 17 + 8192);
         uint16_t *XK = (uint16_t *)scratch(kSlotX1CK, (size_t)pad256(nc) * kbw1 * 2 + 64);
         MN_REQUIRE(so && XK, MN_ENOMEM, "mn_knn: symmetric-sweep scratch allocation failed");
         auto arr = [&](int i) { return so + (size_t)i * (((nn * 4) + 255) & ~(size_t)255); };
@@ -2214,12 +2243,16 @@ static int knn_x1(const float *Q, int64_t nq, const float *C, int64_t nc, int32_
         int *pi = (int *)arr(1), *iota = (int *)arr(2);
         float *tauP = (float *)arr(3), *teffP = (float *)arr(4), *hcP = (float *)arr(5),
               *Up = (float *)arr(6), *Vp = (float *)arr(7), *zdlt = (float *)arr(8),
-              *scP = (float *)arr(9), *h16 = (float *)arr(10), *r16 = (float *)arr(11);
-        hipLaunchKernelGGL(k_iota, dim3((unsigned)((nc + 255) / 256)), dim3(256), 0, s, iota, nc);
-        MN_HIP_TRY(sort_f32_pairs(tau0, skey, iota, pi, nc, s));
+              *scP = (float *)arr(9), *h16 = (float *)arr(10), *r16 = (float *)arr(11),
+              *s16 = (float *)arr(12), *alr = (float *)arr(13), *tfr = (float *)arr(14),
+              *tcr = (float *)arr(15);
         float kmax = 0.f;
-        MN_HIP_TRY(hipMemcpyAsync(&kmax, skey + nc - 1, 4, hipMemcpyDeviceToHost, s));
-        MN_HIP_TRY(hipStreamSynchronize(s));
+        {   // any non-finite threshold: the query-major sweep (below)
+            hipLaunchKernelGGL(k_iota, dim3((unsigned)((nc + 255) / 256)), dim3(256), 0, s, iota, nc);
+            MN_HIP_TRY(sort_f32_pairs(tau0, skey, iota, pi, nc, s));
+            MN_HIP_TRY(hipMemcpyAsync(&kmax, skey + nc - 1, 4, hipMemcpyDeviceToHost, s));
+            MN_HIP_TRY(hipStreamSynchronize(s));
+        }
         if (!(kmax < __builtin_inff())) {
             // fall back to the query-major sweep: its copies were skipped
             sym = false;
@@ -2228,17 +2261,29 @@ static int knn_x1(const float *Q, int64_t nq, const float *C, int64_t nc, int32_
             MN_KCHECK(s, "k_prep_x1");
         } else {
             // fp16 operands x 2^e with a per-row e, the per-pair bound folded
-            // into the thresholds (k_prep_f16r, k_sym_pos)
+            // into the thresholds: statistics by row, the rows' fold / certificate
+            // thresholds, rows sorted by the fold threshold, the fp16 copy in
+            // that order (k_prep_f16r, k_sym_row, k_sym_pos)
             const int64_t blocks = std::min<int64_t>((nc + 7) / 8, 16384);
-            if (vec4)
-                hipLaunchKernelGGL(k_prep_f16r<true>, dim3((unsigned)blocks), dim3(256), 0, s, C,
-                                   nc, d, dp, pi, XK, h16, r16, scP, pst1);
-            else
-                hipLaunchKernelGGL(k_prep_f16r<false>, dim3((unsigned)blocks), dim3(256), 0, s, C,
-                                   nc, d, dp, pi, XK, h16, r16, scP, pst1);
+            auto f16r = [&](const int *pm, uint16_t *K, float *hv, float *rv, float *sv) {
+                if (vec4)
+                    hipLaunchKernelGGL(k_prep_f16r<true>, dim3((unsigned)blocks), dim3(256), 0, s, C,
+                                       nc, d, dp, pm, K, hv, rv, sv, pst1);
+                else
+                    hipLaunchKernelGGL(k_prep_f16r<false>, dim3((unsigned)blocks), dim3(256), 0, s, C,
+                                       nc, d, dp, pm, K, hv, rv, sv, pst1);
+            };
+            f16r(nullptr, nullptr, h16, r16, s16);
+            MN_KCHECK(s, "k_prep_f16r<stats>");
+            hipLaunchKernelGGL(k_sym_row, dim3((unsigned)((nc + 255) / 256)), dim3(256), 0, s,
+                               nc, tau0, qn, h16, r16, d, dp, alr, tfr, tcr);
+            MN_KCHECK(s, "k_sym_row");
+            hipLaunchKernelGGL(k_iota, dim3((unsigned)((nc + 255) / 256)), dim3(256), 0, s, iota, nc);
+            MN_HIP_TRY(sort_f32_pairs(tfr, skey, iota, pi, nc, s));
+            f16r(pi, XK, nullptr, nullptr, nullptr);
             MN_KCHECK(s, "k_prep_f16r");
             hipLaunchKernelGGL(k_sym_pos, dim3((unsigned)((nc + 255) / 256)), dim3(256), 0, s,
-                               nc, pi, tau0, qn, h16, r16, scP, d, dp, tauP, teffP, Up, Vp, hcP);
+                               nc, pi, qn, alr, tfr, tcr, s16, tauP, teffP, Up, Vp, hcP, scP);
             MN_HIP_TRY(hipMemsetAsync(zdlt, 0, nn * 4, s));
             MN_KCHECK(s, "k_sym_pos");
             // block table (gram_sweep2.hpp sym_block_table): order 2 (default,
