@@ -159,20 +159,47 @@ int mn_knn_l2_f64(const void *Q, int64_t nq, const void *C, int64_t nc, int32_t 
                   int32_t x_is_f64, const int64_t *q_ids, int32_t k, int32_t use_sqrt,
                   int32_t *out_idx, double *out_dist, void *stream);
 
-/* Row-sharded multi-GPU build (SURVEY.md §8(b) mn_knn_sharded_f32, §8(e)
- * strategy A) on a caller-owned RCCL communicator (an ncclComm_t, passed as
- * void*; one rank per GPU, rank r holding rows [r n_local, (r+1) n_local) of X).
- * The shards are all-gathered, every rank computes the exact per-shard top-k
- * of all N queries against its resident shard (mn_knn_f32_qc, queries in
- * chunks of query_chunk rows; <= 0: 2^21), the lists are exchanged so each
- * query's owner receives its R lists (grouped ncclSend/ncclRecv) and merged
- * (mn_knn_merge_f32).  out_idx / out_dist [n_local][k]: the rank's rows of the
- * global graph, global ids, bit-identical to a single-GPU mn_knn_f32 of X.
- * opts as mn_knn_f32 (opts->stream is used for every operation).  Collective:
- * every rank calls it with the same n_local, d and opts->k.  <= 16 ranks. */
+/* Row-sharded multi-GPU build (SURVEY.md §8(b) mn_knn_sharded_f32, §8(e)) on
+ * a caller-owned RCCL communicator (an ncclComm_t, passed as void*; one rank
+ * per GPU, rank r holding rows [r n_local, (r+1) n_local) of X).  The shards
+ * are all-gathered.  Symmetric form (self kNN, MN_L2SQ, algo AUTO / BF16X1,
+ * world > 1): each rank computes its rows' sweep thresholds against a global
+ * sample, the thresholds are all-gathered, every rank sweeps its share of the
+ * node-wide symmetric tile table (each unordered tile pair once) and
+ * re-ranks all rows' admitted candidates, the partial lists go to the rows'
+ * owners (grouped ncclSend/ncclRecv), which merge and certify them.  Per-shard
+ * form (otherwise): exact per-shard top-k of all N queries against the
+ * resident shard (mn_knn_f32_qc, chunks of query_chunk rows; <= 0: 2^21),
+ * the exchange, mn_knn_merge_f32.  out_idx / out_dist [n_local][k]: the
+ * rank's rows of the global graph, global ids, bit-identical to a single-GPU
+ * mn_knn_f32 of X.  opts as mn_knn_f32 (opts->stream is used for every
+ * operation; timing 1: mn_knn_last_stats has ms_sample = all-gather + stage
+ * A, ms_sweep = the sweep share, ms_rerank = the exchange, ms_fallback = the
+ * merge).  Collective: every rank calls it with the same n_local, d and
+ * opts.  <= 16 ranks. */
 int mn_knn_sharded_f32(const float *X_shard, int64_t n_local, int32_t d, void *rccl_comm,
                        const mn_knn_opts *opts, int64_t query_chunk, int32_t *out_idx,
                        float *out_dist);
+/* The symmetric form of mn_knn_sharded_f32 with `world` ranks simulated on
+ * ONE device (tests and single-GPU measurement of one rank's share): X_all
+ * [n_tot][d] (device) stands for the all-gathered shards (n_tot a multiple of
+ * world <= 16); every rank's stages run in turn and the exchange is a strided
+ * read.  out_idx / out_dist [n_tot][k]: the global graph, bit-identical to
+ * mn_knn_f32.  rank_ms (host, may be NULL) [world][3]: per rank the stage A
+ * (phase-1 thresholds), stage B (sweep share + partial re-rank) and stage C
+ * (merge + certify + exact scan) milliseconds.  MN_ENOTSUP when the symmetric
+ * form does not apply (the RCCL entry then runs its per-shard form). */
+int mn_knn_sharded_sim_f32(const float *X_all, int64_t n_tot, int32_t d, int32_t world,
+                           const mn_knn_opts *opts, int32_t *out_idx, float *out_dist,
+                           float *rank_ms);
+/* Host only (no device work): rank `rank`'s share of the symmetric form's
+ * node-wide tile table over nbk 256-row blocks — entries (I, Jfirst, tiles,
+ * stride) = row block I against column blocks Jfirst + t stride, t < tiles
+ * (J >= I; empty padding entries have tiles 0).  Over all ranks every tile
+ * (I, J >= I) appears exactly once.  out4 [cap][4] (may be NULL: count only);
+ * *n_out = entries; MN_ECAP when cap is too small. */
+int mn_sym_share_table(int32_t nbk, int32_t rank, int32_t world, int32_t *out4, int64_t cap,
+                       int64_t *n_out);
 /* RCCL communicator helpers for callers without an RCCL binding of their own:
  * rank 0 creates the 128-byte id and distributes it; each rank then inits. */
 int mn_rccl_unique_id(void *out_128_bytes);

@@ -600,55 +600,76 @@ inline SweepPlan plan_sweep(int64_t nq, int64_t nc2, double expect) {
 //     different XCDs share a column range (one Infinity-Cache fill); each
 //     XCD's list is padded with empty entries to a common length (the
 //     kernel's xcd_remap gives XCD x the contiguous range x L .. x L + L - 1).
-inline std::vector<int4> sym_block_table(int nbk, int TPB, int order) {
-    std::vector<int4> tab;
-    if (order == 2) {
-        constexpr int GR = 4, GC = 8, NX = 8;
-        const int T8 = std::max(1, TPB / GC);  // tiles per block
-        const int W = GC * T8;                 // column range of a group
-        // groups in time order: column range outer (shared across XCDs), row
-        // band inner; the full groups (every block T8 tiles: they finish
-        // together, so the next group starts in step) first, then the ragged
-        // ones near the diagonal; group g goes to XCD g % 8
-        std::vector<std::vector<int4>> full, part;
-        for (int J0 = 0; J0 < nbk; J0 += W) {
-            for (int I0 = 0; I0 < nbk && I0 < J0 + W - 1; I0 += GR) {
-                std::vector<int4> grp;
-                bool all = true;
-                for (int r = 0; r < GR; ++r)
-                    for (int c = 0; c < GC; ++c) {
-                        const int I = I0 + r;
-                        if (I >= nbk) { all = false; continue; }
-                        // J = J0 + c + GC t with I < J < min(nbk, J0 + W)
-                        const int Jend = std::min(nbk, J0 + W);
-                        const int t0 = (J0 + c <= I) ? (I - (J0 + c)) / GC + 1 : 0;
-                        const int Jf = J0 + c + GC * t0;
-                        if (Jf >= Jend) { all = false; continue; }
-                        const int cnt = (Jend - 1 - Jf) / GC + 1;
-                        all = all && cnt == T8;
-                        grp.push_back(make_int4(I, Jf, cnt, GC));
-                    }
-                if (!grp.empty()) (all ? full : part).push_back(grp);
-            }
+//   sharded (sym_block_table_share): the order-2 table of an N-row problem
+//     split over `world` ranks (row-sharded build, shard.hip): the groups in
+//     time order are dealt in rounds of 8 (one per XCD), each round to the
+//     least-loaded rank so far, and diagonal tile I to rank (I / 8) % world, so every tile
+//     runs on exactly one rank, each rank's share keeps the XCD-group
+//     structure, and the full groups (equal tile counts) spread evenly.
+//     world = 1 is order 2.
+inline std::vector<int4> sym_block_table_share(int nbk, int TPB, int rank, int world) {
+    constexpr int GR = 4, GC = 8, NX = 8;
+    const int T8 = std::max(1, TPB / GC);  // tiles per block
+    const int W = GC * T8;                 // column range of a group
+    // groups in time order: column range outer (shared across XCDs), row band
+    // inner; the full groups (every block T8 tiles: they finish together, so
+    // the next group starts in step) first, then the ragged ones near the
+    // diagonal; group g goes to XCD g % 8
+    std::vector<std::vector<int4>> full, part;
+    for (int J0 = 0; J0 < nbk; J0 += W) {
+        for (int I0 = 0; I0 < nbk && I0 < J0 + W - 1; I0 += GR) {
+            std::vector<int4> grp;
+            bool all = true;
+            for (int r = 0; r < GR; ++r)
+                for (int c = 0; c < GC; ++c) {
+                    const int I = I0 + r;
+                    if (I >= nbk) { all = false; continue; }
+                    // J = J0 + c + GC t with I < J < min(nbk, J0 + W)
+                    const int Jend = std::min(nbk, J0 + W);
+                    const int t0 = (J0 + c <= I) ? (I - (J0 + c)) / GC + 1 : 0;
+                    const int Jf = J0 + c + GC * t0;
+                    if (Jf >= Jend) { all = false; continue; }
+                    const int cnt = (Jend - 1 - Jf) / GC + 1;
+                    all = all && cnt == T8;
+                    grp.push_back(make_int4(I, Jf, cnt, GC));
+                }
+            if (!grp.empty()) (all ? full : part).push_back(grp);
         }
-        std::vector<std::vector<int4>> xl(NX);
-        size_t g = 0;
-        for (auto *list : {&full, &part})
-            for (auto &grp : *list) {
-                auto &dst = xl[g++ % NX];
-                dst.insert(dst.end(), grp.begin(), grp.end());
-            }
-        // the diagonal tiles: one-tile blocks, spread over the XCDs
-        for (int I = 0; I < nbk; ++I) xl[I % NX].push_back(make_int4(I, I, 1, 1));
-        size_t L = 0;
-        for (auto &x : xl) L = std::max(L, x.size());
-        tab.reserve(L * NX);
-        for (auto &x : xl) {
-            tab.insert(tab.end(), x.begin(), x.end());
-            tab.insert(tab.end(), L - x.size(), make_int4(0, 0, 0, 1));
-        }
-        return tab;
     }
+    std::vector<const std::vector<int4> *> all;
+    for (auto *list : {&full, &part})
+        for (auto &grp : *list) all.push_back(&grp);
+    // rounds of NX groups in time order, each to the least-loaded rank so far
+    // (ties: the lowest rank) — the ragged groups near the diagonal vary in size
+    std::vector<long> load((size_t)world, 0);
+    std::vector<std::vector<int4>> xl(NX);
+    for (size_t g0 = 0; g0 < all.size(); g0 += NX) {
+        long t = 0;
+        for (size_t g = g0; g < std::min(all.size(), g0 + NX); ++g)
+            for (const int4 &e : *all[g]) t += e.z;
+        const int dst = (int)(std::min_element(load.begin(), load.end()) - load.begin());
+        load[(size_t)dst] += t;
+        if (dst != rank) continue;
+        for (size_t g = g0; g < std::min(all.size(), g0 + NX); ++g)
+            xl[g % NX].insert(xl[g % NX].end(), all[g]->begin(), all[g]->end());
+    }
+    // the diagonal tiles: one-tile blocks, spread over the XCDs
+    for (int I = 0; I < nbk; ++I)
+        if ((I / NX) % world == rank) xl[I % NX].push_back(make_int4(I, I, 1, 1));
+    size_t L = 0;
+    for (auto &x : xl) L = std::max(L, x.size());
+    std::vector<int4> tab;
+    tab.reserve(L * NX);
+    for (auto &x : xl) {
+        tab.insert(tab.end(), x.begin(), x.end());
+        tab.insert(tab.end(), L - x.size(), make_int4(0, 0, 0, 1));
+    }
+    return tab;
+}
+
+inline std::vector<int4> sym_block_table(int nbk, int TPB, int order) {
+    if (order == 2) return sym_block_table_share(nbk, TPB, 0, 1);
+    std::vector<int4> tab;
     tab.reserve((size_t)nbk * ((size_t)nbk / TPB + 2) / 2 + 16);
     if (order == 1) {
         std::vector<int> key;

@@ -39,6 +39,7 @@
 #include "common.hpp"
 #include "gram_bf16.hpp"
 #include "gram_sweep2.hpp"
+#include "shard_sym.hpp"
 
 namespace mn {
 
@@ -1315,6 +1316,21 @@ __global__ __launch_bounds__(64 * WPB) void k_rerank_x1(
         if (lane + 64 * r >= M) ix[r] = INT_MAX;
     wave_bitonic_sort<NR>(dd, ix);
     const int keff = (int)min((int64_t)min(k, M), nvalid_max);
+    if (!fb_list) {
+        // partial mode (one rank's share of a row-sharded symmetric sweep,
+        // shard_share): the exact top-k of this share's admitted candidates,
+        // certified after the owner's merge (k_merge_certify); a forced row
+        // (overflow, too many candidates) is marked idx -2 in slot 0
+        if (forced) {
+            for (int e = lane; e < k; e += 64) {
+                out_idx[qo * k + e] = e == 0 ? -2 : -1;
+                out_dist[qo * k + e] = __builtin_inff();
+            }
+            return;
+        }
+        wave_store_list<NR>(dd, ix, k, keff, out_idx + qo * k, out_dist + qo * k);
+        return;
+    }
     bool cert = !forced;
     if (cert && T < __builtin_inff() && keff > 0) {
         const float Dk = wave_elem<NR>(dd, keff - 1);
@@ -1844,6 +1860,7 @@ __global__ __launch_bounds__(256) void k_merge_parts(const int32_t *__restrict__
 namespace {
 thread_local mn_knn_stats t_stats{};
 }
+mn_knn_stats &knn_stats_ref() { return t_stats; }
 
 // perm = the golden-ratio bijection of k_perm_init over n rows, in scratch slot
 // `slot`; with_inverse: ipos = perm + n (position of row r in the order);
@@ -2611,6 +2628,334 @@ static int knn_x1(const float *Q, int64_t nq, const float *C, int64_t nc, int32_
         t_stats.ms_fallback = tm.ms(4 + o, 5 + o);
         t_stats.ms_total = tm.ms(0, 5 + o);
     }
+    return MN_OK;
+}
+
+// ---------------------------------------------------------------------------
+// 6. row-sharded symmetric sweep (shard.hip): the SW_SYM
+// pipeline of knn_x1 over all N rows, its block table dealt over the ranks
+// ---------------------------------------------------------------------------
+// Stage A (shard_phase1, per rank): tau0 of the rank's own rows from the
+// phase-1 generator against the GLOBAL sample (the first m0 rows of the
+// golden-ratio order over all N rows), as knn_x1 computes it.
+// Stage B (shard_share, per rank, after the tau0 / norm all-gather): every
+// rank builds the same per-row bounds, the same Tf order and the same fp16
+// copy of all N rows (deterministic kernels and radix sort), sweeps ITS share
+// of the order-2 block table (ksw2::sym_block_table_share: every tile on
+// exactly one rank) and re-ranks all N rows in partial mode: per row the exact
+// top-k of the candidates its tiles admitted (k_rerank_x1, fb_list == NULL).
+// Stage C (shard_finish, per owner, after the exchange): merge the parts of
+// the owner's rows and certify them with the row's certificate threshold Tc
+// (k_merge_certify) — the union of the parts' admitted candidates is exactly
+// the single-GPU sweep's, so the certificate is the same; uncertified rows go
+// to the split exact scan against all N rows (X_all is resident on every rank).
+ShardPlan shard_plan(int64_t N, int d, int k, int world) {
+    ShardPlan p{};
+    p.N = N;
+    p.d = d;
+    p.dp = (d + 255) / 256 * 256;
+    p.nkb = p.dp / 32;
+    p.k = k;
+    p.world = world;
+    p.L1 = std::min(std::max((3 * k + 3) / 8, 12), 48);
+    const char *fs = knob("MN_SH_SAMPLE_DIV");  // tuning build: sample = N / div
+    const int64_t div = (fs && *fs) ? std::max(2, atoi(fs)) : 24;
+    p.m0 = std::max<int64_t>(N / div, (int64_t)64 * p.L1);
+    p.m0 = (p.m0 + 255) / 256 * 256;
+    // as knn_x1: the two-phase form needs a corpus well past the sample;
+    // the sweep's grid and the int32 ids bound N
+    p.ok = k >= 1 && k <= knn::KMAX && d >= 1 && p.m0 + 4 * ksw2::BC <= N && N * 32 < INT_MAX &&
+           world >= 1 && world <= knn::MAX_PARTS;
+    return p;
+}
+
+static void shard_prep(const float *X, int64_t n, int d, int dp, const int *pm, uint16_t *R,
+                       float *nv, float *hcv, float *hv, float *rv, unsigned *cmax, int *flags,
+                       hipStream_t s) {
+    if (n == 0) return;
+    const bool vec4 = (d % 4 == 0) && ((uintptr_t)X % 16 == 0);
+    const int64_t blocks = std::min<int64_t>((n + 7) / 8, 16384);
+    if (vec4)
+        hipLaunchKernelGGL(knn::k_prep_x1<true>, dim3((unsigned)blocks), dim3(256), 0, s, X, n, d, dp,
+                           pm, R, (uint16_t *)nullptr, nv, hcv, hv, rv, cmax, flags + 3, 1, 0,
+                           (unsigned *)nullptr);
+    else
+        hipLaunchKernelGGL(knn::k_prep_x1<false>, dim3((unsigned)blocks), dim3(256), 0, s, X, n, d,
+                           dp, pm, R, (uint16_t *)nullptr, nv, hcv, hv, rv, cmax, flags + 3, 1, 0,
+                           (unsigned *)nullptr);
+}
+
+int shard_phase1(const float *X_all, const ShardPlan &pl, int64_t row0, int64_t nl, hipStream_t s,
+                 float *tau0_o, float *qn_o) {
+    using namespace knn;
+    const int64_t N = pl.N, m0 = pl.m0;
+    const int d = pl.d, dp = pl.dp;
+    uint16_t *QR = (uint16_t *)scratch(kSlotX1QR, (size_t)nl * dp * 2 + 64);
+    uint16_t *CR = (uint16_t *)scratch(kSlotX1CR, (size_t)m0 * dp * 2 + 64);
+    char *aux = (char *)scratch(kSlotX1Aux, (size_t)nl * 16 + (size_t)m0 * 8 + 256);
+    int *flags = (int *)scratch(kSlotFlags, 128);
+    int *perm = make_perm(N, kSlotPerm, 0, s);
+    MN_REQUIRE(QR && CR && aux && flags && perm, MN_ENOMEM, "shard_phase1: scratch allocation failed");
+    float *qhn = (float *)aux, *qrn = qhn + nl, *tq = qrn + nl, *dlt = tq + nl;
+    float *cnv = dlt + nl, *chc = cnv + m0;
+    unsigned *cmax = (unsigned *)flags;
+    MN_HIP_TRY(hipMemsetAsync(flags, 0, 128, s));
+    // maxima over the rows and the sample (both enter the phase-1 bound)
+    shard_prep(X_all + row0 * (int64_t)d, nl, d, dp, nullptr, QR, qn_o, nullptr, qhn, qrn, cmax,
+               flags, s);
+    shard_prep(X_all, m0, d, dp, perm, CR, cnv, chc, nullptr, nullptr, cmax, flags, s);
+    MN_KCHECK(s, "k_prep_x1<shard>");
+    int hflags[8] = {0};
+    MN_HIP_TRY(hipMemcpyAsync(hflags, flags, 32, hipMemcpyDeviceToHost, s));
+    MN_HIP_TRY(hipStreamSynchronize(s));
+    MN_REQUIRE(hflags[3] == 0, MN_ENONFINITE,
+               "mn_knn_sharded: input contains NaN/inf (the reference panics in partial_cmp().unwrap())");
+    if (hflags[4] != 0) return 1;  // too large for the bf16 bound: the per-shard path
+    const kb16::GramPlan gp = kb16::plan_gram(nl, m0, pl.L1, 1, 1);
+    const size_t nbuf1 = (size_t)nl * gp.S * gp.cap;
+    uint2 *cbuf1 = (uint2 *)scratch(kSlotLists, nbuf1 * sizeof(uint2) + 64);
+    char *meta1 = (char *)scratch(kSlotListMeta, (size_t)nl * gp.S * 8 + 64);
+    MN_REQUIRE(cbuf1 && meta1, MN_ENOMEM, "shard_phase1: phase-1 buffer allocation failed");
+    int *bcnt1 = (int *)meta1;
+    float *btau1 = (float *)(meta1 + (size_t)nl * gp.S * 4);
+    const int64_t bq = (nl + kb16::BM - 1) / kb16::BM;
+    hipLaunchKernelGGL((kb16::k_gram_bf16<kb16::GM_L2H, 0>), dim3((unsigned)(bq * gp.S)),
+                       dim3(kb16::NT), 0, s, QR, nl, CR, m0, dp, row0, (int64_t)0, 0, qn_o, cnv,
+                       pl.L1, (int)gp.S, gp.chunk, gp.cap, cbuf1, bcnt1, btau1);
+    MN_KCHECK(s, "k_gram_bf16<L2H, shard>");
+    hipLaunchKernelGGL(k_tau_x1, dim3((unsigned)((nl + 255) / 256)), dim3(256), 0, s, nl,
+                       (int)gp.S, btau1, qn_o, qhn, qrn, cmax, d, dp, tq, tau0_o, dlt,
+                       (unsigned *)nullptr);
+    MN_KCHECK(s, "k_tau_x1<shard>");
+    return MN_OK;
+}
+
+__global__ __launch_bounds__(256) void k_flag_nonfinite(const float *__restrict__ v, int64_t n,
+                                                        int *__restrict__ flag) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const bool bad = i < n && !__builtin_isfinite(v[i]);
+    if (__any(bad) && (threadIdx.x & 63) == 0) atomicOr(flag, 1);
+}
+
+int shard_share(const float *X_all, const ShardPlan &pl, const float *tau0_all,
+                const float *qn_all, int rank, int world, hipStream_t s, int32_t *pidx,
+                float *pdist, float *tc_all, int64_t *n_cand) {
+    using namespace knn;
+    const int64_t N = pl.N;
+    const int d = pl.d, dp = pl.dp, nkb = pl.nkb, k = pl.k;
+    const size_t nn = (size_t)N;
+    const int pst1 = nkb + 1;  // tile-major panel stride (knn_x1's TM_PAD 1)
+    const int64_t kbw1 = (int64_t)pst1 * 32;
+    const int64_t npad = (N + 255) / 256 * 256;
+    const bool vec4 = (d % 4 == 0) && ((uintptr_t)X_all % 16 == 0);
+    int *flags = (int *)scratch(kSlotFlags, 128);
+    char *so = (char *)scratch(kSlotSymOrd, nn * 4 * 17 + 8192);
+    uint16_t *XK = (uint16_t *)scratch(kSlotX1CK, (size_t)npad * kbw1 * 2 + 64);
+    int *big_list = (int *)scratch(kSlotFallback, sizeof(int) * nn + 64);
+    MN_REQUIRE(flags && so && XK && big_list, MN_ENOMEM, "shard_share: scratch allocation failed");
+    auto arr = [&](int i) { return so + (size_t)i * (((nn * 4) + 255) & ~(size_t)255); };
+    float *skey = (float *)arr(0);
+    int *pi = (int *)arr(1), *iota = (int *)arr(2);
+    float *tauP = (float *)arr(3), *teffP = (float *)arr(4), *hcP = (float *)arr(5),
+          *Up = (float *)arr(6), *Vp = (float *)arr(7), *zdlt = (float *)arr(8),
+          *scP = (float *)arr(9), *h16 = (float *)arr(10), *r16 = (float *)arr(11),
+          *s16 = (float *)arr(12), *alr = (float *)arr(13), *tfr = (float *)arr(14);
+    const unsigned g256 = (unsigned)((N + 255) / 256);
+    MN_HIP_TRY(hipMemsetAsync(flags, 0, 128, s));
+    // a non-finite threshold would break the column fold: the per-shard path
+    hipLaunchKernelGGL(k_flag_nonfinite, dim3(g256), dim3(256), 0, s, tau0_all, N, flags);
+    MN_KCHECK(s, "k_flag_nonfinite");
+    int hbad = 0;
+    MN_HIP_TRY(hipMemcpyAsync(&hbad, flags, 4, hipMemcpyDeviceToHost, s));
+    MN_HIP_TRY(hipStreamSynchronize(s));
+    if (hbad) return 1;
+    const int64_t blocks = std::min<int64_t>((N + 7) / 8, 16384);
+    auto f16r = [&](const int *pm, uint16_t *K, float *hv, float *rv, float *sv) {
+        if (vec4)
+            hipLaunchKernelGGL(k_prep_f16r<true>, dim3((unsigned)blocks), dim3(256), 0, s, X_all, N,
+                               d, dp, pm, K, hv, rv, sv, pst1);
+        else
+            hipLaunchKernelGGL(k_prep_f16r<false>, dim3((unsigned)blocks), dim3(256), 0, s, X_all,
+                               N, d, dp, pm, K, hv, rv, sv, pst1);
+    };
+    f16r(nullptr, nullptr, h16, r16, s16);
+    MN_KCHECK(s, "k_prep_f16r<stats, shard>");
+    hipLaunchKernelGGL(k_sym_row, dim3(g256), dim3(256), 0, s, N, tau0_all, qn_all, h16, r16, d,
+                       dp, alr, tfr, tc_all);
+    MN_KCHECK(s, "k_sym_row<shard>");
+    hipLaunchKernelGGL(k_iota, dim3(g256), dim3(256), 0, s, iota, N);
+    MN_HIP_TRY(sort_f32_pairs(tfr, skey, iota, pi, N, s));
+    f16r(pi, XK, nullptr, nullptr, nullptr);
+    MN_KCHECK(s, "k_prep_f16r<shard>");
+    hipLaunchKernelGGL(k_sym_pos, dim3(g256), dim3(256), 0, s, N, pi, qn_all, alr, tfr, tc_all,
+                       s16, tauP, teffP, Up, Vp, hcP, scP);
+    MN_HIP_TRY(hipMemsetAsync(zdlt, 0, nn * 4, s));
+    MN_KCHECK(s, "k_sym_pos<shard>");
+    const int nbk = (int)((N + ksw2::BC - 1) / ksw2::BC);
+    const std::vector<int4> tab = ksw2::sym_block_table_share(nbk, 256, rank, world);
+    int4 *dtab = (int4 *)scratch(kSlotSymTab, tab.size() * sizeof(int4) + 64);
+    MN_REQUIRE(dtab, MN_ENOMEM, "shard_share: block table allocation failed");
+    MN_REQUIRE(tab.size() < INT_MAX, MN_ENOTSUP, "shard_share: sweep grid too large");
+    MN_HIP_TRY(hipMemcpyAsync(dtab, tab.data(), tab.size() * sizeof(int4), hipMemcpyHostToDevice, s));
+    // per-row buffers: the share holds ~1/world of the ~L1 N / m0 candidates
+    // of a row; the same floor as the single-GPU sweep
+    const double expect = (double)pl.L1 * (double)N / (double)pl.m0 / world;
+    const char *cpe = knob("MN_SH_CAP");  // tuning build: per-row buffer entries
+    const int cap2 = (cpe && *cpe) ? std::max(64, atoi(cpe))
+                                   : std::max(256, (int)((2.5 * expect + 64.0 + 15.0) / 16.0) * 16);
+    uint2 *cbuf2 = (uint2 *)scratch(kSlotX1Buf2, nn * cap2 * sizeof(uint2) + 64);
+    int *cnt2 = (int *)scratch(kSlotX1Meta2, nn * 4 + 64);
+    MN_REQUIRE(cbuf2 && cnt2, MN_ENOMEM, "shard_share: sweep buffer allocation failed (%zu MB)",
+               (nn * cap2 * sizeof(uint2)) >> 20);
+    MN_HIP_TRY(hipMemsetAsync(cnt2, 0, nn * 4, s));
+    if (!tab.empty()) {
+        ksw2::SymArgs sa{dtab, Vp, Up, scP};
+        hipLaunchKernelGGL((ksw2::k_gram_sweep2<0, ksw2::SW_SYM, true, true>), dim3((unsigned)tab.size()),
+                           dim3(ksw2::NT), 0, s, XK, N, XK, N, nkb, (int64_t)0, (int64_t)0, 1, Up,
+                           teffP, Vp, (int64_t)0, 1, (int64_t)0, cap2, cbuf2, cnt2, pst1, sa);
+        MN_KCHECK(s, "k_gram_sweep2<SYM, shard>");
+    }
+    // partial re-rank of every row: 128 candidates a wave first, the rows with
+    // more (up to 1024) in a second launch
+    int *big_count = flags + 6;
+    const float rel = (d + 8.0f) * 0x1p-24f;
+    const int64_t nvalid = N - 1;
+#define MN_RRS(NRV, WPB, V, NB, QL, QN, BCN, BL)                                                  \
+    hipLaunchKernelGGL((k_rerank_x1<NRV, WPB, V>), dim3((unsigned)(NB)), dim3(64 * WPB), 0, s,   \
+                       X_all, N, X_all, d, (int64_t)0, 0, 0, (const uint2 *)nullptr,              \
+                       (const int *)nullptr, tauP, 1, cap2, cbuf2, cnt2, zdlt, k, nvalid, QL, QN, \
+                       BCN, BL, pi, (int64_t)0, 1, pi, (float *)nullptr, pidx, pdist,             \
+                       (int *)nullptr, (int *)nullptr, rel, (int *)nullptr)
+    const int64_t nb1 = (N + 3) / 4;
+    if (vec4) MN_RRS(2, 4, true, nb1, (const int *)nullptr, (const int *)nullptr, big_count, big_list);
+    else MN_RRS(2, 4, false, nb1, (const int *)nullptr, (const int *)nullptr, big_count, big_list);
+    MN_KCHECK(s, "k_rerank_x1<partial>");
+    int nbig = 0;
+    MN_HIP_TRY(hipMemcpyAsync(&nbig, big_count, 4, hipMemcpyDeviceToHost, s));
+    MN_HIP_TRY(hipStreamSynchronize(s));
+    if (nbig > 0) {
+        if (vec4) MN_RRS(16, 1, true, nbig, big_list, big_count, (int *)nullptr, (int *)nullptr);
+        else MN_RRS(16, 1, false, nbig, big_list, big_count, (int *)nullptr, (int *)nullptr);
+        MN_KCHECK(s, "k_rerank_x1<partial, wide>");
+    }
+#undef MN_RRS
+    if (n_cand) {
+        unsigned long long *nc64 = (unsigned long long *)(flags + 8);
+        MN_HIP_TRY(hipMemsetAsync(nc64, 0, 8, s));
+        hipLaunchKernelGGL(k_count_cands, dim3(1024), dim3(256), 0, s, cnt2, N, cap2, nc64);
+        MN_KCHECK(s, "k_count_cands<shard>");
+        unsigned long long h = 0;
+        MN_HIP_TRY(hipMemcpyAsync(&h, nc64, 8, hipMemcpyDeviceToHost, s));
+        MN_HIP_TRY(hipStreamSynchronize(s));
+        *n_cand = (int64_t)h;
+    }
+    return MN_OK;
+}
+
+// One thread per owned row: merge the parts' exact lists (each (dist, id)
+// ordered; part p row q at p * pstride + q * k) and certify the merged top-k
+// with the row's certificate Tc > D_k.  A part's idx -2 in slot 0 (a forced
+// row) or fewer than kneed entries leave the row uncertified: ub = the merged
+// k-th exact distance (an upper bound of D_k) and the row listed.
+__global__ __launch_bounds__(256) void k_merge_certify(
+    const int32_t *__restrict__ pidx, const float *__restrict__ pdist, int P, int64_t pstride,
+    int64_t nl, int k, int kneed, const float *__restrict__ tc, int32_t *__restrict__ out_idx,
+    float *__restrict__ out_dist, float *__restrict__ ub, int *__restrict__ fb_count,
+    int *__restrict__ fb_list, int *__restrict__ why) {
+    const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= nl) return;
+    int head[knn::MAX_PARTS];
+    bool forced = false;
+#pragma unroll
+    for (int p = 0; p < knn::MAX_PARTS; ++p) {
+        head[p] = 0;
+        if (p < P && pidx[p * pstride + q * k] == -2) forced = true;
+    }
+    int m = 0;
+    float Dk = __builtin_inff();
+    for (int r = 0; r < k; ++r) {
+        int bp = -1;
+        float bd = __builtin_inff();
+        int bi = INT_MAX;
+#pragma unroll
+        for (int p = 0; p < knn::MAX_PARTS; ++p) {
+            if (p >= P) break;
+            const int h = head[p];
+            if (h >= k) continue;
+            const int64_t off = p * pstride + q * k + h;
+            const int ci = pidx[off];
+            if (ci < 0) continue;
+            const float cd = pdist[off];
+            if (bp < 0 || key_less(cd, ci, bd, bi)) { bp = p; bd = cd; bi = ci; }
+        }
+#pragma unroll
+        for (int p = 0; p < knn::MAX_PARTS; ++p)
+            if (p == bp) head[p]++;
+        out_idx[q * k + r] = bp < 0 ? -1 : bi;
+        out_dist[q * k + r] = bp < 0 ? __builtin_inff() : bd;
+        if (bp >= 0) {
+            ++m;
+            if (r == kneed - 1) Dk = bd;
+        }
+    }
+    bool cert = !forced && m >= kneed;
+    if (cert && kneed > 0) cert = tc[q] > Dk;  // NaN-safe: false => exact scan
+    if (!cert) {
+        ub[q] = (m >= kneed && kneed > 0) ? Dk : __builtin_inff();
+        fb_list[atomicAdd(fb_count, 1)] = (int)q;
+        if (why) atomicAdd(&why[forced ? 0 : m < kneed ? 1 : 2], 1);
+    }
+}
+
+int shard_finish(const float *X_all, const ShardPlan &pl, int64_t row0, int64_t nl, int parts,
+                 int64_t part_stride, const int32_t *pidx, const float *pdist, const float *tc_all,
+                 hipStream_t s, int32_t *out_idx, float *out_dist, int *n_fallback) {
+    using namespace knn;
+    const int64_t N = pl.N;
+    const int d = pl.d, k = pl.k;
+    int *flags = (int *)scratch(kSlotFlags, 128);
+    char *fb = (char *)scratch(kSlotFallback, sizeof(int) * (size_t)nl * 2 + 256);
+    MN_REQUIRE(flags && fb, MN_ENOMEM, "shard_finish: scratch allocation failed");
+    int *fb_list = (int *)fb;
+    float *ub = (float *)(fb + (((size_t)nl * 4 + 255) & ~(size_t)255));
+    int *fb_count = flags + 5;
+    MN_HIP_TRY(hipMemsetAsync(fb_count, 0, 4, s));
+    const int kneed = (int)std::min<int64_t>(k, N - 1);
+    // MN_X1_DEBUG=1: why rows stay uncertified (stderr)
+    const char *dbe = getenv("MN_X1_DEBUG");
+    int *why = (dbe && *dbe == '1') ? flags + 20 : nullptr;
+    if (why) MN_HIP_TRY(hipMemsetAsync(why, 0, 12, s));
+    hipLaunchKernelGGL(k_merge_certify, dim3((unsigned)((nl + 255) / 256)), dim3(256), 0, s, pidx,
+                       pdist, parts, part_stride, nl, k, kneed, tc_all + row0, out_idx, out_dist, ub,
+                       fb_count, fb_list, why);
+    MN_KCHECK(s, "k_merge_certify");
+    int nfb = 0;
+    MN_HIP_TRY(hipMemcpyAsync(&nfb, fb_count, 4, hipMemcpyDeviceToHost, s));
+    MN_HIP_TRY(hipStreamSynchronize(s));
+    if (why) {
+        int h[3] = {0};
+        MN_HIP_TRY(hipMemcpy(h, why, 12, hipMemcpyDeviceToHost));
+        fprintf(stderr, "mn_knn sharded rows %lld..: uncertified forced %d, < k %d, bound %d\n",
+                (long long)row0, h[0], h[1], h[2]);
+    }
+    if (n_fallback) *n_fallback = nfb;
+    if (nfb == 0) return MN_OK;
+    const float *Q = X_all + row0 * (int64_t)d;
+    int rc = fb_split_scan(Q, X_all, N, d, row0, 0, 1, k, fb_list, nfb, ub, false, out_idx,
+                           out_dist, s);
+    if (rc < 0) return rc;
+    if (rc == 1) {  // outside the split scan's limits: the exact scan per row
+        const bool vec4 = (d % 4 == 0) && ((uintptr_t)X_all % 16 == 0);
+        const unsigned fgrid = (unsigned)std::min<int64_t>(nfb, 1024);
+        if (vec4)
+            hipLaunchKernelGGL(k_fallback<true>, dim3(fgrid), dim3(FB_THREADS), 0, s, Q, X_all, N, d,
+                               row0, (int64_t)0, 1, k, fb_count, fb_list, out_idx, out_dist);
+        else
+            hipLaunchKernelGGL(k_fallback<false>, dim3(fgrid), dim3(FB_THREADS), 0, s, Q, X_all, N,
+                               d, row0, (int64_t)0, 1, k, fb_count, fb_list, out_idx, out_dist);
+        MN_KCHECK(s, "k_fallback<shard>");
+    }
+    MN_HIP_TRY(hipStreamSynchronize(s));
     return MN_OK;
 }
 

@@ -1,5 +1,14 @@
 """Row-sharded multi-GPU kNN graph build, one process per GPU.
 
+The production entry is the library's mn_knn_sharded_f32 (knn_sharded_capi
+below: RCCL inside the library).  Its symmetric form — each rank sweeps its
+share of the node-wide symmetric tile table (mn_sym_share_table), the partial
+lists of every row go to the row's owner, which merges and certifies them — is
+mirrored by sharded_knn_sym over torch.distributed, so the exchange pattern
+runs under `gloo` on the CPU with stand-in stages (tests/test_dist.py).
+
+The per-shard form (sharded_knn):
+
 Rank r owns rows [r*n_loc, (r+1)*n_loc) of X as its corpus shard (resident).
 1. all-gather the query rows (every row of X) over RCCL/xGMI;
 2. exact per-shard top-k of ALL queries against the local shard
@@ -41,6 +50,39 @@ def sharded_knn(X_shard: torch.Tensor, k: int, knn_fn=None, merge_fn=None, group
     dist.all_to_all_single(recv_i.view(world, -1), part_i.contiguous().view(world, -1), group=group)
     dist.all_to_all_single(recv_d.view(world, -1), part_d.contiguous().view(world, -1), group=group)
     return merge_fn(recv_i, recv_d)
+
+
+def share_table(nbk: int, rank: int, world: int):
+    """mn_sym_share_table: rank's entries (I, Jfirst, tiles, stride) of the
+    node-wide symmetric tile table over nbk row blocks (host only)."""
+    import ctypes as C
+    import numpy as np
+    from . import _lib
+    n = C.c_int64()
+    _lib.check(_lib.lib().mn_sym_share_table(nbk, rank, world, None, 0, C.byref(n)))
+    out = np.zeros((max(n.value, 1), 4), np.int32)
+    _lib.check(_lib.lib().mn_sym_share_table(nbk, rank, world, out.ctypes.data_as(C.c_void_p),
+                                             n.value, C.byref(n)))
+    return out[:n.value]
+
+
+def sharded_knn_sym(X_shard: torch.Tensor, k: int, share_fn, finish_fn, group=None):
+    """The symmetric form's exchange (mn_knn_sharded_f32, shard.hip): all-gather
+    of the shards, share_fn(Xall, k, rank, world) -> this rank's partial lists of
+    ALL rows [N, k] (the exact top-k of the pairs in its share of the tile table),
+    one all-to-all so each row's owner holds the R partial lists, finish_fn(parts_idx
+    [R, n_loc, k], parts_dist, row0) -> the owner's rows (merge + certify)."""
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    n_loc, d = X_shard.shape
+    Xall = torch.empty((world * n_loc, d), dtype=X_shard.dtype, device=X_shard.device)
+    dist.all_gather_into_tensor(Xall, X_shard.contiguous(), group=group)
+    part_i, part_d = share_fn(Xall, k, rank, world)
+    recv_i = torch.empty((world, n_loc, k), dtype=part_i.dtype, device=part_i.device)
+    recv_d = torch.empty((world, n_loc, k), dtype=part_d.dtype, device=part_d.device)
+    dist.all_to_all_single(recv_i.view(world, -1), part_i.contiguous().view(world, -1), group=group)
+    dist.all_to_all_single(recv_d.view(world, -1), part_d.contiguous().view(world, -1), group=group)
+    return finish_fn(recv_i, recv_d, rank * n_loc)
 
 
 # ---- the same build behind the library's C entry (caller-owned RCCL comm) ----
@@ -89,3 +131,26 @@ def knn_sharded_capi(X_shard: torch.Tensor, k: int, comm: RcclComm, query_chunk:
     _lib.check(_lib.lib().mn_knn_sharded_f32(ptr(X_shard), n, d, comm.handle, C.byref(o),
                                              query_chunk, ptr(idx), ptr(dd)))
     return idx, dd
+
+
+def knn_sharded_sim(X_all: torch.Tensor, k: int, world: int, timing: bool = False, stream=None):
+    """mn_knn_sharded_sim_f32: the symmetric sharded build of `world` ranks
+    simulated on this device (X_all = the all-gathered shards).  Returns (idx
+    [n, k] int32, dist [n, k] f32, rank_ms [world][3] = per rank the stage A /
+    B / C milliseconds, stats)."""
+    import ctypes as C
+    import numpy as np
+    from . import _lib
+    from ._torch import ptr, require_cuda, stream_handle
+    from .knn import last_stats
+    X_all = require_cuda(X_all, torch.float32, "X_all", 2)
+    n, d = X_all.shape
+    idx = torch.empty((n, k), dtype=torch.int32, device=X_all.device)
+    dd = torch.empty((n, k), dtype=torch.float32, device=X_all.device)
+    ms = np.zeros((world, 3), dtype=np.float32)
+    o = _lib.KnnOpts(k=k, metric=_lib.MN_L2SQ, exclude_self=1, margin=0,
+                     timing=1 if timing else 0, algo=_lib.MN_KNN_AUTO,
+                     stream=stream_handle(stream))
+    _lib.check(_lib.lib().mn_knn_sharded_sim_f32(ptr(X_all), n, d, world, C.byref(o), ptr(idx),
+                                                 ptr(dd), ms.ctypes.data_as(C.c_void_p)))
+    return idx, dd, ms, last_stats()
