@@ -2797,9 +2797,11 @@ int shard_share(const float *X_all, const ShardPlan &pl, const float *tau0_all,
     MN_REQUIRE(dtab, MN_ENOMEM, "shard_share: block table allocation failed");
     MN_REQUIRE(tab.size() < INT_MAX, MN_ENOTSUP, "shard_share: sweep grid too large");
     MN_HIP_TRY(hipMemcpyAsync(dtab, tab.data(), tab.size() * sizeof(int4), hipMemcpyHostToDevice, s));
-    // per-row buffers: the share holds ~1/world of the ~L1 N / m0 candidates
-    // of a row; the same floor as the single-GPU sweep
-    const double expect = (double)pl.L1 * (double)N / (double)pl.m0 / world;
+    // per-row buffers: a share holds ~1/world of the ~L1 N / m0 candidates of
+    // a row on average, but unevenly (a row's candidates in one column range
+    // go to one rank): a 256-entry cap overflowed 0.9% of the rows at C2 with
+    // 8 ranks (profiles/r04/r04_shard_probe.log), the single-GPU cap none
+    const double expect = (double)pl.L1 * (double)N / (double)pl.m0;
     const char *cpe = knob("MN_SH_CAP");  // tuning build: per-row buffer entries
     const int cap2 = (cpe && *cpe) ? std::max(64, atoi(cpe))
                                    : std::max(256, (int)((2.5 * expect + 64.0 + 15.0) / 16.0) * 16);
