@@ -60,6 +60,10 @@ int mn_fill_uniform_f32(float *X, int64_t n, int32_t d, uint64_t seed,
  * Bhattacharyya kernels; exported so callers and tests can check them.  x ==
  * NULL evaluates the consecutive f32 bit patterns bits0 + i (i < n). */
 int mn_libm_f32(const float *x, int64_t n, uint32_t bits0, int32_t fn, float *out, void *stream);
+/* The library's f64 pow on device arrays, out[i] = pow(x[i], y[i]): glibc's
+ * pow restated (the reference's f64::powf: the rational kernel's
+ * (d / sigma)^p, src_legacy/laplacian.rs:256; sorted_index.rs:65). */
+int mn_libm_pow_f64(const double *x, const double *y, int64_t n, double *out, void *stream);
 
 /* ---------------------------------------------------------------------- */
 /* K1 — brute-force kNN (Gram on MFMA + LDS top-k + exact re-rank)        */

@@ -43,6 +43,7 @@
 #include <cstring>
 
 #include "common.hpp"
+#include "glibc_f64.hpp"
 #include "gram_bf16.hpp"
 #include "gram_sweep2.hpp"
 
@@ -151,7 +152,7 @@ __device__ __forceinline__ double cos_dist(double dot, double ni, double nj) {
 
 __device__ __forceinline__ double weight_of(double d, double sigma, double p) {
     const double x = d / sigma;
-    const double pw = p == 2.0 ? x * x : (p == 1.0 ? x : pow(x, p));
+    const double pw = glibc::pow_glibc(x, p);  // glibc pow (glibc_f64.hpp), every p
     return 1.0 / (1.0 + pw);
 }
 

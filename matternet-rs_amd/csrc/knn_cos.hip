@@ -36,6 +36,7 @@
 #include <vector>
 
 #include "common.hpp"
+#include "glibc_f64.hpp"
 
 namespace mn {
 namespace kcos {
@@ -419,7 +420,7 @@ __global__ void k_cand_pairs(const int32_t *__restrict__ cand, int f, int L,
 
 __device__ __forceinline__ double weight_of(double d, double sigma, double p) {
     const double x = d / sigma;
-    const double pw = p == 2.0 ? x * x : (p == 1.0 ? x : pow(x, p));
+    const double pw = glibc::pow_glibc(x, p);  // glibc pow (glibc_f64.hpp), every p
     return 1.0 / (1.0 + pw);
 }
 

@@ -35,6 +35,7 @@
 #include <vector>
 
 #include "common.hpp"
+#include "glibc_f64.hpp"
 #include "scan.hpp"
 
 namespace mn {
@@ -52,11 +53,9 @@ constexpr int BLOCK_CAP = 16384;  // rows sorted in one block's LDS (packed 8-B 
 constexpr int EMPTY = INT_MAX;  // sentinel column of an invalid forward slot
 constexpr uint64_t SENT = ~0ull;  // sentinel packed key (column << 32 | entry)
 
-__device__ __forceinline__ double pw(double x, double p) {
-    if (p == 2.0) return x * x;
-    if (p == 1.0) return x;
-    return pow(x, p);
-}
+// (d / sigma)^p as the reference's f64::powf = glibc pow (glibc_f64.hpp),
+// for every p (pow(x, 2) need not round like x * x)
+__device__ __forceinline__ double pw(double x, double p) { return glibc::pow_glibc(x, p); }
 
 // Slot s = i*k + r of the kNN rows: neighbour j and edge weight w; false if
 // the slot carries no edge (empty, self loop, filtered).  laplacian.rs:245-260

@@ -8,6 +8,7 @@
 
 #include "common.hpp"
 #include "glibc_f32.hpp"
+#include "glibc_f64.hpp"
 
 namespace mn {
 
@@ -141,6 +142,14 @@ __global__ void k_fill_uniform_f32(float *__restrict__ X, int64_t total, int32_t
 }  // namespace mn
 
 namespace mn {
+__global__ __launch_bounds__(256) void k_libm_pow_f64(const double *__restrict__ x,
+                                                      const double *__restrict__ y, int64_t n,
+                                                      double *__restrict__ out) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x)
+        out[i] = glibc::pow_glibc(x[i], y[i]);
+}
+
 __global__ __launch_bounds__(256) void k_libm_f32(const float *__restrict__ x, int64_t n,
                                                   uint32_t bits0, int fn, float *__restrict__ out) {
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
@@ -223,6 +232,19 @@ int mn_libm_f32(const float *x, int64_t n, uint32_t bits0, int32_t fn, float *ou
     hipStream_t s = (hipStream_t)stream;
     hipLaunchKernelGGL(mn::k_libm_f32, dim3((unsigned)blocks), dim3(256), 0, s, x, n, bits0, fn,
                        out);
+    MN_HIP_TRY(hipGetLastError());
+    MN_HIP_TRY(hipStreamSynchronize(s));
+    return MN_OK;
+}
+
+// The library's f64 pow (glibc_f64.hpp) on device arrays: out[i] = pow(x[i], y[i]).
+int mn_libm_pow_f64(const double *x, const double *y, int64_t n, double *out, void *stream) {
+    MN_REQUIRE(x && y && out && n >= 0, MN_EINVAL, "mn_libm_pow_f64: bad args");
+    if (n == 0) return MN_OK;
+    int64_t blocks = (n + 255) / 256;
+    if (blocks > 65536) blocks = 65536;
+    hipStream_t s = (hipStream_t)stream;
+    hipLaunchKernelGGL(mn::k_libm_pow_f64, dim3((unsigned)blocks), dim3(256), 0, s, x, y, n, out);
     MN_HIP_TRY(hipGetLastError());
     MN_HIP_TRY(hipStreamSynchronize(s));
     return MN_OK;

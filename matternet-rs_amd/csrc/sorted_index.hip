@@ -24,6 +24,7 @@
 #include <cstdlib>
 
 #include "common.hpp"
+#include "glibc_f64.hpp"
 #include "scan.hpp"
 
 namespace mn {
@@ -531,7 +532,7 @@ extern "C" int mn_sorted_range_bylambda(const double *keys, const int64_t *order
                MN_EINVAL, "mn_sorted_range_bylambda: NULL pointer");
     if (nq == 0) return MN_OK;
     hipStream_t s = (hipStream_t)stream;
-    const double band = std_dev / pow(2.0, p);  // sorted_index.rs:65
+    const double band = std_dev / mn::glibc::pow_glibc(2.0, p);  // sorted_index.rs:65 (glibc pow)
     hipLaunchKernelGGL(k_range_bylambda, dim3(grid(nq)), dim3(256), 0, s, keys, order, n, band,
                        lambda_q, nq, k, out_idx, out_lambda, out_count);
     MN_HIP_TRY(hipGetLastError());

@@ -121,6 +121,7 @@ SIGNATURES = {
     "mn_knn_f32_qc": (C.c_int, [P, I64, P, I64, I32, I64, I64, C.POINTER(KnnOpts), P, P]),
     "mn_knn_merge_f32": (C.c_int, [P, P, I32, I64, I32, P, P, P]),
     "mn_knn_l2_f64": (C.c_int, [P, I64, P, I64, I32, I32, P, I32, I32, P, P, P]),
+    "mn_libm_pow_f64": (C.c_int, [P, P, I64, P, P]),
     "mn_knn_sharded_f32": (C.c_int, [P, I64, I32, P, C.POINTER(KnnOpts), I64, P, P]),
     "mn_knn_sharded_sim_f32": (C.c_int, [P, I64, I32, I32, C.POINTER(KnnOpts), P, P, P]),
     "mn_sym_share_table": (C.c_int, [I32, I32, I32, P, I64, P]),

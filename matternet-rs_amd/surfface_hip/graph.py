@@ -130,7 +130,11 @@ def _weight_can_drop(eps: float, sigma: float, p: float) -> bool:
         # sigma = 0 or a negative base with a fractional p give inf / NaN, the
         # weight then fails the `> 1e-12` filter (no Python raise)
         with np.errstate(all="ignore"):
-            t = np.power(np.float64(d) / np.float64(sigma), np.float64(p))
+            base = np.float64(d) / np.float64(sigma)
+            try:  # math.pow is the C library's pow (numpy may vectorise its own)
+                t = np.float64(math.pow(float(base), float(p)))
+            except (ValueError, OverflowError):
+                t = np.power(base, np.float64(p))
             return np.float64(1.0) / (np.float64(1.0) + t)
     # NaN-safe: a NaN weight can drop (it fails the filter)
     return not (min(w(0.0), w(dmax)) > 1e-12) or bool(np.isnan(w(0.0)) or np.isnan(w(dmax)))

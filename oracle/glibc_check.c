@@ -152,3 +152,12 @@ int or_glibc_tables(int which, uint64_t *out) {
     out[36] = asu64(SHIFT);
     return 37;
 }
+
+/* the host glibc pow elementwise (what Rust's f64::powf calls): the checker
+ * for the device restatement (glibc_f64.hpp; numpy's power may dispatch to a
+ * vector math library instead of libm on AVX-512 hosts) */
+int or_pow_f64(const double *x, const double *y, int64_t n, double *out) {
+    if (!x || !y || !out || n < 0) return OR_EINVAL;
+    for (int64_t i = 0; i < n; ++i) out[i] = pow(x[i], y[i]);
+    return 0;
+}

@@ -290,7 +290,7 @@ int or_knn_cos_f64(const float *X, int64_t n, int32_t d, int32_t topk,
                 double dist = 1.0 - (cs > 0.0 ? cs : 0.0);
                 if (!(dist <= eps)) continue;
                 double nd = dist / sigma;
-                double wgt = 1.0 / (1.0 + (p == 2.0 ? nd * nd : pow(nd, p)));
+                double wgt = 1.0 / (1.0 + pow(nd, p)); /* f64::powf = glibc pow, every p */
                 if (!(wgt > 1e-12)) continue;
                 if (cnt < topk) {
                     buf[cnt].d = dist; buf[cnt].w = wgt; buf[cnt].j = (int32_t)j;
@@ -372,7 +372,7 @@ int or_knn_cos_f64d(const double *X, int64_t n, int32_t d, int32_t topk,
                 double dist = 1.0 - (cs > 0.0 ? cs : 0.0);
                 if (!(dist <= eps)) continue;
                 double nd = dist / sigma;
-                double wgt = 1.0 / (1.0 + (p == 2.0 ? nd * nd : pow(nd, p)));
+                double wgt = 1.0 / (1.0 + pow(nd, p)); /* f64::powf = glibc pow, every p */
                 if (!(wgt > 1e-12)) continue;
                 if (cnt < topk) {
                     buf[cnt].d = dist; buf[cnt].w = wgt; buf[cnt].j = (int32_t)j;
@@ -465,7 +465,7 @@ int or_knn_cos_bf16_rows(const uint16_t *X, int64_t n, int32_t d, int32_t topk,
                 double dist = 1.0 - (cs > 0.0 ? cs : 0.0);
                 if (!(dist <= eps)) continue;
                 double nd = dist / sigma;
-                double wgt = 1.0 / (1.0 + (p == 2.0 ? nd * nd : pow(nd, p)));
+                double wgt = 1.0 / (1.0 + pow(nd, p)); /* f64::powf = glibc pow, every p */
                 if (!(wgt > 1e-12)) continue;
                 if (cnt < topk) {
                     buf[cnt].d = dist; buf[cnt].w = wgt; buf[cnt].j = (int32_t)j;

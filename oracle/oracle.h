@@ -296,6 +296,8 @@ int or_search_lambda_aware_hybrid(const double *X, int64_t n, int32_t f, const d
 /* glibc_check.c: the host glibc logf / expf (what the reference's f32::ln /
  * f32::exp call) and a host copy of the device restatement (csrc/glibc_f32.hpp). */
 int or_libm_f32(const float *x, int64_t n, uint32_t bits0, int fn, float *out, int nthreads);
+/* the host glibc pow elementwise: out[i] = pow(x[i], y[i]) (the reference's f64::powf) */
+int or_pow_f64(const double *x, const double *y, int64_t n, double *out);
 int64_t or_libm_mismatch(uint32_t bits0, int64_t n, int fn, const float *got);
 int64_t or_glibc_restated_check(int fn, int64_t stride);
 int or_glibc_tables(int which, uint64_t *out);

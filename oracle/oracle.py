@@ -49,6 +49,7 @@ def _declare(L):
     L.or_knn_l2sq_f32.argtypes = [P, I64, I32, I32, I64, I64, C.c_int, C.c_int, P, P]
     L.or_knn_l2sq_rows_f32.argtypes = [P, I64, I32, I32, P, I64, C.c_int, P, P]
     L.or_libm_f32.argtypes = [P, I64, C.c_uint32, C.c_int, P, C.c_int]
+    L.or_pow_f64.argtypes = [P, P, I64, P]
     L.or_libm_mismatch.argtypes = [C.c_uint32, I64, C.c_int, P]
     L.or_libm_mismatch.restype = I64
     L.or_glibc_restated_check.argtypes = [C.c_int, I64]
@@ -462,3 +463,12 @@ def glibc_tables_from_libm(path=None):
     # rest: shift_scaled, poly[3], shift, invln2_scaled, poly_scaled[3]
     exp = np.concatenate([tab, rest[[6, 7, 8]], rest[[5]], rest[[4]]])
     return log, exp
+
+
+def pow_f64(x, y):
+    """The host glibc pow elementwise (or_pow_f64): the reference's f64::powf."""
+    x = np.ascontiguousarray(x, dtype=np.float64)
+    y = np.ascontiguousarray(np.broadcast_to(np.asarray(y, np.float64), x.shape), dtype=np.float64)
+    out = np.empty_like(x)
+    _check(lib().or_pow_f64(_p(x), _p(y), x.size, _p(out)), "pow_f64")
+    return out

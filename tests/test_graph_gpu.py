@@ -80,17 +80,16 @@ def test_k_cluster_f32_centroids(topk, eps):
 
 def test_f64_items_and_sigma_p():
     """build_laplacian_matrix on f64 items not representable in f32, with an
-    explicit sigma and p (laplacian.rs:256).  p = 1.5 takes pow(): the device's
-    (OCML, <= 1 ulp) where the reference calls glibc pow (< 1 ulp), so the
-    weights agree within a few ulp (structure exact); p = 2 (the default) and
-    p = 1 are bit-exact (x * x, x)."""
+    explicit sigma and p (laplacian.rs:256): the device pow is glibc's
+    restated (glibc_f64.hpp), so p = 1.5 and p = 2 (the default) are both
+    bit-exact against the oracle's host pow."""
     import surfface_hip as S
     rng = np.random.default_rng(4)
     T = rng.normal(size=(70, 500)) + 0.3  # rows = nodes
     params = S.GraphParams(eps=0.9, k=6, topk=12, p=1.5, sigma=0.4)
     gl = S.build_laplacian_matrix(torch.from_numpy(T).cuda(), params)
     assert gl.nnodes == 500  # laplacian.rs:129,165-168: n = the column count of `transposed`
-    _csr_equal(gl.matrix, _oracle_graph(T, 12, 0.9, 0.4, 1.5), rtol=1e-15)
+    _csr_equal(gl.matrix, _oracle_graph(T, 12, 0.9, 0.4, 1.5))  # glibc pow restated: bit-exact
     params2 = S.GraphParams(eps=0.9, k=6, topk=12, p=2.0, sigma=0.4)
     gl2 = S.build_laplacian_matrix(torch.from_numpy(T).cuda(), params2)
     _csr_equal(gl2.matrix, _oracle_graph(T, 12, 0.9, 0.4, 2.0))

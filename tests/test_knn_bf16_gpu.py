@@ -58,8 +58,8 @@ def test_item_graph_pow_weights():
     ri, rd, rw = O.knn_cos(Xf, 7, **kw)
     np.testing.assert_array_equal(i, ri)
     np.testing.assert_array_equal(d, rd)
-    # device pow vs glibc pow: within 2 ulp
-    np.testing.assert_allclose(w, rw, rtol=5e-16, atol=0)
+    # the device pow is glibc's restated (glibc_f64.hpp): weights bit-exact
+    np.testing.assert_array_equal(w.view(np.uint64), rw.view(np.uint64))
 
 
 def test_ties_force_exact_fallback():

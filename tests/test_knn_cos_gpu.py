@@ -47,8 +47,8 @@ def test_feature_graph_eps_sigma_p_filters_and_zero_columns():
     ri, rd, rw = ref_cols(X, 6, **kw)
     np.testing.assert_array_equal(i, ri)
     np.testing.assert_array_equal(d, rd)
-    # pow(x, 3) device vs glibc: weights within 2 ulp
-    np.testing.assert_allclose(w, rw, rtol=5e-16, atol=0)
+    # the device pow is glibc's restated (glibc_f64.hpp): weights bit-exact
+    np.testing.assert_array_equal(w.view(np.uint64), rw.view(np.uint64))
 
 
 def test_ties_force_exact_fallback():

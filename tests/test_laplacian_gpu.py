@@ -25,9 +25,15 @@ def lap(idx, val, **kw):
     return m.to_numpy() + (deg.cpu().numpy(),)
 
 
+def host_pow(x, p):
+    """The reference's f64::powf = the host glibc pow (oracle or_pow_f64: numpy's
+    power may use a vector math library, or sqrt / square for scalar exponents)."""
+    return O.pow_f64(x, p)
+
+
 def rational_weights(dist, eps, sigma, p):
     d = dist.astype(np.float64)
-    w = 1.0 / (1.0 + (d / sigma) ** 2) if p == 2.0 else 1.0 / (1.0 + np.power(d / sigma, p))
+    w = 1.0 / (1.0 + host_pow(d / sigma, p))
     valid = (d <= eps) & (w > 1e-12)
     return np.where(valid, w, 0.0), valid
 
@@ -72,13 +78,31 @@ def test_union_eps_filter_and_hub_rows():
     # network) are covered by test_large_hub_rows_device_sort
     assert st["big_rows"] >= 2
     d = dist
-    w = 1.0 / (1.0 + np.power(d / 0.7, 3.0))
+    w = 1.0 / (1.0 + host_pow(d / 0.7, 3.0))
     valid = (d <= 1.5) & (w > 1e-12) & (idx >= 0)
     rip, rix, riv = O.laplacian_union(np.where(valid, idx, -1).astype(np.int32), w)
     np.testing.assert_array_equal(ip, rip)
     np.testing.assert_array_equal(ix, rix)
-    # pow(x, 3) on the device vs glibc may differ in the last ulp: values within 4 ulp
-    np.testing.assert_allclose(iv, riv, rtol=1e-15, atol=0)
+    # the device pow is glibc's restated (glibc_f64.hpp): bit-exact
+    np.testing.assert_array_equal(iv.view(np.uint64), riv.view(np.uint64))
+
+
+@pytest.mark.parametrize("p", [0.5, 3.0, 2.7, 1.0, 2.0])
+def test_rational_kernel_exponents_bit_exact(p):
+    """laplacian.rs:256 `1 / (1 + (d / sigma).powf(p))` for p in {0.5, 3, 2.7}
+    (and the shortcut-prone 1, 2): the weights and the assembled Laplacian bit
+    for bit against the oracle with the host glibc pow."""
+    n, k = 20000, 16
+    rng = np.random.default_rng(int(p * 10))
+    idx = rng.integers(0, n, size=(n, k)).astype(np.int32)
+    dist = rng.uniform(0, 3.0, size=(n, k)).astype(np.float64)
+    ip, ix, iv, deg = lap(idx, dist, weight_kernel="rational", eps=2.5, sigma=0.9, p=p)
+    w, valid = rational_weights(dist, 2.5, 0.9, p)
+    valid &= idx != np.arange(n)[:, None]
+    rip, rix, riv = O.laplacian_union(np.where(valid, idx, -1).astype(np.int32), w)
+    np.testing.assert_array_equal(ip, rip)
+    np.testing.assert_array_equal(ix, rix)
+    np.testing.assert_array_equal(iv.view(np.uint64), riv.view(np.uint64))
 
 
 @pytest.mark.parametrize("sym", ["union", "max"])

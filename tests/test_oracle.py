@@ -512,3 +512,27 @@ def test_glibc_logf_expf_restatement():
     np.testing.assert_array_equal(np.array(vals[36:], np.uint64), O.glibc_tables(1))
     assert O.glibc_restated_check(0, 61) == 0
     assert O.glibc_restated_check(1, 61) == 0
+
+
+def test_glibc_pow_restatement_host():
+    """The kernels' f64 pow (csrc/glibc_f64.hpp: glibc's pow restated with the
+    host libm's own tables) against the host pow: random and structured (x, p)
+    — the weight kernel's (d / sigma)^p for p in {0.5, 2, 3, 2.7, ...}, wide x
+    and y, subnormal / overflowing results, negative x with integer y, the
+    special values — bit for bit (tests/native/pow_check.cpp, built with g++)."""
+    import shutil
+    import subprocess
+    import tempfile
+    gxx = shutil.which("g++")
+    if gxx is None:
+        pytest.skip("g++ not installed")
+    with tempfile.TemporaryDirectory() as td:
+        exe = os.path.join(td, "pow_check")
+        subprocess.run([gxx, "-O2", "-std=c++17", "-mfma", "-ffp-contract=off",
+                        "-I", os.path.join(ROOT, "tests", "native", "stub"),
+                        "-I", os.path.join(ROOT, "matternet-rs_amd", "csrc"),
+                        os.path.join(ROOT, "tests", "native", "pow_check.cpp"), "-o", exe],
+                       check=True, capture_output=True)
+        r = subprocess.run([exe, "1000000"], capture_output=True, text=True, timeout=300)
+    print(r.stdout)
+    assert r.returncode == 0 and "mismatches 0" in r.stdout, r.stdout + r.stderr
