@@ -358,12 +358,11 @@ def c3_legs(S, X, idx, dist, k):
     ent = S.energy.last_stats()["entries"]
     gbs = ebytes / ms / 1e6
     # bound: HBM (X streamed once, L resident); the f64 work per
-    # row (7 f64 ops per stored entry and row) is reported beside it.  The pass
-    # is two kernels (k_row_tau: the Median tau; k_energy_rows2: the entry
-    # loop), each streaming X: the algorithmic bytes count X once
-    f64_ops = 7.0 * ent * n
+    # row is reported beside it (k_energy_rows3, one pass over X: the tau
+    # select inline, the list-A identity at 5 f64 ops per entry and row)
+    f64_ops = 5.0 * ent * n
     out["energy_rows"] = {"ms": round(ms, 3), "GB_per_s": round(gbs, 1), "entries_per_row": ent,
-                          "roofline": {"bound": "hbm", "kernel": "k_row_tau + k_energy_rows2",
+                          "roofline": {"bound": "hbm", "kernel": "k_energy_rows3",
                                        "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS,
                                        "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4),
                                        "traffic": None, "bytes_per_launch": ebytes,
@@ -376,7 +375,7 @@ def c3_legs(S, X, idx, dist, k):
     # used when the kernel and shape match
     try:
         pe = json.load(open(os.path.join(ROOT, "bench_pmc_energy.json")))
-        if pe.get("rows") == n and pe.get("dim") == f and "k_energy_rows2" in pe.get("kernel", ""):
+        if pe.get("rows") == n and pe.get("dim") == f and "k_energy_rows3" in pe.get("kernel", ""):
             out["energy_rows"]["roofline"]["traffic"] = pe.get("hbm_bytes_per_launch")
             out["energy_rows"]["roofline"]["traffic_kernel"] = pe.get("kernel")
             out["energy_rows"]["roofline"]["traffic_source"] = pe.get("source")

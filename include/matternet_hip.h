@@ -126,7 +126,10 @@ typedef struct mn_knn_stats {
  * graphs are mn_knn_cos_columns_f32 / mn_knn_cos_bf16.  Output row i:
  * out_idx[i*k + r], out_dist[i*k + r] in (dist asc, idx asc) order —
  * bit-identical to the reference's sequential f32 fold and stable sort.
- * Slots beyond min(k, n-1): idx -1, dist +inf.  metric MN_L2SQ or MN_L2. */
+ * Slots beyond min(k, n-1): idx -1, dist +inf.  metric MN_L2SQ or MN_L2.
+ * 1 <= k <= 512: k <= 64 through the candidate generators (opts->algo); k > 64
+ * (the reference takes any k) through the exact split scan of every row
+ * (each 1024-row corpus part's best k, merged; d <= ~2300). */
 int mn_knn_f32(const float *X, int64_t n, int32_t d, const mn_knn_opts *opts,
                int32_t *out_idx, float *out_dist);
 

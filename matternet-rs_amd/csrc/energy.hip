@@ -945,7 +945,8 @@ __global__ __launch_bounds__(64 * E3<S64>::WAVES) void k_energy_rows3(
     const float *__restrict__ X, int64_t n, int f, int64_t na, int64_t naP, int64_t nb,
     int64_t nbP, const uint32_t *__restrict__ geij, const double *__restrict__ gev,
     const double *__restrict__ gdgm, double mA_g, int g_mode, int tau_mode, double tau_param,
-    int pct_rank, double *__restrict__ Eo, double *__restrict__ Go, double *__restrict__ Lo) {
+    int pct_rank, double *__restrict__ Eo, double *__restrict__ Go, double *__restrict__ Lo,
+    const int32_t *__restrict__ gperm) {
     extern __shared__ __attribute__((aligned(16))) unsigned char dsm[];
     constexpr int NW = E3<S64>::WAVES, XB = E3<S64>::XB;
     typedef typename std::conditional<S64, double2, float2>::type stage_t;
@@ -977,6 +978,14 @@ __global__ __launch_bounds__(64 * E3<S64>::WAVES) void k_energy_rows3(
     }
     for (int c = threadIdx.x; c < fpad; c += blockDim.x) sdg[c] = c < f ? gdgm[c] : 0.0;
     if (lane == 0) xs[fpad] = stage_t{0, 0};
+    // the stage slot of each of this lane's columns (gperm: the bank-balanced
+    // column order the conflict-free entry lists were built for)
+    int slot[NR];
+#pragma unroll
+    for (int r = 0; r < NR; ++r) {
+        const int c = lane + 64 * r;
+        slot[r] = (gperm && c < f) ? gperm[c] : c;
+    }
     __syncthreads();
     const unsigned char *xsb = (const unsigned char *)xs;
     const bool mean_tau = g_mode == MN_G_TAUMODE && tau_mode == MN_TAU_MEAN;
@@ -1011,8 +1020,8 @@ __global__ __launch_bounds__(64 * E3<S64>::WAVES) void k_energy_rows3(
             const int c = lane + 64 * r;
             if (c < f) {
                 const double x0 = (double)cur[0][r], x1 = (double)cur[1][r];
-                if constexpr (S64) xs[c] = make_double2(x0, x1);
-                else xs[c] = make_float2(cur[0][r], cur[1][r]);
+                if constexpr (S64) xs[slot[r]] = make_double2(x0, x1);
+                else xs[slot[r]] = make_float2(cur[0][r], cur[1][r]);
                 const double dgc = sdg[c];
                 const double q0 = x0 * x0, q1 = x1 * x1;
                 den[0] += q0;
@@ -1592,6 +1601,127 @@ __global__ __launch_bounds__(256) void k_energy_signals_finish(const double *__r
 
 }  // namespace energy
 
+// LDS-bank-conflict-free entry lists for the f32 stage of k_energy_rows3
+// (float2 per column: ds_read_b64 serves lanes 0-31 and 32-63 as two groups;
+// column slot s sits on bank pair s mod 32).  A group of 32 entries whose
+// x_i slots are distinct mod 32 and whose x_j slots are distinct mod 32
+// gathers conflict-free: a matching in the bipartite multigraph of (slot(i)
+// mod 32, slot(j) mod 32).  Edge-colouring it with max-degree colours
+// (Konig; alternating-path recolouring) gives the groups; the column order
+// (slot) is chosen first to balance both degree sides over the 32 classes.
+// Each list is padded to whole E2_CH chunks with zero-slot, zero-weight
+// entries (exact no-ops); the summation order changes (O(u) of the terms).
+struct ConflictFree {
+    std::vector<uint32_t> eij;  // (slot(i) | slot(j) << 16), list A then B
+    std::vector<double> ev;
+    std::vector<int32_t> perm;  // column -> stage slot
+    int64_t na = 0, nb = 0;     // padded lengths
+};
+static ConflictFree conflict_free_lists(const std::vector<uint32_t> &e, const std::vector<double> &v,
+                                        int64_t na, int f, int M, int chunk) {
+    ConflictFree out;
+    const int64_t ne = (int64_t)e.size();
+    const int fpad = (f + 3) & ~3;
+    // column order: columns by total degree, each to the class with the least
+    // max(side-i load, side-j load) that still has room
+    std::vector<int64_t> dgi(f, 0), dgj(f, 0);
+    for (int64_t q = 0; q < ne; ++q) {
+        dgi[e[q] & 0xFFFFu]++;
+        dgj[e[q] >> 16]++;
+    }
+    std::vector<int> cols(f);
+    for (int c = 0; c < f; ++c) cols[c] = c;
+    std::stable_sort(cols.begin(), cols.end(),
+                     [&](int a, int b) { return dgi[a] + dgj[a] > dgi[b] + dgj[b]; });
+    const int cap = (f + M - 1) / M;
+    std::vector<int64_t> li(M, 0), lj(M, 0);
+    std::vector<int> used(M, 0);
+    out.perm.assign(f, 0);
+    for (int c : cols) {
+        int best = -1;
+        int64_t bv = 0;
+        for (int k = 0; k < M; ++k) {
+            if (used[k] >= cap || k + M * used[k] >= fpad) continue;
+            const int64_t val = std::max(li[k] + dgi[c], lj[k] + dgj[c]);
+            if (best < 0 || val < bv) { best = k; bv = val; }
+        }
+        out.perm[c] = best + M * used[best];
+        used[best]++;
+        li[best] += dgi[c];
+        lj[best] += dgj[c];
+    }
+    const uint32_t zpair = (uint32_t)fpad | ((uint32_t)fpad << 16);
+    auto colour = [&](int64_t q0, int64_t q1) -> int64_t {
+        const int64_t m = q1 - q0;
+        if (m == 0) return 0;
+        std::vector<int> da(M, 0), db(M, 0);
+        std::vector<int> ea(m), eb(m);
+        for (int64_t q = 0; q < m; ++q) {
+            ea[q] = out.perm[e[q0 + q] & 0xFFFFu] % M;
+            eb[q] = out.perm[e[q0 + q] >> 16] % M;
+            da[ea[q]]++;
+            db[eb[q]]++;
+        }
+        int D = 0;
+        for (int k = 0; k < M; ++k) D = std::max(D, std::max(da[k], db[k]));
+        // at[side][vertex][colour] = edge or -1
+        std::vector<int> atA((size_t)M * D, -1), atB((size_t)M * D, -1), col(m, -1);
+        auto free_at = [&](std::vector<int> &at, int x) {
+            for (int c = 0; c < D; ++c)
+                if (at[(size_t)x * D + c] < 0) return c;
+            return -1;
+        };
+        for (int64_t q = 0; q < m; ++q) {
+            const int a = ea[q], b = eb[q];
+            const int ca = free_at(atA, a), cb = free_at(atB, b);
+            if (atB[(size_t)b * D + ca] >= 0) {
+                // flip the (ca, cb) alternating path from b: afterwards ca is
+                // free at b (the path cannot end at a in a bipartite graph)
+                std::vector<int> path;
+                int x = b;
+                bool sideB = true;
+                int c = ca;
+                for (;;) {
+                    const int ed = sideB ? atB[(size_t)x * D + c] : atA[(size_t)x * D + c];
+                    if (ed < 0) break;
+                    path.push_back(ed);
+                    x = sideB ? ea[ed] : eb[ed];
+                    sideB = !sideB;
+                    c = c == ca ? cb : ca;
+                }
+                for (int ed : path) {
+                    atA[(size_t)ea[ed] * D + col[ed]] = -1;
+                    atB[(size_t)eb[ed] * D + col[ed]] = -1;
+                }
+                for (int ed : path) {
+                    col[ed] = col[ed] == ca ? cb : ca;
+                    atA[(size_t)ea[ed] * D + col[ed]] = ed;
+                    atB[(size_t)eb[ed] * D + col[ed]] = ed;
+                }
+            }
+            col[q] = ca;
+            atA[(size_t)a * D + ca] = (int)q;
+            atB[(size_t)b * D + ca] = (int)q;
+        }
+        // groups of M slots: colour classes, zero entries in the gaps; whole chunks
+        const int64_t len = ((int64_t)D * M + chunk - 1) / chunk * chunk;
+        const size_t base = out.eij.size();
+        out.eij.resize(base + len, zpair);
+        out.ev.resize(base + len, 0.0);
+        std::vector<int> fill(D, 0);
+        for (int64_t q = 0; q < m; ++q) {
+            const size_t slotq = base + (size_t)col[q] * M + fill[col[q]]++;
+            const uint32_t ij = e[q0 + q];
+            out.eij[slotq] = (uint32_t)out.perm[ij & 0xFFFFu] | ((uint32_t)out.perm[ij >> 16] << 16);
+            out.ev[slotq] = v[q0 + q];
+        }
+        return len;
+    };
+    out.na = colour(0, na);
+    out.nb = colour(na, ne);
+    return out;
+}
+
 static thread_local mn_energy_stats t_energy_stats{};
 
 static int energy_impl(const mn_csr *L, const float *X, int64_t n, int32_t f,
@@ -1677,18 +1807,54 @@ static int energy_impl(const mn_csr *L, const float *X, int64_t n, int32_t f,
     MN_HIP_TRY(hipMemcpyAsync(off, ho.data(), 16 * (size_t)f, hipMemcpyHostToDevice, s));
     // K3 v3 (one pass over X, the list-A identity) for a symmetric L whose
     // lists fit its LDS plan; else k_row_tau + k_energy_rows2
-    const int64_t naP3 = (na + E2_CH - 1) / E2_CH * E2_CH;
-    const int64_t nbP3 = (ne - na + E2_CH - 1) / E2_CH * E2_CH;
-    // tuning build: MN_ENERGY_V3 = 0 the two-kernel path, 2 the float2 stage
-    // at 16 waves a block (A/B); default 1: the double2 stage at 8 waves
+    int64_t naP3 = (na + E2_CH - 1) / E2_CH * E2_CH;
+    int64_t nbP3 = (ne - na + E2_CH - 1) / E2_CH * E2_CH;
+    // default 2: the float2 stage at 16 waves a block (C3 median 2.31-2.48
+    // ms vs 2.84-2.92 for the double2 stage at 8 waves, fixed tau 1.42 vs
+    // 1.49: profiles/r04/r04_energy_ab.log).  Tuning build: MN_ENERGY_V3 = 0
+    // the two-kernel path, 1 the double2 stage, 3 the float2 stage with the
+    // host-ordered bank-conflict-free lists (slower: fixed 1.74 ms — the
+    // kernel is VALU-bound, 17 VALU a lane per entry pair, not LDS-bound)
     const char *v3e = knob("MN_ENERGY_V3");
-    const int v3k = (v3e && *v3e) ? atoi(v3e) : 1;
-    const bool s64 = v3k != 2;
+    const int v3k = (v3e && *v3e) ? atoi(v3e) : 2;
+    const bool s64 = v3k == 1;
     const bool v3 = split && sym && nr <= 16 && v3k != 0 &&
                     e3_lds_bytes(naP3 + nbP3, f, s64 ? E3<true>::WAVES : E3<false>::WAVES,
                                  s64 ? E3<true>::XB : E3<false>::XB) <= LDS_BUDGET;
     hipLaunchKernelGGL(k_fill_entries, dim3(fb), dim3(256), 0, s, L->indptr, L->indices, vals, f,
                        sym, opts->g_mode, split, off, eij, ev, dg, v3 ? 1 : 0);
+    // v3k 3: the f32 stage with LDS-bank-conflict-free entry lists (host
+    // order, conflict_free_lists) in a bank-balanced column order
+    const int32_t *perm3 = nullptr;
+    const uint32_t *eij3 = eij;
+    const double *ev3 = ev;
+    int64_t naO = na, nbO = ne - na;
+    if (v3 && v3k == 3) {
+        std::vector<uint32_t> he((size_t)ne);
+        std::vector<double> hv((size_t)ne);
+        if (ne > 0) {
+            MN_HIP_TRY(hipMemcpyAsync(he.data(), eij, 4 * (size_t)ne, hipMemcpyDeviceToHost, s));
+            MN_HIP_TRY(hipMemcpyAsync(hv.data(), ev, 8 * (size_t)ne, hipMemcpyDeviceToHost, s));
+            MN_HIP_TRY(hipStreamSynchronize(s));
+        }
+        ConflictFree cf = conflict_free_lists(he, hv, na, f, 32, E2_CH);
+        const size_t nbytes = cf.eij.size() * 12 + (size_t)f * 4 + 256;
+        char *cb = (char *)scratch(kSlotGeneric1, nbytes);
+        MN_REQUIRE(cb, MN_ENOMEM, "mn_energy_rows: list scratch allocation failed");
+        double *dv = (double *)cb;
+        uint32_t *de = (uint32_t *)(cb + cf.eij.size() * 8);
+        int32_t *dp = (int32_t *)(cb + ((cf.eij.size() * 12 + 15) & ~(size_t)15));
+        MN_HIP_TRY(hipMemcpyAsync(dv, cf.ev.data(), 8 * cf.ev.size(), hipMemcpyHostToDevice, s));
+        MN_HIP_TRY(hipMemcpyAsync(de, cf.eij.data(), 4 * cf.eij.size(), hipMemcpyHostToDevice, s));
+        MN_HIP_TRY(hipMemcpyAsync(dp, cf.perm.data(), 4 * (size_t)f, hipMemcpyHostToDevice, s));
+        if (e3_lds_bytes(cf.na + cf.nb, f, E3<false>::WAVES, E3<false>::XB) <= LDS_BUDGET) {
+            perm3 = dp;
+            eij3 = de;
+            ev3 = dv;
+            naO = naP3 = cf.na;
+            nbO = nbP3 = cf.nb;
+        }
+    }
     int pct_rank = 0;
     if (opts->tau_mode == MN_TAU_PERCENTILE) {
         double pp = opts->tau_param;
@@ -1714,8 +1880,9 @@ static int energy_impl(const mn_csr *L, const float *X, int64_t n, int32_t f,
         MN_HIP_TRY(hipFuncSetAttribute((const void *)k_energy_rows3<NRV, S6>,                   \
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)sh3));  \
         hipLaunchKernelGGL((k_energy_rows3<NRV, S6>), dim3((unsigned)blocks3), dim3(64 * nw3),  \
-                           sh3, s, X, n, f, na, naP3, ne - na, nbP3, eij, ev, dg, mA_g,         \
-                           opts->g_mode, opts->tau_mode, opts->tau_param, pct_rank, E, G, lam); \
+                           sh3, s, X, n, f, naO, naP3, nbO, nbP3, eij3, ev3, dg, mA_g,          \
+                           opts->g_mode, opts->tau_mode, opts->tau_param, pct_rank, E, G, lam,  \
+                           perm3);                                                              \
     } while (0)
 #define MN_E3S(NRV) do { if (s64) MN_E3(NRV, true); else MN_E3(NRV, false); } while (0)
         if (nr <= 4) MN_E3S(4);

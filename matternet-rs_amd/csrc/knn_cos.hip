@@ -404,6 +404,18 @@ __global__ void k_extra_pairs(const int32_t *__restrict__ cand, const double *__
     }
 }
 
+__global__ void k_all_cand(int f, int32_t *__restrict__ cand) {
+    const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= (int64_t)f * f) return;
+    const int i = (int)(q / f), j = (int)(q % f);
+    cand[q] = i == j ? INT_MAX : j;
+}
+
+__global__ void k_iota32(int32_t *__restrict__ v, int n) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) v[i] = i;
+}
+
 __global__ void k_fill_f64(double *__restrict__ p, int64_t n, double v) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) p[i] = v;
@@ -503,15 +515,36 @@ __global__ __launch_bounds__(256) void k_fb_finish(const int32_t *__restrict__ f
     }
     wave_bitonic_sort<NR>(d, ix);
     const int keff = min(topk, f - 1);
-    const double wv = weight_of(d[0], sigma, p);
-    const bool keep = lane < keff && d[0] <= eps && wv > 1e-12;
-    const uint64_t km = __ballot(keep);
-    const int nkeep = __popcll(~km) == 0 ? 64 : (int)__builtin_ctzll(~km);
-    if (lane < topk) {
-        const bool k2 = lane < nkeep;
-        out_idx[(int64_t)i * topk + lane] = k2 ? ix[0] : -1;
-        out_dist[(int64_t)i * topk + lane] = k2 ? d[0] : __builtin_inf();
-        if (out_w) out_w[(int64_t)i * topk + lane] = k2 ? wv : 0.0;
+    // the filter is monotone in dist: a prefix of the sorted list survives
+    // (element e = lane + 64 r); topk may exceed 64 here (every register)
+    int nkeep = 0;
+    bool open = true;
+#pragma unroll
+    for (int r = 0; r < NR; ++r) {
+        const int e = lane + 64 * r;
+        const double wv = weight_of(d[r], sigma, p);
+        const bool keep = e < keff && d[r] <= eps && wv > 1e-12;
+        const uint64_t km = __ballot(keep);
+        if (open) {
+            const int run = __popcll(~km) == 0 ? 64 : (int)__builtin_ctzll(~km);
+            nkeep += run;
+            open = run == 64;
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < NR; ++r) {
+        const int e = lane + 64 * r;
+        if (e < topk) {
+            const bool k2 = e < nkeep;
+            out_idx[(int64_t)i * topk + e] = k2 ? ix[r] : -1;
+            out_dist[(int64_t)i * topk + e] = k2 ? d[r] : __builtin_inf();
+            if (out_w) out_w[(int64_t)i * topk + e] = k2 ? weight_of(d[r], sigma, p) : 0.0;
+        }
+    }
+    for (int e = 64 * NR + lane; e < topk; e += 64) {  // topk beyond the f - 1 nodes
+        out_idx[(int64_t)i * topk + e] = -1;
+        out_dist[(int64_t)i * topk + e] = __builtin_inf();
+        if (out_w) out_w[(int64_t)i * topk + e] = 0.0;
     }
 }
 
@@ -558,7 +591,10 @@ static int knn_cos_columns_impl(const T *X, int64_t n, int32_t f, const mn_cos_o
     MN_REQUIRE(o && X && out_idx && out_dist, MN_EINVAL, "mn_knn_cos_columns: NULL argument");
     MN_REQUIRE(n >= 1 && f >= 2 && f <= FMAXC, MN_EINVAL,
                "mn_knn_cos_columns_f32: need n >= 1 and 2 <= f <= %d", FMAXC);
-    MN_REQUIRE(o->topk >= 1 && o->topk <= 64, MN_ENOTSUP, "mn_knn_cos_columns_f32: topk in [1,64]");
+    MN_REQUIRE(o->topk >= 1, MN_EINVAL, "mn_knn_cos_columns_f32: topk >= 1");
+    // topk > 64 (graph.rs topk is any usize): every node through the exact
+    // all-pairs path (k_fb_finish writes any topk <= f - 1, padding beyond)
+    const bool all_exact = o->topk > 64;
     MN_REQUIRE(o->sigma > 0.0, MN_EINVAL, "mn_knn_cos_columns_f32: sigma must be > 0");
     const int margin = o->margin > 0 ? o->margin : 16;
     const int L = std::min(std::min(o->topk + margin, LMAXC), f - 1);
@@ -598,39 +634,47 @@ static int knn_cos_columns_impl(const T *X, int64_t n, int32_t f, const mn_cos_o
     MN_HIP_TRY(stream_wait(side, s));
     hipLaunchKernelGGL(k_col_norms<T>, dim3((unsigned)((f + 3) / 4)), dim3(64), 0, side, XT, n, f, nrm);
     MN_KCHECK(side, "k_col_norms");
-    hipLaunchKernelGGL(k_gram_f64<T>, dim3((unsigned)(ntri * nchunk)), dim3(256), 0, s, X, n, f, ntile,
-                       kchunk, nchunk, G);
-    MN_HIP_TRY(hipGetLastError());
-    MN_HIP_TRY(stream_wait(s, side));
-    tm.mark();
     const int nr = (f + 63) / 64;
-#define MN_SEL(NRV) hipLaunchKernelGGL(k_cos_select<NRV>, dim3(grid(f, 4)), dim3(256), 0, s, G, nrm, f, L, cand, capx, gnext)
-    if (nr <= 1) MN_SEL(1); else if (nr <= 2) MN_SEL(2); else if (nr <= 4) MN_SEL(4);
-    else if (nr <= 8) MN_SEL(8); else if (nr <= 16) MN_SEL(16); else if (nr <= 32) MN_SEL(32);
-    else MN_SEL(64);
-#undef MN_SEL
-    // exact distances: the first kq candidates of every node, then the ones
-    // whose lower bound can still reach the top k (the rest stay +inf)
-    // |d~ - d| bound: f64 accumulation of n products (f64 inputs: each product
-    // rounded once more), norms and the quotient, with a factor-2 margin
-    const double delta = 2.0 * ((double)n + (sizeof(T) == 8 ? 17.0 : 16.0)) * 0x1p-53 + 1e-300;
-    const int kq = std::min(o->topk, L);
-    const int fkq = f * kq;
-    hipLaunchKernelGGL(k_fill_f64, dim3(grid((int64_t)f * L)), dim3(256), 0, s, cdist,
-                       (int64_t)f * L, __builtin_inf());
-    // one pass over one list: [first kq of every node | near ties], the
-    // count of the latter appended on the device (flags[1])
-    hipLaunchKernelGGL(k_first_pairs, dim3(grid((int64_t)f * kq)), dim3(256), 0, s, f, L, kq, pi);
-    MN_HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)(flags + 1), fkq, 1, s));
-    if (L > kq)
-        hipLaunchKernelGGL(k_extra_pairs, dim3(grid(f)), dim3(256), 0, s, cand, capx, f, L, kq,
-                           delta, pi, flags + 1);
-    hipLaunchKernelGGL(k_cos_exact_wave<T>, dim3(grid((int64_t)f * L, 16)), dim3(256), 0, s, XT, n, pi,
-                       flags + 1, (int64_t)f * L, cand, L, nrm, cdist);
-    hipLaunchKernelGGL(k_cos_finish, dim3(grid(f, 4)), dim3(256), 0, s, cand, cdist, gnext, f, L,
-                       o->topk, o->eps, o->sigma, o->p, delta, out_idx, out_dist, out_w, flags,
-                       fb_list);
-    MN_HIP_TRY(hipGetLastError());
+    if (all_exact) {
+        MN_HIP_TRY(stream_wait(s, side));
+        tm.mark();
+        hipLaunchKernelGGL(k_iota32, dim3(grid(f)), dim3(256), 0, s, fb_list, f);
+        MN_HIP_TRY(hipMemcpyAsync(flags, &f, 4, hipMemcpyHostToDevice, s));
+        MN_HIP_TRY(hipGetLastError());
+    } else {
+        hipLaunchKernelGGL(k_gram_f64<T>, dim3((unsigned)(ntri * nchunk)), dim3(256), 0, s, X, n, f, ntile,
+                           kchunk, nchunk, G);
+        MN_HIP_TRY(hipGetLastError());
+        MN_HIP_TRY(stream_wait(s, side));
+        tm.mark();
+    #define MN_SEL(NRV) hipLaunchKernelGGL(k_cos_select<NRV>, dim3(grid(f, 4)), dim3(256), 0, s, G, nrm, f, L, cand, capx, gnext)
+        if (nr <= 1) MN_SEL(1); else if (nr <= 2) MN_SEL(2); else if (nr <= 4) MN_SEL(4);
+        else if (nr <= 8) MN_SEL(8); else if (nr <= 16) MN_SEL(16); else if (nr <= 32) MN_SEL(32);
+        else MN_SEL(64);
+    #undef MN_SEL
+        // exact distances: the first kq candidates of every node, then the ones
+        // whose lower bound can still reach the top k (the rest stay +inf)
+        // |d~ - d| bound: f64 accumulation of n products (f64 inputs: each product
+        // rounded once more), norms and the quotient, with a factor-2 margin
+        const double delta = 2.0 * ((double)n + (sizeof(T) == 8 ? 17.0 : 16.0)) * 0x1p-53 + 1e-300;
+        const int kq = std::min(o->topk, L);
+        const int fkq = f * kq;
+        hipLaunchKernelGGL(k_fill_f64, dim3(grid((int64_t)f * L)), dim3(256), 0, s, cdist,
+                           (int64_t)f * L, __builtin_inf());
+        // one pass over one list: [first kq of every node | near ties], the
+        // count of the latter appended on the device (flags[1])
+        hipLaunchKernelGGL(k_first_pairs, dim3(grid((int64_t)f * kq)), dim3(256), 0, s, f, L, kq, pi);
+        MN_HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)(flags + 1), fkq, 1, s));
+        if (L > kq)
+            hipLaunchKernelGGL(k_extra_pairs, dim3(grid(f)), dim3(256), 0, s, cand, capx, f, L, kq,
+                               delta, pi, flags + 1);
+        hipLaunchKernelGGL(k_cos_exact_wave<T>, dim3(grid((int64_t)f * L, 16)), dim3(256), 0, s, XT, n, pi,
+                           flags + 1, (int64_t)f * L, cand, L, nrm, cdist);
+        hipLaunchKernelGGL(k_cos_finish, dim3(grid(f, 4)), dim3(256), 0, s, cand, cdist, gnext, f, L,
+                           o->topk, o->eps, o->sigma, o->p, delta, out_idx, out_dist, out_w, flags,
+                           fb_list);
+        MN_HIP_TRY(hipGetLastError());
+    }
     tm.mark();
     int nfb = 0;
     MN_HIP_TRY(hipMemcpyAsync(&nfb, flags, 4, hipMemcpyDeviceToHost, s));
@@ -642,8 +686,17 @@ static int knn_cos_columns_impl(const T *X, int64_t n, int32_t f, const mn_cos_o
         MN_HIP_TRY(hipMalloc(&fpi, 4 * np));
         MN_HIP_TRY(hipMalloc(&fpj, 4 * np));
         MN_HIP_TRY(hipMalloc(&fd, 8 * np));
-        hipLaunchKernelGGL(k_fb_pairs, dim3(grid(np)), dim3(256), 0, s, fb_list, flags, f, fpi, fpj);
-        hipLaunchKernelGGL(k_cos_exact<T>, dim3(grid(np)), dim3(256), 0, s, XT, n, fpi, fpj, np, nrm, fd);
+        if (all_exact) {
+            // every ordered pair: the wave form (four ordered LDS chains a wave),
+            // node i = slot / f (fb_list is the identity here), cand = j or
+            // INT_MAX on the diagonal
+            hipLaunchKernelGGL(k_all_cand, dim3(grid(np)), dim3(256), 0, s, f, fpj);
+            hipLaunchKernelGGL(k_cos_exact_wave<T>, dim3(grid(np, 16)), dim3(256), 0, s, XT, n,
+                               (const int32_t *)nullptr, (const int *)nullptr, np, fpj, f, nrm, fd);
+        } else {
+            hipLaunchKernelGGL(k_fb_pairs, dim3(grid(np)), dim3(256), 0, s, fb_list, flags, f, fpi, fpj);
+            hipLaunchKernelGGL(k_cos_exact<T>, dim3(grid(np)), dim3(256), 0, s, XT, n, fpi, fpj, np, nrm, fd);
+        }
 #define MN_FB(NRV) hipLaunchKernelGGL(k_fb_finish<NRV>, dim3(grid(nfb, 4)), dim3(256), 0, s, fb_list, flags, fd, f, o->topk, o->eps, o->sigma, o->p, out_idx, out_dist, out_w)
         if (nr <= 1) MN_FB(1); else if (nr <= 2) MN_FB(2); else if (nr <= 4) MN_FB(4);
         else if (nr <= 8) MN_FB(8); else if (nr <= 16) MN_FB(16); else if (nr <= 32) MN_FB(32);

@@ -62,6 +62,7 @@ constexpr int QCAP = 48;            // LDS candidate queue per query
 constexpr int QPRE = QCAP - 16;     // merge before a column tile if cnt > QPRE
 constexpr int LMAX = 128 - QCAP;    // L + QCAP <= 128 (two elements per lane)
 constexpr int KMAX = 64;            // k limit of the C ABI
+constexpr int KBIG = 512;           // k limit of the exact split-scan path (k > KMAX)
 constexpr int KLIST = KMAX + 8;     // internal list limit (MN_L2's extended L2^2 list;
                                     // the fallback keeps it per thread in LDS)
 constexpr int FB_THREADS = 128;
@@ -1206,6 +1207,15 @@ __global__ __launch_bounds__(256) void k_sym_pos(int64_t n, const int *__restric
     scP[p] = (float)s;
 }
 
+__global__ __launch_bounds__(256) void k_fill_empty(int32_t *__restrict__ idx, float *__restrict__ dist,
+                                                    int64_t n) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) {
+        idx[i] = -1;
+        dist[i] = __builtin_inff();
+    }
+}
+
 __global__ __launch_bounds__(256) void k_iota(int *__restrict__ v, int64_t n) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) v[i] = (int)i;
@@ -1744,7 +1754,7 @@ static int fb_split_scan(const float *Q, const float *C, int64_t nc, int d, int6
                          hipStream_t s) {
     const int keff_max = k;
     const size_t ldsmax = 160 * 1024;
-    if (nc < 1 || k > KLIST || d < 1 ||
+    if (nc < 1 || k > KBIG || d < 1 ||
         (size_t)d * FSQ * 4 + (size_t)FSQ * FSC * 4 + (size_t)FSC * 8 + 16 > ldsmax)
         return 1;
     static bool attr = false;  // dynamic LDS beyond 64 KB (once per process)
@@ -2976,13 +2986,39 @@ static int knn_f32_impl(const float *Q, int64_t nq, const float *C, int64_t nc, 
     MN_REQUIRE(opts->metric == MN_L2SQ || opts->metric == MN_L2, MN_ENOTSUP,
                "mn_knn_f32: metric %d not supported here", opts->metric);
     const int k = opts->k;
-    MN_REQUIRE(k >= 1 && k <= KMAX, MN_ENOTSUP, "mn_knn: k=%d outside [1,%d]", k, KMAX);
+    MN_REQUIRE(k >= 1 && k <= KBIG, MN_ENOTSUP, "mn_knn: k=%d outside [1,%d]", k, KBIG);
     const int algo = opts->algo;
     MN_REQUIRE(algo >= MN_KNN_AUTO && algo <= MN_KNN_BF16X1, MN_EINVAL, "mn_knn: bad algo %d",
                algo);
     MN_REQUIRE(q_off >= 0 && c_off >= 0 && q_off + nq <= INT_MAX && c_off + nc <= INT_MAX,
                MN_EINVAL, "mn_knn: global ids must fit int32");
     t_stats.n_queries = nq;
+    if (k > KMAX) {
+        // k beyond the candidate generators' lists (mst.rs:317 takes any k):
+        // every row through the exact split scan — every corpus part's best k
+        // by the reference fold (rooted for MN_L2), merged by (dist, id)
+        t_stats.algo = MN_KNN_F32;
+        if (nq == 0) return MN_OK;
+        hipStream_t s = (hipStream_t)opts->stream;
+        int *rows = (int *)scratch(kSlotFallback, sizeof(int) * (size_t)nq + 64);
+        MN_REQUIRE(rows, MN_ENOMEM, "mn_knn: row list allocation failed");
+        hipLaunchKernelGGL(k_iota, dim3((unsigned)((nq + 255) / 256)), dim3(256), 0, s, rows, nq);
+        MN_KCHECK(s, "k_iota");
+        const int excl = opts->exclude_self ? 1 : 0;
+        const int rc = nc > 0 ? fb_split_scan(Q, C, nc, d, q_off, c_off, excl, k, rows, (int)nq,
+                                              nullptr, opts->metric == MN_L2, out_idx, out_dist, s)
+                              : 1;
+        if (rc < 0) return rc;
+        if (rc == 1) {
+            MN_REQUIRE(nc == 0, MN_ENOTSUP, "mn_knn: k=%d > %d needs d <= %d", k, KMAX,
+                       (int)((160 * 1024 - FSQ * FSC * 4 - FSC * 8 - 16) / (FSQ * 4)));
+            hipLaunchKernelGGL(k_fill_empty, dim3((unsigned)((nq * k + 255) / 256)), dim3(256), 0, s,
+                               out_idx, out_dist, nq * (int64_t)k);
+            MN_KCHECK(s, "k_fill_empty");
+        }
+        MN_HIP_TRY(hipStreamSynchronize(s));
+        return MN_OK;
+    }
     // MN_L2: the L2^2 graph k2 = k + 8 long, then k_l2_order (root order)
     const bool l2 = opts->metric == MN_L2 && nq > 0;
     const int k2 = l2 ? k + 8 : k;  // <= KLIST

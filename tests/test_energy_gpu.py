@@ -330,3 +330,23 @@ def test_v3_single_pass_matches_two_kernel_path(gm, tau, monkeypatch):
     for a, b, r in ((E3, E2, rE), (G3, G2, rG), (l3, l2, rl)):
         np.testing.assert_allclose(a, b, rtol=RTOL, atol=ATOL)
         np.testing.assert_allclose(a, r, rtol=RTOL, atol=ATOL)
+
+
+@pytest.mark.parametrize("v3", ["2", "3"])
+@pytest.mark.parametrize("tau", ["median", "fixed"])
+def test_v3_stage_variants_match_oracle(v3, tau, monkeypatch):
+    """The f32-stage single pass (MN_ENERGY_V3=2) and the same kernel with the
+    host-ordered, LDS-bank-conflict-free entry lists in a bank-balanced column
+    order (MN_ENERGY_V3=3, conflict_free_lists) against the oracle at 1e-9."""
+    import surfface_hip as S
+    ip, ix, iv = feature_laplacian()
+    X = datagen.uniform(3001, 768, seed=47)
+    X[7] = 0.0
+    tm = {"median": (S.TauMode.Median, O.TAU_MEDIAN, 0.0),
+          "fixed": (S.TauMode.Fixed(0.2), O.TAU_FIXED, 0.2)}[tau]
+    monkeypatch.setenv("MN_ENERGY_V3", v3)
+    with S._lib.use_tuning():
+        E3, G3, l3 = run(X, ip, ix, iv, 0, tm[0])
+    rE, rG, rl = O.energy_rows(X, ip, ix, iv, 0, tm[1], tm[2])
+    for a, r in ((E3, rE), (G3, rG), (l3, rl)):
+        np.testing.assert_allclose(a, r, rtol=RTOL, atol=ATOL)

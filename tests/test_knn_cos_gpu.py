@@ -67,3 +67,17 @@ def test_long_profiles_sampled_nodes():
     ri, rd, rw = ref_cols(X, 4, q=(100, 108))
     exact((i[100:108], d[100:108], w[100:108]), (ri, rd, rw))
     assert st["n_uncertified"] == 0
+
+
+@pytest.mark.parametrize("topk", [65, 150, 300])
+def test_feature_graph_topk_beyond_64(topk):
+    """graph.rs topk is any usize: topk > 64 takes the exact all-pairs path
+    (every node's f - 1 exact distances, sorted, filtered, padded past f - 1)
+    — bit-exact vs the oracle, including topk > f - 1 (300 > 199)."""
+    X = datagen.clustered(3000, 200, seed=9, blobs=7)
+    kw = dict(eps=0.95, sigma=0.5, p=2.7)
+    i, d, w, st = hip_cols(X, topk, **kw)
+    ri, rd, rw = ref_cols(X, topk, **kw)
+    np.testing.assert_array_equal(i, ri)
+    np.testing.assert_array_equal(d.view(np.uint64), rd.view(np.uint64))
+    np.testing.assert_array_equal(w.view(np.uint64), rw.view(np.uint64))

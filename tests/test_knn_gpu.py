@@ -438,3 +438,22 @@ def test_euclidean_k64_extended_list(algo_e):
     ridx, rdist = _euclid_rows_np(X, rows, k)
     np.testing.assert_array_equal(r.idx.cpu().numpy()[rows], ridx)
     np.testing.assert_array_equal(r.dist.cpu().numpy()[rows].view(np.uint32), rdist.view(np.uint32))
+
+
+@pytest.mark.parametrize("k", [100, 512])
+def test_large_k_exact_split_scan(k):
+    """k beyond the generators' 64 (mst.rs:317 takes any k): every row through
+    the exact split scan — bit-exact vs the oracle, self excluded, and the
+    MN_L2 root order for k = 100 (ties of equal roots by index)."""
+    import surfface_hip as S
+    X = datagen.clustered(20000, 48, seed=31, blobs=12, dup_frac=0.01, zero_frac=0.002)
+    r = S.knn_l2sq(torch.from_numpy(X).cuda(), k)
+    ridx, rdist = O.knn_l2sq(X, k)
+    np.testing.assert_array_equal(r.idx.cpu().numpy(), ridx)
+    np.testing.assert_array_equal(r.dist.cpu().numpy().view(np.uint32), rdist.view(np.uint32))
+    if k == 100:
+        Xs = X[:3000].copy()
+        r = S.knn_l2sq(torch.from_numpy(Xs).cuda(), 100, euclidean=True)
+        ridx, rdist = oracle_euclidean(Xs, 100)
+        np.testing.assert_array_equal(r.idx.cpu().numpy(), ridx)
+        np.testing.assert_array_equal(r.dist.cpu().numpy().view(np.uint32), rdist.view(np.uint32))
