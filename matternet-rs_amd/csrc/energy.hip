@@ -32,6 +32,7 @@
 #include <algorithm>
 #include <climits>
 #include <cmath>
+#include <cstdio>
 #include <cstdlib>
 #include <type_traits>
 #include <vector>
@@ -60,10 +61,22 @@ struct Vals {
 // The block finds the row of its first entry once (upper_bound on indptr);
 // each thread gallops forward from there to its own row, then binary-searches
 // the transposed entry (j, i) in row j.
+// Symmetry check (round 4: the upper entries only).  Every stored entry
+// (i, j > i) must find a stored (j, i) with the same value (binary search of
+// row j), and the stored upper and lower entry counts must be equal
+// (ucount[0] += #upper - #lower per block): the matches map the upper
+// entries into the lower ones injectively, so equal counts make it a
+// bijection — the same verdict as searching every off-diagonal entry, and a
+// stricter one for duplicated entries (an (i, j) stored twice against one
+// (j, i) is asymmetric here, as the symmetric lists' multiplicity 2 would
+// double-count it).  Half the searches of the round-3 check.
+// asym bit 1: asymmetric; bit 2: a column index out of range.
 __global__ __launch_bounds__(256) void k_check_sym(const int64_t *__restrict__ ip,
                                                    const int32_t *__restrict__ ix, Vals v, int f,
-                                                   int64_t nnz, int *__restrict__ asym) {
+                                                   int64_t nnz, int *__restrict__ asym,
+                                                   unsigned long long *__restrict__ ucount) {
     __shared__ int64_t r0s;
+    __shared__ int bal[4];
     const int64_t p0 = (int64_t)blockIdx.x * blockDim.x;
     if (threadIdx.x == 0) {
         int64_t lo = 0, hi = f;  // last row r with ip[r] <= p0
@@ -75,26 +88,42 @@ __global__ __launch_bounds__(256) void k_check_sym(const int64_t *__restrict__ i
     }
     __syncthreads();
     const int64_t p = p0 + threadIdx.x;
-    if (p >= nnz) return;
-    // row i: the r >= r0 with ip[r] <= p < ip[r + 1] (gallop, then bisect)
-    int64_t lo = r0s, step = 1, hi = lo;
-    while (hi < f && ip[hi + 1] <= p) { lo = hi + 1; hi = min<int64_t>(hi + step, f - 1); step <<= 1; }
-    while (lo < hi) {
-        const int64_t mid = (lo + hi) >> 1;
-        if (ip[mid + 1] <= p) lo = mid + 1; else hi = mid;
+    int d = 0;  // +1 upper, -1 lower
+    if (p < nnz) {
+        // row i: the r >= r0 with ip[r] <= p < ip[r + 1] (gallop, then bisect)
+        int64_t lo = r0s, step = 1, hi = lo;
+        while (hi < f && ip[hi + 1] <= p) { lo = hi + 1; hi = min<int64_t>(hi + step, f - 1); step <<= 1; }
+        while (lo < hi) {
+            const int64_t mid = (lo + hi) >> 1;
+            if (ip[mid + 1] <= p) lo = mid + 1; else hi = mid;
+        }
+        const int i = (int)lo;
+        const int j = ix[p];
+        if (j < 0 || j >= f) {
+            atomicOr(asym, 2);
+        } else if (j < i) {
+            d = -1;
+        } else if (j > i) {
+            d = 1;
+            int64_t a = ip[j], b = ip[j + 1] - 1, hit = -1;
+            while (a <= b) {
+                const int64_t mid = (a + b) >> 1;
+                const int c = ix[mid];
+                if (c == i) { hit = mid; break; }
+                if (c < i) a = mid + 1; else b = mid - 1;
+            }
+            if (hit < 0 || v[hit] != v[p]) atomicOr(asym, 1);
+        }
     }
-    const int i = (int)lo;
-    const int j = ix[p];
-    if (j < 0 || j >= f) { atomicOr(asym, 2); return; }
-    if (j == i) return;
-    int64_t a = ip[j], b = ip[j + 1] - 1, hit = -1;
-    while (a <= b) {
-        const int64_t mid = (a + b) >> 1;
-        const int c = ix[mid];
-        if (c == i) { hit = mid; break; }
-        if (c < i) a = mid + 1; else b = mid - 1;
+    // the block's upper - lower balance: one atomic per block
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) d += __shfl_xor(d, o);
+    if ((threadIdx.x & 63) == 0) bal[threadIdx.x >> 6] = d;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const int tb = bal[0] + bal[1] + bal[2] + bal[3];
+        if (tb != 0) atomicAdd(ucount, (unsigned long long)(long long)tb);
     }
-    if (hit < 0 || v[hit] != v[p]) atomicOr(asym, 1);
 }
 
 // Every stored CSR entry (i, j, v) the reduction needs goes to one list,
@@ -1465,6 +1494,117 @@ __global__ __launch_bounds__(512) void k_diffuse_rows(
     }
 }
 
+// Round 4: the same folds with L's entries interleaved on the host by groups
+// of DF_G sweeps — slot ((base_G + t) DF_G + u) 64 + l holds entry t of the
+// feature row lane l folds in sweep DF_G G + u (rows by length; rows shorter
+// than the group's longest padded with (0, f): the zero slot x[f], an exact
+// no-op, as a fold from +0.0 never holds -0.0) — so a wave's value / column
+// reads are contiguous (conflict-free) and DF_G independent folds advance per
+// step with their loads in flight together (no branch between them).
+template <bool XF64, int DF_G, int DF_T>
+__global__ __launch_bounds__(512) void k_diffuse_rows2(
+    const void *__restrict__ Xin, int64_t n, int f, const double *__restrict__ giv,
+    const int32_t *__restrict__ gic, int64_t S, const int32_t *__restrict__ gsw,
+    const int32_t *__restrict__ gperm, double eta, int steps, int matvec,
+    double *__restrict__ Xout) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char dsm[];
+    const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int nw = blockDim.x >> 6;
+    const int nsw = (f + 63) / 64;
+    // LDS: [val f64 x S | col i32 x S] | x [waves][2][f + 1] f64 (slot f = 0)
+    double *iv = (double *)dsm;
+    int32_t *ic = (int32_t *)(dsm + (size_t)S * 8);
+    const size_t lb = (((size_t)S * 12) + 15) & ~(size_t)15;
+    double *xb = (double *)(dsm + lb) + (size_t)w * 2 * (f + 1);
+    for (int64_t q = threadIdx.x; q < S; q += blockDim.x) {
+        iv[q] = giv[q];
+        ic[q] = gic[q];
+    }
+    __syncthreads();
+    constexpr int MAXG = (DF_SW + DF_G - 1) / DF_G;
+    int si[DF_SW], sb[MAXG], sl[MAXG];
+#pragma unroll
+    for (int g = 0; g < DF_SW; ++g) si[g] = gperm[min(lane + 64 * g, f - 1)];
+    const int ngr = (nsw + DF_G - 1) / DF_G;
+#pragma unroll
+    for (int G = 0; G < MAXG; ++G) {
+        sb[G] = G < ngr ? gsw[2 * G] : 0;
+        sl[G] = G < ngr ? gsw[2 * G + 1] : 0;
+    }
+    if (lane == 0) {
+        xb[f] = 0.0;
+        xb[f + 1 + f] = 0.0;
+    }
+    // f32 rows: the next row's values are loaded during this row's steps
+    float nxt[DF_SW];
+    auto load_row = [&](int64_t r) {
+        const __amdgpu_buffer_rsrc_t rs = row_rsrc((const float *)Xin + min(r, n - 1) * f, f);
+#pragma unroll
+        for (int q = 0; q < DF_SW; ++q) nxt[q] = row_at(rs, lane + 64 * q);
+    };
+    const int64_t rstride = (int64_t)gridDim.x * nw;
+    if (!XF64) load_row((int64_t)blockIdx.x * nw + w);
+    for (int64_t row = (int64_t)blockIdx.x * nw + w; row < n; row += rstride) {
+        double *x = xb, *y = xb + (f + 1);
+        if (!XF64) {
+#pragma unroll
+            for (int r = 0; r < DF_SW; ++r)
+                if (lane + 64 * r < f) x[lane + 64 * r] = (double)nxt[r];
+            if (row + rstride < n) load_row(row + rstride);
+        } else {
+            for (int i = lane; i < f; i += 64) x[i] = ((const double *)Xin)[row * f + i];
+        }
+        __builtin_amdgcn_wave_barrier();
+        const int ns = matvec ? 1 : steps;
+        for (int st = 0; st < ns; ++st) {
+            // groups of DF_G sweeps advance together, padded to the group's
+            // longest row: DF_G independent folds per step, their loads issued
+            // ahead with no branch in the way (each fold keeps its order)
+#pragma unroll
+            for (int G = 0; G < MAXG; ++G) {
+                if (G >= ngr) break;
+                const int base = __builtin_amdgcn_readfirstlane(sb[G]);
+                const int len = __builtin_amdgcn_readfirstlane(sl[G]);
+                double sum[DF_G];
+#pragma unroll
+                for (int u = 0; u < DF_G; ++u) sum[u] = 0.0;
+                const double *pv = iv + (size_t)base * (DF_G * 64) + lane;
+                const int32_t *pc = ic + (size_t)base * (DF_G * 64) + lane;
+                // DF_T entries of each fold per iteration (len is a multiple)
+                for (int t = 0; t < len; t += DF_T) {
+                    int c[DF_T][DF_G];
+                    double v[DF_T][DF_G], xv[DF_T][DF_G];
+#pragma unroll
+                    for (int e = 0; e < DF_T; ++e)
+#pragma unroll
+                        for (int u = 0; u < DF_G; ++u) {
+                            c[e][u] = pc[((t + e) * DF_G + u) * 64];
+                            v[e][u] = pv[((t + e) * DF_G + u) * 64];
+                        }
+#pragma unroll
+                    for (int e = 0; e < DF_T; ++e)
+#pragma unroll
+                        for (int u = 0; u < DF_G; ++u) xv[e][u] = x[c[e][u]];
+#pragma unroll
+                    for (int e = 0; e < DF_T; ++e)
+#pragma unroll
+                        for (int u = 0; u < DF_G; ++u) sum[u] = sum[u] + v[e][u] * xv[e][u];
+                }
+#pragma unroll
+                for (int u = 0; u < DF_G; ++u) {
+                    const int g = DF_G * G + u;
+                    if (g < DF_SW && g < nsw && lane + 64 * g < f)
+                        y[si[g < DF_SW ? g : 0]] = matvec ? sum[u] : x[si[g < DF_SW ? g : 0]] - eta * sum[u];
+                }
+            }
+            __builtin_amdgcn_wave_barrier();
+            double *t = x; x = y; y = t;
+        }
+        for (int i = lane; i < f; i += 64) Xout[row * f + i] = x[i];
+        __builtin_amdgcn_wave_barrier();
+    }
+}
+
 // ---- item-graph orientation: energy of the F feature signals (length n) ----
 // node_energy_and_dispersion(X^T, L_items) (energymaps.rs:923-1045 with the
 // n x n item Laplacian; SURVEY §8(d) orientation (ii)): per signal s_f =
@@ -1767,16 +1907,17 @@ static int energy_impl(const mn_csr *L, const float *X, int64_t n, int32_t f,
 
     Timer tm;
     tm.start(opts->timing != 0, s);
-    MN_HIP_TRY(hipMemsetAsync(flag, 0, 8, s));
+    MN_HIP_TRY(hipMemsetAsync(flag, 0, 16, s));
+    unsigned long long *ubal = (unsigned long long *)(flag + 2);
     const unsigned fb = (unsigned)((f + 255) / 256);
     if (L->nnz > 0)
         hipLaunchKernelGGL(k_check_sym, dim3((unsigned)((L->nnz + 255) / 256)), dim3(256), 0, s,
-                           L->indptr, L->indices, vals, f, L->nnz, flag);
-    int hflag = 0;
-    MN_HIP_TRY(hipMemcpyAsync(&hflag, flag, 4, hipMemcpyDeviceToHost, s));
+                           L->indptr, L->indices, vals, f, L->nnz, flag, ubal);
+    int hflag[4] = {0, 0, 0, 0};
+    MN_HIP_TRY(hipMemcpyAsync(hflag, flag, 16, hipMemcpyDeviceToHost, s));
     MN_HIP_TRY(hipStreamSynchronize(s));
-    MN_REQUIRE(!(hflag & 2), MN_EINVAL, "mn_energy_rows: Laplacian column index out of range");
-    const int sym = (hflag & 1) ? 0 : 1;
+    MN_REQUIRE(!(hflag[0] & 2), MN_EINVAL, "mn_energy_rows: Laplacian column index out of range");
+    const int sym = ((hflag[0] & 1) || hflag[2] != 0 || hflag[3] != 0) ? 0 : 1;
     // k_energy_rows2 (default for f <= 1024; MN_ENERGY_V1=1: the round-2
     // kernels) takes the diagonal apart from the entry lists
     const char *v1e = knob("MN_ENERGY_V1");
@@ -2054,12 +2195,14 @@ static int energy_signals_impl(const mn_csr *L, const float *X, int64_t n, int32
     const int64_t nbu = (n + rpb - 1) / rpb;
     double *part = (double *)scratch(kSlotGeneric0, sizeof(double) * (size_t)nbu * 4 * f + 64);
     MN_REQUIRE(flag && part, MN_ENOMEM, "mn_energy_signals: scratch allocation failed");
-    MN_HIP_TRY(hipMemsetAsync(flag, 0, 8, s));
+    MN_HIP_TRY(hipMemsetAsync(flag, 0, 16, s));
     if (L->nnz > 0)
         hipLaunchKernelGGL(k_check_sym, dim3((unsigned)((L->nnz + 255) / 256)), dim3(256), 0, s,
-                           L->indptr, L->indices, Vals{L->values, 0}, (int)n, L->nnz, flag);
-    int hflag = 0;
-    MN_HIP_TRY(hipMemcpyAsync(&hflag, flag, 4, hipMemcpyDeviceToHost, s));
+                           L->indptr, L->indices, Vals{L->values, 0}, (int)n, L->nnz, flag,
+                           (unsigned long long *)(flag + 2));
+    int hflag4[4] = {0, 0, 0, 0};
+    MN_HIP_TRY(hipMemcpyAsync(hflag4, flag, 16, hipMemcpyDeviceToHost, s));
+    const int hflag = hflag4[0] | ((hflag4[2] != 0 || hflag4[3] != 0) ? 1 : 0);
     MN_HIP_TRY(hipStreamSynchronize(s));
     MN_REQUIRE(!(hflag & 2), MN_EINVAL, "mn_energy_signals: Laplacian column index out of range");
     const int sym = (hflag & 1) ? 0 : 1;
@@ -2109,6 +2252,89 @@ static int diffuse_impl(const mn_csr *L, const void *X, int32_t x_is_f64, int64_
     int32_t *perm = (int32_t *)scratch(kSlotGeneric2, (size_t)f * 4 + 64);
     MN_REQUIRE(perm, MN_ENOMEM, "mn_diffuse_rows: scratch allocation failed");
     MN_HIP_TRY(hipMemcpyAsync(perm, hperm.data(), 4 * (size_t)f, hipMemcpyHostToDevice, s));
+    // round 4 fast path (f <= 1024): L interleaved by sweep (k_diffuse_rows2)
+    {
+        const int nsw = (f + 63) / 64;
+        // sweeps per group: all of them for f <= 768 (12 independent folds a
+        // step), else 4; tuning build: MN_DIFFUSE_G in {2, 4, 6, 12}
+        // folds per group DF_G x entries per iteration DF_T at C3 (4 steps):
+        // (2, 1) 9.5 ms, (2, 2) 10.0, (4, 1) 10.1, (4, 2) 10.5, (2, 4) 11.2,
+        // (6, 1) 11.3, (1, 2) 11.7, (1, 4) 12.9, (12, 1) 15.4; the round-3
+        // kernel 14.8 (profiles/r04/r04_diffusion_ab.log) — padding to the
+        // group's longest row outweighs more independent folds; tuning build:
+        // MN_DIFFUSE_GT = "G,T" with G in {1, 2, 4}, T in {1, 2, 4}
+        const char *dge = knob("MN_DIFFUSE_GT");
+        int DF_G = 2, DF_T = 1;
+        if (dge && *dge) sscanf(dge, "%d,%d", &DF_G, &DF_T);
+        if (DF_G != 1 && DF_G != 2 && DF_G != 4) DF_G = 2;
+        if (DF_T != 1 && DF_T != 2 && DF_T != 4) DF_T = 1;
+        const int ngr = (nsw + DF_G - 1) / DF_G;
+        std::vector<int32_t> sw(2 * (size_t)ngr);
+        int64_t S = 0;  // in steps of DF_G x 64 slots
+        for (int G = 0; G < ngr; ++G) {
+            int64_t mx = 0;
+            for (int q = 64 * DF_G * G; q < std::min(f, 64 * DF_G * (G + 1)); ++q) {
+                const int i = hperm[q];
+                mx = std::max<int64_t>(mx, hip_[i + 1] - hip_[i]);
+            }
+            mx = (mx + DF_T - 1) / DF_T * DF_T;
+            sw[2 * G] = (int32_t)S;
+            sw[2 * G + 1] = (int32_t)mx;
+            S += mx;
+        }
+        S *= DF_G;  // in steps of 64 slots
+        const size_t lb2 = ((size_t)S * 64 * 12 + 15) & ~(size_t)15;
+        const size_t pw2 = (size_t)2 * (f + 1) * 8;
+        const char *dfe = knob("MN_DIFFUSE_V1");  // tuning build: 1 = the round-3 kernel (A/B)
+        if (f <= 64 * DF_SW && lb2 + pw2 <= LDS_BUDGET && S * 64 < INT_MAX && !(dfe && *dfe == '1')) {
+            std::vector<int32_t> hix((size_t)nnz);
+            std::vector<double> hv((size_t)nnz);
+            if (nnz > 0) {
+                MN_HIP_TRY(hipMemcpyAsync(hix.data(), L->indices, 4 * (size_t)nnz, hipMemcpyDeviceToHost, s));
+                MN_HIP_TRY(hipMemcpyAsync(hv.data(), L->values, 8 * (size_t)nnz, hipMemcpyDeviceToHost, s));
+                MN_HIP_TRY(hipStreamSynchronize(s));
+            }
+            const size_t slots = (size_t)S * 64;
+            std::vector<double> iv(slots, 0.0);
+            std::vector<int32_t> ic(slots, f);  // pads: the zero slot
+            for (int g = 0; g < nsw; ++g)
+                for (int l = 0; l < 64 && 64 * g + l < f; ++l) {
+                    const int i = hperm[64 * g + l];
+                    const int G = g / DF_G, u = g % DF_G;
+                    for (int64_t p = hip_[i]; p < hip_[i + 1]; ++p) {
+                        const size_t q = ((size_t)(sw[2 * G] + (p - hip_[i])) * DF_G + u) * 64 + l;
+                        const int c = hix[p];
+                        MN_REQUIRE(c >= 0 && c < f, MN_EINVAL, "mn_diffuse_rows: column index out of range");
+                        iv[q] = hv[p];
+                        ic[q] = c;
+                    }
+                }
+            char *gb = (char *)scratch(kSlotGeneric3, slots * 12 + sw.size() * 4 + 256);
+            MN_REQUIRE(gb, MN_ENOMEM, "mn_diffuse_rows: scratch allocation failed");
+            double *div = (double *)gb;
+            int32_t *dic = (int32_t *)(gb + slots * 8);
+            int32_t *dsw = (int32_t *)(gb + ((slots * 12 + 15) & ~(size_t)15));
+            MN_HIP_TRY(hipMemcpyAsync(div, iv.data(), slots * 8, hipMemcpyHostToDevice, s));
+            MN_HIP_TRY(hipMemcpyAsync(dic, ic.data(), slots * 4, hipMemcpyHostToDevice, s));
+            MN_HIP_TRY(hipMemcpyAsync(dsw, sw.data(), sw.size() * 4, hipMemcpyHostToDevice, s));
+            const int nw2 = (int)std::min<size_t>(8, (LDS_BUDGET - lb2) / pw2);
+            const size_t sh2 = lb2 + (size_t)nw2 * pw2;
+            const int64_t blocks2 = std::min<int64_t>((n + nw2 - 1) / nw2, 2048);
+            auto kf = x_is_f64 ? k_diffuse_rows2<true, 2, 1> : k_diffuse_rows2<false, 2, 1>;
+#define MN_DFK(G, T) \
+    if (DF_G == G && DF_T == T) kf = x_is_f64 ? k_diffuse_rows2<true, G, T> : k_diffuse_rows2<false, G, T>
+            MN_DFK(1, 1); MN_DFK(1, 2); MN_DFK(1, 4); MN_DFK(2, 2); MN_DFK(2, 4);
+            MN_DFK(4, 1); MN_DFK(4, 2); MN_DFK(4, 4);
+#undef MN_DFK
+            MN_HIP_TRY(hipFuncSetAttribute((const void *)kf, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                           (int)sh2));
+            hipLaunchKernelGGL(kf, dim3((unsigned)blocks2), dim3(64 * nw2), sh2, s, X, n, f, div, dic,
+                               (int64_t)slots, dsw, perm, eta, steps, matvec, out);
+            MN_KCHECK(s, "k_diffuse_rows2");
+            MN_HIP_TRY(hipStreamSynchronize(s));
+            return MN_OK;
+        }
+    }
     const size_t lbytes = ((size_t)nnz * 12 + (size_t)(2 * f + 1) * 4 + 15) & ~(size_t)15;
     const size_t per_wave = (size_t)2 * f * 8;
     const int l_in_lds = lbytes + per_wave <= LDS_BUDGET ? 1 : 0;
