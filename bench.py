@@ -55,6 +55,8 @@ def parse():
                     help="target CPU time of the sampled cpu_baseline leg (0 = skip)")
     ap.add_argument("--no-c5", dest="c5", action="store_false",
                     help="skip the configs[4] leg (1M x 3072 bf16 cosine item graph + SF-GRASS)")
+    ap.add_argument("--no-c4-sim", dest="c4_sim", action="store_false",
+                    help="skip the configs[3] leg at N=1 (8M x 768 as 8 simulated ranks)")
     ap.add_argument("--c5-rows", type=int, default=1_048_576)
     ap.add_argument("--c5-dim", type=int, default=3072)
     ap.add_argument("--c5-parity-rows", type=int, default=3,
@@ -115,13 +117,18 @@ def main():
             gram_ms.append(r.stats.get("ms_sweep") or r.stats["ms_gram"])
             last["stats"] = r.stats
             return r.idx, r.dist, r.stats
-        # the C entry: all-gather of the shards, exact per-shard top-k of every
-        # query in query chunks, list exchange, merge (csrc/shard.hip)
+        # the C entry (csrc/shard.hip): all-gather of the shards, then the
+        # symmetric form (this rank's share of the node-wide SW_SYM tile table,
+        # partial re-rank, exchange, merge + certify; ms_sweep = the share), or
+        # the per-shard form (query chunks; the last chunk's stats x chunks)
         idx, dd = knn_sharded_capi(X, k, comm, query_chunk=a.query_chunk, timing=True,
                                    stream=stream)
-        st = S.knn.last_stats()  # the last query chunk's generator stats
-        chunks = (n_tot + a.query_chunk - 1) // a.query_chunk
-        gram_ms.append((st.get("ms_sweep") or st["ms_gram"]) * chunks)
+        st = S.knn.last_stats()
+        if st.get("sweep_slices") == -1:
+            gram_ms.append(st.get("ms_sweep") or st["ms_gram"])
+        else:
+            chunks = (n_tot + a.query_chunk - 1) // a.query_chunk
+            gram_ms.append((st.get("ms_sweep") or st["ms_gram"]) * chunks)
         last["stats"] = st
         return idx, dd, st
 
@@ -185,8 +192,10 @@ def main():
             kname = "k_gram_sweep2<SW_SYM>"
             kfull = "k_gram_sweep2<0, 2, true, true>"
         flops_launch = 2.0 * nq * nc_sw * d
-        nbk = (n_loc + 255) // 256
-        flops_exec = 2.0 * 256 * 256 * d * nbk * (nbk + 1) / 2 if sym else flops_launch
+        # executed: the upper-triangle 256 x 256 tiles of the n_tot rows, a
+        # rank's 1/world share of them (the sharded symmetric form)
+        nbk = (n_tot + 255) // 256
+        flops_exec = 2.0 * 256 * 256 * d * nbk * (nbk + 1) / 2 / world if sym else flops_launch
         achieved = flops_launch / (gms * 1e-3) / 1e12
         ms_all = float(st0["ms_gram"])
         roof = {"bound": "mfma", "kernel": kname, "achieved": round(achieved, 3),
@@ -258,6 +267,10 @@ def main():
     if a.c5 and world == 1:
         c5 = c5_leg(S, _lib, L, a, dev, stream)
 
+    c4 = None
+    if a.c4_sim and world == 1:
+        c4 = c4_sim_leg(S, _lib, L, a, dev, stream)
+
     cpu = None
     parity = None
     energy_cpu = None
@@ -291,9 +304,10 @@ def main():
                        "n_rows": n_tot, "dim": d, "k": k, "rows_per_gpu": n_loc,
                        "metric_space": "squared L2 (reference sequential f32 fold)",
                        "parallelism": ("single GPU (no collective)" if world == 1 else
-                                       f"corpus row-shard x{world} (mn_knn_sharded_f32): RCCL "
-                                       "all-gather of queries, exact per-shard top-k, grouped "
-                                       "send/recv of the lists + merge")},
+                                       f"row-shard x{world} (mn_knn_sharded_f32): RCCL "
+                                       "all-gather of the shards and thresholds, each rank's "
+                                       "share of the node-wide symmetric tile table, grouped "
+                                       "send/recv of the partial lists, merge + certify")},
             "roofline": roof,
             "cpu_baseline": cpu,
             "parity_sample": parity,
@@ -301,6 +315,7 @@ def main():
             "energy": energy,
             "c3_legs": c3,
             "c5_leg": c5,
+            "c4_sim_leg": c4,
             "knn_stats": {kk: (round(v, 3) if isinstance(v, float) else v)
                           for kk, v in st.items()},
         }
@@ -424,6 +439,56 @@ def c3_legs(S, X, idx, dist, k):
         "GB_per_s": round(n * f * 4 * ((nq + 31) // 32) / ms / 1e6, 1)}
     ms, _ = _timed(lambda: S.search_lambda_aware_hybrid(X, lam_n, Qs, lq, 32, 0.7))
     out["lambda_aware_search"]["hybrid_ms"] = round(ms, 3)
+    return out
+
+
+def c4_sim_leg(S, _lib, L, a, dev, stream, R=8):
+    """BASELINE.json configs[3] on ONE GPU: 8M x 768 (8 ranks x the per-GPU
+    rows) through mn_knn_sharded_sim_f32 — every rank's stages of the symmetric
+    sharded build run in turn on this device (the exchange a strided read), so
+    a rank's share of the real 8-GPU build = its stage A + B + C time here,
+    plus the all-gathers (X: 7/8 of 24.6 GB a rank over xGMI; tau0 / norms
+    64 MB) and the list exchange (2 GB), which the simulation does not run.
+    One row per shard checked bit-exact against the oracle over all rows."""
+    from oracle import oracle as O
+    from surfface_hip.dist import knn_sharded_sim
+    n_loc, d, k = a.rows_per_gpu, a.dim, a.k
+    n_tot = R * n_loc
+    Xall = torch.empty((n_tot, d), dtype=torch.float32, device=dev)
+    for r0 in range(0, n_tot, n_loc):  # each rank's shard: the same counter stream
+        _lib.check(L.mn_fill_uniform_f32(Xall[r0:r0 + n_loc].data_ptr(), n_loc, d, a.seed, r0,
+                                         stream.cuda_stream))
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    idx, dist, ms, st = knn_sharded_sim(Xall, k, R, timing=True, stream=stream)
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    share = ms.sum(axis=1)
+    mx = float(share.max()) / 1e3
+    out = {"workload": f"C4: {n_tot} x {d} f32 exact kNN k={k}, {R} ranks simulated on one GPU "
+                       "(mn_knn_sharded_sim_f32)",
+           "rank_share_s": [round(float(x) / 1e3, 3) for x in share],
+           "max_share_s": round(mx, 3),
+           "stage_ms_max": {"A_thresholds": round(float(ms[:, 0].max()), 1),
+                            "B_sweep_share": round(float(ms[:, 1].max()), 1),
+                            "C_merge_certify": round(float(ms[:, 2].max()), 1)},
+           "pairs_per_s_at_max_share": n_tot * float(n_tot) / mx,
+           "excluded": "RCCL all-gathers (X 21.5 GB received a rank, thresholds) and the "
+                       "partial-list exchange (2 GB): not run by the simulation",
+           "n_uncertified": st["n_uncertified"], "n_candidates": st["n_candidates"],
+           "sim_wall_s": round(wall, 2)}
+    if a.c5_parity_rows > 0:
+        rng = np.random.default_rng(11)
+        q = np.array([r * n_loc + int(rng.integers(n_loc)) for r in range(R)], np.int64)
+        Ch = Xall.cpu().numpy()
+        ri, rd = O.knn_l2sq_qc(Ch[q], q, Ch, 0, k, nthreads=cpu_threads())
+        gi = idx[torch.from_numpy(q).to(dev)].cpu().numpy()
+        gd = dist[torch.from_numpy(q).to(dev)].cpu().numpy()
+        out["parity_sample"] = {"rows": q.tolist(), "bit_exact": bool(
+            np.array_equal(gi, ri) and np.array_equal(gd.view(np.uint32), rd.view(np.uint32)))}
+        del Ch
+    del Xall, idx, dist
+    torch.cuda.empty_cache()
     return out
 
 
@@ -584,7 +649,16 @@ def cpu_baseline(X, idx, dd, k, target_s):
                         "sample": f"rows 0..{fr - 1} x {n} (mode 0: all n-1 distances collected "
                                   f"and sorted per row), {fel:.1f}s",
                         "rows_bit_exact": f_ok},
-           "host": host_info()}
+           "host": host_info(),
+           "cores_note": ("the box allots this job OMP_NUM_THREADS=16 of the host's hardware "
+                          "threads (one GPU's share; the affinity mask lists the whole machine, "
+                          "which the other GPUs' jobs share), so the baseline runs 16 threads; "
+                          "full_host_upper_bound scales it linearly to the affinity count "
+                          "(an extrapolation, not a measurement)")}
+    aff = cpu["host"].get("affinity_cpus")
+    if aff and aff > threads:
+        cpu["full_host_upper_bound"] = {"value": cpu["value"] * aff / threads, "cores": aff,
+                                        "basis": "linear scaling of the measured value"}
     parity = {"rows_checked": m, "rows_bit_exact": ok, "plus_calibration_rows": threads,
               "calibration_bit_exact": bool(np.array_equal(i0, idx.cpu().numpy()[cal]))}
     return cpu, parity

@@ -839,11 +839,17 @@ __global__ __launch_bounds__(ANT) void k_lap_bscatter(const int32_t *__restrict_
 // record) and are gathered only for the kept entries, so a bucket is 8 B per
 // entry of LDS and two buckets share a CU.  Entry index e < BR k: forward
 // slot e of the bucket; else reverse record e0 + e - BR k.
-constexpr int BT = 512;        // threads per bucket block
+constexpr int BT = 1024;       // threads per bucket block (16 waves, 4 rows each)
 constexpr int BKEYS = 8192;    // LDS-staged entries per bucket
 
+// Round 4: the weights sit in LDS beside the keys (key payload = the stage
+// position, wt[position]), so a row's sort / dedupe / fold never waits on a
+// global gather (round 3 re-read the forward slot or the reverse record per
+// kept entry: k_lap_bucket was latency-bound, SQ wait_any 0.55-0.79); 128 KB
+// a bucket, one 16-wave block per CU.
 struct alignas(16) BucketSmem {
     uint64_t key[BKEYS];
+    double w[BKEYS];
     int rlen[BR];
     int roff[BR + 1];
     int rfill[BR];
@@ -851,27 +857,11 @@ struct alignas(16) BucketSmem {
     int big[BR];
 };
 
-__device__ __forceinline__ double bucket_w(uint32_t e, int64_t row0, int k, int64_t e0,
-                                           const int32_t *__restrict__ nbr,
-                                           const void *__restrict__ val, int val_f64, int64_t n,
-                                           const Params &P, const int4 *__restrict__ rec) {
-    if (e < (uint32_t)(BR * k)) {
-        const int64_t i = row0 + e / k, sl = row0 * k + e;
-        int32_t j;
-        double w;
-        bool bd;
-        slot_edge(nbr, val, val_f64, n, i, sl, P, j, w, bd);
-        return w;
-    }
-    const int4 rc = rec[e0 + (e - (uint32_t)(BR * k))];
-    return __longlong_as_double(((long long)rc.w << 32) | (long long)(unsigned)rc.z);
-}
-
 // one block per bucket of BR rows; offs (the rows' segment starts, int64) is
 // written here: segment = k forward slots + the reverse entries, bucket
 // regions in bucket order.  Kept entries go to the segment starts (the
 // layout k_write_csr reads).
-__global__ __launch_bounds__(BT) __attribute__((amdgpu_waves_per_eu(4))) void k_lap_bucket(
+__global__ __launch_bounds__(BT) void k_lap_bucket(
     const int32_t *__restrict__ nbr, const void *__restrict__ val, int val_f64, int64_t n, int k,
     Params P, const int64_t *__restrict__ bstart, const int4 *__restrict__ rec,
     int64_t *__restrict__ offs, int32_t *__restrict__ col, double *__restrict__ wt,
@@ -917,7 +907,8 @@ __global__ __launch_bounds__(BT) __attribute__((amdgpu_waves_per_eu(4))) void k_
         const bool ok = slot_edge(nbr, val, val_f64, n, i, sl, P, j, w, bd);
         const int p = sm.roff[r] + q;
         if (staged) {
-            sm.key[p] = ok ? (((uint64_t)(uint32_t)j << 32) | (uint32_t)e) : SENT;
+            sm.key[p] = ok ? (((uint64_t)(uint32_t)j << 32) | (uint32_t)p) : SENT;
+            sm.w[p] = w;
         } else {
             col[gbase + p] = ok ? j : EMPTY;
             wt[gbase + p] = w;
@@ -927,7 +918,8 @@ __global__ __launch_bounds__(BT) __attribute__((amdgpu_waves_per_eu(4))) void k_
         const int4 rc = rec[e];
         const int p = sm.roff[rc.y] + k + atomicAdd(&sm.rfill[rc.y], 1);
         if (staged) {
-            sm.key[p] = ((uint64_t)(uint32_t)rc.x << 32) | (uint32_t)(BR * k + (e - e0));
+            sm.key[p] = ((uint64_t)(uint32_t)rc.x << 32) | (uint32_t)p;
+            sm.w[p] = __longlong_as_double(((long long)rc.w << 32) | (long long)(unsigned)rc.z);
         } else {
             col[gbase + p] = rc.x;
             wt[gbase + p] = __longlong_as_double(((long long)rc.w << 32) |
@@ -940,9 +932,7 @@ __global__ __launch_bounds__(BT) __attribute__((amdgpu_waves_per_eu(4))) void k_
         for (int e = lane; e < mr; e += 64) {
             const uint64_t x = sm.key[o + e];
             col[gbase + o + e] = x == SENT ? EMPTY : (int)(x >> 32);
-            wt[gbase + o + e] = x == SENT ? 0.0
-                                          : bucket_w((uint32_t)x, row0, k, e0, nbr, val, val_f64,
-                                                     n, P, rec);
+            wt[gbase + o + e] = x == SENT ? 0.0 : sm.w[(uint32_t)x];
         }
     };
     for (int r = wv; r < nr; r += BT / 64) {
@@ -956,9 +946,7 @@ __global__ __launch_bounds__(BT) __attribute__((amdgpu_waves_per_eu(4))) void k_
             continue;
         }
         auto keyf = [&](int e) { return sm.key[o + e]; };
-        auto wf = [&](uint32_t e) {
-            return bucket_w(e, row0, k, e0, nbr, val, val_f64, n, P, rec);
-        };
+        auto wf = [&](uint32_t e) { return sm.w[e]; };
         const int rc = packed_row_any<4>(keyf, wf, mr, i, gbase + o, P.sym, col, wt, uniq, kept,
                                          deg64, deg32);
         if (rc != 1) {  // longer rows / duplicate ids: the wave kernel <16> from global
