@@ -24,10 +24,10 @@ def pick(prefix):
     return max(c, key=lambda k: ks[k]["total_ms"]) if c else None
 
 
-# the energy pass is two kernels since round 3 (k_row_tau: Median tau, then
-# k_energy_rows2): their bytes per call are summed
+# the energy pass is one kernel since round 4 (k_energy_rows3: the tau select
+# inline, X streamed once); a list of prefixes is summed per call
 for fname, prefixes, extra in (("bench_pmc_gram.json", ("k_gram_sweep2<0, 2, true",), {"rows_per_gpu": n}),
-                               ("bench_pmc_energy.json", ("k_row_tau", "k_energy_rows2"), {"rows": n})):
+                               ("bench_pmc_energy.json", ("k_energy_rows3",), {"rows": n})):
     kk = [pick(p) for p in prefixes]
     if not all(kk) or any("fetch_bytes" not in ks[k] or "write_bytes" not in ks[k] for k in kk):
         print("no PMC data for", prefixes)
