@@ -2113,6 +2113,174 @@ static int knn_f32_core(const float *Q, int64_t nq, const float *C, int64_t nc, 
 // Host driver of MN_KNN_BF16X1 (section 2c).  Returns 1 (nothing written)
 // when some row is too large for the single-bf16 bound: the caller then runs
 // the split generator.
+// ---- phase 1 as a sweep (round 4) -------------------------------------------
+// The list generator (k_gram_bf16<GM_L2H>, ~0.2 of the MFMA peak: 130 ms at
+// C2) keeps a sorted list per row while it scans the sample.  Here: (a) the
+// list generator on a pre-sample (the first m0 / P1_DIV sample positions, list
+// P1_L0) gives each row a threshold T0 = its P1_L0-th best key there; (b) the
+// query-major sweep (k_gram_sweep2<SW_L2>, tile-major copies) buffers every
+// sample pair with key < T0 (expected ~P1_DIV P1_L0 a row); (c) k_p1_select
+// takes each row's L1-th smallest buffered key = the sample's L1-th best key,
+// the list generator's threshold (an overflowing buffer gives a larger key:
+// still a threshold; correctness rests on the certificate); (d) rows with fewer
+// than L1 buffered keys (T0 below the sample's L1-th key) run the list
+// generator on their own.  btau1 [nq] (one slice) as before.  C2 (same box,
+// profiles/r04/r04_p1_ab.log): 130.7 -> 97.1 ms (pre 23.3, sweep 64.5, select
+// 0.8, 48.8k rows to (d)); (4, 16) 104.8 ms, (6, 16) 103.7, (6, 24) 108.9 —
+// fewer buffered keys beat a cheaper pre-sample; outputs identical.
+constexpr int P1_L0 = 4, P1_DIV = 8;
+
+// one wave per row: the L1-th smallest of the row's buffered keys (repeated
+// minimum with multiplicities: exact, <= L1 rounds); fewer than L1 keys: the
+// row is listed for (d)
+template <int NR>
+__global__ __launch_bounds__(256) void k_p1_select(int64_t nq, const int *__restrict__ cnt,
+                                                   const uint2 *__restrict__ buf, int cap, int L1,
+                                                   float *__restrict__ btau, int *__restrict__ fb_count,
+                                                   int *__restrict__ fb_list) {
+    const int lane = threadIdx.x & 63;
+    const int64_t q = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    if (q >= nq) return;
+    int c = cnt[q];
+    c = (c < 0 || c > cap) ? cap : c;  // -1: overflow, the buffer is full
+    if (c < L1) {
+        if (lane == 0) {
+            btau[q] = __builtin_inff();
+            fb_list[atomicAdd(fb_count, 1)] = (int)q;
+        }
+        return;
+    }
+    float kk[NR];
+#pragma unroll
+    for (int r = 0; r < NR; ++r) {
+        const int e = lane + 64 * r;
+        kk[r] = e < c ? __uint_as_float(buf[q * (int64_t)cap + e].x) : __builtin_inff();
+    }
+    float t = -__builtin_inff(), res = __builtin_inff();
+    int need = L1;
+    for (int it = 0; it < L1; ++it) {
+        float m = __builtin_inff();
+#pragma unroll
+        for (int r = 0; r < NR; ++r) m = fminf(m, kk[r] > t ? kk[r] : __builtin_inff());
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) m = fminf(m, __shfl_xor(m, o));
+        int eq = 0;
+#pragma unroll
+        for (int r = 0; r < NR; ++r) eq += (int)__popcll(__ballot(kk[r] == m));
+        if (eq >= need) { res = m; break; }
+        need -= eq;
+        t = m;
+    }
+    if (lane == 0) btau[q] = res;
+}
+
+__global__ __launch_bounds__(256) void k_gather_bf16_rows(const uint16_t *__restrict__ R, int dp,
+                                                          const float *__restrict__ qn,
+                                                          const int *__restrict__ rows, int nfb,
+                                                          uint16_t *__restrict__ out,
+                                                          float *__restrict__ qn_out) {
+    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e < (int64_t)nfb * dp) {
+        const int64_t i = e / dp;
+        out[e] = R[(int64_t)rows[i] * dp + (e - i * dp)];
+    }
+    if (e < nfb) qn_out[e] = qn[rows[e]];
+}
+
+__global__ __launch_bounds__(256) void k_scatter_tau(const int *__restrict__ rows, int nfb,
+                                                     const float *__restrict__ v,
+                                                     float *__restrict__ out) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < nfb) out[rows[i]] = v[i];
+}
+
+static int sweep_phase1(const uint16_t *QR, const uint16_t *QK, int64_t nq, const uint16_t *CR,
+                        const uint16_t *CKs, int64_t m0, int d, int dp, int nkb, int pst1,
+                        int64_t q_off, int L1, const float *qn, const float *qhn, const float *qrn,
+                        const float *cnv, const float *chc, const unsigned *cmax, float *tq,
+                        float *tau0, float *dlt, float *btau1, int *fb_list, int *cntr,
+                        hipStream_t s) {
+    using namespace knn;
+    Timer tdb;  // tuning build, MN_X1_DEBUG: the steps' times
+    tdb.start(knob("MN_X1_DEBUG") != nullptr, s);
+    // (a) the pre-sample: the list generator, list P1_L0, over the first m00
+    const char *l0e = knob("MN_P1_L0"), *dve = knob("MN_P1_DIV");  // tuning build: experiments
+    const int L0 = (l0e && *l0e) ? std::min(std::max(atoi(l0e), 2), 32) : P1_L0;
+    const int dv = (dve && *dve) ? std::max(2, atoi(dve)) : P1_DIV;
+    int64_t m00 = std::max<int64_t>(m0 / dv, (int64_t)64 * L0);
+    m00 = std::min<int64_t>(m0, (m00 + 255) / 256 * 256);
+    const kb16::GramPlan p0 = kb16::plan_gram(nq, m00, L0, 1, 1);
+    // (phase-2 / escalation slots: the caller's phase-1 list slots stay valid
+    // for the query-major fallback)
+    uint2 *cb0 = (uint2 *)scratch(kSlotX1Esc, (size_t)nq * p0.S * p0.cap * sizeof(uint2) + 64);
+    int *bc0 = (int *)scratch(kSlotX1Meta2, (size_t)nq * p0.S * 4 + 64);
+    MN_REQUIRE(cb0 && bc0, MN_ENOMEM, "mn_knn: pre-sample buffer allocation failed");
+    const int64_t bq = (nq + kb16::BM - 1) / kb16::BM;
+    hipLaunchKernelGGL((kb16::k_gram_bf16<kb16::GM_L2H, 0>), dim3((unsigned)(bq * p0.S)),
+                       dim3(kb16::NT), 0, s, QR, nq, CR, m00, dp, q_off, (int64_t)0, 0, qn, cnv,
+                       L0, (int)p0.S, p0.chunk, p0.cap, cb0, bc0, btau1);
+    MN_KCHECK(s, "k_gram_bf16<L2H, pre-sample>");
+    hipLaunchKernelGGL(k_tau_x1, dim3((unsigned)((nq + 255) / 256)), dim3(256), 0, s, nq,
+                       (int)p0.S, btau1, qn, qhn, qrn, cmax, d, dp, tq, tau0, dlt,
+                       (unsigned *)nullptr);
+    MN_KCHECK(s, "k_tau_x1<pre-sample>");
+    tdb.mark();
+    // (b) the sweep of the sample with T0
+    const double expect = (double)L0 * (double)m0 / (double)m00;
+    const int cap = std::min(512, std::max(64, (int)((2.5 * expect + 64.0 + 15.0) / 16.0) * 16));
+    uint2 *cbuf = (uint2 *)scratch(kSlotX1Buf2, (size_t)nq * cap * sizeof(uint2) + 64);
+    int *cnt = (int *)scratch(kSlotX1Meta2, (size_t)nq * 4 + 64);
+    MN_REQUIRE(cbuf && cnt, MN_ENOMEM, "mn_knn: phase-1 sweep buffer allocation failed");
+    MN_HIP_TRY(hipMemsetAsync(cnt, 0, (size_t)nq * 4, s));
+    const int64_t nqb = (nq + ksw2::BQ - 1) / ksw2::BQ;
+    MN_REQUIRE(nqb < INT_MAX && nq * 32 < INT_MAX, MN_ENOTSUP, "mn_knn: phase-1 sweep grid too large");
+    hipLaunchKernelGGL((ksw2::k_gram_sweep2<0, ksw2::SW_L2, true>), dim3((unsigned)nqb),
+                       dim3(ksw2::NT), 0, s, QK, nq, CKs, m0, nkb, q_off, (int64_t)0, 0, tq, tau0, chc,
+                       (int64_t)0, 1, m0, cap, cbuf, cnt, pst1, ksw2::SymArgs{});
+    MN_KCHECK(s, "k_gram_sweep2<SW_L2, phase 1>");
+    tdb.mark();
+    // (c) the L1-th smallest buffered key per row
+    MN_HIP_TRY(hipMemsetAsync(cntr, 0, 4, s));
+    const unsigned g4 = (unsigned)((nq + 3) / 4);
+    if (cap <= 128)
+        hipLaunchKernelGGL(k_p1_select<2>, dim3(g4), dim3(256), 0, s, nq, cnt, cbuf, cap, L1, btau1, cntr, fb_list);
+    else if (cap <= 256)
+        hipLaunchKernelGGL(k_p1_select<4>, dim3(g4), dim3(256), 0, s, nq, cnt, cbuf, cap, L1, btau1, cntr, fb_list);
+    else
+        hipLaunchKernelGGL(k_p1_select<8>, dim3(g4), dim3(256), 0, s, nq, cnt, cbuf, cap, L1, btau1, cntr, fb_list);
+    MN_KCHECK(s, "k_p1_select");
+    int nfb = 0;
+    MN_HIP_TRY(hipMemcpyAsync(&nfb, cntr, 4, hipMemcpyDeviceToHost, s));
+    tdb.mark();
+    MN_HIP_TRY(hipStreamSynchronize(s));
+    if (tdb.on)
+        fprintf(stderr, "sweep_phase1: pre-sample %lld, cap %d, rows short of L1 %d; ms pre %.2f sweep %.2f select %.2f\n",
+                (long long)m00, cap, nfb, tdb.ms(0, 1), tdb.ms(1, 2), tdb.ms(2, 3));
+    if (nfb == 0) return MN_OK;
+    // (d) the rows T0 left short: the list generator on them alone
+    const kb16::GramPlan pf = kb16::plan_gram(nfb, m0, L1, 1, 1);
+    const size_t gb = (size_t)nfb * dp * 2, lb = (size_t)nfb * pf.S * pf.cap * sizeof(uint2);
+    char *g = (char *)scratch(kSlotX1Esc, gb + lb + (size_t)nfb * pf.S * 8 + (size_t)nfb * 8 + 1024);
+    MN_REQUIRE(g, MN_ENOMEM, "mn_knn: phase-1 fallback allocation failed");
+    uint16_t *QRf = (uint16_t *)g;
+    uint2 *cbf = (uint2 *)(g + ((gb + 255) & ~(size_t)255));
+    int *bcf = (int *)((char *)cbf + ((lb + 255) & ~(size_t)255));
+    float *btf = (float *)(bcf + (size_t)nfb * pf.S);
+    float *qnf = btf + (size_t)nfb * pf.S;
+    hipLaunchKernelGGL(k_gather_bf16_rows, dim3((unsigned)(((int64_t)nfb * dp + 255) / 256)), dim3(256),
+                       0, s, QR, dp, qn, fb_list, nfb, QRf, qnf);
+    MN_KCHECK(s, "k_gather_bf16_rows");
+    const int64_t bqf = (nfb + kb16::BM - 1) / kb16::BM;
+    hipLaunchKernelGGL((kb16::k_gram_bf16<kb16::GM_L2H, 0>), dim3((unsigned)(bqf * pf.S)),
+                       dim3(kb16::NT), 0, s, QRf, (int64_t)nfb, CR, m0, dp, (int64_t)0, (int64_t)0, 0,
+                       qnf, cnv, L1, (int)pf.S, pf.chunk, pf.cap, cbf, bcf, btf);
+    MN_KCHECK(s, "k_gram_bf16<L2H, phase-1 fallback>");
+    hipLaunchKernelGGL(k_scatter_tau, dim3((unsigned)((nfb + 255) / 256)), dim3(256), 0, s, fb_list,
+                       nfb, btf, btau1);
+    MN_KCHECK(s, "k_scatter_tau");
+    return MN_OK;
+}
+
 static int knn_x1(const float *Q, int64_t nq, const float *C, int64_t nc, int32_t d,
                   int64_t q_off, int64_t c_off, const mn_knn_opts *opts, int32_t *out_idx,
                   float *out_dist) {
@@ -2202,11 +2370,20 @@ static int knn_x1(const float *Q, int64_t nq, const float *C, int64_t nc, int32_
             hipLaunchKernelGGL(k_prep_x1<false>, dim3((unsigned)blocks), dim3(256), 0, s, X, n, d,
                                dp, pm, R, K, nv, hcv, hv, rv, cmax, flags + 3, corpus, pst1, amax);
     };
+    // phase 1 as a sweep (round 4, SW_SYM only; tuning build: MN_P1_SWEEP=0
+    // keeps the list generator): tile-major copies of the rows and the sample
+    const char *p1e = knob("MN_P1_SWEEP");
+    const bool p1s = sym && !(p1e && *p1e == '0');
+    uint16_t *CKs = nullptr;
+    if (p1s) {
+        CKs = (uint16_t *)scratch(kSlotGeneric3, (size_t)pad256(m0) * kbw1 * 2 + 64);
+        MN_REQUIRE(CKs, MN_ENOMEM, "mn_knn: sample copy allocation failed");
+    }
     if (sym) {
         // phase 1 only: the rows (maxima over them: Q == C) and the sample;
         // the sweep copy is built in tau0 order below
-        prep(Q, nq, nullptr, QR, nullptr, qn, nullptr, qhn, qrn, 1);
-        prep(C, m0, perm, CR, nullptr, cnv, chc, nullptr, nullptr, 0);
+        prep(Q, nq, nullptr, QR, p1s ? QK : nullptr, qn, nullptr, qhn, qrn, 1);
+        prep(C, m0, perm, CR, CKs, cnv, chc, nullptr, nullptr, 0);
     } else {
         prep(Q, nq, nullptr, QR, QK, qn, nullptr, qhn, qrn, 0);
         prep(C, nc, perm, CR, CK, cnv, chc, nullptr, nullptr, 1);
@@ -2231,7 +2408,11 @@ static int knn_x1(const float *Q, int64_t nq, const float *C, int64_t nc, int32_
                (nbuf1 * sizeof(uint2)) >> 20);
     int *bcnt1 = (int *)meta1;
     float *btau1 = (float *)(meta1 + (size_t)nq * pl.S * 4);
-    {
+    if (p1s) {
+        const int rc1 = sweep_phase1(QR, QK, nq, CR, CKs, m0, d, dp, nkb, pst1, q_off, L1, qn, qhn, qrn,
+                                     cnv, chc, cmax, tq, tau0, dlt, btau1, fb_list, flags + 20, s);
+        if (rc1 != MN_OK) return rc1;
+    } else {
         const int64_t bq = (nq + kb16::BM - 1) / kb16::BM;
         hipLaunchKernelGGL((kb16::k_gram_bf16<kb16::GM_L2H, 0>), dim3((unsigned)(bq * pl.S)),
                            dim3(kb16::NT), 0, s, QR, nq, CR, m0, dp, q_off, (int64_t)0, 0, qn, cnv,
@@ -2281,8 +2462,20 @@ static int knn_x1(const float *Q, int64_t nq, const float *C, int64_t nc, int32_
             MN_HIP_TRY(hipStreamSynchronize(s));
         }
         if (!(kmax < __builtin_inff())) {
-            // fall back to the query-major sweep: its copies were skipped
+            // fall back to the query-major sweep: its copies were skipped (and
+            // a sweep phase 1 left no sample lists: the list generator)
             sym = false;
+            if (p1s) {
+                const int64_t bq = (nq + kb16::BM - 1) / kb16::BM;
+                hipLaunchKernelGGL((kb16::k_gram_bf16<kb16::GM_L2H, 0>), dim3((unsigned)(bq * pl.S)),
+                                   dim3(kb16::NT), 0, s, QR, nq, CR, m0, dp, q_off, (int64_t)0, 0, qn,
+                                   cnv, L1, (int)pl.S, pl.chunk, pl.cap, cbuf1, bcnt1, btau1);
+                MN_KCHECK(s, "k_gram_bf16<L2H>");
+                hipLaunchKernelGGL(k_tau_x1, dim3((unsigned)((nq + 255) / 256)), dim3(256), 0, s, nq,
+                                   (int)pl.S, btau1, qn, qhn, qrn, cmax, d, dp, tq, tau0, dlt,
+                                   (unsigned *)nullptr);
+                MN_KCHECK(s, "k_tau_x1");
+            }
             prep(Q, nq, nullptr, nullptr, QK, qn, nullptr, qhn, qrn, 0);
             prep(C, nc, perm, nullptr, CK, cnv, chc, nullptr, nullptr, 1);
             MN_KCHECK(s, "k_prep_x1");

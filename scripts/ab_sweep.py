@@ -19,8 +19,13 @@ from surfface_hip import _lib  # noqa: E402
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 1_000_000
 d = int(sys.argv[2]) if len(sys.argv) > 2 else 768
 rounds = int(sys.argv[3]) if len(sys.argv) > 3 else 2
-X = torch.empty((n, d), dtype=torch.float32, device="cuda")
-_lib.check(_lib.lib().mn_fill_uniform_f32(X.data_ptr(), n, d, 42, 0, None))
+if os.environ.get("AB_DATA") == "clustered":  # the SURVEY §8(d) clustered distribution
+    sys.path.append(os.path.join(ROOT, "tests"))
+    import datagen  # noqa: E402
+    X = torch.from_numpy(datagen.clustered(n, d, seed=7)).cuda()
+else:
+    X = torch.empty((n, d), dtype=torch.float32, device="cuda")
+    _lib.check(_lib.lib().mn_fill_uniform_f32(X.data_ptr(), n, d, 42, 0, None))
 torch.cuda.synchronize()
 ref = None
 VERS = os.environ.get("AB_ENVS", "MN_X1_SYM=1").split(";")
@@ -39,7 +44,8 @@ for r in range(rounds):
         torch.cuda.synchronize()
         st = out.stats
         res[v].append({"ms_sweep": round(st["ms_sweep"], 2), "ms_total": round(st["ms_total"], 2),
-                       "ms_rerank": round(st["ms_rerank"], 2),
+                       "ms_rerank": round(st["ms_rerank"], 2), "ms_sample": round(st["ms_sample"], 2),
+                       "ms_norms": round(st["ms_norms"], 2),
                        "n_cand": st["n_candidates"], "unc": st["n_uncertified"],
                        "esc": st["n_escalated"], "wall": round(time.time() - t, 3)})
         if ref is None:
