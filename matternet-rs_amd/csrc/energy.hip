@@ -70,7 +70,8 @@ struct Vals {
 // stricter one for duplicated entries (an (i, j) stored twice against one
 // (j, i) is asymmetric here, as the symmetric lists' multiplicity 2 would
 // double-count it).  Half the searches of the round-3 check.
-// asym bit 1: asymmetric; bit 2: a column index out of range.
+// asym bit 1: asymmetric; bit 2: a column index out of range; bit 4: a row
+// whose columns are not strictly ascending.
 __global__ __launch_bounds__(256) void k_check_sym(const int64_t *__restrict__ ip,
                                                    const int32_t *__restrict__ ix, Vals v, int f,
                                                    int64_t nnz, int *__restrict__ asym,
@@ -99,6 +100,9 @@ __global__ __launch_bounds__(256) void k_check_sym(const int64_t *__restrict__ i
         }
         const int i = (int)lo;
         const int j = ix[p];
+        // bit 4: a row not strictly ascending (the signal kernel's prefix skip
+        // needs sorted rows)
+        if (p + 1 < ip[i + 1] && !(ix[p + 1] > j)) atomicOr(asym, 4);
         if (j < 0 || j >= f) {
             atomicOr(asym, 2);
         } else if (j < i) {
@@ -1613,10 +1617,24 @@ __global__ __launch_bounds__(512) void k_diffuse_rows2(
 // threads over the signals (coalesced row loads of X); per stored entry
 // (i, j, v) the row x_j is gathered once and serves every signal.  Block
 // partials [block][4][f] (num, den, S, Q) are summed in a fixed order.
-template <int FPT>
+// Round 4: an entry's multiplicities and weights are folded into three
+// per-entry coefficients (uniform: scalar registers) — num += (m v)(x_i x_j),
+// S += (mg w) d^2, Q += (mg w^2) d^4 with w = -v, d = x_i - x_j (the same sums
+// as m v x_i x_j, mg e, mg e^2 with e = w d^2, reassociated: 8 f64 operations
+// per entry and signal instead of 14, within the 1e-9 tolerance) — entries
+// outside the dispersion's pair set carry zero S / Q coefficients (exact
+// no-ops: no branch); for a symmetric L with ascending rows (k_check_sym bit
+// 4 clear) a row's j < i prefix is skipped by a binary search instead of
+// being walked.  NE entries' gathers are issued together (C3, same process,
+// profiles/r04/r04_signals_ab.log: NE 4 18.5 ms, 2 18.1-19.5, 8 20.0; the
+// round-3 kernel 22.5 ms in the bench).  Measured and dropped: one wave per
+// row with dwordx4 gathers (12 signals a lane, the entry's coefficients once
+// per wave): 27 ms — 218 VGPRs, two waves a SIMD, the gathers' latency
+// exposed.
+template <int FPT, int NE>
 __global__ __launch_bounds__(256) void k_energy_signals(
     const float *__restrict__ X, int64_t n, int f, const int64_t *__restrict__ ip,
-    const int32_t *__restrict__ ix, const double *__restrict__ v, int sym, int g_mode,
+    const int32_t *__restrict__ ix, const double *__restrict__ v, int sym, int skip, int g_mode,
     int64_t rows_per_block, double *__restrict__ part) {
     const int t = threadIdx.x;
     const int64_t r0 = (int64_t)blockIdx.x * rows_per_block, r1 = min(n, r0 + rows_per_block);
@@ -1635,44 +1653,46 @@ __global__ __launch_bounds__(256) void k_energy_signals(
                 den[u] += xi[u] * xi[u];
             }
         }
-        const int64_t p0 = ip[i], p1 = ip[i + 1];
-        // 4 entries at a time: their x_j rows are gathered together (an entry
-        // skipped by the symmetric walk gets a zero-length resource: no
-        // traffic), then folded in entry order (same arithmetic as one by one)
-        for (int64_t p = p0; p < p1; p += 4) {
-            int jj[4];
-            double vv[4];
-            bool ok[4];
-            float xjf[4][FPT];
+        int64_t p0 = ip[i];
+        const int64_t p1 = ip[i + 1];
+        if (skip) {  // ascending row: the first entry with j >= i
+            int64_t lo = p0, hi = p1;
+            while (lo < hi) {
+                const int64_t mid = (lo + hi) >> 1;
+                if (ix[mid] < i) lo = mid + 1; else hi = mid;
+            }
+            p0 = lo;
+        }
+        for (int64_t p = p0; p < p1; p += NE) {
+            double cm[NE], ca[NE], cq[NE];
+            float xjf[NE][FPT];
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
+            for (int u = 0; u < NE; ++u) {
                 const bool in = p + u < p1;
-                jj[u] = in ? ix[p + u] : 0;
-                vv[u] = in ? v[p + u] : 0.0;
-                ok[u] = in && !(sym && jj[u] < i);  // (j, i) covers j < i
-                const __amdgpu_buffer_rsrc_t rs = row_rsrc(X + (int64_t)jj[u] * f, ok[u] ? f : 0);
+                const int j = in ? ix[p + u] : 0;
+                const double vv = in ? v[p + u] : 0.0;
+                const bool ok = in && !(sym && j < i);  // (j, i) covers j < i
+                const bool g = ok && j != i && -vv > 0.0 && (g_mode == MN_G_TAUMODE || sym || j > i);
+                cm[u] = ok ? ((j != i) ? mnum : 1.0) * vv : 0.0;
+                ca[u] = g ? mg * -vv : 0.0;
+                cq[u] = g ? mg * (vv * vv) : 0.0;
+                // a skipped entry gets a zero-length resource: reads 0, no traffic
+                const __amdgpu_buffer_rsrc_t rs = row_rsrc(X + (int64_t)j * f, ok ? f : 0);
 #pragma unroll
                 for (int w = 0; w < FPT; ++w) xjf[u][w] = row_at(rs, t + 256 * w);
             }
             __builtin_amdgcn_sched_barrier(0);  // the gathers issue before the folds
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                if (!ok[u]) continue;
-                const int j = jj[u];
-                const bool g = j != i && -vv[u] > 0.0 && (g_mode == MN_G_TAUMODE || sym || j > i);
-                const double m = (j != i) ? mnum : 1.0;
+            for (int u = 0; u < NE; ++u)
 #pragma unroll
                 for (int w = 0; w < FPT; ++w) {
                     const double xj = (double)xjf[u][w];
-                    num[w] += m * (vv[u] * (xi[w] * xj));
-                    if (g) {
-                        const double dd = xi[w] - xj;
-                        const double e = (dd * dd) * (-vv[u]);
-                        S[w] += mg * e;
-                        Q[w] += mg * (e * e);
-                    }
+                    num[w] = __builtin_fma(cm[u], xi[w] * xj, num[w]);
+                    const double dd = xi[w] - xj;
+                    const double d2 = dd * dd;
+                    S[w] = __builtin_fma(ca[u], d2, S[w]);
+                    Q[w] = __builtin_fma(cq[u], d2 * d2, Q[w]);
                 }
-            }
         }
     }
     double *pb = part + (size_t)blockIdx.x * 4 * f;
@@ -2206,10 +2226,25 @@ static int energy_signals_impl(const mn_csr *L, const float *X, int64_t n, int32
     MN_HIP_TRY(hipStreamSynchronize(s));
     MN_REQUIRE(!(hflag & 2), MN_EINVAL, "mn_energy_signals: Laplacian column index out of range");
     const int sym = (hflag & 1) ? 0 : 1;
+    const int skip = sym && !(hflag4[0] & 4);  // symmetric, ascending rows
     const int fpt = (f + 255) / 256;
+    const char *nee = knob("MN_SIG_NE");  // tuning build: entries per gather batch (2 / 4 / 8)
+    const int ne = (nee && *nee) ? atoi(nee) : 4;
 #define MN_ES(FP)                                                                               \
-    hipLaunchKernelGGL(k_energy_signals<FP>, dim3((unsigned)nbu), dim3(256), 0, s, X, n, f,     \
-                       L->indptr, L->indices, (const double *)L->values, sym, g_mode, rpb, part)
+    do {                                                                                        \
+        if (ne == 2)                                                                            \
+            hipLaunchKernelGGL((k_energy_signals<FP, 2>), dim3((unsigned)nbu), dim3(256), 0, s, X, \
+                               n, f, L->indptr, L->indices, (const double *)L->values, sym, skip, \
+                               g_mode, rpb, part);                                              \
+        else if (ne != 8)                                                                       \
+            hipLaunchKernelGGL((k_energy_signals<FP, 4>), dim3((unsigned)nbu), dim3(256), 0, s, X, \
+                               n, f, L->indptr, L->indices, (const double *)L->values, sym, skip, \
+                               g_mode, rpb, part);                                              \
+        else                                                                                    \
+            hipLaunchKernelGGL((k_energy_signals<FP, 8>), dim3((unsigned)nbu), dim3(256), 0, s, X, \
+                               n, f, L->indptr, L->indices, (const double *)L->values, sym, skip, \
+                               g_mode, rpb, part);                                              \
+    } while (0)
     if (fpt <= 1) MN_ES(1); else if (fpt <= 2) MN_ES(2); else if (fpt <= 3) MN_ES(3);
     else if (fpt <= 4) MN_ES(4); else if (fpt <= 8) MN_ES(8); else MN_ES(16);
 #undef MN_ES

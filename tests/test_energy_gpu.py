@@ -232,6 +232,33 @@ def test_item_graph_signal_orientation(gm):
     rE2, rG2, _ = O.energy_rows(np.ascontiguousarray(X.T), ip, ix, iv2, og, O.TAU_MEDIAN)
     np.testing.assert_allclose(E2.cpu().numpy(), rE2, rtol=RTOL, atol=ATOL)
     np.testing.assert_allclose(G2.cpu().numpy(), rG2, rtol=RTOL, atol=ATOL)
+    # symmetric, but rows stored in shuffled column order (k_check_sym bit 4):
+    # the j < i prefix skip must not be taken
+    rng = np.random.default_rng(3)
+    ix3, iv3 = ix.copy(), iv.copy()
+    for r in range(len(ip) - 1):
+        a, b = int(ip[r]), int(ip[r + 1])
+        pr = rng.permutation(b - a)
+        ix3[a:b], iv3[a:b] = ix[a:b][pr], iv[a:b][pr]
+    E3, G3 = S.signal_energy_and_dispersion(torch.from_numpy(X).cuda(), csr_dev(ip, ix3, iv3), gm)
+    np.testing.assert_allclose(E3.cpu().numpy(), rE, rtol=RTOL, atol=ATOL)
+    np.testing.assert_allclose(G3.cpu().numpy(), rG, rtol=RTOL, atol=ATOL)
+
+
+def test_item_graph_signals_768():
+    """The C3 shape's 768 signals (three per thread) on a smaller item graph:
+    the per-entry coefficient form (num / S / Q) within 1e-9 of the oracle."""
+    import surfface_hip as S
+    X = datagen.uniform(3000, 768, seed=52)
+    idx, dist = O.knn_l2sq(X, 8)
+    L, _ = S.build_laplacian_from_knn(torch.from_numpy(idx).cuda(), torch.from_numpy(dist).cuda(),
+                                      eps=1e30, sigma=8.0)
+    ip, ix, iv = L.to_numpy()
+    for gm, og in ((0, O.G_TAUMODE), (1, O.G_ENERGYMAPS)):
+        E, G = S.signal_energy_and_dispersion(torch.from_numpy(X).cuda(), L, gm)
+        rE, rG, _ = O.energy_rows(np.ascontiguousarray(X.T), ip, ix, iv, og, O.TAU_MEDIAN)
+        np.testing.assert_allclose(E.cpu().numpy(), rE, rtol=RTOL, atol=ATOL)
+        np.testing.assert_allclose(G.cpu().numpy(), rG, rtol=RTOL, atol=ATOL)
 
 
 @pytest.mark.parametrize("tau", ["median", "pct"])
