@@ -56,12 +56,10 @@ struct Vals {
     }
 };
 
-// Symmetry / range check, one thread per stored entry (a row-per-thread walk
-// left the kNN item graph's hub rows, thousands of entries, on one thread).
-// The block finds the row of its first entry once (upper_bound on indptr);
-// each thread gallops forward from there to its own row, then binary-searches
-// the transposed entry (j, i) in row j.
-// Symmetry check (round 4: the upper entries only).  Every stored entry
+// Symmetry / range / order check of an n x n CSR (round 4: one wave per row,
+// lanes over the row's entries; the round-3 form — a thread per entry that
+// first located its row by an upper-bound search on indptr — spent most of
+// its 1.6 ms at C3 on those dependent searches).  Every stored upper entry
 // (i, j > i) must find a stored (j, i) with the same value (binary search of
 // row j), and the stored upper and lower entry counts must be equal
 // (ucount[0] += #upper - #lower per block): the matches map the upper
@@ -69,66 +67,57 @@ struct Vals {
 // bijection — the same verdict as searching every off-diagonal entry, and a
 // stricter one for duplicated entries (an (i, j) stored twice against one
 // (j, i) is asymmetric here, as the symmetric lists' multiplicity 2 would
-// double-count it).  Half the searches of the round-3 check.
+// double-count it).
 // asym bit 1: asymmetric; bit 2: a column index out of range; bit 4: a row
 // whose columns are not strictly ascending.
 __global__ __launch_bounds__(256) void k_check_sym(const int64_t *__restrict__ ip,
-                                                   const int32_t *__restrict__ ix, Vals v, int f,
-                                                   int64_t nnz, int *__restrict__ asym,
+                                                   const int32_t *__restrict__ ix, Vals v, int n,
+                                                   int *__restrict__ asym,
                                                    unsigned long long *__restrict__ ucount) {
-    __shared__ int64_t r0s;
     __shared__ int bal[4];
-    const int64_t p0 = (int64_t)blockIdx.x * blockDim.x;
-    if (threadIdx.x == 0) {
-        int64_t lo = 0, hi = f;  // last row r with ip[r] <= p0
-        while (lo < hi) {
-            const int64_t mid = (lo + hi + 1) >> 1;
-            if (ip[mid] <= p0) lo = mid; else hi = mid - 1;
-        }
-        r0s = lo;
-    }
-    __syncthreads();
-    const int64_t p = p0 + threadIdx.x;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int64_t nw = (int64_t)gridDim.x * 4;
     int d = 0;  // +1 upper, -1 lower
-    if (p < nnz) {
-        // row i: the r >= r0 with ip[r] <= p < ip[r + 1] (gallop, then bisect)
-        int64_t lo = r0s, step = 1, hi = lo;
-        while (hi < f && ip[hi + 1] <= p) { lo = hi + 1; hi = min<int64_t>(hi + step, f - 1); step <<= 1; }
-        while (lo < hi) {
-            const int64_t mid = (lo + hi) >> 1;
-            if (ip[mid + 1] <= p) lo = mid + 1; else hi = mid;
-        }
-        const int i = (int)lo;
-        const int j = ix[p];
-        // bit 4: a row not strictly ascending (the signal kernel's prefix skip
-        // needs sorted rows)
-        if (p + 1 < ip[i + 1] && !(ix[p + 1] > j)) atomicOr(asym, 4);
-        if (j < 0 || j >= f) {
-            atomicOr(asym, 2);
-        } else if (j < i) {
-            d = -1;
-        } else if (j > i) {
-            d = 1;
-            int64_t a = ip[j], b = ip[j + 1] - 1, hit = -1;
-            while (a <= b) {
-                const int64_t mid = (a + b) >> 1;
-                const int c = ix[mid];
-                if (c == i) { hit = mid; break; }
-                if (c < i) a = mid + 1; else b = mid - 1;
+    int bad = 0;
+    for (int64_t i = (int64_t)blockIdx.x * 4 + wv; i < n; i += nw) {
+        const int64_t a0 = ip[i], b0 = ip[i + 1];
+        for (int64_t p = a0 + lane; p < b0; p += 64) {
+            const int j = ix[p];
+            if (p + 1 < b0 && !(ix[p + 1] > j)) bad |= 4;
+            if (j < 0 || j >= n) {
+                bad |= 2;
+            } else if (j < i) {
+                d -= 1;
+            } else if (j > i) {
+                d += 1;
+                int64_t a = ip[j], b = ip[j + 1] - 1, hit = -1;
+                while (a <= b) {
+                    const int64_t mid = (a + b) >> 1;
+                    const int c = ix[mid];
+                    if (c == i) { hit = mid; break; }
+                    if (c < i) a = mid + 1; else b = mid - 1;
+                }
+                if (hit < 0 || v[hit] != v[p]) bad |= 1;
             }
-            if (hit < 0 || v[hit] != v[p]) atomicOr(asym, 1);
         }
     }
-    // the block's upper - lower balance: one atomic per block
+    // one flag atomic per wave that found something, one balance atomic per block
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) d += __shfl_xor(d, o);
-    if ((threadIdx.x & 63) == 0) bal[threadIdx.x >> 6] = d;
+    for (int o = 32; o > 0; o >>= 1) {
+        d += __shfl_xor(d, o);
+        bad |= __shfl_xor(bad, o);
+    }
+    if (lane == 0 && bad) atomicOr(asym, bad);
+    if (lane == 0) bal[wv] = d;
     __syncthreads();
     if (threadIdx.x == 0) {
         const int tb = bal[0] + bal[1] + bal[2] + bal[3];
         if (tb != 0) atomicAdd(ucount, (unsigned long long)(long long)tb);
     }
 }
+
+// grid of the check: a wave per row, at most 32768 blocks (grid-stride beyond)
+inline unsigned check_sym_grid(int64_t n) { return (unsigned)std::max<int64_t>(1, std::min<int64_t>((n + 3) / 4, 32768)); }
 
 // Every stored CSR entry (i, j, v) the reduction needs goes to one list,
 // packed (i | j << 16) + an f64 value:
@@ -1931,8 +1920,8 @@ static int energy_impl(const mn_csr *L, const float *X, int64_t n, int32_t f,
     unsigned long long *ubal = (unsigned long long *)(flag + 2);
     const unsigned fb = (unsigned)((f + 255) / 256);
     if (L->nnz > 0)
-        hipLaunchKernelGGL(k_check_sym, dim3((unsigned)((L->nnz + 255) / 256)), dim3(256), 0, s,
-                           L->indptr, L->indices, vals, f, L->nnz, flag, ubal);
+        hipLaunchKernelGGL(k_check_sym, dim3(check_sym_grid(f)), dim3(256), 0, s,
+                           L->indptr, L->indices, vals, f, flag, ubal);
     int hflag[4] = {0, 0, 0, 0};
     MN_HIP_TRY(hipMemcpyAsync(hflag, flag, 16, hipMemcpyDeviceToHost, s));
     MN_HIP_TRY(hipStreamSynchronize(s));
@@ -2217,8 +2206,8 @@ static int energy_signals_impl(const mn_csr *L, const float *X, int64_t n, int32
     MN_REQUIRE(flag && part, MN_ENOMEM, "mn_energy_signals: scratch allocation failed");
     MN_HIP_TRY(hipMemsetAsync(flag, 0, 16, s));
     if (L->nnz > 0)
-        hipLaunchKernelGGL(k_check_sym, dim3((unsigned)((L->nnz + 255) / 256)), dim3(256), 0, s,
-                           L->indptr, L->indices, Vals{L->values, 0}, (int)n, L->nnz, flag,
+        hipLaunchKernelGGL(k_check_sym, dim3(check_sym_grid(n)), dim3(256), 0, s,
+                           L->indptr, L->indices, Vals{L->values, 0}, (int)n, flag,
                            (unsigned long long *)(flag + 2));
     int hflag4[4] = {0, 0, 0, 0};
     MN_HIP_TRY(hipMemcpyAsync(hflag4, flag, 16, hipMemcpyDeviceToHost, s));

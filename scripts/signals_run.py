@@ -26,7 +26,7 @@ L, _ = S.build_laplacian_from_knn(out.idx, out.dist, weight_kernel="rational", s
                                   eps=float("inf"), sigma=1.0, p=2.0)
 del out
 torch.cuda.synchronize()
-VERS = os.environ.get("AB_ENVS", "MN_SIG_NE=8").split(";")
+VERS = os.environ.get("AB_ENVS", "MN_SIG_NONE=0").split(";")
 ref = None
 for r in range(reps):
     for v in VERS:
