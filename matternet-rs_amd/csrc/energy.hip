@@ -1598,6 +1598,135 @@ __global__ __launch_bounds__(512) void k_diffuse_rows2(
     }
 }
 
+// Round 4b: the same folds with an iteration's E = DF_G x DF_T entries of a
+// lane stored contiguously — values as E/2 double2 pieces [it][h][lane],
+// columns as int2 / int4 pieces [it][q][lane] — so a lane's values and
+// columns come in by ds_read_b128 (b64 for two columns; 16-B lane stride:
+// conflict-free) instead of one ds_read_b64 / b32 per entry: the value /
+// column reads were 12 of the 20 LDS bytes an entry costs, on the narrow
+// instructions, and the kernel is LDS-bound.  Entry k = e DF_G + u of an
+// iteration is entry t = DF_T it + e of fold u; pads (0, f) read the zero slot.
+// C3 (same process, profiles/r04/r04_diffusion_v3_ab.log, bit-identical):
+// rows2 (2, 1) 9.62-9.69 ms -> rows3 (2, 1) 8.94-8.96, (4, 1) 8.80-8.94, (2, 2)
+// 8.89-8.92, (2, 4) 9.59, (1, 2) 11.2, (1, 4) 12.0.  What bounds it: ~2.5 KB of
+// LDS reads per (2, 1) iteration and wave (a 1-KB value piece, 512-B columns,
+// two 512-B x gathers), ~54 iterations per row and step: ~540 GB over the
+// 1M rows x 4 steps, ~120 B/clk per CU at 8.9 ms — the LDS array's rate for
+// the b64 gathers.
+template <bool XF64, int DF_G, int DF_T>
+__global__ __launch_bounds__(512) void k_diffuse_rows3(
+    const void *__restrict__ Xin, int64_t n, int f, const double *__restrict__ giv,
+    const int32_t *__restrict__ gic, int64_t S, const int32_t *__restrict__ gsw,
+    const int32_t *__restrict__ gperm, double eta, int steps, int matvec,
+    double *__restrict__ Xout) {
+    constexpr int E = DF_G * DF_T;
+    static_assert(E == 2 || E == 4 || E == 8, "E in {2, 4, 8}");
+    extern __shared__ __attribute__((aligned(16))) unsigned char dsm[];
+    const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int nw = blockDim.x >> 6;
+    const int nsw = (f + 63) / 64;
+    // LDS: [val f64 x S | col i32 x S] | x [waves][2][f + 1] f64 (slot f = 0)
+    double *iv = (double *)dsm;
+    int32_t *ic = (int32_t *)(dsm + (size_t)S * 8);
+    const size_t lb = (((size_t)S * 12) + 15) & ~(size_t)15;
+    double *xb = (double *)(dsm + lb) + (size_t)w * 2 * (f + 1);
+    {   // S is a multiple of 64 E: 16-B pieces
+        const double2 *g2 = (const double2 *)giv;
+        double2 *l2 = (double2 *)iv;
+        for (int64_t q = threadIdx.x; q < S / 2; q += blockDim.x) l2[q] = g2[q];
+        const int4 *c4 = (const int4 *)gic;
+        int4 *lc4 = (int4 *)ic;
+        for (int64_t q = threadIdx.x; q < S / 4; q += blockDim.x) lc4[q] = c4[q];
+    }
+    __syncthreads();
+    constexpr int MAXG = (DF_SW + DF_G - 1) / DF_G;
+    int si[DF_SW], sb[MAXG], sl[MAXG];
+#pragma unroll
+    for (int g = 0; g < DF_SW; ++g) si[g] = gperm[min(lane + 64 * g, f - 1)];
+    const int ngr = (nsw + DF_G - 1) / DF_G;
+#pragma unroll
+    for (int G = 0; G < MAXG; ++G) {
+        sb[G] = G < ngr ? gsw[2 * G] : 0;
+        sl[G] = G < ngr ? gsw[2 * G + 1] : 0;
+    }
+    if (lane == 0) {
+        xb[f] = 0.0;
+        xb[f + 1 + f] = 0.0;
+    }
+    float nxt[DF_SW];
+    auto load_row = [&](int64_t r) {
+        const __amdgpu_buffer_rsrc_t rs = row_rsrc((const float *)Xin + min(r, n - 1) * f, f);
+#pragma unroll
+        for (int q = 0; q < DF_SW; ++q) nxt[q] = row_at(rs, lane + 64 * q);
+    };
+    const int64_t rstride = (int64_t)gridDim.x * nw;
+    if (!XF64) load_row((int64_t)blockIdx.x * nw + w);
+    const double2 *iv2 = (const double2 *)iv;
+    for (int64_t row = (int64_t)blockIdx.x * nw + w; row < n; row += rstride) {
+        double *x = xb, *y = xb + (f + 1);
+        if (!XF64) {
+#pragma unroll
+            for (int r = 0; r < DF_SW; ++r)
+                if (lane + 64 * r < f) x[lane + 64 * r] = (double)nxt[r];
+            if (row + rstride < n) load_row(row + rstride);
+        } else {
+            for (int i = lane; i < f; i += 64) x[i] = ((const double *)Xin)[row * f + i];
+        }
+        __builtin_amdgcn_wave_barrier();
+        const int ns = matvec ? 1 : steps;
+        for (int st = 0; st < ns; ++st) {
+#pragma unroll
+            for (int G = 0; G < MAXG; ++G) {
+                if (G >= ngr) break;
+                const int base = __builtin_amdgcn_readfirstlane(sb[G]);
+                const int len = __builtin_amdgcn_readfirstlane(sl[G]);
+                double sum[DF_G];
+#pragma unroll
+                for (int u = 0; u < DF_G; ++u) sum[u] = 0.0;
+                for (int it = base; it < base + len; ++it) {
+                    double v[E];
+                    int c[E];
+#pragma unroll
+                    for (int h = 0; h < E / 2; ++h) {
+                        const double2 t = iv2[((size_t)it * (E / 2) + h) * 64 + lane];
+                        v[2 * h] = t.x;
+                        v[2 * h + 1] = t.y;
+                    }
+                    if constexpr (E == 2) {
+                        const int2 t = ((const int2 *)ic)[(size_t)it * 64 + lane];
+                        c[0] = t.x;
+                        c[1] = t.y;
+                    } else {
+#pragma unroll
+                        for (int q = 0; q < E / 4; ++q) {
+                            const int4 t = ((const int4 *)ic)[((size_t)it * (E / 4) + q) * 64 + lane];
+                            c[4 * q] = t.x; c[4 * q + 1] = t.y; c[4 * q + 2] = t.z; c[4 * q + 3] = t.w;
+                        }
+                    }
+                    double xv[E];
+#pragma unroll
+                    for (int k = 0; k < E; ++k) xv[k] = x[c[k]];
+#pragma unroll
+                    for (int e = 0; e < DF_T; ++e)
+#pragma unroll
+                        for (int u = 0; u < DF_G; ++u)
+                            sum[u] = sum[u] + v[e * DF_G + u] * xv[e * DF_G + u];
+                }
+#pragma unroll
+                for (int u = 0; u < DF_G; ++u) {
+                    const int g = DF_G * G + u;
+                    if (g < DF_SW && g < nsw && lane + 64 * g < f)
+                        y[si[g < DF_SW ? g : 0]] = matvec ? sum[u] : x[si[g < DF_SW ? g : 0]] - eta * sum[u];
+                }
+            }
+            __builtin_amdgcn_wave_barrier();
+            double *t = x; x = y; y = t;
+        }
+        for (int i = lane; i < f; i += 64) Xout[row * f + i] = x[i];
+        __builtin_amdgcn_wave_barrier();
+    }
+}
+
 // ---- item-graph orientation: energy of the F feature signals (length n) ----
 // node_energy_and_dispersion(X^T, L_items) (energymaps.rs:923-1045 with the
 // n x n item Laplacian; SURVEY §8(d) orientation (ii)): per signal s_f =
@@ -2310,6 +2439,69 @@ static int diffuse_impl(const mn_csr *L, const void *X, int32_t x_is_f64, int64_
         const size_t lb2 = ((size_t)S * 64 * 12 + 15) & ~(size_t)15;
         const size_t pw2 = (size_t)2 * (f + 1) * 8;
         const char *dfe = knob("MN_DIFFUSE_V1");  // tuning build: 1 = the round-3 kernel (A/B)
+        const char *d3e = knob("MN_DIFFUSE_V3");  // tuning build: 0 = the round-4 rows2 layout
+        const int E3 = DF_G * DF_T;
+        if (f <= 64 * DF_SW && lb2 + pw2 <= LDS_BUDGET && S * 64 < INT_MAX && !(dfe && *dfe == '1') &&
+            !(d3e && *d3e == '0') && (E3 == 2 || E3 == 4 || E3 == 8)) {
+            // k_diffuse_rows3 layout: iteration it of group G (sw in iterations)
+            std::vector<int32_t> sw3(2 * (size_t)ngr);
+            int64_t nit = 0;
+            for (int G = 0; G < ngr; ++G) {
+                sw3[2 * G] = (int32_t)nit;
+                sw3[2 * G + 1] = sw[2 * G + 1] / DF_T;
+                nit += sw[2 * G + 1] / DF_T;
+            }
+            const size_t slots = (size_t)nit * 64 * E3;
+            std::vector<int32_t> hix((size_t)nnz);
+            std::vector<double> hv((size_t)nnz);
+            if (nnz > 0) {
+                MN_HIP_TRY(hipMemcpyAsync(hix.data(), L->indices, 4 * (size_t)nnz, hipMemcpyDeviceToHost, s));
+                MN_HIP_TRY(hipMemcpyAsync(hv.data(), L->values, 8 * (size_t)nnz, hipMemcpyDeviceToHost, s));
+                MN_HIP_TRY(hipStreamSynchronize(s));
+            }
+            std::vector<double> iv(slots, 0.0);
+            std::vector<int32_t> ic(slots, f);  // pads: the zero slot
+            for (int g = 0; g < nsw; ++g)
+                for (int l = 0; l < 64 && 64 * g + l < f; ++l) {
+                    const int i = hperm[64 * g + l];
+                    const int G = g / DF_G, u = g % DF_G;
+                    for (int64_t p = hip_[i]; p < hip_[i + 1]; ++p) {
+                        const int64_t t = p - hip_[i];
+                        const int64_t it = sw3[2 * G] + t / DF_T;
+                        const int k = (int)(t % DF_T) * DF_G + u;
+                        const size_t qv = (((size_t)it * (E3 / 2) + k / 2) * 64 + l) * 2 + k % 2;
+                        const size_t qc = E3 == 2 ? ((size_t)it * 64 + l) * 2 + k
+                                                  : (((size_t)it * (E3 / 4) + k / 4) * 64 + l) * 4 + k % 4;
+                        const int c = hix[p];
+                        MN_REQUIRE(c >= 0 && c < f, MN_EINVAL, "mn_diffuse_rows: column index out of range");
+                        iv[qv] = hv[p];
+                        ic[qc] = c;
+                    }
+                }
+            char *gb = (char *)scratch(kSlotGeneric3, slots * 12 + sw3.size() * 4 + 256);
+            MN_REQUIRE(gb, MN_ENOMEM, "mn_diffuse_rows: scratch allocation failed");
+            double *div = (double *)gb;
+            int32_t *dic = (int32_t *)(gb + slots * 8);
+            int32_t *dsw = (int32_t *)(gb + ((slots * 12 + 15) & ~(size_t)15));
+            MN_HIP_TRY(hipMemcpyAsync(div, iv.data(), slots * 8, hipMemcpyHostToDevice, s));
+            MN_HIP_TRY(hipMemcpyAsync(dic, ic.data(), slots * 4, hipMemcpyHostToDevice, s));
+            MN_HIP_TRY(hipMemcpyAsync(dsw, sw3.data(), sw3.size() * 4, hipMemcpyHostToDevice, s));
+            const int nw2 = (int)std::min<size_t>(8, (LDS_BUDGET - lb2) / pw2);
+            const size_t sh2 = lb2 + (size_t)nw2 * pw2;
+            const int64_t blocks2 = std::min<int64_t>((n + nw2 - 1) / nw2, 2048);
+            auto kf = x_is_f64 ? k_diffuse_rows3<true, 2, 1> : k_diffuse_rows3<false, 2, 1>;
+#define MN_DFK(G, T) \
+    if (DF_G == G && DF_T == T) kf = x_is_f64 ? k_diffuse_rows3<true, G, T> : k_diffuse_rows3<false, G, T>
+            MN_DFK(1, 2); MN_DFK(1, 4); MN_DFK(2, 2); MN_DFK(2, 4); MN_DFK(4, 1); MN_DFK(4, 2);
+#undef MN_DFK
+            MN_HIP_TRY(hipFuncSetAttribute((const void *)kf, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                           (int)sh2));
+            hipLaunchKernelGGL(kf, dim3((unsigned)blocks2), dim3(64 * nw2), sh2, s, X, n, f, div, dic,
+                               (int64_t)slots, dsw, perm, eta, steps, matvec, out);
+            MN_KCHECK(s, "k_diffuse_rows3");
+            MN_HIP_TRY(hipStreamSynchronize(s));
+            return MN_OK;
+        }
         if (f <= 64 * DF_SW && lb2 + pw2 <= LDS_BUDGET && S * 64 < INT_MAX && !(dfe && *dfe == '1')) {
             std::vector<int32_t> hix((size_t)nnz);
             std::vector<double> hv((size_t)nnz);
