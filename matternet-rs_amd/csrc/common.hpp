@@ -28,6 +28,11 @@ inline const char *knob(const char *name) { return getenv(name); }
 #else
 inline const char *knob(const char *) { return nullptr; }
 #endif
+// integer knob with a default (the release build: always the default)
+inline int knob_int(const char *name, int dflt) {
+    const char *e = knob(name);
+    return (e && *e) ? atoi(e) : dflt;
+}
 
 // Grow-only device scratch, one set of slots per (thread, device).  Growing
 // frees the old block (hipFree synchronises), so never call it while kernels

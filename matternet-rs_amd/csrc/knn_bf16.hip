@@ -753,9 +753,174 @@ hipError_t sort_f32_pairs(const float *keys_in, float *keys_out, const int *vals
 
 static thread_local mn_knn_stats t_bf16_stats{};
 
-static int knob_int(const char *name, int dflt) {
-    const char *e = knob(name);
-    return (e && *e) ? atoi(e) : dflt;
+// ---- phase 1 as a sweep (round 4; C2's knn_f32.hip sweep_phase1, cosine form)
+// (a) the list generator (k_gram_bf16<GM_COS>) on a pre-sample — the first
+// m0 / CP1_DIV sample positions, list CP1_L0 — gives each row a cosine
+// threshold t0; (b) the query-major SW_COS sweep of every position against the
+// sample positions [0, m0) buffers the pairs with cos~ > t0 (keys k = t0|q| -
+// q.c/|c|, so -cos~ = k/|q| - t0); (c) k_p1_select_cos takes each position's
+// L1-th smallest buffered key -> btau1[row] = k/|q| - t0 = -(the sample's L1-th
+// best cos~), the list generator's own output (an overflowing buffer gives a
+// lower threshold: more candidates; the certificate does not depend on it);
+// (d) rows with fewer than L1 buffered keys run the list generator alone.
+constexpr int CP1_L0 = 4, CP1_DIV = 8;
+
+template <int NR>
+__global__ __launch_bounds__(256) void k_p1_select_cos(int64_t n, kb16::Perm pm, const int *__restrict__ cnt,
+                                                       const uint2 *__restrict__ buf, int cap, int L1,
+                                                       const double *__restrict__ xn,
+                                                       const float *__restrict__ t0,
+                                                       float *__restrict__ btau,
+                                                       int *__restrict__ fb_count,
+                                                       int *__restrict__ fb_list) {
+    const int lane = threadIdx.x & 63;
+    const int64_t p = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    if (p >= n) return;
+    const int64_t r = pm(p);
+    int c = cnt[p];
+    c = (c < 0 || c > cap) ? cap : c;  // -1: overflow, the buffer is full
+    if (c < L1) {
+        if (lane == 0) {
+            btau[r] = __builtin_inff();
+            fb_list[atomicAdd(fb_count, 1)] = (int)r;
+        }
+        return;
+    }
+    float kk[NR];
+#pragma unroll
+    for (int u = 0; u < NR; ++u) {
+        const int e = lane + 64 * u;
+        kk[u] = e < c ? __uint_as_float(buf[p * (int64_t)cap + e].x) : __builtin_inff();
+    }
+    float t = -__builtin_inff(), res = __builtin_inff();
+    int need = L1;
+    for (int it = 0; it < L1; ++it) {
+        float m = __builtin_inff();
+#pragma unroll
+        for (int u = 0; u < NR; ++u) m = fminf(m, kk[u] > t ? kk[u] : __builtin_inff());
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) m = fminf(m, __shfl_xor(m, o));
+        int eq = 0;
+#pragma unroll
+        for (int u = 0; u < NR; ++u) eq += (int)__popcll(__ballot(kk[u] == m));
+        if (eq >= need) { res = m; break; }
+        need -= eq;
+        t = m;
+    }
+    if (lane == 0) btau[r] = (float)((double)res / xn[r] - (double)t0[r]);
+}
+
+__global__ __launch_bounds__(256) void k_gather_rows_bf16(const uint16_t *__restrict__ X, int d,
+                                                          const float *__restrict__ xinv,
+                                                          const int *__restrict__ rows, int nfb,
+                                                          uint16_t *__restrict__ out,
+                                                          float *__restrict__ inv_out) {
+    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // 16 B each
+    const int d8 = d / 8;
+    if (e < (int64_t)nfb * d8) {
+        const int64_t i = e / d8;
+        const int c = (int)(e - i * d8);
+        *reinterpret_cast<uint4 *>(out + i * d + 8 * c) =
+            *reinterpret_cast<const uint4 *>(X + (int64_t)rows[i] * d + 8 * c);
+    }
+    if (e < nfb) inv_out[e] = xinv[rows[e]];
+}
+
+// min over the S slices of each fallback row's threshold -> btau[row]
+__global__ __launch_bounds__(256) void k_scatter_min(const int *__restrict__ rows, int nfb, int S,
+                                                     const float *__restrict__ v,
+                                                     float *__restrict__ out) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nfb) return;
+    float m = __builtin_inff();
+    for (int q = 0; q < S; ++q) m = fminf(m, v[(int64_t)i * S + q]);
+    out[rows[i]] = m;
+}
+
+// Phase 1 by sweep: btau1 [n] (one slice) for k_tau_cos; XK holds the
+// position-order tile-major copy on return.
+static int cos_sweep_phase1(const uint16_t *X, int64_t n, int32_t d, int dp, int nkb, int pst,
+                            const kb16::Perm &pm, const uint16_t *XR, int64_t m0, int L1,
+                            const double *xn, const float *xinv, const float *invp,
+                            const float *negn, float *tcos, float *tq_pos, uint16_t *XK,
+                            float *btau1, int *cntr, int *fb_list, hipStream_t s) {
+    using namespace kb16;
+    const int L0 = knob_int("MN_BF16_P1_L0", CP1_L0);
+    const int dv = std::max(2, knob_int("MN_BF16_P1_DIV", CP1_DIV));
+    {   // position-order copy of every row (the queries and the sample)
+        const int64_t nt = (n + 255) / 256 * 256 * 4 * nkb;
+        hipLaunchKernelGGL(k_to_kb32, dim3((unsigned)((nt + 255) / 256)), dim3(256), 0, s, X, n, d,
+                           dp, pm, XK, pst, (const int *)nullptr);
+        MN_KCHECK(s, "k_to_kb32 (phase 1)");
+    }
+    // (a) pre-sample
+    int64_t m00 = std::max<int64_t>(m0 / dv, (int64_t)64 * L0);
+    m00 = std::min<int64_t>(m0, (m00 + 255) / 256 * 256);
+    const GramPlan p0 = plan_gram(n, m00, L0, 1, 1);
+    uint2 *cb0 = (uint2 *)scratch(kSlotX1Esc, (size_t)n * p0.S * p0.cap * sizeof(uint2) + 64);
+    char *m0b = (char *)scratch(kSlotX1Meta2, (size_t)n * p0.S * 8 + 64);
+    MN_REQUIRE(cb0 && m0b, MN_ENOMEM, "mn_knn_cos_bf16: pre-sample buffer allocation failed");
+    int *bc0 = (int *)m0b;
+    float *bt0 = (float *)(m0b + (size_t)n * p0.S * 4);
+    const int64_t bq = (n + BM - 1) / BM;
+    hipLaunchKernelGGL((k_gram_bf16<GM_COS, 0>), dim3((unsigned)(bq * p0.S)), dim3(NT), 0, s, X, n, XR,
+                       m00, d, (int64_t)0, (int64_t)0, 0, xinv, invp, L0, (int)p0.S, p0.chunk, p0.cap,
+                       cb0, bc0, bt0);
+    MN_KCHECK(s, "k_gram_bf16<COS> (pre-sample)");
+    hipLaunchKernelGGL(k_tau_cos, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, n, (int)p0.S,
+                       bt0, xn, pm, tcos, tq_pos);
+    MN_KCHECK(s, "k_tau_cos (pre-sample)");
+    // (b) the sweep of the sample positions with t0
+    const double expect = (double)L0 * (double)m0 / (double)m00;
+    const int cap = std::min(512, std::max(64, (int)((2.5 * expect + 64.0 + 15.0) / 16.0) * 16));
+    uint2 *cbuf = (uint2 *)scratch(kSlotX1Buf2, (size_t)n * cap * sizeof(uint2) + 64);
+    int *cnt = (int *)scratch(kSlotX1Meta2, (size_t)n * 4 + 64);
+    MN_REQUIRE(cbuf && cnt, MN_ENOMEM, "mn_knn_cos_bf16: phase-1 sweep buffer allocation failed");
+    MN_HIP_TRY(hipMemsetAsync(cnt, 0, (size_t)n * 4, s));
+    const int64_t nqb = (n + ksw2::BQ - 1) / ksw2::BQ;
+    hipLaunchKernelGGL((ksw2::k_gram_sweep2<0, ksw2::SW_COS, true>), dim3((unsigned)nqb), dim3(ksw2::NT),
+                       0, s, XK, n, XK, m0, nkb, (int64_t)0, (int64_t)0, 0, tq_pos, tq_pos, negn,
+                       (int64_t)0, 1, m0, cap, cbuf, cnt, pst, ksw2::SymArgs{});
+    MN_KCHECK(s, "k_gram_sweep2<COS> (phase 1)");
+    // (c) the L1-th smallest key per position
+    MN_HIP_TRY(hipMemsetAsync(cntr, 0, 4, s));
+    const unsigned g4 = (unsigned)((n + 3) / 4);
+    if (cap <= 128)
+        hipLaunchKernelGGL(k_p1_select_cos<2>, dim3(g4), dim3(256), 0, s, n, pm, cnt, cbuf, cap, L1, xn, tcos, btau1, cntr, fb_list);
+    else if (cap <= 256)
+        hipLaunchKernelGGL(k_p1_select_cos<4>, dim3(g4), dim3(256), 0, s, n, pm, cnt, cbuf, cap, L1, xn, tcos, btau1, cntr, fb_list);
+    else
+        hipLaunchKernelGGL(k_p1_select_cos<8>, dim3(g4), dim3(256), 0, s, n, pm, cnt, cbuf, cap, L1, xn, tcos, btau1, cntr, fb_list);
+    MN_KCHECK(s, "k_p1_select_cos");
+    int nfb = 0;
+    MN_HIP_TRY(hipMemcpyAsync(&nfb, cntr, 4, hipMemcpyDeviceToHost, s));
+    MN_HIP_TRY(hipStreamSynchronize(s));
+    if (knob("MN_BF16_DEBUG"))
+        fprintf(stderr, "cos_sweep_phase1: pre-sample %lld, cap %d, rows short of L1 %d\n",
+                (long long)m00, cap, nfb);
+    if (nfb == 0) return MN_OK;
+    // (d) the rows t0 left short: the list generator on them alone
+    const GramPlan pf = plan_gram(nfb, m0, L1, 1, 1);
+    const size_t gb = (size_t)nfb * d * 2, lb = (size_t)nfb * pf.S * pf.cap * sizeof(uint2);
+    char *g = (char *)scratch(kSlotX1Esc, gb + lb + (size_t)nfb * pf.S * 8 + (size_t)nfb * 4 + 1024);
+    MN_REQUIRE(g, MN_ENOMEM, "mn_knn_cos_bf16: phase-1 fallback allocation failed");
+    uint16_t *Xf = (uint16_t *)g;
+    uint2 *cbf = (uint2 *)(g + ((gb + 255) & ~(size_t)255));
+    int *bcf = (int *)((char *)cbf + ((lb + 255) & ~(size_t)255));
+    float *btf = (float *)(bcf + (size_t)nfb * pf.S);
+    float *invf = btf + (size_t)nfb * pf.S;
+    hipLaunchKernelGGL(k_gather_rows_bf16, dim3((unsigned)(((int64_t)nfb * (d / 8) + 255) / 256)),
+                       dim3(256), 0, s, X, d, xinv, fb_list, nfb, Xf, invf);
+    MN_KCHECK(s, "k_gather_rows_bf16");
+    const int64_t bqf = (nfb + BM - 1) / BM;
+    hipLaunchKernelGGL((k_gram_bf16<GM_COS, 0>), dim3((unsigned)(bqf * pf.S)), dim3(NT), 0, s, Xf,
+                       (int64_t)nfb, XR, m0, d, (int64_t)0, (int64_t)0, 0, invf, invp, L1, (int)pf.S,
+                       pf.chunk, pf.cap, cbf, bcf, btf);
+    MN_KCHECK(s, "k_gram_bf16<COS> (phase-1 fallback)");
+    hipLaunchKernelGGL(k_scatter_min, dim3((unsigned)((nfb + 255) / 256)), dim3(256), 0, s, fb_list,
+                       nfb, (int)pf.S, btf, btau1);
+    MN_KCHECK(s, "k_scatter_min");
+    return MN_OK;
 }
 
 // Two-phase generator for self graphs (see the header).  X [n][d] row-major
@@ -813,7 +978,10 @@ static int knn_cos_bf16_x1(const uint16_t *X, int64_t n, int32_t d, const mn_cos
     MN_REQUIRE(buf1 && meta1, MN_ENOMEM, "mn_knn_cos_bf16: phase-1 buffer allocation failed");
     int *cnt1 = (int *)meta1;
     float *btau1 = (float *)(meta1 + (size_t)n * pl.S * 4);
-    {
+    // phase 1 by sweep (round 4; SW_COS_SYM only — the query-major sweep reads
+    // the phase-1 lists; tuning build: MN_BF16_P1_SWEEP=0 keeps the list generator)
+    const bool p1s = sym_planned && tmaj && knob_int("MN_BF16_P1_SWEEP", 1) != 0;
+    auto list_phase1 = [&]() -> int {
         const int64_t bq = (n + BM - 1) / BM;
         hipLaunchKernelGGL((k_gram_bf16<GM_COS, 0>), dim3((unsigned)(bq * pl.S)), dim3(NT), 0, s, X,
                            n, XR, m0, d, (int64_t)0, (int64_t)0, 0, xinv, invp, L1, (int)pl.S,
@@ -822,6 +990,18 @@ static int knn_cos_bf16_x1(const uint16_t *X, int64_t n, int32_t d, const mn_cos
         hipLaunchKernelGGL(k_tau_cos, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, n,
                            (int)pl.S, btau1, xn, pm, tcos, tq_pos);
         MN_KCHECK(s, "k_tau_cos");
+        return MN_OK;
+    };
+    if (p1s) {
+        const int rc1 = cos_sweep_phase1(X, n, d, dp, nkb, pst, pm, XR, m0, L1, xn, xinv, invp, negn,
+                                         tcos, tq_pos, XK, btau1, flags + 6, fb_list, s);
+        if (rc1 != MN_OK) return rc1;
+        hipLaunchKernelGGL(k_tau_cos, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, n, 1,
+                           btau1, xn, pm, tcos, tq_pos);
+        MN_KCHECK(s, "k_tau_cos");
+    } else {
+        const int rc1 = list_phase1();
+        if (rc1 != MN_OK) return rc1;
     }
     tm.mark();
     // phase 2, SW_COS_SYM (default, MN_BF16_SYM=0: the query-major sweep):
@@ -852,6 +1032,11 @@ static int knn_cos_bf16_x1(const uint16_t *X, int64_t n, int32_t d, const mn_cos
         MN_HIP_TRY(hipStreamSynchronize(s));
         if (bad) {
             sym = false;
+            // the query-major sweep reads the sample lists: the list generator
+            if (p1s) {
+                const int rc1 = list_phase1();
+                if (rc1 != MN_OK) return rc1;
+            }
         } else {
             MN_HIP_TRY(sort_f32_pairs(key, skey, iota, pi, n, s));
         }
@@ -887,7 +1072,7 @@ static int knn_cos_bf16_x1(const uint16_t *X, int64_t n, int32_t d, const mn_cos
     MN_REQUIRE(buf2 && cnt2, MN_ENOMEM, "mn_knn_cos_bf16: sweep buffer allocation failed");
     if (sym) {
         const int nbk = (int)((n + ksw2::BC - 1) / ksw2::BC);
-        const std::vector<int4> tab = ksw2::sym_block_table(nbk, 256, 1);
+        const std::vector<int4> tab = ksw2::sym_block_table(nbk, 256, knob_int("MN_BF16_SYM_ORDER", 2));
         int4 *dtab = (int4 *)scratch(kSlotSymTab, tab.size() * sizeof(int4) + 64);
         MN_REQUIRE(dtab, MN_ENOMEM, "mn_knn_cos_bf16: block table allocation failed");
         MN_HIP_TRY(hipMemcpyAsync(dtab, tab.data(), tab.size() * sizeof(int4),
