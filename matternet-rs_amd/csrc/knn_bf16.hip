@@ -763,7 +763,10 @@ static thread_local mn_knn_stats t_bf16_stats{};
 // best cos~), the list generator's own output (an overflowing buffer gives a
 // lower threshold: more candidates; the certificate does not depend on it);
 // (d) rows with fewer than L1 buffered keys run the list generator alone.
-constexpr int CP1_L0 = 4, CP1_DIV = 8;
+// C5 (1M x 3072, same process, profiles/r04/r04_c5_p1_params.log): the list
+// generator 501 ms; (L0, div) = (4, 8) 430 ms (135k rows short), (6, 8) 375
+// (10k), (8, 8) 380, (8, 6) 396, (6, 12) 361 (1.5k short); outputs identical.
+constexpr int CP1_L0 = 6, CP1_DIV = 12;
 
 template <int NR>
 __global__ __launch_bounds__(256) void k_p1_select_cos(int64_t n, kb16::Perm pm, const int *__restrict__ cnt,
