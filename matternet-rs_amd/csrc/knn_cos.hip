@@ -146,31 +146,33 @@ __device__ __forceinline__ void load16(const double *p, bool vec, double (&o)[16
 }
 
 // The products are the reference's fl(a*b) in f64 (exact for f32 inputs).
-template <typename T>
+// PFD chunks of both profiles in flight ahead of the chain (registers)
+template <typename T, int PFD = 2>
 __device__ __forceinline__ double ordered_dot4(const T *__restrict__ a,
                                                const T *__restrict__ b, int64_t n,
                                                double (*buf)[4][CHP]) {
     const int lane = threadIdx.x & 63, g = lane >> 4, gl = lane & 15;
     const int64_t nfull = n / CH;
     const bool vec = ((((uintptr_t)a) | ((uintptr_t)b)) & 15) == 0;
-    T ra[2][16], rb[2][16];
+    T ra[PFD][16], rb[PFD][16];
     auto fetch = [&](int64_t c, T (&pa)[16], T (&pb)[16]) {
         const int64_t o = c * CH + 16 * gl;
         load16(a + o, vec, pa);
         load16(b + o, vec, pb);
     };
-    if (nfull > 0) fetch(0, ra[0], rb[0]);
-    if (nfull > 1) fetch(1, ra[1], rb[1]);
-    double acc = -0.0;
-    for (int64_t c0 = 0; c0 < nfull; c0 += 2) {
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
+    for (int h = 0; h < PFD; ++h)
+        if (nfull > h) fetch(h, ra[h], rb[h]);
+    double acc = -0.0;
+    for (int64_t c0 = 0; c0 < nfull; c0 += PFD) {
+#pragma unroll
+        for (int h = 0; h < PFD; ++h) {
             const int64_t c = c0 + h;
             if (c >= nfull) break;
-            double *bb = buf[h][g];
+            double *bb = buf[h & 1][g];
 #pragma unroll
             for (int u = 0; u < 16; ++u) bb[16 * gl + u] = (double)ra[h][u] * (double)rb[h][u];
-            if (c + 2 < nfull) fetch(c + 2, ra[h], rb[h]);
+            if (c + PFD < nfull) fetch(c + PFD, ra[h], rb[h]);
             __builtin_amdgcn_wave_barrier();
             acc = lds_chain_f64<CH>(acc, bb);
             __builtin_amdgcn_wave_barrier();
@@ -348,7 +350,7 @@ __global__ __launch_bounds__(256) void k_cos_exact(const T *__restrict__ XT, int
 
 // one wave per listed pair q: (node i = pi[q], candidate slot) -> dist[slot]
 // four listed pairs per wave, pair q = (node i, candidate slot) -> dist[slot]
-template <typename T>
+template <typename T, int PFD = 2>
 __global__ __launch_bounds__(256) void k_cos_exact_wave(const T *__restrict__ XT, int64_t n,
                                                         const int32_t *__restrict__ plist,
                                                         const int *__restrict__ pcount,
@@ -375,7 +377,7 @@ __global__ __launch_bounds__(256) void k_cos_exact_wave(const T *__restrict__ XT
     }
     const bool dot = act && denom > 1e-12;  // else cos = 0 without a dot
     const T *pa = XT + (int64_t)(dot ? i : 0) * n, *pb = XT + (int64_t)(dot ? j : 0) * n;
-    const double acc = ordered_dot4(pa, pb, n, buf[w]);
+    const double acc = ordered_dot4<T, PFD>(pa, pb, n, buf[w]);
     if ((threadIdx.x & 15) == 0 && act) dist[slot] = dot ? cos_dist(acc, nrm[i], nrm[j]) : 1.0;
 }
 
@@ -668,7 +670,13 @@ static int knn_cos_columns_impl(const T *X, int64_t n, int32_t f, const mn_cos_o
         if (L > kq)
             hipLaunchKernelGGL(k_extra_pairs, dim3(grid(f)), dim3(256), 0, s, cand, capx, f, L, kq,
                                delta, pi, flags + 1);
-        hipLaunchKernelGGL(k_cos_exact_wave<T>, dim3(grid((int64_t)f * L, 16)), dim3(256), 0, s, XT, n, pi,
+        // chunks in flight ahead of the chains: 4 (C3, same process,
+        // profiles/r04/r04_c3_pf_ab.log: exact pass 8.33-8.42 ms vs 8.44-8.68 at
+        // 2 — the chains are bound by their adds, not by the loads); tuning build: MN_COS_PF
+        const int pfd = knob_int("MN_COS_PF", 4);
+        auto kx = k_cos_exact_wave<T, 2>;
+        if (pfd == 4) kx = k_cos_exact_wave<T, 4>;
+        hipLaunchKernelGGL(kx, dim3(grid((int64_t)f * L, 16)), dim3(256), 0, s, XT, n, pi,
                            flags + 1, (int64_t)f * L, cand, L, nrm, cdist);
         hipLaunchKernelGGL(k_cos_finish, dim3(grid(f, 4)), dim3(256), 0, s, cand, cdist, gnext, f, L,
                            o->topk, o->eps, o->sigma, o->p, delta, out_idx, out_dist, out_w, flags,
