@@ -146,23 +146,24 @@ __device__ __forceinline__ void load16(const double *p, bool vec, double (&o)[16
 }
 
 // The products are the reference's fl(a*b) in f64 (exact for f32 inputs).
-// PFD chunks of both profiles in flight ahead of the chain (registers)
-template <typename T, int PFD = 2>
+// PFD chunks of both profiles in flight ahead of the chain (registers); SQ:
+// a == b (the norms: one load, the square)
+template <typename T, int PFD = 2, bool SQ = false>
 __device__ __forceinline__ double ordered_dot4(const T *__restrict__ a,
                                                const T *__restrict__ b, int64_t n,
                                                double (*buf)[4][CHP]) {
     const int lane = threadIdx.x & 63, g = lane >> 4, gl = lane & 15;
     const int64_t nfull = n / CH;
     const bool vec = ((((uintptr_t)a) | ((uintptr_t)b)) & 15) == 0;
-    T ra[PFD][16], rb[PFD][16];
+    T ra[PFD][16], rb[SQ ? 1 : PFD][16];
     auto fetch = [&](int64_t c, T (&pa)[16], T (&pb)[16]) {
         const int64_t o = c * CH + 16 * gl;
         load16(a + o, vec, pa);
-        load16(b + o, vec, pb);
+        if constexpr (!SQ) load16(b + o, vec, pb);
     };
 #pragma unroll
     for (int h = 0; h < PFD; ++h)
-        if (nfull > h) fetch(h, ra[h], rb[h]);
+        if (nfull > h) fetch(h, ra[h], rb[SQ ? 0 : h]);
     double acc = -0.0;
     for (int64_t c0 = 0; c0 < nfull; c0 += PFD) {
 #pragma unroll
@@ -171,8 +172,9 @@ __device__ __forceinline__ double ordered_dot4(const T *__restrict__ a,
             if (c >= nfull) break;
             double *bb = buf[h & 1][g];
 #pragma unroll
-            for (int u = 0; u < 16; ++u) bb[16 * gl + u] = (double)ra[h][u] * (double)rb[h][u];
-            if (c + PFD < nfull) fetch(c + PFD, ra[h], rb[h]);
+            for (int u = 0; u < 16; ++u)
+                bb[16 * gl + u] = (double)ra[h][u] * (double)(SQ ? ra[h][u] : rb[SQ ? 0 : h][u]);
+            if (c + PFD < nfull) fetch(c + PFD, ra[h], rb[SQ ? 0 : h]);
             __builtin_amdgcn_wave_barrier();
             acc = lds_chain_f64<CH>(acc, bb);
             __builtin_amdgcn_wave_barrier();
@@ -190,7 +192,7 @@ __global__ __launch_bounds__(64) void k_col_norms(const T *__restrict__ XT, int6
     const int g = threadIdx.x >> 4;
     const int i = blockIdx.x * 4 + g;
     const T *p = XT + (int64_t)min(i, f - 1) * n;
-    const double acc = ordered_dot4(p, p, n, buf);
+    const double acc = ordered_dot4<T, 4, true>(p, p, n, buf);
     if ((threadIdx.x & 15) == 0 && i < f) nrm[i] = __builtin_sqrt(acc);
 }
 
@@ -220,18 +222,24 @@ __global__ __launch_bounds__(256) void k_gram_f64(const T *__restrict__ X, int64
 #pragma unroll
         for (int b = 0; b < 2; ++b) acc[a][b] = f64x4{0.0, 0.0, 0.0, 0.0};
     const int lr = threadIdx.x >> 4, lc4 = (threadIdx.x & 15) * 4;  // 16 rows x 16 x 4 values
-    for (int64_t kb = k0; kb < k1; kb += GK) {
+    const int ca = bi * GT + lc4, cb = bj * GT + lc4;
+    // the next stage's rows are loaded while this stage computes (round 4b)
+    auto load = [&](int64_t kb, T (&va)[4], T (&vb)[4]) {
         const int64_t row = kb + lr;
-        T va[4] = {0, 0, 0, 0}, vb[4] = {0, 0, 0, 0};
+#pragma unroll
+        for (int u = 0; u < 4; ++u) va[u] = vb[u] = (T)0;
         if (row < k1) {
             const T *pr = X + row * f;
-            const int ca = bi * GT + lc4, cb = bj * GT + lc4;
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
                 va[u] = ca + u < f ? pr[ca + u] : (T)0;
                 vb[u] = cb + u < f ? pr[cb + u] : (T)0;
             }
         }
+    };
+    T va[4], vb[4];
+    if (k0 < k1) load(k0, va, vb);
+    for (int64_t kb = k0; kb < k1; kb += GK) {
         __syncthreads();
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
@@ -239,6 +247,7 @@ __global__ __launch_bounds__(256) void k_gram_f64(const T *__restrict__ X, int64
             Bs[lr][lc4 + u] = vb[u];
         }
         __syncthreads();
+        if (kb + GK < k1) load(kb + GK, va, vb);
 #pragma unroll
         for (int s = 0; s < GK / 4; ++s) {
             const int kr = s * 4 + (lane >> 4);
@@ -627,13 +636,15 @@ static int knn_cos_columns_impl(const T *X, int64_t n, int32_t f, const mn_cos_o
     tm.start(o->timing != 0, s);
     MN_HIP_TRY(hipMemsetAsync(G, 0, sizeof(double) * (size_t)f * f, s));
     MN_HIP_TRY(hipMemsetAsync(flags, 0, 64, s));
-    hipLaunchKernelGGL(k_transpose<T>, dim3(grid(n, 64), (unsigned)((f + 63) / 64)), dim3(256), 0, s,
-                       X, n, f, XT);
-    // the exact norms (768 latency-bound chains) run on the side stream while
-    // the Gram occupies the MFMAs
+    // the transpose and the exact norms (768 latency-bound chains) run on the
+    // side stream while the Gram (it reads X itself) occupies the MFMAs
+    // (round 4b: the transpose was ahead of the Gram on the main stream)
     hipStream_t side = side_stream();
     MN_REQUIRE(side, MN_EHIP, "mn_knn_cos_columns_f32: side stream creation failed");
     MN_HIP_TRY(stream_wait(side, s));
+    hipLaunchKernelGGL(k_transpose<T>, dim3(grid(n, 64), (unsigned)((f + 63) / 64)), dim3(256), 0, side,
+                       X, n, f, XT);
+    MN_KCHECK(side, "k_transpose");
     hipLaunchKernelGGL(k_col_norms<T>, dim3((unsigned)((f + 3) / 4)), dim3(64), 0, side, XT, n, f, nrm);
     MN_KCHECK(side, "k_col_norms");
     const int nr = (f + 63) / 64;

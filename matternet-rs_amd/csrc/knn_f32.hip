@@ -2874,18 +2874,16 @@ ShardPlan shard_plan(int64_t N, int d, int k, int world) {
 
 static void shard_prep(const float *X, int64_t n, int d, int dp, const int *pm, uint16_t *R,
                        float *nv, float *hcv, float *hv, float *rv, unsigned *cmax, int *flags,
-                       hipStream_t s) {
+                       hipStream_t s, uint16_t *K = nullptr, int tm = 0) {
     if (n == 0) return;
     const bool vec4 = (d % 4 == 0) && ((uintptr_t)X % 16 == 0);
     const int64_t blocks = std::min<int64_t>((n + 7) / 8, 16384);
     if (vec4)
         hipLaunchKernelGGL(knn::k_prep_x1<true>, dim3((unsigned)blocks), dim3(256), 0, s, X, n, d, dp,
-                           pm, R, (uint16_t *)nullptr, nv, hcv, hv, rv, cmax, flags + 3, 1, 0,
-                           (unsigned *)nullptr);
+                           pm, R, K, nv, hcv, hv, rv, cmax, flags + 3, 1, tm, (unsigned *)nullptr);
     else
         hipLaunchKernelGGL(knn::k_prep_x1<false>, dim3((unsigned)blocks), dim3(256), 0, s, X, n, d,
-                           dp, pm, R, (uint16_t *)nullptr, nv, hcv, hv, rv, cmax, flags + 3, 1, 0,
-                           (unsigned *)nullptr);
+                           dp, pm, R, K, nv, hcv, hv, rv, cmax, flags + 3, 1, tm, (unsigned *)nullptr);
 }
 
 int shard_phase1(const float *X_all, const ShardPlan &pl, int64_t row0, int64_t nl, hipStream_t s,
@@ -2903,10 +2901,25 @@ int shard_phase1(const float *X_all, const ShardPlan &pl, int64_t row0, int64_t 
     float *cnv = dlt + nl, *chc = cnv + m0;
     unsigned *cmax = (unsigned *)flags;
     MN_HIP_TRY(hipMemsetAsync(flags, 0, 128, s));
+    // phase 1 as knn_x1's symmetric path runs it (round 4b: the sweep with a
+    // pre-sample threshold, sweep_phase1; tuning build: MN_P1_SWEEP=0 keeps the
+    // list generator): tile-major copies of the rows and the sample
+    const bool p1s = knob_int("MN_P1_SWEEP", 1) != 0;
+    const int nkb = pl.nkb, pst1 = nkb + 1;
+    const int64_t kbw1 = (int64_t)pst1 * 32;
+    uint16_t *QK = nullptr, *CKs = nullptr;
+    int *fbl = nullptr;
+    if (p1s) {
+        QK = (uint16_t *)scratch(kSlotX1QK, (size_t)((nl + 255) / 256 * 256) * kbw1 * 2 + 64);
+        CKs = (uint16_t *)scratch(kSlotGeneric3, (size_t)((m0 + 255) / 256 * 256) * kbw1 * 2 + 64);
+        fbl = (int *)scratch(kSlotFallback, sizeof(int) * (size_t)nl + 64);
+        MN_REQUIRE(QK && CKs && fbl, MN_ENOMEM, "shard_phase1: sweep copy allocation failed");
+    }
     // maxima over the rows and the sample (both enter the phase-1 bound)
     shard_prep(X_all + row0 * (int64_t)d, nl, d, dp, nullptr, QR, qn_o, nullptr, qhn, qrn, cmax,
-               flags, s);
-    shard_prep(X_all, m0, d, dp, perm, CR, cnv, chc, nullptr, nullptr, cmax, flags, s);
+               flags, s, QK, p1s ? pst1 : 0);
+    shard_prep(X_all, m0, d, dp, perm, CR, cnv, chc, nullptr, nullptr, cmax, flags, s, CKs,
+               p1s ? pst1 : 0);
     MN_KCHECK(s, "k_prep_x1<shard>");
     int hflags[8] = {0};
     MN_HIP_TRY(hipMemcpyAsync(hflags, flags, 32, hipMemcpyDeviceToHost, s));
@@ -2914,6 +2927,17 @@ int shard_phase1(const float *X_all, const ShardPlan &pl, int64_t row0, int64_t 
     MN_REQUIRE(hflags[3] == 0, MN_ENONFINITE,
                "mn_knn_sharded: input contains NaN/inf (the reference panics in partial_cmp().unwrap())");
     if (hflags[4] != 0) return 1;  // too large for the bf16 bound: the per-shard path
+    if (p1s) {
+        float *bt = (float *)scratch(kSlotListMeta, (size_t)nl * 4 + 64);
+        MN_REQUIRE(bt, MN_ENOMEM, "shard_phase1: threshold allocation failed");
+        const int rc1 = sweep_phase1(QR, QK, nl, CR, CKs, m0, d, dp, nkb, pst1, row0, pl.L1, qn_o, qhn,
+                                     qrn, cnv, chc, cmax, tq, tau0_o, dlt, bt, fbl, flags + 20, s);
+        if (rc1 != MN_OK) return rc1;
+        hipLaunchKernelGGL(k_tau_x1, dim3((unsigned)((nl + 255) / 256)), dim3(256), 0, s, nl, 1, bt,
+                           qn_o, qhn, qrn, cmax, d, dp, tq, tau0_o, dlt, (unsigned *)nullptr);
+        MN_KCHECK(s, "k_tau_x1<shard>");
+        return MN_OK;
+    }
     const kb16::GramPlan gp = kb16::plan_gram(nl, m0, pl.L1, 1, 1);
     const size_t nbuf1 = (size_t)nl * gp.S * gp.cap;
     uint2 *cbuf1 = (uint2 *)scratch(kSlotLists, nbuf1 * sizeof(uint2) + 64);
