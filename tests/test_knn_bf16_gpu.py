@@ -151,6 +151,25 @@ def test_two_phase_edge_rows_and_one_phase_agree(monkeypatch):
     exact((i, d, w), (i1, d1, w1))
 
 
+def test_phase1_sweep_matches_list_generator(monkeypatch):
+    """Phase 1 by sweep (round 4b, knn_bf16.hip cos_sweep_phase1) vs the list
+    generator (MN_BF16_P1_SWEEP=0), and with a pre-sample list of 2
+    (MN_BF16_P1_L0) that leaves many rows to the fallback: bit-exact vs the
+    oracle every time."""
+    Xt, Xf = bf16_rows(datagen.clustered(12000, 96, seed=31, blobs=20, dup_frac=0.01,
+                                         zero_frac=0.002))
+    ref = O.knn_cos(Xf, 16)
+    with _lib.use_tuning():
+        for env in ({}, {"MN_BF16_P1_L0": "2"}, {"MN_BF16_P1_SWEEP": "0"}):
+            for kk in ("MN_BF16_P1_L0", "MN_BF16_P1_SWEEP"):
+                monkeypatch.delenv(kk, raising=False)
+            for kk, vv in env.items():
+                monkeypatch.setenv(kk, vv)
+            i, dd, w, st = hip(Xt, 16)
+            assert st["sample_rows"] > 0, (env, st)
+            exact((i, dd, w), ref)
+
+
 @pytest.mark.parametrize("n,d,topk", [(2048 + 1024, 768, 32), (9000, 40, 3), (4500, 3072, 64)])
 def test_two_phase_shapes(n, d, topk):
     """two-phase at the smallest size it runs at, a d that is not a multiple

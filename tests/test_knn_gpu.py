@@ -282,6 +282,29 @@ def test_bf16x1_symmetric_sweep_matches_query_major(kind, monkeypatch):
     assert_exact(idx0, dist0, ridx, rdist)
 
 
+@pytest.mark.parametrize("kind", ["uniform", "clustered"])
+def test_phase1_sweep_matches_list_generator(kind, monkeypatch):
+    """Phase 1 by sweep (round 4b, knn_f32.hip sweep_phase1: pre-sample list
+    generator -> threshold, SW_L2 sweep of the sample, exact L1-th key select,
+    the list generator for the rows left short) vs the list generator over the
+    whole sample (MN_P1_SWEEP=0): the same thresholds up to rounding, graphs
+    bit-exact vs the oracle either way; a pre-sample list of 2 (MN_P1_L0)
+    leaves many rows short and forces the fallback."""
+    n, d, k = 40_000, 64, 16
+    X = (datagen.uniform(n, d, seed=21) if kind == "uniform"
+         else datagen.clustered(n, d, seed=22, blobs=16, dup_frac=0.01, zero_frac=0.002))
+    ridx, rdist = O.knn_l2sq(X, k)
+    with _lib.use_tuning():
+        for env in ({}, {"MN_P1_L0": "2"}, {"MN_P1_SWEEP": "0"}):
+            for kk in ("MN_P1_L0", "MN_P1_SWEEP"):
+                monkeypatch.delenv(kk, raising=False)
+            for kk, vv in env.items():
+                monkeypatch.setenv(kk, vv)
+            idx, dist, st = hip_knn(X, k, algo="bf16x1", timing=True)
+            assert st["sweep_slices"] == -1 and st["sample_rows"] > 0, (env, st)
+            assert_exact(idx, dist, ridx, rdist)
+
+
 def test_uncertified_rows_batched_fallback():
     """Rows no certificate settles (all-zero rows: exact ties far beyond k)
     against a corpus >= 2^16 go through the batched split-generator pass
