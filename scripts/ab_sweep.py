@@ -33,9 +33,9 @@ res = {v: [] for v in VERS}
 probe = {v: [] for v in VERS}
 for r in range(rounds):
     for v in VERS:
-        for k_ in {kv.split("=")[0] for vv in VERS for kv in vv.split(",")}:
+        for k_ in {kv.split("=")[0] for vv in VERS for kv in vv.replace("+", ",").split(",")}:
             os.environ.pop(k_, None)  # a variant sets only its own keys
-        for kv in v.split(","):
+        for kv in v.replace("+", ",").split(","):
             k_, val = kv.split("=")
             os.environ[k_] = val
         os.environ.pop("MN_X1_PROBE", None)
