@@ -608,7 +608,10 @@ inline SweepPlan plan_sweep(int64_t nq, int64_t nc2, double expect) {
 //     structure, and the full groups (equal tile counts) spread evenly.
 //     world = 1 is order 2.
 inline std::vector<int4> sym_block_table_share(int nbk, int TPB, int rank, int world) {
-    constexpr int GR = 4, GC = 8, NX = 8;
+    // group shape GR x GC = 32 (tuning build: MN_SYM_GR in {2, 4, 8, 16})
+    const int gre = knob_int("MN_SYM_GR", 4);
+    const int GR = (gre == 2 || gre == 8 || gre == 16) ? gre : 4, GC = 32 / GR;
+    constexpr int NX = 8;
     const int T8 = std::max(1, TPB / GC);  // tiles per block
     const int W = GC * T8;                 // column range of a group
     // groups in time order: column range outer (shared across XCDs), row band
