@@ -607,10 +607,13 @@ inline SweepPlan plan_sweep(int64_t nq, int64_t nc2, double expect) {
 //     runs on exactly one rank, each rank's share keeps the XCD-group
 //     structure, and the full groups (equal tile counts) spread evenly.
 //     world = 1 is order 2.
-inline std::vector<int4> sym_block_table_share(int nbk, int TPB, int rank, int world) {
-    // group shape GR x GC = 32 (tuning build: MN_SYM_GR in {2, 4, 8, 16})
-    const int gre = knob_int("MN_SYM_GR", 4);
-    const int GR = (gre == 2 || gre == 8 || gre == 16) ? gre : 4, GC = 32 / GR;
+//   group shape gr x 32/gr (row blocks x column phases): 4 x 8 by default;
+//   C2's knn_x1 uses 2 x 16 (d = 768: 754 vs 759-760 ms same process, 8 x 4
+//   767-769, 16 x 2 785, 1 x 32 755-782; C5's d = 3072 prefers 4 x 8: 2711 vs
+//   2803-2817 ms — profiles/r04/r04_gr_ab*.log); tuning build: MN_SYM_GR
+inline std::vector<int4> sym_block_table_share(int nbk, int TPB, int rank, int world, int gr = 4) {
+    const int gre = knob_int("MN_SYM_GR", gr);
+    const int GR = (gre == 1 || gre == 2 || gre == 8 || gre == 16) ? gre : 4, GC = 32 / GR;
     constexpr int NX = 8;
     const int T8 = std::max(1, TPB / GC);  // tiles per block
     const int W = GC * T8;                 // column range of a group
@@ -670,8 +673,8 @@ inline std::vector<int4> sym_block_table_share(int nbk, int TPB, int rank, int w
     return tab;
 }
 
-inline std::vector<int4> sym_block_table(int nbk, int TPB, int order) {
-    if (order == 2) return sym_block_table_share(nbk, TPB, 0, 1);
+inline std::vector<int4> sym_block_table(int nbk, int TPB, int order, int gr = 4) {
+    if (order == 2) return sym_block_table_share(nbk, TPB, 0, 1, gr);
     std::vector<int4> tab;
     tab.reserve((size_t)nbk * ((size_t)nbk / TPB + 2) / 2 + 16);
     if (order == 1) {

@@ -2517,7 +2517,7 @@ static int knn_x1(const float *Q, int64_t nq, const float *C, int64_t nc, int32_
             const int TPB = (tpe2 && *tpe2) ? std::max(1, atoi(tpe2)) : 256;
             const char *ore = knob("MN_SYM_ORDER");
             const int order = (ore && *ore) ? atoi(ore) : 2;
-            const std::vector<int4> tab = ksw2::sym_block_table(nbk, TPB, order);
+            const std::vector<int4> tab = ksw2::sym_block_table(nbk, TPB, order, 2);  // 2 x 16 groups
             int4 *dtab = (int4 *)scratch(kSlotSymTab, tab.size() * sizeof(int4) + 64);
             MN_REQUIRE(dtab, MN_ENOMEM, "mn_knn: block table allocation failed");
             MN_HIP_TRY(hipMemcpyAsync(dtab, tab.data(), tab.size() * sizeof(int4),
