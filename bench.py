@@ -137,16 +137,15 @@ def main():
     for i in range(a.warmup):
         step()
         if world > 1 and i == 0:
-            # time budget (N>1: every rank does N x the C2 work per step): one
-            # warmup step measured, then warmup + steps capped to fit
+            # time budget (N>1: every rank does N x the C2 work per step): the
+            # first warmup step measured, the timed steps capped to fit (the
+            # warmup runs exactly as requested)
             torch.cuda.synchronize()
             tw = torch.tensor([time.perf_counter() - t_w], dtype=torch.float64, device=dev)
             dist.all_reduce(tw, op=dist.ReduceOp.MAX)
             per = float(tw.item())
-            left = max(a.time_budget_s - per, 0.0)
-            a.warmup = 1
+            left = max(a.time_budget_s - per * a.warmup, 0.0)
             a.steps = max(1, min(a.steps, int(left / max(per, 1e-3))))
-            break
     if world > 1 and warm_req == 0:
         # no warmup step to measure: budget on the estimate of N x ~2 s per step
         a.steps = max(1, min(a.steps, int(a.time_budget_s / (2.0 * world))))
@@ -444,11 +443,12 @@ def c3_legs(S, X, idx, dist, k):
 
 def c4_sim_leg(S, _lib, L, a, dev, stream, R=8):
     """BASELINE.json configs[3] on ONE GPU: 8M x 768 (8 ranks x the per-GPU
-    rows) through mn_knn_sharded_sim_f32 — every rank's stages of the symmetric
-    sharded build run in turn on this device (the exchange a strided read), so
-    a rank's share of the real 8-GPU build = its stage A + B + C time here,
-    plus the all-gathers (X: 7/8 of 24.6 GB a rank over xGMI; tau0 / norms
-    64 MB) and the list exchange (2 GB), which the simulation does not run.
+    rows) through mn_knn_sharded_sim_f32 — mn_knn_sharded_f32's driver over
+    the loopback transport: every rank's stages of the symmetric sharded
+    build run in turn on this device, the collectives as device copies, so a
+    rank's share of the real 8-GPU build = its stage A + B + C time here,
+    plus the RCCL all-gathers (X: 7/8 of 24.6 GB a rank over xGMI; tau0 /
+    norms 64 MB) and the list exchange (2 GB), which are not in the shares.
     One row per shard checked bit-exact against the oracle over all rows."""
     from oracle import oracle as O
     from surfface_hip.dist import knn_sharded_sim
@@ -474,7 +474,8 @@ def c4_sim_leg(S, _lib, L, a, dev, stream, R=8):
                             "C_merge_certify": round(float(ms[:, 2].max()), 1)},
            "pairs_per_s_at_max_share": n_tot * float(n_tot) / mx,
            "excluded": "RCCL all-gathers (X 21.5 GB received a rank, thresholds) and the "
-                       "partial-list exchange (2 GB): not run by the simulation",
+                       "partial-list exchange (2 GB): device copies of the loopback transport "
+                       "here, outside the stage shares",
            "n_uncertified": st["n_uncertified"], "n_candidates": st["n_candidates"],
            "sim_wall_s": round(wall, 2)}
     if a.c5_parity_rows > 0:

@@ -36,6 +36,8 @@ extern "C" {
 #define MN_ECAP (-4)       /* output capacity too small (nnz_out holds need)   */
 #define MN_EHIP (-5)       /* HIP runtime error                                 */
 #define MN_ENOTSUP (-6)    /* unsupported parameter combination                 */
+#define MN_ECOMM (-7)      /* a collective failed or missed its deadline; the
+                              RCCL communicator was aborted (mn_rccl_set_timeout) */
 
 /* ---------------------------------------------------------------------- */
 /* Library / memory plumbing                                              */
@@ -180,22 +182,32 @@ int mn_knn_l2_f64(const void *Q, int64_t nq, const void *C, int64_t nc, int32_t 
  * the exchange, mn_knn_merge_f32.  out_idx / out_dist [n_local][k]: the
  * rank's rows of the global graph, global ids, bit-identical to a single-GPU
  * mn_knn_f32 of X.  opts as mn_knn_f32 (opts->stream is used for every
- * operation; timing 1: mn_knn_last_stats has ms_sample = all-gather + stage
- * A, ms_sweep = the sweep share, ms_rerank = the exchange, ms_fallback = the
- * merge).  Collective: every rank calls it with the same n_local, d and
- * opts.  <= 16 ranks. */
+ * operation; timing 1: mn_knn_last_stats has ms_norms = the all-gathers,
+ * ms_sample = stage A, ms_sweep = stage B (the per-shard form: its query
+ * passes), ms_rerank = the exchange, ms_fallback = stage C (the merge),
+ * ms_total = the call).  Collective: every rank calls it with the same
+ * n_local, d and opts.  <= 16 ranks.  Failure detection: a status agreement
+ * precedes every collective phase (a rank whose stage failed returns its own
+ * code, the others MN_EHIP "another rank failed"), and every collective is
+ * waited for by polling the stream and ncclCommGetAsyncError against the
+ * mn_rccl_set_timeout deadline: an RCCL error or a peer that never arrives
+ * ends the call with MN_ECOMM after ncclCommAbort (destroying that
+ * communicator afterwards is a no-op; later calls on it return MN_EINVAL). */
 int mn_knn_sharded_f32(const float *X_shard, int64_t n_local, int32_t d, void *rccl_comm,
                        const mn_knn_opts *opts, int64_t query_chunk, int32_t *out_idx,
                        float *out_dist);
-/* The symmetric form of mn_knn_sharded_f32 with `world` ranks simulated on
- * ONE device (tests and single-GPU measurement of one rank's share): X_all
- * [n_tot][d] (device) stands for the all-gathered shards (n_tot a multiple of
- * world <= 16); every rank's stages run in turn and the exchange is a strided
- * read.  out_idx / out_dist [n_tot][k]: the global graph, bit-identical to
- * mn_knn_f32.  rank_ms (host, may be NULL) [world][3]: per rank the stage A
- * (phase-1 thresholds), stage B (sweep share + partial re-rank) and stage C
- * (merge + certify + exact scan) milliseconds.  MN_ENOTSUP when the symmetric
- * form does not apply (the RCCL entry then runs its per-shard form). */
+/* The same sharded build with `world` ranks on ONE device (tests and
+ * single-GPU measurement of one rank's share): the driver of
+ * mn_knn_sharded_f32 over a loopback transport — rank r on its own stream,
+ * its stages run in turn, device copies for the all-gathers and the
+ * exchange (the same buffer layout and offsets as over RCCL).  X_all
+ * [n_tot][d] (device) holds the shards (rank r's at r n_tot / world; n_tot a
+ * multiple of world <= 16).  Either form, chosen as mn_knn_sharded_f32
+ * chooses it for world ranks.  out_idx / out_dist [n_tot][k]: the global
+ * graph, bit-identical to mn_knn_f32.  rank_ms (host, may be NULL)
+ * [world][3]: per rank the stage A (phase-1 thresholds), stage B (sweep share
+ * + partial re-rank; per-shard form: the query passes) and stage C (merge +
+ * certify + exact scan) milliseconds. */
 int mn_knn_sharded_sim_f32(const float *X_all, int64_t n_tot, int32_t d, int32_t world,
                            const mn_knn_opts *opts, int32_t *out_idx, float *out_dist,
                            float *rank_ms);
@@ -213,6 +225,9 @@ int mn_rccl_unique_id(void *out_128_bytes);
 int mn_rccl_comm_init(const void *unique_id_128_bytes, int32_t world, int32_t rank,
                       void **comm_out);
 int mn_rccl_comm_destroy(void *comm);
+/* Process-wide deadline (seconds, default 600) for one collective of
+ * mn_knn_sharded_f32, including the wait for the slowest peer's stage. */
+int mn_rccl_set_timeout(double seconds);
 
 /* Statistics of the calling thread's last mn_knn_* call. */
 int mn_knn_last_stats(mn_knn_stats *out);

@@ -1831,6 +1831,7 @@ static int fb_split_scan(const float *Q, const float *C, int64_t nc, int d, int6
 // 5. merge of exact per-shard lists (row-sharded multi-GPU build)
 // ---------------------------------------------------------------------------
 constexpr int MAX_PARTS = 16;
+static_assert(MAX_PARTS == kMaxShardRanks, "the sharded build merges up to MAX_PARTS parts");
 
 __global__ __launch_bounds__(256) void k_merge_parts(const int32_t *__restrict__ pidx,
                                                      const float *__restrict__ pdist, int P,

@@ -1,28 +1,47 @@
 // shard.hip — the row-sharded multi-GPU kNN build behind one C entry
-// (SURVEY.md §8(b) `mn_knn_sharded_f32`, §8(e)) on a caller-owned RCCL
-// communicator: one process (or thread) per GPU, each holding its row shard.
+// (SURVEY.md §8(b) `mn_knn_sharded_f32`, §8(e)): one process (or thread) per
+// GPU, each holding its row shard, on a caller-owned RCCL communicator.
 //
-// Symmetric form (round 4; self kNN, L2^2, the bf16x1 generator applies):
-//   1. ncclAllGather of the shards -> X_all resident on every rank;
+// ONE driver (sharded_drive) runs the build for the ranks a call drives over a
+// Transport that carries its collectives:
+//   * RcclTransport — one rank, the caller's communicator over xGMI; every
+//     collective is waited for by polling the stream and ncclCommGetAsyncError
+//     against a deadline (mn_rccl_set_timeout), so a peer that dies inside a
+//     collective ends the call with MN_ECOMM (communicator aborted) instead of
+//     hanging every other rank;
+//   * LoopbackTransport — all R ranks of a simulated node on ONE device, each
+//     on its own stream, device copies standing in for the collectives
+//     (mn_knn_sharded_sim_f32: tests and single-GPU measurement of a share).
+// The buffer layout, the exchange offsets, the in-place all-gathers and the
+// status agreement are therefore the same code under both.
+//
+// Symmetric form (self kNN, L2^2, the bf16x1 generator applies, world > 1):
+//   1. all-gather of the shards -> X_all resident on every rank;
 //   2. stage A: tau0 of the rank's rows against the global phase-1 sample;
-//      ncclAllGather of tau0 and the row norms;
+//      in-place all-gathers of tau0 and the row norms;
 //   3. stage B: every rank builds the same Tf order and fp16 copy of all N
 //      rows and sweeps ITS share of the symmetric block table (every
-//      unordered pair of tiles once over the whole node — half the Gram of
-//      the per-shard form), then re-ranks every row in partial mode;
-//   4. grouped ncclSend/ncclRecv: each row's owner receives the R partial lists;
+//      unordered pair of tiles once over the whole node), then re-ranks every
+//      row in partial mode -> part lists of all rows [N][k];
+//   4. exchange: each row's owner receives the R part lists of its rows
+//      ([R][n_local][k], part p = the lists rank p computed);
 //   5. stage C: merge + certify (the certificate of the single-GPU sweep:
 //      the union of the parts' admitted candidates is the same set), exact
 //      split scan of the rare uncertified rows against X_all.
 // Per-shard form (other metrics / generators, or when the symmetric form
 // does not apply — decided collectively):
-//   exact per-shard top-k of all N queries against the resident shard
+//   exact per-shard top-k of all N queries against the rank's shard
 //   (mn_knn_f32_qc, query chunks), the exchange, mn_knn_merge_f32.
 // Both are exact: bit-identical to a single-GPU mn_knn_f32 of X.
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <atomic>
+#include <chrono>
 #include <cstring>
+#include <mutex>
+#include <set>
+#include <thread>
 #include <vector>
 
 #include "common.hpp"
@@ -37,6 +56,25 @@
             return MN_EHIP;                                                        \
         }                                                                          \
     } while (0)
+
+namespace {
+
+using mn::set_error;
+
+// process-wide deadline of one collective (mn_rccl_set_timeout)
+std::atomic<double> g_timeout_s{600.0};
+
+// communicators this library aborted after a failed / timed-out collective:
+// ncclCommAbort frees them, so mn_rccl_comm_destroy must not touch them again
+std::mutex g_abort_mu;
+std::set<void *> g_aborted;
+
+bool comm_aborted(void *c) {
+    std::lock_guard<std::mutex> g(g_abort_mu);
+    return g_aborted.count(c) != 0;
+}
+
+}  // namespace
 
 extern "C" {
 
@@ -58,6 +96,11 @@ int mn_rccl_comm_init(const void *unique_id_128_bytes, int32_t world, int32_t ra
     std::memcpy(&id, unique_id_128_bytes, sizeof(id));
     ncclComm_t c = nullptr;
     MN_NCCL_TRY(ncclCommInitRank(&c, world, id, rank));
+    {
+        // a new communicator may reuse the address of an aborted one
+        std::lock_guard<std::mutex> g(g_abort_mu);
+        g_aborted.erase((void *)c);
+    }
     *comm_out = (void *)c;
     return MN_OK;
 }
@@ -65,15 +108,24 @@ int mn_rccl_comm_init(const void *unique_id_128_bytes, int32_t world, int32_t ra
 int mn_rccl_comm_destroy(void *comm) {
     mn::clear_error();
     if (!comm) return MN_OK;
+    {
+        std::lock_guard<std::mutex> g(g_abort_mu);
+        if (g_aborted.erase(comm)) return MN_OK;  // already released by ncclCommAbort
+    }
     MN_NCCL_TRY(ncclCommDestroy((ncclComm_t)comm));
+    return MN_OK;
+}
+
+int mn_rccl_set_timeout(double seconds) {
+    mn::clear_error();
+    MN_REQUIRE(seconds > 0.0, MN_EINVAL, "mn_rccl_set_timeout: seconds must be > 0");
+    g_timeout_s.store(seconds);
     return MN_OK;
 }
 
 }  // extern "C"
 
 namespace {
-
-using mn::set_error;
 
 struct DevBufs {
     std::vector<void *> v;
@@ -93,41 +145,483 @@ bool sym_applies(const mn::ShardPlan &pl, const mn_knn_opts *o) {
            (o->algo == MN_KNN_AUTO || o->algo == MN_KNN_BF16X1);
 }
 
-// the per-rank status agreement before each collective phase: max over ranks
-// of (0 ok, 1 per-shard form, 2 error) — a rank that failed must not leave
-// the others waiting in a collective
-int agree(ncclComm_t c, hipStream_t s, int *dflag, int mine, int *out) {
-    if (hipMemcpyAsync(dflag, &mine, 4, hipMemcpyHostToDevice, s) != hipSuccess) return MN_EHIP;
-    if (ncclAllReduce(dflag, dflag, 1, ncclInt32, ncclMax, c, s) != ncclSuccess) {
-        set_error("ncclAllReduce of the shard status failed");
-        return MN_EHIP;
+// ---- transports -------------------------------------------------------------
+
+// The collectives of the sharded build for the ranks one call drives ("local
+// ranks" l = 0 .. nlocal-1, global rank rank(l)).  Buffers are per local rank;
+// sizes in bytes.  Every call returns with its data in place (or an error).
+class Transport {
+  public:
+    virtual ~Transport() = default;
+    virtual int world() const = 0;
+    virtual int nlocal() const = 0;
+    virtual int rank(int l) const = 0;
+    virtual hipStream_t stream(int l) const = 0;
+    // local rank l's stage work has been issued on stream(l)
+    virtual int stage_done(int l) = 0;
+    // recv[l] [world][bytes] <- every rank's send; in place when send[l] ==
+    // recv[l] + rank(l) * bytes
+    virtual int all_gather(const void *const *send, void *const *recv, size_t bytes,
+                           const char *what) = 0;
+    // for each of `na` arrays: block p of send[l] (bytes at p * bytes) goes to
+    // rank p, which receives it as block rank(l) of its recv
+    virtual int all_to_all(int na, const void *const *const *send, void *const *const *recv,
+                           size_t bytes, const char *what) = 0;
+    // *out = max over every rank of mine[l] (0 ok, 1 per-shard form, 2 error)
+    virtual int agree(const int *mine, int *out) = 0;
+};
+
+#ifdef MN_TUNING
+__global__ void k_stall(uint64_t ticks) {  // fault injection (tuning build only)
+    const uint64_t t0 = wall_clock64();
+    while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(127);
+}
+#endif
+
+class RcclTransport final : public Transport {
+  public:
+    RcclTransport(ncclComm_t c, hipStream_t s) : c_(c), s_(s), timeout_(g_timeout_s.load()) {}
+    ~RcclTransport() override {
+        if (pin_) (void)hipHostFree(pin_);
     }
-    if (hipMemcpyAsync(out, dflag, 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
-        hipStreamSynchronize(s) != hipSuccess)
-        return MN_EHIP;
-    return MN_OK;
+    int init() {
+        MN_NCCL_TRY(ncclCommCount(c_, &world_));
+        MN_NCCL_TRY(ncclCommUserRank(c_, &rank_));
+        MN_HIP_TRY(hipHostMalloc((void **)&pin_, 64, hipHostMallocDefault));
+        if (hipMalloc((void **)&dflag_, 64) != hipSuccess) {
+            set_error("mn_knn_sharded_f32: device allocation failed");
+            return MN_ENOMEM;
+        }
+        bufs_.v.push_back(dflag_);
+        // tuning build: stall the stream before the first collective (tests of
+        // the deadline: the call must end with MN_ECOMM, not hang)
+#ifdef MN_TUNING
+        const int stall_ms = mn::knob_int("MN_SHARD_STALL_MS", 0);
+        if (stall_ms > 0) {
+            int dev = 0, khz = 0;
+            MN_HIP_TRY(hipGetDevice(&dev));
+            MN_HIP_TRY(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev));
+            hipLaunchKernelGGL(k_stall, dim3(1), dim3(64), 0, s_, (uint64_t)stall_ms * (uint64_t)khz);
+            MN_HIP_TRY(hipGetLastError());
+        }
+#endif
+        return MN_OK;
+    }
+    int world() const override { return world_; }
+    int nlocal() const override { return 1; }
+    int rank(int) const override { return rank_; }
+    hipStream_t stream(int) const override { return s_; }
+    int stage_done(int) override { return MN_OK; }
+
+    int all_gather(const void *const *send, void *const *recv, size_t bytes,
+                   const char *what) override {
+        const ncclResult_t r = ncclAllGather(send[0], recv[0], bytes, ncclChar, c_, s_);
+        if (r != ncclSuccess) return fail(what, ncclGetErrorString(r));
+        return wait(what);
+    }
+    int all_to_all(int na, const void *const *const *send, void *const *const *recv, size_t bytes,
+                   const char *what) override {
+        ncclResult_t r = ncclGroupStart();
+        for (int a = 0; a < na && r == ncclSuccess; ++a)
+            for (int p = 0; p < world_ && r == ncclSuccess; ++p) {
+                r = ncclSend((const char *)send[a][0] + (size_t)p * bytes, bytes, ncclChar, p, c_, s_);
+                if (r == ncclSuccess)
+                    r = ncclRecv((char *)recv[a][0] + (size_t)p * bytes, bytes, ncclChar, p, c_, s_);
+            }
+        const ncclResult_t r2 = ncclGroupEnd();
+        if (r != ncclSuccess || r2 != ncclSuccess)
+            return fail(what, ncclGetErrorString(r != ncclSuccess ? r : r2));
+        return wait(what);
+    }
+    // pinned host flag: every copy is asynchronous, so the only blocking
+    // point is the polled wait
+    int agree(const int *mine, int *out) override {
+        pin_[0] = mine[0];
+        MN_HIP_TRY(hipMemcpyAsync(dflag_, pin_, 4, hipMemcpyHostToDevice, s_));
+        const ncclResult_t r = ncclAllReduce(dflag_, dflag_, 1, ncclInt32, ncclMax, c_, s_);
+        if (r != ncclSuccess) return fail("ncclAllReduce of the shard status", ncclGetErrorString(r));
+        MN_HIP_TRY(hipMemcpyAsync(pin_ + 1, dflag_, 4, hipMemcpyDeviceToHost, s_));
+        const int rc = wait("the shard status all-reduce");
+        if (rc != MN_OK) return rc;
+        *out = pin_[1];
+        return MN_OK;
+    }
+
+  private:
+    // the stream drained, or the communicator aborted: an RCCL async error,
+    // or no completion before the deadline (a peer died or stalled)
+    int wait(const char *what) {
+        using clk = std::chrono::steady_clock;
+        const auto t0 = clk::now();
+        int nap_us = 20;
+        for (;;) {
+            const hipError_t e = hipStreamQuery(s_);
+            if (e == hipSuccess) return MN_OK;
+            if (e != hipErrorNotReady) {
+                set_error("%s: stream error %s", what, hipGetErrorString(e));
+                return MN_EHIP;
+            }
+            ncclResult_t ae = ncclSuccess;
+            const ncclResult_t q = ncclCommGetAsyncError(c_, &ae);
+            if (q != ncclSuccess) return fail(what, ncclGetErrorString(q));
+            if (ae != ncclSuccess && ae != ncclInProgress) return fail(what, ncclGetErrorString(ae));
+            const double el = std::chrono::duration<double>(clk::now() - t0).count();
+            if (el > timeout_) {
+                char why[160];
+                snprintf(why, sizeof(why), "no completion within %.3g s (a peer rank failed or stalled)",
+                         timeout_);
+                return fail(what, why);
+            }
+            std::this_thread::sleep_for(std::chrono::microseconds(nap_us));
+            nap_us = std::min(nap_us * 2, 1000);
+        }
+    }
+    int fail(const char *what, const char *why) {
+        (void)ncclCommAbort(c_);
+        {
+            std::lock_guard<std::mutex> g(g_abort_mu);
+            g_aborted.insert((void *)c_);
+        }
+        set_error("mn_knn_sharded_f32: %s: %s; the RCCL communicator was aborted "
+                  "(mn_rccl_comm_destroy on it is a no-op)", what, why);
+        return MN_ECOMM;
+    }
+
+    ncclComm_t c_;
+    hipStream_t s_;
+    double timeout_;
+    int world_ = 1, rank_ = 0;
+    int *pin_ = nullptr, *dflag_ = nullptr;
+    DevBufs bufs_;
+};
+
+// R ranks on one device: rank l on stream l (rank 0 on the caller's stream),
+// stages one rank at a time (they share the calling thread's scratch), the
+// collectives as device copies between full drains.
+class LoopbackTransport final : public Transport {
+  public:
+    LoopbackTransport(int world, hipStream_t s0) : s_((size_t)world, s0) {}
+    ~LoopbackTransport() override {
+        for (size_t l = 1; l < s_.size(); ++l)
+            if (s_[l]) (void)hipStreamDestroy(s_[l]);
+    }
+    int init() {
+        for (size_t l = 1; l < s_.size(); ++l) {
+            s_[l] = nullptr;
+            MN_HIP_TRY(hipStreamCreateWithFlags(&s_[l], hipStreamNonBlocking));
+        }
+        return MN_OK;
+    }
+    int world() const override { return (int)s_.size(); }
+    int nlocal() const override { return (int)s_.size(); }
+    int rank(int l) const override { return l; }
+    hipStream_t stream(int l) const override { return s_[(size_t)l]; }
+    int stage_done(int l) override {
+        MN_HIP_TRY(hipStreamSynchronize(s_[(size_t)l]));
+        return MN_OK;
+    }
+    int all_gather(const void *const *send, void *const *recv, size_t bytes, const char *) override {
+        const int R = world();
+        MN_HIP_TRY(drain());
+        std::set<const void *> done;  // a receive buffer shared by ranks takes each block once
+        for (int l = 0; l < R; ++l)
+            for (int r = 0; r < R; ++r) {
+                char *dst = (char *)recv[l] + (size_t)r * bytes;
+                if (dst == (const char *)send[r] || !done.insert(dst).second) continue;  // in place
+                MN_HIP_TRY(hipMemcpyAsync(dst, send[r], bytes, hipMemcpyDeviceToDevice, s_[(size_t)l]));
+            }
+        MN_HIP_TRY(drain());
+        return MN_OK;
+    }
+    int all_to_all(int na, const void *const *const *send, void *const *const *recv, size_t bytes,
+                   const char *) override {
+        const int R = world();
+        MN_HIP_TRY(drain());
+        for (int a = 0; a < na; ++a)
+            for (int l = 0; l < R; ++l)
+                for (int p = 0; p < R; ++p)
+                    MN_HIP_TRY(hipMemcpyAsync((char *)recv[a][l] + (size_t)p * bytes,
+                                              (const char *)send[a][p] + (size_t)l * bytes, bytes,
+                                              hipMemcpyDeviceToDevice, s_[(size_t)l]));
+        MN_HIP_TRY(drain());
+        return MN_OK;
+    }
+    int agree(const int *mine, int *out) override {
+        int m = 0;
+        for (int l = 0; l < world(); ++l) m = std::max(m, mine[l]);
+        *out = m;
+        return MN_OK;
+    }
+
+  private:
+    hipError_t drain() {
+        for (hipStream_t s : s_) {
+            const hipError_t e = hipStreamSynchronize(s);
+            if (e != hipSuccess) return e;
+        }
+        return hipSuccess;
+    }
+    std::vector<hipStream_t> s_;
+};
+
+// ---- the driver ---------------------------------------------------------------
+
+// tuning build: MN_SHARD_FAIL=<stage><rank> fails that rank's stage A or B
+// after it ran (tests of the status agreement)
+int injected(char stage, int rank) {
+    const char *e = mn::knob("MN_SHARD_FAIL");
+    if (!e || e[0] != stage || atoi(e + 1) != rank) return MN_OK;
+    set_error("mn_knn_sharded_f32: injected failure of stage %c on rank %d", stage, rank);
+    return MN_EINVAL;
 }
 
-int status_of(int rc) { return rc == MN_OK ? 0 : rc == 1 ? 1 : 2; }
+// per local rank: events at fixed slots, so the stage times have the same
+// meaning in both forms (a slot not reached is recorded with the next one)
+enum Slot { kStart, kGathered, kStageA, kGathered2, kStageB, kExchanged, kEnd, kSlots };
 
-// rank r's rows of every part list [N][k] go to rank r: part p of the
-// receive buffer [R][nl][k] = the list computed on rank p
-int exchange(ncclComm_t c, hipStream_t s, int world, int64_t nl, int k, const int32_t *li,
-             const float *ld, int32_t *pi, float *pd) {
-    if (ncclGroupStart() != ncclSuccess) return MN_EHIP;
-    int rc = MN_OK;
-    for (int p = 0; p < world && rc == MN_OK; ++p) {
-        const size_t cnt = (size_t)nl * k;
-        if (ncclSend(li + (size_t)p * cnt, cnt, ncclInt32, p, c, s) != ncclSuccess ||
-            ncclSend(ld + (size_t)p * cnt, cnt, ncclFloat32, p, c, s) != ncclSuccess ||
-            ncclRecv(pi + (size_t)p * cnt, cnt, ncclInt32, p, c, s) != ncclSuccess ||
-            ncclRecv(pd + (size_t)p * cnt, cnt, ncclFloat32, p, c, s) != ncclSuccess)
-            rc = MN_EHIP;
+struct RankTimer {
+    bool on = false;
+    hipStream_t s = nullptr;
+    hipEvent_t ev[kSlots] = {};
+    int next = 0;
+    int start(bool enable, hipStream_t stream) {
+        on = enable;
+        s = stream;
+        if (!on) return MN_OK;
+        for (auto &e : ev) MN_HIP_TRY(hipEventCreate(&e));
+        upto(kStart);
+        return MN_OK;
     }
-    if (ncclGroupEnd() != ncclSuccess || rc != MN_OK) {
-        set_error("grouped ncclSend/ncclRecv of the per-shard lists failed");
+    void upto(int slot) {
+        if (!on) return;
+        for (; next <= slot; ++next) (void)hipEventRecord(ev[next], s);
+    }
+    float ms(int a, int b) const {
+        if (!on || a >= next || b >= next) return 0.f;
+        (void)hipEventSynchronize(ev[b]);
+        float t = 0.f;
+        (void)hipEventElapsedTime(&t, ev[a], ev[b]);
+        return t;
+    }
+    ~RankTimer() {
+        for (auto &e : ev)
+            if (e) (void)hipEventDestroy(e);
+    }
+};
+
+struct RankIO {
+    const float *x_shard;  // [n_local][d]
+    int32_t *out_idx;      // [n_local][k]
+    float *out_dist;
+};
+
+struct DriveOut {
+    std::vector<float> rank_ms;  // [nlocal][3]: stage A, stage B, stage C
+    mn_knn_stats st{};
+};
+
+// The build for T's local ranks.  xall_given (may be NULL): the all-gathered
+// shards already resident (the loopback's X_all: the gather is in place).
+// allow_sym1: the symmetric form also on one rank (tuning build).
+int sharded_drive(Transport &T, const RankIO *io, int64_t nl, int d, const mn_knn_opts *opts,
+                  int64_t query_chunk, const float *xall_given, bool allow_sym1, bool timing,
+                  DriveOut *res) {
+    using namespace mn;
+    const int R = T.world(), NL = T.nlocal(), k = opts->k;
+    const int64_t N = nl * R;
+    MN_REQUIRE(N <= INT32_MAX, MN_EINVAL, "mn_knn_sharded_f32: ids must fit int32");
+    MN_REQUIRE(R <= kMaxShardRanks, MN_ENOTSUP, "mn_knn_sharded_f32: at most %d ranks (merge width)",
+               kMaxShardRanks);
+    const size_t lb = 4 * (size_t)nl * k;  // bytes of one rank's block of a [*][k] list
+    // per local rank: X_all, part lists of all rows li/ld [N][k], received
+    // parts pi/pd [R][n_local][k], per-row tau0 / norms / Tc [3][N]
+    DevBufs B;
+    std::vector<float *> xall(NL);
+    std::vector<int32_t *> li(NL), pi(NL);
+    std::vector<float *> ld(NL), pd(NL), rowv(NL);
+    for (int l = 0; l < NL; ++l) {
+        xall[l] = xall_given ? (float *)xall_given : (float *)B.get(sizeof(float) * (size_t)N * d);
+        li[l] = (int32_t *)B.get(lb * R);
+        ld[l] = (float *)B.get(lb * R);
+        pi[l] = (int32_t *)B.get(lb * R);
+        pd[l] = (float *)B.get(lb * R);
+        rowv[l] = (float *)B.get(4 * (size_t)N * 3 + 64);
+        if (!xall[l] || !li[l] || !ld[l] || !pi[l] || !pd[l] || !rowv[l]) {
+            set_error("mn_knn_sharded_f32: device allocation failed");
+            return MN_ENOMEM;
+        }
+    }
+    auto tau0 = [&](int l) { return rowv[l]; };
+    auto qn = [&](int l) { return rowv[l] + N; };
+    auto tc = [&](int l) { return rowv[l] + 2 * N; };
+    std::vector<RankTimer> tm(NL);
+    for (int l = 0; l < NL; ++l) {
+        const int trc = tm[l].start(timing, T.stream(l));
+        if (trc != MN_OK) return trc;
+    }
+    std::vector<int> rc(NL, MN_OK), st_of(NL, 0);
+    int agreed = 0;
+    // after an agreement: 0 continue; else the code this rank returns (never
+    // the internal status 1; a healthy rank whose peer failed says so)
+    auto settle = [&]() -> int {
+        if (agreed != 2) return MN_OK;
+        for (int l = 0; l < NL; ++l)
+            if (rc[l] < 0) return rc[l];
+        set_error("mn_knn_sharded_f32: another rank failed");
         return MN_EHIP;
+    };
+    auto status = [](int r) { return r == MN_OK ? 0 : r == 1 ? 1 : 2; };
+
+    // 1. the shards everywhere
+    {
+        std::vector<const void *> snd(NL);
+        std::vector<void *> rcv(NL);
+        for (int l = 0; l < NL; ++l) {
+            snd[l] = io[l].x_shard;
+            rcv[l] = xall[l];
+        }
+        const int grc = T.all_gather(snd.data(), rcv.data(), sizeof(float) * (size_t)nl * d,
+                                     "the all-gather of the shards");
+        if (grc != MN_OK) return grc;
     }
+    const ShardPlan pl = shard_plan(N, d, k, R);
+    bool sym = (R > 1 || allow_sym1) && sym_applies(pl, opts);
+    int64_t ncand = 0;
+    int nfb = 0;
+    if (sym) {
+        // 2. stage A, then every rank's tau0 / norms everywhere (in place)
+        for (int l = 0; l < NL; ++l) {
+            tm[l].upto(kGathered);  // per rank: the loopback runs the ranks' stages in turn
+            const int64_t row0 = (int64_t)T.rank(l) * nl;
+            rc[l] = shard_phase1(xall[l], pl, row0, nl, T.stream(l), tau0(l) + row0, qn(l) + row0);
+            if (rc[l] == MN_OK) rc[l] = injected('A', T.rank(l));
+            tm[l].upto(kStageA);
+            const int drc = T.stage_done(l);
+            if (drc != MN_OK && rc[l] >= 0) rc[l] = drc;
+            st_of[l] = status(rc[l]);
+        }
+        const int arc = T.agree(st_of.data(), &agreed);
+        if (arc != MN_OK) return arc;
+        if (const int e = settle()) return e;
+        sym = agreed == 0;
+    }
+    if (sym) {
+        std::vector<const void *> snd(NL);
+        std::vector<void *> rcv(NL);
+        const size_t rb = sizeof(float) * (size_t)nl;
+        for (int l = 0; l < NL; ++l) {
+            snd[l] = tau0(l) + (int64_t)T.rank(l) * nl;
+            rcv[l] = tau0(l);
+        }
+        int grc = T.all_gather(snd.data(), rcv.data(), rb, "the all-gather of the thresholds");
+        if (grc != MN_OK) return grc;
+        for (int l = 0; l < NL; ++l) {
+            snd[l] = qn(l) + (int64_t)T.rank(l) * nl;
+            rcv[l] = qn(l);
+        }
+        grc = T.all_gather(snd.data(), rcv.data(), rb, "the all-gather of the row norms");
+        if (grc != MN_OK) return grc;
+        // 3. stage B: this rank's share, part lists of all rows
+        for (int l = 0; l < NL; ++l) {
+            tm[l].upto(kGathered2);
+            int64_t nc1 = 0;
+            rc[l] = shard_share(xall[l], pl, tau0(l), qn(l), T.rank(l), R, T.stream(l), li[l], ld[l],
+                                tc(l), timing ? &nc1 : nullptr);
+            if (rc[l] == MN_OK) rc[l] = injected('B', T.rank(l));
+            tm[l].upto(kStageB);
+            const int drc = T.stage_done(l);
+            if (drc != MN_OK && rc[l] >= 0) rc[l] = drc;
+            st_of[l] = status(rc[l]);
+            ncand += nc1;
+        }
+        const int arc = T.agree(st_of.data(), &agreed);
+        if (arc != MN_OK) return arc;
+        if (const int e = settle()) return e;
+        sym = agreed == 0;  // 1: a non-finite threshold anywhere (the same verdict everywhere)
+    }
+    if (sym) {
+        // 4. the exchange, 5. stage C
+        const void *const *snd[2] = {(const void *const *)li.data(), (const void *const *)ld.data()};
+        void *const *rcv[2] = {(void *const *)pi.data(), (void *const *)pd.data()};
+        const int xrc = T.all_to_all(2, snd, rcv, lb, "the exchange of the part lists");
+        if (xrc != MN_OK) return xrc;
+        for (int l = 0; l < NL; ++l) {
+            tm[l].upto(kExchanged);
+            int nf = 0;
+            const int frc = shard_finish(xall[l], pl, (int64_t)T.rank(l) * nl, nl, R, (int64_t)nl * k,
+                                         pi[l], pd[l], tc(l), T.stream(l), io[l].out_idx,
+                                         io[l].out_dist, &nf);
+            if (frc != MN_OK) return frc;  // nothing collective follows
+            tm[l].upto(kEnd);
+            const int drc = T.stage_done(l);
+            if (drc != MN_OK) return drc;
+            nfb += nf;
+        }
+    } else {
+        // the per-shard form: exact per-shard top-k of every query against
+        // the rank's shard, the exchange, the merge
+        const int64_t qc = query_chunk > 0 ? query_chunk : ((int64_t)1 << 21);
+        for (int l = 0; l < NL; ++l) {
+            tm[l].upto(kGathered2);
+            mn_knn_opts o = *opts;
+            o.stream = T.stream(l);
+            o.timing = 0;
+            int r = MN_OK;
+            for (int64_t a = 0; a < N && r == MN_OK; a += qc) {
+                const int64_t b = std::min(N, a + qc);
+                r = mn_knn_f32_qc(xall[l] + a * d, b - a, io[l].x_shard, nl, d, a,
+                                  (int64_t)T.rank(l) * nl, &o, li[l] + a * k, ld[l] + a * k);
+            }
+            rc[l] = r;
+            tm[l].upto(kStageB);
+            const int drc = T.stage_done(l);
+            if (drc != MN_OK && rc[l] >= 0) rc[l] = drc;
+            st_of[l] = rc[l] == MN_OK ? 0 : 2;
+        }
+        // a failed rank must not leave the others waiting in the exchange
+        const int arc = T.agree(st_of.data(), &agreed);
+        if (arc != MN_OK) return arc;
+        if (const int e = settle()) return e;
+        const void *const *snd[2] = {(const void *const *)li.data(), (const void *const *)ld.data()};
+        void *const *rcv[2] = {(void *const *)pi.data(), (void *const *)pd.data()};
+        const int xrc = T.all_to_all(2, snd, rcv, lb, "the exchange of the per-shard lists");
+        if (xrc != MN_OK) return xrc;
+        for (int l = 0; l < NL; ++l) {
+            tm[l].upto(kExchanged);
+            const int mrc = mn_knn_merge_f32(pi[l], pd[l], R, nl, k, io[l].out_idx, io[l].out_dist,
+                                             T.stream(l));
+            if (mrc != MN_OK) return mrc;
+            tm[l].upto(kEnd);
+            const int drc = T.stage_done(l);
+            if (drc != MN_OK) return drc;
+        }
+    }
+    for (int l = 0; l < NL; ++l) MN_HIP_TRY(hipStreamSynchronize(T.stream(l)));
+    mn_knn_stats &st = res->st;
+    st = mn_knn_stats{};
+    st.n_queries = nl * NL;
+    st.algo = sym ? MN_KNN_BF16X1 : MN_KNN_AUTO;
+    st.sweep_slices = sym ? -1 : 0;
+    st.sample_rows = sym ? pl.m0 : 0;
+    st.n_uncertified = nfb;
+    st.n_candidates = ncand;
+    res->rank_ms.assign((size_t)NL * 3, 0.f);
+    for (int l = 0; l < NL; ++l) {
+        const RankTimer &t = tm[l];
+        const float a = t.ms(kGathered, kStageA), b = t.ms(kGathered2, kStageB),
+                    c = t.ms(kExchanged, kEnd);
+        res->rank_ms[(size_t)l * 3] = a;
+        res->rank_ms[(size_t)l * 3 + 1] = b;
+        res->rank_ms[(size_t)l * 3 + 2] = c;
+        // max over the local ranks (the share that bounds the node)
+        st.ms_norms = std::max(st.ms_norms, t.ms(kStart, kGathered) + t.ms(kStageA, kGathered2));
+        st.ms_sample = std::max(st.ms_sample, a);
+        st.ms_sweep = std::max(st.ms_sweep, b);
+        st.ms_rerank = std::max(st.ms_rerank, t.ms(kStageB, kExchanged));
+        st.ms_fallback = std::max(st.ms_fallback, c);
+        st.ms_total = std::max(st.ms_total, t.ms(kStart, kEnd));
+    }
+    st.ms_gram = st.ms_sample + st.ms_sweep;
     return MN_OK;
 }
 
@@ -144,114 +638,18 @@ int mn_knn_sharded_f32(const float *X_shard, int64_t n_local, int32_t d, void *c
                "mn_knn_sharded_f32: NULL argument");
     MN_REQUIRE(n_local >= 1 && d >= 1 && opts->k >= 1, MN_EINVAL,
                "mn_knn_sharded_f32: bad shape");
-    ncclComm_t c = (ncclComm_t)comm;
-    int world = 1, rank = 0;
-    MN_NCCL_TRY(ncclCommCount(c, &world));
-    MN_NCCL_TRY(ncclCommUserRank(c, &rank));
-    hipStream_t s = (hipStream_t)opts->stream;
-    const int k = opts->k;
-    const int64_t n_tot = n_local * world;
-    MN_REQUIRE(n_tot <= INT32_MAX, MN_EINVAL, "mn_knn_sharded_f32: ids must fit int32");
-    MN_REQUIRE(world <= 16, MN_ENOTSUP, "mn_knn_sharded_f32: at most 16 ranks (merge width)");
-    const size_t part_b = (size_t)world * n_local * k;  // entries of [R][n_local][k]
-    // device buffers owned by the call: X_all, the part lists of all rows
-    // [N][k], the received parts [R][n_local][k], the per-row arrays
-    DevBufs B;
-    void *xall = B.get(sizeof(float) * (size_t)n_tot * d);
-    int32_t *li = (int32_t *)B.get(4 * (size_t)n_tot * k);
-    float *ld = (float *)B.get(4 * (size_t)n_tot * k);
-    int32_t *pi = (int32_t *)B.get(4 * part_b);
-    float *pd = (float *)B.get(4 * part_b);
-    float *rowv = (float *)B.get(4 * (size_t)n_tot * 3 + 64);
-    int *dflag = (int *)B.get(64);
-    if (!xall || !li || !ld || !pi || !pd || !rowv || !dflag) {
-        set_error("mn_knn_sharded_f32: device allocation failed");
-        return MN_ENOMEM;
-    }
-    float *tau0_all = rowv, *qn_all = rowv + n_tot, *tc_all = rowv + 2 * n_tot;
-    mn_knn_stats st{};
-    st.n_queries = n_local;
-    st.algo = MN_KNN_BF16X1;
-    Timer tm;
-    tm.start(opts->timing != 0, s);
-    // 1. all-gather of the shards (rank r's rows at r * n_local)
-    MN_NCCL_TRY(ncclAllGather(X_shard, xall, (size_t)n_local * d, ncclFloat32, c, s));
-    const float *X_all = (const float *)xall;
-    const ShardPlan pl = shard_plan(n_tot, d, k, world);
-    bool sym = world > 1 && sym_applies(pl, opts);
-    int agreed = 0, rc = MN_OK;
-    int64_t ncand = 0;
-    int nfb = 0;
-    if (sym) {
-        // 2. stage A, then every rank's tau0 / norms everywhere
-        rc = shard_phase1(X_all, pl, (int64_t)rank * n_local, n_local, s, tau0_all + rank * n_local,
-                          qn_all + rank * n_local);
-        const int arc = agree(c, s, dflag, status_of(rc), &agreed);
-        if (arc != MN_OK) return arc;
-        if (agreed == 2) return rc != MN_OK ? rc : MN_EHIP;
-        sym = agreed == 0;
-    }
-    tm.mark();
-    if (sym) {
-        MN_NCCL_TRY(ncclAllGather(tau0_all + rank * n_local, tau0_all, (size_t)n_local, ncclFloat32,
-                                  c, s));
-        MN_NCCL_TRY(ncclAllGather(qn_all + rank * n_local, qn_all, (size_t)n_local, ncclFloat32, c,
-                                  s));
-        // 3. stage B: this rank's share, partial lists of all rows
-        rc = shard_share(X_all, pl, tau0_all, qn_all, rank, world, s, li, ld, tc_all,
-                         opts->timing ? &ncand : nullptr);
-        const int arc = agree(c, s, dflag, status_of(rc), &agreed);
-        if (arc != MN_OK) return arc;
-        if (agreed == 2) return rc != MN_OK ? rc : MN_EHIP;
-        sym = agreed == 0;  // 1: a non-finite threshold anywhere (same on every rank)
-    }
-    tm.mark();
-    if (sym) {
-        // 4. the exchange, 5. stage C
-        rc = exchange(c, s, world, n_local, k, li, ld, pi, pd);
-        if (rc != MN_OK) return rc;
-        tm.mark();
-        rc = shard_finish(X_all, pl, (int64_t)rank * n_local, n_local, world,
-                          (int64_t)n_local * k, pi, pd, tc_all, s, out_idx, out_dist, &nfb);
-        if (rc != MN_OK) return rc;
-        st.sweep_slices = -1;
-    } else {
-        // the per-shard form: exact per-shard top-k of every query against
-        // this rank's shard, the exchange, the merge
-        mn_knn_opts o = *opts;
-        o.stream = s;
-        const int64_t qc = query_chunk > 0 ? query_chunk : ((int64_t)1 << 21);
-        for (int64_t a = 0; a < n_tot && rc == MN_OK; a += qc) {
-            const int64_t b = std::min(n_tot, a + qc);
-            rc = mn_knn_f32_qc(X_all + a * d, b - a, X_shard, n_local, d, a,
-                               (int64_t)rank * n_local, &o, li + a * k, ld + a * k);
-        }
-        // a failed rank must not leave the others waiting in the exchange
-        const int arc = agree(c, s, dflag, rc == MN_OK ? 0 : 2, &agreed);
-        if (arc != MN_OK) return arc;
-        if (agreed != 0) return rc != MN_OK ? rc : MN_EHIP;
-        tm.mark();
-        rc = exchange(c, s, world, n_local, k, li, ld, pi, pd);
-        if (rc != MN_OK) return rc;
-        tm.mark();
-        rc = mn_knn_merge_f32(pi, pd, world, n_local, k, out_idx, out_dist, s);
-        if (rc != MN_OK) return rc;
-        st.algo = MN_KNN_AUTO;
-    }
-    tm.mark();
-    MN_HIP_TRY(hipStreamSynchronize(s));
-    st.n_uncertified = nfb;
-    st.n_candidates = ncand;
-    st.sample_rows = sym ? pl.m0 : 0;
-    if (tm.on) {
-        st.ms_sample = tm.ms(0, 1);   // all-gather + stage A
-        st.ms_sweep = tm.ms(1, 2);    // stage B (per-shard form: the qc passes)
-        st.ms_gram = st.ms_sample + st.ms_sweep;
-        st.ms_rerank = tm.ms(2, 3);   // the exchange
-        st.ms_fallback = tm.ms(3, 4); // stage C / the merge
-        st.ms_total = tm.ms(0, 4);
-    }
-    knn_stats_ref() = st;
+    MN_REQUIRE(!comm_aborted(comm), MN_EINVAL,
+               "mn_knn_sharded_f32: the communicator was aborted by an earlier call");
+    RcclTransport T((ncclComm_t)comm, (hipStream_t)opts->stream);
+    const int irc = T.init();
+    if (irc != MN_OK) return irc;
+    const RankIO io{X_shard, out_idx, out_dist};
+    DriveOut res;
+    const bool sym1 = knob_int("MN_SHARD_SYM1", 0) != 0;  // tuning build: world-1 symmetric form
+    const int rc = sharded_drive(T, &io, n_local, d, opts, query_chunk, nullptr, sym1,
+                                 opts->timing != 0, &res);
+    if (rc != MN_OK) return rc;
+    knn_stats_ref() = res.st;
     return MN_OK;
 }
 
@@ -278,89 +676,37 @@ int mn_sym_share_table(int32_t nbk, int32_t rank, int32_t world, int32_t *out4, 
     return MN_OK;
 }
 
-// The symmetric sharded build of `world` ranks simulated on ONE device: X_all
-// [n_tot][d] (device) stands for the all-gathered shards, the stages of every
-// rank run in turn on this device and the exchange is a strided read of the
-// part lists.  out [n_tot][k]: the global graph (bit-identical to mn_knn_f32).
-// rank_ms [world][3] (host, may be NULL): per rank the stage A, stage B and
-// stage C milliseconds (device events) — a rank's share of the real build.
-// MN_ENOTSUP when the symmetric form does not apply (see mn_knn_sharded_f32).
+// The sharded build of `world` ranks on ONE device through the loopback
+// transport: X_all [n_tot][d] (device) holds the shards (rank r's at r *
+// n_tot / world, so the all-gather is in place); the same driver as
+// mn_knn_sharded_f32 runs every rank's stages in turn and the collectives as
+// device copies.  out [n_tot][k]: the global graph (bit-identical to
+// mn_knn_f32).  rank_ms [world][3] (host, may be NULL): per rank the stage A,
+// stage B and stage C milliseconds (device events) — a rank's share of the
+// real build.
 int mn_knn_sharded_sim_f32(const float *X_all, int64_t n_tot, int32_t d, int32_t world,
                            const mn_knn_opts *opts, int32_t *out_idx, float *out_dist,
                            float *rank_ms) {
     using namespace mn;
     clear_error();
     MN_REQUIRE(X_all && opts && out_idx && out_dist, MN_EINVAL, "mn_knn_sharded_sim_f32: NULL argument");
-    MN_REQUIRE(world >= 1 && world <= 16 && n_tot >= world && n_tot % world == 0 && d >= 1 &&
-                   opts->k >= 1 && n_tot <= INT32_MAX,
+    MN_REQUIRE(world >= 1 && world <= kMaxShardRanks && n_tot >= world && n_tot % world == 0 &&
+                   d >= 1 && opts->k >= 1 && n_tot <= INT32_MAX,
                MN_EINVAL, "mn_knn_sharded_sim_f32: bad shape (n_tot a multiple of world <= 16)");
-    hipStream_t s = (hipStream_t)opts->stream;
-    const int k = opts->k;
     const int64_t nl = n_tot / world;
-    const ShardPlan pl = shard_plan(n_tot, d, k, world);
-    MN_REQUIRE(sym_applies(pl, opts), MN_ENOTSUP,
-               "mn_knn_sharded_sim_f32: the symmetric sharded form does not apply");
-    DevBufs B;
-    int32_t *li = (int32_t *)B.get(4 * (size_t)world * n_tot * k);
-    float *ld = (float *)B.get(4 * (size_t)world * n_tot * k);
-    float *rowv = (float *)B.get(4 * (size_t)n_tot * 3 + 64);
-    MN_REQUIRE(li && ld && rowv, MN_ENOMEM, "mn_knn_sharded_sim_f32: device allocation failed");
-    float *tau0_all = rowv, *qn_all = rowv + n_tot, *tc_all = rowv + 2 * n_tot;
-    std::vector<float> ms((size_t)world * 3, 0.f);
-    int64_t ncand = 0;
-    int nfb_tot = 0;
-    for (int r = 0; r < world; ++r) {
-        Timer t;
-        t.start(true, s);
-        const int rc = shard_phase1(X_all, pl, r * nl, nl, s, tau0_all + r * nl, qn_all + r * nl);
-        MN_REQUIRE(rc != 1, MN_ENOTSUP, "mn_knn_sharded_sim_f32: values too large for the bf16 bound");
-        if (rc != MN_OK) return rc;
-        t.mark();
-        MN_HIP_TRY(hipStreamSynchronize(s));
-        ms[(size_t)r * 3] = t.ms(0, 1);
-    }
-    for (int r = 0; r < world; ++r) {
-        Timer t;
-        t.start(true, s);
-        int64_t nc1 = 0;
-        const int rc = shard_share(X_all, pl, tau0_all, qn_all, r, world, s, li + (size_t)r * n_tot * k,
-                                   ld + (size_t)r * n_tot * k, tc_all, &nc1);
-        MN_REQUIRE(rc != 1, MN_ENOTSUP, "mn_knn_sharded_sim_f32: non-finite thresholds");
-        if (rc != MN_OK) return rc;
-        t.mark();
-        MN_HIP_TRY(hipStreamSynchronize(s));
-        ms[(size_t)r * 3 + 1] = t.ms(0, 1);
-        ncand += nc1;
-    }
-    for (int o = 0; o < world; ++o) {
-        Timer t;
-        t.start(true, s);
-        int nfb = 0;
-        const int rc = shard_finish(X_all, pl, o * nl, nl, world, n_tot * k, li + (size_t)o * nl * k,
-                                    ld + (size_t)o * nl * k, tc_all, s, out_idx + (size_t)o * nl * k,
-                                    out_dist + (size_t)o * nl * k, &nfb);
-        if (rc != MN_OK) return rc;
-        t.mark();
-        MN_HIP_TRY(hipStreamSynchronize(s));
-        ms[(size_t)o * 3 + 2] = t.ms(0, 1);
-        nfb_tot += nfb;
-    }
-    mn_knn_stats st{};
-    st.n_queries = n_tot;
-    st.algo = MN_KNN_BF16X1;
-    st.n_uncertified = nfb_tot;
-    st.n_candidates = ncand;
-    st.sample_rows = pl.m0;
-    st.sweep_slices = -1;
-    for (int r = 0; r < world; ++r) {
-        st.ms_sample = std::max(st.ms_sample, ms[(size_t)r * 3]);
-        st.ms_sweep = std::max(st.ms_sweep, ms[(size_t)r * 3 + 1]);
-        st.ms_fallback = std::max(st.ms_fallback, ms[(size_t)r * 3 + 2]);
-    }
-    st.ms_gram = st.ms_sample + st.ms_sweep;
-    st.ms_total = st.ms_gram + st.ms_fallback;
-    knn_stats_ref() = st;
-    if (rank_ms) std::memcpy(rank_ms, ms.data(), sizeof(float) * ms.size());
+    LoopbackTransport T(world, (hipStream_t)opts->stream);
+    const int irc = T.init();
+    if (irc != MN_OK) return irc;
+    std::vector<RankIO> io((size_t)world);
+    for (int r = 0; r < world; ++r)
+        io[(size_t)r] = RankIO{X_all + (size_t)r * nl * d, out_idx + (size_t)r * nl * opts->k,
+                               out_dist + (size_t)r * nl * opts->k};
+    DriveOut res;
+    const int rc = sharded_drive(T, io.data(), nl, d, opts, 0, X_all, false,
+                                 opts->timing != 0 || rank_ms != nullptr, &res);
+    if (rc != MN_OK) return rc;
+    knn_stats_ref() = res.st;
+    if (rank_ms) std::memcpy(rank_ms, res.rank_ms.data(), sizeof(float) * res.rank_ms.size());
     return MN_OK;
 }
 

@@ -8,6 +8,9 @@
 
 namespace mn {
 
+// ranks of one sharded build (the merge width of k_merge_certify / mn_knn_merge_f32)
+constexpr int kMaxShardRanks = 16;
+
 struct ShardPlan {
     int64_t N, m0;  // all rows; the global phase-1 sample
     int d, dp, nkb, k, L1, world;

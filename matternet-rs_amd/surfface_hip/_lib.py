@@ -17,9 +17,10 @@ LIB_PATH = os.path.join(os.path.dirname(PKG_DIR), "libmatternet_hip.so")
 # release library above ignores every MN_* tuning variable.
 TUNING_LIB_PATH = os.path.join(os.path.dirname(PKG_DIR), "libmatternet_hip_tuning.so")
 
-MN_OK, MN_EINVAL, MN_ENOMEM, MN_ENONFINITE, MN_ECAP, MN_EHIP, MN_ENOTSUP = 0, -1, -2, -3, -4, -5, -6
+MN_OK, MN_EINVAL, MN_ENOMEM, MN_ENONFINITE, MN_ECAP, MN_EHIP, MN_ENOTSUP, MN_ECOMM = \
+    0, -1, -2, -3, -4, -5, -6, -7
 _NAMES = {-1: "MN_EINVAL", -2: "MN_ENOMEM", -3: "MN_ENONFINITE", -4: "MN_ECAP", -5: "MN_EHIP",
-          -6: "MN_ENOTSUP"}
+          -6: "MN_ENOTSUP", -7: "MN_ECOMM"}
 
 MN_L2SQ, MN_COS_RECT, MN_L2 = 0, 1, 2
 
@@ -128,6 +129,7 @@ SIGNATURES = {
     "mn_rccl_unique_id": (C.c_int, [P]),
     "mn_rccl_comm_init": (C.c_int, [P, I32, I32, C.POINTER(C.c_void_p)]),
     "mn_rccl_comm_destroy": (C.c_int, [P]),
+    "mn_rccl_set_timeout": (C.c_int, [C.c_double]),
     "mn_knn_last_stats": (C.c_int, [C.POINTER(KnnStats)]),
     "mn_laplacian_from_knn": (C.c_int, [P, P, I32, I64, I32, C.POINTER(LapOpts), C.POINTER(Csr), P]),
     "mn_csr_free": (C.c_int, [C.POINTER(Csr)]),

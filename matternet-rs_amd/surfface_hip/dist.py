@@ -114,6 +114,14 @@ class RcclComm:
             self.handle = None
 
 
+def set_collective_timeout(seconds: float) -> None:
+    """mn_rccl_set_timeout: the deadline of one collective of
+    mn_knn_sharded_f32 (process-wide; past it the communicator is aborted and
+    the call raises MN_ECOMM)."""
+    from . import _lib
+    _lib.check(_lib.lib().mn_rccl_set_timeout(float(seconds)))
+
+
 def knn_sharded_capi(X_shard: torch.Tensor, k: int, comm: RcclComm, query_chunk: int = 0,
                      margin: int = 16, timing: bool = False, stream=None):
     """mn_knn_sharded_f32: this rank's rows of the global exact kNN graph
@@ -133,11 +141,14 @@ def knn_sharded_capi(X_shard: torch.Tensor, k: int, comm: RcclComm, query_chunk:
     return idx, dd
 
 
-def knn_sharded_sim(X_all: torch.Tensor, k: int, world: int, timing: bool = False, stream=None):
-    """mn_knn_sharded_sim_f32: the symmetric sharded build of `world` ranks
-    simulated on this device (X_all = the all-gathered shards).  Returns (idx
-    [n, k] int32, dist [n, k] f32, rank_ms [world][3] = per rank the stage A /
-    B / C milliseconds, stats)."""
+def knn_sharded_sim(X_all: torch.Tensor, k: int, world: int, timing: bool = False, stream=None,
+                    algo: int | None = None):
+    """mn_knn_sharded_sim_f32: the sharded build of `world` ranks on this
+    device — mn_knn_sharded_f32's driver over the loopback transport (X_all =
+    the shards, rank r's at r * n / world).  `algo` (default AUTO) picks the
+    form as the RCCL entry would: AUTO / BF16X1 the symmetric form, F32 /
+    BF16X3 the per-shard form.  Returns (idx [n, k] int32, dist [n, k] f32,
+    rank_ms [world][3] = per rank the stage A / B / C milliseconds, stats)."""
     import ctypes as C
     import numpy as np
     from . import _lib
@@ -149,7 +160,8 @@ def knn_sharded_sim(X_all: torch.Tensor, k: int, world: int, timing: bool = Fals
     dd = torch.empty((n, k), dtype=torch.float32, device=X_all.device)
     ms = np.zeros((world, 3), dtype=np.float32)
     o = _lib.KnnOpts(k=k, metric=_lib.MN_L2SQ, exclude_self=1, margin=0,
-                     timing=1 if timing else 0, algo=_lib.MN_KNN_AUTO,
+                     timing=1 if timing else 0,
+                     algo=_lib.MN_KNN_AUTO if algo is None else algo,
                      stream=stream_handle(stream))
     _lib.check(_lib.lib().mn_knn_sharded_sim_f32(ptr(X_all), n, d, world, C.byref(o), ptr(idx),
                                                  ptr(dd), ms.ctypes.data_as(C.c_void_p)))

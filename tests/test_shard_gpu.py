@@ -1,9 +1,14 @@
-"""Row-sharded kNN on one GPU: the symmetric sharded build
-(mn_knn_sharded_sim_f32: every rank's stages in turn, the exchange a strided
-read) at the C2 size and at the full C4 size, the per-shard form
-(mn_knn_f32_qc + mn_knn_merge_f32) it falls back to, and the C entry
-mn_knn_sharded_f32 on a single-rank RCCL communicator.  All bit-identical to
-the unsharded graph."""
+"""Row-sharded kNN on one GPU.  mn_knn_sharded_f32 and
+mn_knn_sharded_sim_f32 are ONE driver (csrc/shard.hip sharded_drive) over two
+transports: RCCL (the caller's communicator) and a one-device loopback (R
+ranks, each on its own stream, device copies for the all-gathers and the
+exchange, the same [R][n_local][k] layout and offsets).  Tested here: the
+symmetric form through the loopback at R = 2, 3, 8 (C2 size) and R = 8 at the
+full C4 size, the per-shard form through the loopback, the symmetric branch
+of the RCCL entry on a one-rank communicator (tuning-build switch), the
+collective deadline (a stalled stream ends the call with MN_ECOMM and the
+communicator aborted), and an injected stage failure.  Graphs are
+bit-identical to the unsharded one."""
 import numpy as np
 import pytest
 import torch
@@ -19,25 +24,146 @@ def _uniform(n, d, seed=42):
     return X
 
 
-def test_eight_simulated_shards_at_c2_size_bit_exact():
-    """The symmetric sharded schedule with 8 ranks at the C2 size: every tile
-    of the node-wide table on exactly one rank, partial lists merged and
-    certified by the rows' owners — the unsharded graph bit for bit."""
+@pytest.mark.parametrize("R", [8, 3, 2])
+def test_simulated_shards_at_c2_size_bit_exact(R):
+    """The symmetric sharded schedule at the C2 size through the loopback
+    transport: every tile of the node-wide table on exactly one rank, partial
+    lists exchanged into [R][n_local][k] and merged + certified by the rows'
+    owners — the unsharded graph bit for bit (R = 3: a world that does not
+    divide the 8-group rounds evenly)."""
     import json
 
     import surfface_hip as S
     from surfface_hip.dist import knn_sharded_sim
-    n, d, k, R = 1_000_000, 768, 32, 8
+    n, d, k = 1_000_000 - 1_000_000 % R, 768, 32
     X = _uniform(n, d)
     full = S.knn_l2sq(X, k)
     idx, dist, ms, st = knn_sharded_sim(X, k, R, timing=True)
-    print("C2 as 8 simulated ranks", json.dumps({"rank_ms": ms.round(2).tolist(),
-                                                 "n_uncertified": st["n_uncertified"],
-                                                 "n_candidates": st["n_candidates"]}))
+    print(f"C2 as {R} simulated ranks", json.dumps({"rank_ms": ms.round(2).tolist(),
+                                                   "n_uncertified": st["n_uncertified"],
+                                                   "n_candidates": st["n_candidates"],
+                                                   "sweep_slices": st["sweep_slices"]}))
+    assert st["sweep_slices"] == -1  # the symmetric form ran
     assert torch.equal(idx, full.idx)
     assert torch.equal(dist.view(torch.int32), full.dist.view(torch.int32))
     # the shares are balanced: the largest stage-B time within 15% of the mean
     assert ms[:, 1].max() <= 1.15 * ms[:, 1].mean()
+
+
+def test_per_shard_form_through_the_loopback():
+    """The per-shard form of the same driver (a generator the symmetric form
+    does not take): per-shard lists of all queries exchanged and merged."""
+    import surfface_hip as S
+    from surfface_hip import _lib
+    from surfface_hip.dist import knn_sharded_sim
+    n, d, k, R = 120_000, 64, 12, 3
+    X = _uniform(n, d, seed=9)
+    full = S.knn_l2sq(X, k)
+    idx, dist, ms, st = knn_sharded_sim(X, k, R, timing=True, algo=_lib.MN_KNN_BF16X3)
+    assert st["sweep_slices"] == 0 and st["algo"] == _lib.MN_KNN_AUTO
+    assert torch.equal(idx, full.idx)
+    assert torch.equal(dist.view(torch.int32), full.dist.view(torch.int32))
+
+
+def test_capi_symmetric_branch_on_one_rank_rccl():
+    """The RCCL transport's symmetric branch (world 1 via the tuning build's
+    MN_SHARD_SYM1): the all-gathers, status all-reduces and the grouped
+    send/recv exchange through RCCL, bit-exact."""
+    import os
+
+    import surfface_hip as S
+    from surfface_hip import _lib
+    from surfface_hip.dist import RcclComm, knn_sharded_capi
+    X = _uniform(60_000, 96, seed=3)
+    full = S.knn_l2sq(X, 16)
+    os.environ["MN_SHARD_SYM1"] = "1"
+    try:
+        with _lib.use_tuning():
+            comm = RcclComm(RcclComm.unique_id(), 1, 0)
+            try:
+                idx, dist = knn_sharded_capi(X, 16, comm, timing=True)
+                st = S.knn.last_stats()
+            finally:
+                comm.close()
+    finally:
+        del os.environ["MN_SHARD_SYM1"]
+    print("world-1 symmetric RCCL", {kk: st[kk] for kk in ("ms_norms", "ms_sample", "ms_sweep",
+                                                            "ms_rerank", "ms_fallback", "ms_total")})
+    assert st["sweep_slices"] == -1
+    assert 0 < st["ms_sweep"] <= st["ms_total"]
+    assert torch.equal(idx, full.idx)
+    assert torch.equal(dist.view(torch.int32), full.dist.view(torch.int32))
+
+
+def test_capi_collective_deadline_aborts_instead_of_hanging():
+    """A collective that never completes (the stream stalled for 3 s, the
+    deadline 0.5 s) ends the call with MN_ECOMM and the communicator aborted;
+    destroying it is a no-op, a later call on it is refused, and a new
+    communicator works."""
+    import os
+    import time
+
+    import surfface_hip as S
+    from surfface_hip import _lib
+    from surfface_hip.dist import RcclComm, knn_sharded_capi, set_collective_timeout
+    X = _uniform(20_000, 32, seed=5)
+    os.environ["MN_SHARD_STALL_MS"] = "3000"
+    try:
+        with _lib.use_tuning():
+            set_collective_timeout(0.5)
+            comm = RcclComm(RcclComm.unique_id(), 1, 0)
+            t0 = time.perf_counter()
+            with pytest.raises(S.MnError) as ei:
+                knn_sharded_capi(X, 8, comm)
+            el = time.perf_counter() - t0
+            # without the deadline the call would succeed once the stall ends;
+            # the buffers' release still waits for the stall kernel itself
+            # (a real peer failure's RCCL kernels exit on the abort)
+            assert ei.value.code == _lib.MN_ECOMM, ei.value
+            assert "aborted" in str(ei.value) and "within 0.5 s" in str(ei.value), ei.value
+            assert el < 10.0, el
+            with pytest.raises(S.MnError) as e2:
+                knn_sharded_capi(X, 8, comm)
+            assert e2.value.code == _lib.MN_EINVAL
+            comm.close()  # a no-op on the aborted communicator
+            torch.cuda.synchronize()  # the stall kernel drains
+    finally:
+        del os.environ["MN_SHARD_STALL_MS"]
+        with _lib.use_tuning():
+            set_collective_timeout(600.0)
+    with _lib.use_tuning():
+        comm = RcclComm(RcclComm.unique_id(), 1, 0)
+        try:
+            idx, dist = knn_sharded_capi(X, 8, comm)
+        finally:
+            comm.close()
+    full = S.knn_l2sq(X, 8)
+    assert torch.equal(idx, full.idx)
+
+
+@pytest.mark.parametrize("stage", ["A", "B"])
+def test_injected_stage_failure_is_agreed(stage):
+    """A rank whose stage fails (tuning build: MN_SHARD_FAIL=<stage><rank>)
+    reaches the status agreement, no collective runs after it, the call
+    returns the failing stage's code with its message, and the next call is
+    clean."""
+    import os
+
+    import surfface_hip as S
+    from surfface_hip import _lib
+    from surfface_hip.dist import knn_sharded_sim
+    X = _uniform(39_999, 48, seed=6)
+    os.environ["MN_SHARD_FAIL"] = stage + "1"
+    try:
+        with _lib.use_tuning():
+            with pytest.raises(S.MnError) as ei:
+                knn_sharded_sim(X, 8, 3)
+    finally:
+        del os.environ["MN_SHARD_FAIL"]
+    assert ei.value.code == _lib.MN_EINVAL and "injected" in str(ei.value)
+    with _lib.use_tuning():
+        idx, dist, _, _ = knn_sharded_sim(X, 8, 3)
+    assert torch.equal(idx, S.knn_l2sq(X, 8).idx)
 
 
 @pytest.mark.parametrize("R", [2, 3])
@@ -92,7 +218,8 @@ def test_capi_sharded_entry_single_rank():
 
 def test_c4_full_build_as_eight_simulated_ranks():
     """Config 4 (8M x 768, k=32, 8 GPUs) on one GPU: the symmetric sharded
-    build with its 8 ranks run in turn.  A rank's share of the real build is
+    build with its 8 ranks run in turn through the loopback transport (the
+    RCCL entry's driver, the exchange into [8][1M][32] by device copies).  A rank's share of the real build is
     its stage A + B + C time here (plus the all-gathers and the exchange,
     which the simulation does not run); the largest share must stay within
     8 s.  64 sampled rows (8 per shard) bit-exact vs the oracle's sequential
