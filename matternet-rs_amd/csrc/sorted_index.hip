@@ -532,7 +532,12 @@ extern "C" int mn_sorted_range_bylambda(const double *keys, const int64_t *order
                MN_EINVAL, "mn_sorted_range_bylambda: NULL pointer");
     if (nq == 0) return MN_OK;
     hipStream_t s = (hipStream_t)stream;
-    const double band = std_dev / mn::glibc::pow_glibc(2.0, p);  // sorted_index.rs:65 (glibc pow)
+    // sorted_index.rs:65 `2.0_f64.powf(p)`: llvm.pow(2.0, p), which LLVM's
+    // library-call simplifier rewrites to exp2(p) in an optimised build
+    // (replacePowWithExp, no fast-math needed) — the host libm's exp2 here.
+    // glibc pow(2, p) and exp2(p) differ in ~0.1 % of fractional p; a debug
+    // build of the reference calls pow and may differ there.
+    const double band = std_dev / ::exp2(p);
     hipLaunchKernelGGL(k_range_bylambda, dim3(grid(nq)), dim3(256), 0, s, keys, order, n, band,
                        lambda_q, nq, k, out_idx, out_lambda, out_count);
     MN_HIP_TRY(hipGetLastError());

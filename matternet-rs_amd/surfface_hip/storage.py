@@ -29,6 +29,7 @@ from __future__ import annotations
 
 import datetime
 import json
+import math
 import os
 from dataclasses import dataclass, field
 from typing import Dict, Optional
@@ -92,6 +93,17 @@ class FileInfo:
     size_bytes: Optional[int] = None
 
 
+def _finite_or_null(v):
+    """serde_json's f64 serialisation: NaN and +-inf become null."""
+    if isinstance(v, float) and not math.isfinite(v):
+        return None
+    if isinstance(v, dict):
+        return {k: _finite_or_null(x) for k, x in v.items()}
+    if isinstance(v, (list, tuple)):
+        return [_finite_or_null(x) for x in v]
+    return v
+
+
 @dataclass
 class ArrowSpaceMetadata:
     """parquet.rs:31-47 (field order as serialised)."""
@@ -129,13 +141,24 @@ class ArrowSpaceMetadata:
         return val
 
     def lambda_eps(self) -> Optional[float]:
-        return self._typed("lambda_eps", ("F64", "OptionF64"))
+        """ConfigValue::as_f64 (surfface-pipeline/src/builder.rs:1569-1582):
+        NaN reads as -1.0; another variant panics."""
+        v = self._typed("lambda_eps", ("F64", "OptionF64"))
+        if v is not None and isinstance(v, float) and math.isnan(v):
+            return -1.0
+        return v
 
     def lambda_k(self) -> Optional[int]:
         return self._typed("lambda_k", ("Usize", "OptionUsize"))
 
     def synthesis(self):
-        return self._typed("synthesis", ("TauMode",))
+        """ConfigValue::as_tau_mode (builder.rs:1599-1604): None for any other
+        variant (it does not panic, unlike as_f64 / as_usize)."""
+        v = self.get_config("synthesis")
+        if v is None:
+            return None
+        (kind, val), = v.items()
+        return val if kind == "TauMode" else None
 
     def to_json(self) -> str:
         d = {"name_id": self.name_id, "timestamp": self.timestamp, "n_rows": self.n_rows,
@@ -143,7 +166,9 @@ class ArrowSpaceMetadata:
              "files": {k: {"filename": f.filename, "file_type": f.file_type, "rows": f.rows,
                            "cols": f.cols, "nnz": f.nnz, "size_bytes": f.size_bytes}
                        for k, f in self.files.items()}}
-        return json.dumps(d, indent=2)  # serde_json::to_string_pretty: 2 spaces
+        # serde_json::to_string_pretty: 2 spaces; a non-finite f64 is written
+        # as null (serde_json never emits the bare NaN / Infinity tokens)
+        return json.dumps(_finite_or_null(d), indent=2, allow_nan=False)
 
     @classmethod
     def from_json(cls, text: str) -> "ArrowSpaceMetadata":

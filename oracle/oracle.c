@@ -924,7 +924,9 @@ int or_sorted_index(const double *lam, int64_t n, int64_t *order_out,
 /* sorted_index.rs:64-80: BTreeMap::range(OrderedFloat(lo)..=OrderedFloat(hi)) */
 int64_t or_range_bylambda(const double *keys, const int64_t *order, int64_t n, double std_dev,
                           double lq, int64_t k, double p, int64_t *out_idx, double *out_key) {
-    double band = std_dev / pow(2.0, p);
+    /* 2.0_f64.powf(p): LLVM rewrites llvm.pow(2.0, p) to exp2(p) in an
+       optimised build (LibCallSimplifier::replacePowWithExp) */
+    double band = std_dev / exp2(p);
     double lo = lq - band, hi = lq + band;
     if (cmp_ordered_float(lo, hi) > 0) return -1; /* range start > end: panic */
     int64_t cnt = 0;

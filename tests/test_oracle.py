@@ -536,3 +536,28 @@ def test_glibc_pow_restatement_host():
         r = subprocess.run([exe, "1000000"], capture_output=True, text=True, timeout=300)
     print(r.stdout)
     assert r.returncode == 0 and "mismatches 0" in r.stdout, r.stdout + r.stderr
+
+
+
+# a query whose band edge reaches the key 0.75 under exp2(p) but not under
+# glibc pow(2, p) (the two differ in ~0.1 % of fractional p), index [0.25, 0.75]
+EXP2_EDGE = {"lam": [0.25, 0.75], "p": 0.8158310053062214, "lq": 0.6079797068751175}
+
+
+def test_range_band_uses_exp2_like_an_optimised_reference_build():
+    """sorted_index.rs:65 `std / 2.0_f64.powf(p)`: LLVM's library-call
+    simplifier rewrites llvm.pow(2.0, p) to exp2(p) in an optimised build
+    (replacePowWithExp; no fast-math flag needed), so the band is
+    std / exp2(p).  At this query only that band reaches the 0.75 key."""
+    import ctypes
+    libm = ctypes.CDLL("libm.so.6")
+    for fn in (libm.exp2, libm.pow):
+        fn.restype = ctypes.c_double
+    libm.exp2.argtypes = [ctypes.c_double]
+    libm.pow.argtypes = [ctypes.c_double, ctypes.c_double]
+    e = EXP2_EDGE
+    order, keys, std = O.sorted_index(np.array(e["lam"]))
+    assert std == 0.25
+    assert e["lq"] + std / libm.exp2(e["p"]) >= 0.75 > e["lq"] + std / libm.pow(2.0, e["p"])
+    idx, key = O.range_bylambda(keys, order, std, e["lq"], 4, e["p"])
+    assert idx.tolist() == [1] and key.tolist() == [0.75]

@@ -143,3 +143,15 @@ def test_std_pass1_certificate_matches_sequential(case, monkeypatch):
     _, _, rsd = O.sorted_index(lam)
     assert np.float32(sd_seq) == np.float32(rsd)
     assert np.float32(sd) == np.float32(rsd)
+
+
+def test_range_band_exp2_edge():
+    """The band of range_bylambda is std / exp2(p) (an optimised reference
+    build: LLVM rewrites pow(2.0, p) to exp2(p)); the edge case of
+    tests/test_oracle.py, where pow(2, p) would exclude the key."""
+    import surfface_hip as S
+    from test_oracle import EXP2_EDGE as e
+    sl = S.SortedLambdas().build_from(torch.tensor(e["lam"], dtype=torch.float64, device="cuda"))
+    assert sl.std_dev == 0.25
+    out = sl.range_bylambda(e["lq"], 4, e["p"])
+    assert [i for i, _ in out] == [1] and [l for _, l in out] == [0.75]

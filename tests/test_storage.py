@@ -131,3 +131,31 @@ def test_sparse_with_builder_config_writes_metadata(tmp_path):
     assert (f.file_type, f.rows, f.cols, f.nnz, f.size_bytes) == ("sparse", 2, 2, 3, os.path.getsize(fp))
     with pytest.raises(ST.StorageError):
         ST.config_value("F32", 1.0)
+
+
+def test_config_value_accessors_and_nonfinite_json(tmp_path):
+    """ConfigValue semantics (surfface-pipeline/src/builder.rs:1555-1604):
+    as_f64 reads NaN as -1.0 (F64 and OptionF64), as_tau_mode is None for
+    another variant while as_f64 / as_usize panic on one; serde_json writes a
+    non-finite f64 as null, never as a bare NaN token."""
+    md = ST.ArrowSpaceMetadata("m").with_builder_config({
+        "lambda_eps": ST.config_value("F64", float("nan")),
+        "synthesis": ST.config_value("Usize", 3),
+        "lambda_k": ST.config_value("OptionUsize", None)})
+    assert md.lambda_eps() == -1.0
+    assert md.synthesis() is None
+    assert md.lambda_k() is None
+    md.builder_config["lambda_eps"] = ST.config_value("OptionF64", float("nan"))
+    assert md.lambda_eps() == -1.0
+    md.builder_config["lambda_eps"] = ST.config_value("OptionF64", None)
+    assert md.lambda_eps() is None
+    md.builder_config["lambda_eps"] = ST.config_value("Usize", 2)
+    with pytest.raises(ST.StorageError):
+        md.lambda_eps()
+    md.builder_config["lambda_eps"] = ST.config_value("F64", float("inf"))
+    md.builder_config["eps2"] = ST.config_value("OptionF64", float("nan"))
+    text = md.to_json()
+    assert "NaN" not in text and "Infinity" not in text
+    raw = json.loads(text)
+    assert raw["builder_config"]["lambda_eps"] == {"F64": None}
+    assert raw["builder_config"]["eps2"] == {"OptionF64": None}
