@@ -53,9 +53,14 @@ constexpr int WQF = 4;       // 16-query fragments per wave
 constexpr int WCF = 8;       // 16-row corpus fragments per wave
 constexpr int SCAP = 224;    // staged candidates per wave
 
-struct alignas(16) Smem {
+// the LDS-DMA ring is its own LDS object: the compiler's wait insertion then
+// knows the DMA never writes the per-tile arrays below (one shared object made
+// it drain every DMA in flight before each tile's accumulator init)
+struct alignas(16) Ring {
     uint16_t C[NSLOT][BC][KB];   // corpus k-step, 16 KB per slot
     uint16_t Q[NSLOT][BQ][KB];   // query k-step, 16 KB per slot
+};
+struct alignas(16) Smem {
     float hc[2][BC];             // |c|^2 / 2 of a tile (+inf past the slice end)
     float tc[2][BC];             // SW_SYM: tau0 of a tile's rows (off-diagonal keys)
     union {
@@ -70,9 +75,14 @@ struct alignas(16) Smem {
     uint2 stk[NWAVES][SCAP];     // staged candidates per wave: (key bits, global id)
     uint32_t stp[NWAVES][SCAP];  //   and (query in block | buffer position << 8)
 };
-static_assert(sizeof(Smem) <= 163840, "LDS budget");
+static_assert(sizeof(Smem) + sizeof(Ring) <= 163840, "LDS budget");
 
 __device__ __forceinline__ int swz(int r, int c) { return c ^ (((r >> 3) & 1) << 1); }
+
+// byte address of an LDS object (for inline-asm ds_* operands)
+__device__ __forceinline__ uint32_t lds_addr(const void *p) {
+    return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void *)p;
+}
 
 __device__ __forceinline__ int xcd_remap(int orig, int nwg) {
     const int q = nwg / 8, r = nwg % 8, xcd = orig % 8;
@@ -145,15 +155,24 @@ struct SymArgs {
 // F16: the operands are fp16 copies of x 2^e (one v_mfma_f32_16x16x32_f16 per
 // 32 features: the same rate as bf16, 11 significant bits instead of 8, so the
 // residual-norm bound is ~8x tighter); SW_SYM only.
-template <int PROBE, int MODE = SW_L2, bool TM = false, bool F16 = false>
+// V (schedule variant, tuning A/B): 0 = each wave issues its LDS-DMA pieces
+// at the start of its read window; 1 = interleaved with its MFMAs (one piece
+// after every 8), so the read window holds only the fragment reads.
+template <int PROBE, int MODE = SW_L2, bool TM = false, bool F16 = false, int V = 0>
 __global__ __launch_bounds__(NT) void k_gram_sweep2(
     const uint16_t *__restrict__ Qk, int64_t nq, const uint16_t *__restrict__ Ck, int64_t nc,
     int nkb, int64_t q_off, int64_t c_off, int excl, const float *__restrict__ tq,
     const float *__restrict__ tau0, const float *__restrict__ hc, int64_t c_begin, int S,
     int64_t chunk, int cap, uint2 *__restrict__ buf, int *__restrict__ cnt, int pst = 0,
     SymArgs sym = SymArgs{}) {
+    // PROBE 5 / 6 (tuning build, results invalid): every block's rows read
+    // from panel 0 and its column tiles from panel 1 (L2-resident), with /
+    // without the epilogue — the kernel's own ceiling without fabric traffic
+    constexpr bool L2RES = PROBE == 5 || PROBE == 6;
+    constexpr bool EPI = PROBE == 0 || PROBE == 5;
     constexpr bool SYM = MODE == SW_SYM || MODE == SW_COS_SYM;
     constexpr bool COSM = MODE == SW_COS || MODE == SW_COS_SYM;  // product-form acc0, NaN pads
+    __shared__ Ring rg;
     __shared__ Smem sm;
     const int tid = threadIdx.x, lane = tid & 63;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -218,8 +237,10 @@ __global__ __launch_bounds__(NT) void k_gram_sweep2(
     const int co0 = TM ? prow0 * KB + pch : min(bt0 + prow0, cend - 1) * KB + pch;
     const int co1 = TM ? prow1 * KB + pch : min(bt0 + prow1, cend - 1) * KB + pch;
     const int64_t panel = (int64_t)pst * BC * KB;  // TM: elements between 256-row panels
-    const uint16_t *const qpan = TM ? Qk + (int64_t)(q0 / BQ) * panel : Qk;
-    auto cpan = [&](int row0) { return TM ? Ck + (int64_t)(row0 / BC) * panel : Ck; };
+    const uint16_t *const qpan = TM ? Qk + (int64_t)(L2RES ? 0 : q0 / BQ) * panel : Qk;
+    auto cpan = [&](int row0) {
+        return TM ? Ck + (int64_t)(L2RES ? 1 : row0 / BC) * panel : Ck;
+    };
     const uint16_t *cbk = cpan(bt0), *qbk = qpan;
     const int cstep = TM ? BC * KB : (int)nc * KB, qstep = TM ? BQ * KB : (int)nq * KB;
     // LDS-DMA through buffer descriptors: one k-block region ([n][32] bf16,
@@ -233,20 +254,34 @@ __global__ __launch_bounds__(NT) void k_gram_sweep2(
     // (nc * 32, nq * 32 < 2^31 is checked by the driver: the byte counts fit 32 bits)
     const int cbytes = TM ? BC * KB * 2 : (int)(uint32_t)(nc * 64);
     const int qbytes = TM ? BQ * KB * 2 : (int)(uint32_t)(nq * 64);
-    auto dma = [&](__amdgpu_buffer_rsrc_t rs, int voff, uint16_t *lds) {
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void *)lds,
-                                                 16, voff, 0, 0, 0);
+    // LDS-DMA as inline asm (M0 = the LDS destination, one wait state before
+    // the load): the compiler does not track these, so it never drains them
+    // before the epilogue's LDS accesses (it cannot tell that those do not
+    // alias the ring); the ring protocol's counted waits order them instead
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    auto rsrc = [&](const uint16_t *base, int bytes) {
+        const uint64_t a = (uint64_t)(uintptr_t)base;
+        u32x4 r;
+        r.x = __builtin_amdgcn_readfirstlane((uint32_t)a);
+        r.y = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32) & 0xffffu);
+        r.z = (uint32_t)bytes;
+        r.w = 0x00020000u;
+        return r;
     };
-    auto issue = [&]() {
-        if (bti < ntile) {
-            const __amdgpu_buffer_rsrc_t rc =
-                __builtin_amdgcn_make_buffer_rsrc((void *)cbk, (short)0, cbytes, 0x00020000);
-            const __amdgpu_buffer_rsrc_t rq =
-                __builtin_amdgcn_make_buffer_rsrc((void *)qbk, (short)0, qbytes, 0x00020000);
-            dma(rc, cb0, &sm.C[bslot][32 * w][0]);
-            dma(rc, cb1, &sm.C[bslot][32 * w + 16][0]);
-            dma(rq, qb0, &sm.Q[bslot][32 * w][0]);
-            dma(rq, qb1, &sm.Q[bslot][32 * w + 16][0]);
+    auto dma = [&](const u32x4 &rs, int voff, uint16_t *lds) {
+        asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds"
+                     :
+                     : "s"(__builtin_amdgcn_readfirstlane(lds_addr(lds))), "v"(voff), "s"(rs)
+                     : "memory", "m0");
+    };
+    // piece i (0, 1: the corpus tile's rows 32w.. / 32w+16..; 2, 3: the
+    // query panel's) of the next k-step to stage; advance() moves on
+    auto piece = [&](int i) {
+        if (i < 2) dma(rsrc(cbk, cbytes), i ? cb1 : cb0, &rg.C[bslot][32 * w + 16 * i][0]);
+        else dma(rsrc(qbk, qbytes), i == 3 ? qb1 : qb0, &rg.Q[bslot][32 * w + 16 * (i - 2)][0]);
+    };
+    auto advance = [&]() {
+        {
             bslot = (bslot + 1) & (NSLOT - 1);
             cbk += cstep;
             qbk += qstep;
@@ -261,6 +296,17 @@ __global__ __launch_bounds__(NT) void k_gram_sweep2(
                     cb1 = 2 * (min(bt0 + prow1, cend - 1) * KB + pch);
                 }
             }
+        }
+    };
+    auto issue = [&]() {
+        if (bti < ntile) {
+            const u32x4 rc = rsrc(cbk, cbytes);
+            const u32x4 rq = rsrc(qbk, qbytes);
+            dma(rc, cb0, &rg.C[bslot][32 * w][0]);
+            dma(rc, cb1, &rg.C[bslot][32 * w + 16][0]);
+            dma(rq, qb0, &rg.Q[bslot][32 * w][0]);
+            dma(rq, qb1, &rg.Q[bslot][32 * w + 16][0]);
+            advance();
         }
     };
 
@@ -308,24 +354,51 @@ __global__ __launch_bounds__(NT) void k_gram_sweep2(
             }
         }
     };
+    // fragment reads as inline asm: the compiler cannot see that the ring
+    // protocol (counted vmcnt + barrier) already orders them after the
+    // LDS-DMA, and would drain every DMA in flight before them
+    const int chs0 = 8 * swz(fr, fk);
+    const uint32_t qrd = lds_addr(&rg.Q[0][64 * wq + fr][chs0]);
+    const uint32_t crd = lds_addr(&rg.C[0][128 * wc + fr][chs0]);
     auto read_frags = [&](int slot) {
-        const int chs = 8 * swz(fr, fk);
-#pragma unroll
-        for (int f = 0; f < WQF; ++f)
-            fq[f] = *reinterpret_cast<const frag_t *>(&sm.Q[slot][64 * wq + 16 * f + fr][chs]);
+        const uint32_t qa = qrd + (uint32_t)slot * (BQ * KB * 2), ca = crd + (uint32_t)slot * (BC * KB * 2);
+        asm volatile("ds_read_b128 %0, %1" : "=v"(fq[0]) : "v"(qa));
+        asm volatile("ds_read_b128 %0, %1 offset:1024" : "=v"(fq[1]) : "v"(qa));
+        asm volatile("ds_read_b128 %0, %1 offset:2048" : "=v"(fq[2]) : "v"(qa));
+        asm volatile("ds_read_b128 %0, %1 offset:3072" : "=v"(fq[3]) : "v"(qa));
+        asm volatile("ds_read_b128 %0, %1" : "=v"(fc[0]) : "v"(ca));
+        asm volatile("ds_read_b128 %0, %1 offset:1024" : "=v"(fc[1]) : "v"(ca));
+        asm volatile("ds_read_b128 %0, %1 offset:2048" : "=v"(fc[2]) : "v"(ca));
+        asm volatile("ds_read_b128 %0, %1 offset:3072" : "=v"(fc[3]) : "v"(ca));
+        asm volatile("ds_read_b128 %0, %1 offset:4096" : "=v"(fc[4]) : "v"(ca));
+        asm volatile("ds_read_b128 %0, %1 offset:5120" : "=v"(fc[5]) : "v"(ca));
+        asm volatile("ds_read_b128 %0, %1 offset:6144" : "=v"(fc[6]) : "v"(ca));
+        asm volatile("ds_read_b128 %0, %1 offset:7168" : "=v"(fc[7]) : "v"(ca));
+    };
+    static_assert(WQF == 4 && WCF == 8, "read_frags: 4 query and 8 corpus fragments");
+    auto mfma_row = [&](int f) {
 #pragma unroll
         for (int g = 0; g < WCF; ++g)
-            fc[g] = *reinterpret_cast<const frag_t *>(&sm.C[slot][128 * wc + 16 * g + fr][chs]);
+            if constexpr (F16)
+                acc[f][g] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fc[g], fq[f], acc[f][g], 0, 0, 0);
+            else
+                acc[f][g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fc[g], fq[f], acc[f][g], 0, 0, 0);
     };
     auto mfmas = [&]() {
 #pragma unroll
-        for (int f = 0; f < WQF; ++f)
+        for (int f = 0; f < WQF; ++f) mfma_row(f);
+    };
+    // V = 1: the next k-step's four pieces between the MFMA rows
+    auto mfmas_dma = [&]() {
+        const bool go = bti < ntile;
 #pragma unroll
-            for (int g = 0; g < WCF; ++g)
-                if constexpr (F16)
-                    acc[f][g] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fc[g], fq[f], acc[f][g], 0, 0, 0);
-                else
-                    acc[f][g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fc[g], fq[f], acc[f][g], 0, 0, 0);
+        for (int f = 0; f < WQF; ++f) {
+            mfma_row(f);
+            __builtin_amdgcn_sched_barrier(0);
+            if (go) piece(f);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        if (go) advance();
     };
 
     bool dirty = false;  // candidate stores issued since the last counted wait
@@ -445,7 +518,7 @@ __global__ __launch_bounds__(NT) void k_gram_sweep2(
     // candidates of the tile starting at corpus row ct0: positive accumulators
     // (hpar: the hc parity of that tile)
     auto check = [&](int ct0, int hpar, bool diag) {
-        if constexpr (PROBE == 0) {
+        if constexpr (EPI) {
 #pragma unroll
             for (int f = 0; f < WQF; ++f)
 #pragma unroll
@@ -495,14 +568,14 @@ __global__ __launch_bounds__(NT) void k_gram_sweep2(
                 asm volatile("global_load_dword %0, %1, off" : "=v"(scn) : "v"(ps) : "memory");
             }
         }
-        if constexpr (PROBE < 2 || PROBE == 4) issue();  // k-step g + 3
+        if constexpr (V == 0 && (PROBE < 2 || PROBE >= 4)) issue();  // k-step g + 3
         if (kb == 0 && g > 0) {
             // the previous tile's candidates, then this tile's accumulator
             // init (before the fragment reads: the fragments are dead here)
             check(c0 - cstr, par ^ 1, diag0 && ti == 1);
             init_acc(par, false);
         }
-        if constexpr (PROBE < 3 || PROBE == 4) read_frags((int)(g & (NSLOT - 1)));
+        if constexpr (PROBE < 3 || PROBE >= 4) read_frags((int)(g & (NSLOT - 1)));
         if (kb == nkb - 2 && more && wc == 0) {
             // written 2 k-steps (>= 2 barriers) before init_acc reads it
             const int cb = c0 + cstr + 64 * wq + lane;
@@ -510,13 +583,19 @@ __global__ __launch_bounds__(NT) void k_gram_sweep2(
             if constexpr (SYM) sm.tc[par ^ 1][64 * wq + lane] = cb < cend ? tcn : pad;
             if constexpr (F16) sm.sc[par ^ 1][64 * wq + lane] = cb < cend ? scn : 1.f;
         }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        // the fragments are defined here (tied operands), not at the asm reads
+        asm volatile("s_waitcnt lgkmcnt(0)"
+                     : "+v"(fq[0]), "+v"(fq[1]), "+v"(fq[2]), "+v"(fq[3]), "+v"(fc[0]), "+v"(fc[1]),
+                       "+v"(fc[2]), "+v"(fc[3]), "+v"(fc[4]), "+v"(fc[5]), "+v"(fc[6]), "+v"(fc[7])
+                     :
+                     : "memory");
         if (PROBE != 4 && wc == 1) {
             // trailing group: k-step g+1 landed for the window after this one
+            // (V = 1: k-step g+3 is not issued yet)
             const int rem = gtot - 1 - g;
             if (dirty) MN_VMCNT(0);
-            else if (rem >= 3) MN_VMCNT(8);
-            else if (rem == 2) MN_VMCNT(4);
+            else if (V == 0 && rem >= 3) MN_VMCNT(8);
+            else if (rem >= 2) MN_VMCNT(4);
             else MN_VMCNT(0);
             dirty = false;
         }
@@ -525,7 +604,8 @@ __global__ __launch_bounds__(NT) void k_gram_sweep2(
         __builtin_amdgcn_sched_barrier(0);
         // ================= MFMA window of k-step g =================
         __builtin_amdgcn_s_setprio(1);
-        mfmas();
+        if constexpr (V == 1 && (PROBE < 2 || PROBE >= 4)) mfmas_dma();  // k-step g + 3
+        else mfmas();
         __builtin_amdgcn_s_setprio(0);
         __builtin_amdgcn_sched_barrier(0);
         if (PROBE != 4 && wc == 0) {

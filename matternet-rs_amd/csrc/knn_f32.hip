@@ -2548,9 +2548,16 @@ static int knn_x1(const float *Q, int64_t nq, const float *C, int64_t nc, int32_
 #ifdef MN_TUNING
             // timing probes (results invalid): noepi = K loop only, nodma /
             // noread = also without the DMA issue / fragment reads
-            if (probe && *probe)
+            // l2res / l2res_noepi = operands L2-resident (panels 0 / 1)
+            if (knob_int("MN_SW_V", 0) == 1) sk = ksw2::k_gram_sweep2<0, ksw2::SW_SYM, true, true, 1>;
+            if (probe && *probe && knob_int("MN_SW_V", 0) == 1)
+                sk = !strcmp(probe, "l2res_noepi") ? ksw2::k_gram_sweep2<6, ksw2::SW_SYM, true, true, 1>
+                                                   : ksw2::k_gram_sweep2<1, ksw2::SW_SYM, true, true, 1>;
+            else if (probe && *probe)
                 sk = !strcmp(probe, "nodma") ? ksw2::k_gram_sweep2<2, ksw2::SW_SYM, true, true>
                      : !strcmp(probe, "noread") ? ksw2::k_gram_sweep2<3, ksw2::SW_SYM, true, true>
+                     : !strcmp(probe, "l2res") ? ksw2::k_gram_sweep2<5, ksw2::SW_SYM, true, true>
+                     : !strcmp(probe, "l2res_noepi") ? ksw2::k_gram_sweep2<6, ksw2::SW_SYM, true, true>
                                                 : ksw2::k_gram_sweep2<1, ksw2::SW_SYM, true, true>;
 #endif
             hipLaunchKernelGGL(sk, dim3((unsigned)tab.size()), dim3(ksw2::NT), 0, s, XK, nc, XK,
@@ -2853,25 +2860,7 @@ static int knn_x1(const float *Q, int64_t nq, const float *C, int64_t nc, int32_
 // (k_merge_certify) — the union of the parts' admitted candidates is exactly
 // the single-GPU sweep's, so the certificate is the same; uncertified rows go
 // to the split exact scan against all N rows (X_all is resident on every rank).
-ShardPlan shard_plan(int64_t N, int d, int k, int world) {
-    ShardPlan p{};
-    p.N = N;
-    p.d = d;
-    p.dp = (d + 255) / 256 * 256;
-    p.nkb = p.dp / 32;
-    p.k = k;
-    p.world = world;
-    p.L1 = std::min(std::max((3 * k + 3) / 8, 12), 48);
-    const char *fs = knob("MN_SH_SAMPLE_DIV");  // tuning build: sample = N / div
-    const int64_t div = (fs && *fs) ? std::max(2, atoi(fs)) : 24;
-    p.m0 = std::max<int64_t>(N / div, (int64_t)64 * p.L1);
-    p.m0 = (p.m0 + 255) / 256 * 256;
-    // as knn_x1: the two-phase form needs a corpus well past the sample;
-    // the sweep's grid and the int32 ids bound N
-    p.ok = k >= 1 && k <= knn::KMAX && d >= 1 && p.m0 + 4 * ksw2::BC <= N && N * 32 < INT_MAX &&
-           world >= 1 && world <= knn::MAX_PARTS;
-    return p;
-}
+static_assert(knn::KMAX == kShardKMax, "shard_plan's k limit is the C ABI's");
 
 static void shard_prep(const float *X, int64_t n, int d, int dp, const int *pm, uint16_t *R,
                        float *nv, float *hcv, float *hv, float *rv, unsigned *cmax, int *flags,

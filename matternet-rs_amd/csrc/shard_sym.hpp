@@ -1,7 +1,10 @@
 // shard_sym.hpp — stages of the row-sharded symmetric kNN build (knn_f32.hip
 // section 6), driven by shard.hip over RCCL or simulated on one device.
 #pragma once
+#include <algorithm>
+#include <climits>
 #include <cstdint>
+#include <cstdlib>
 
 #include "common.hpp"
 #include "matternet_hip.h"
@@ -17,7 +20,29 @@ struct ShardPlan {
     bool ok;        // the symmetric form applies (else the per-shard path)
 };
 
-ShardPlan shard_plan(int64_t N, int d, int k, int world);
+constexpr int kShardKMax = 64;  // k limit of the candidate generators (knn::KMAX)
+
+// The plan of an N-row build over `world` ranks (host only): the global
+// phase-1 sample m0 (the first N / 24 rows of the golden-ratio order, whole
+// 256-row panels) and whether the symmetric form applies (as knn_x1: a corpus
+// well past the sample; the sweep's grid and int32 ids bound N).
+inline ShardPlan shard_plan(int64_t N, int d, int k, int world) {
+    ShardPlan p{};
+    p.N = N;
+    p.d = d;
+    p.dp = (d + 255) / 256 * 256;
+    p.nkb = p.dp / 32;
+    p.k = k;
+    p.world = world;
+    p.L1 = std::min(std::max((3 * k + 3) / 8, 12), 48);
+    const char *fs = knob("MN_SH_SAMPLE_DIV");  // tuning build: sample = N / div
+    const int64_t div = (fs && *fs) ? std::max(2, atoi(fs)) : 24;
+    p.m0 = std::max<int64_t>(N / div, (int64_t)64 * p.L1);
+    p.m0 = (p.m0 + 255) / 256 * 256;
+    p.ok = k >= 1 && k <= kShardKMax && d >= 1 && p.m0 + 4 * 256 <= N && N * 32 < INT_MAX &&
+           world >= 1 && world <= kMaxShardRanks;
+    return p;
+}
 
 // Stage A: tau0_o / qn_o [nl] of rows [row0, row0 + nl) of X_all.  1: the
 // symmetric form does not apply (values too large for the bf16 bound).
