@@ -360,6 +360,16 @@ def c3_legs(S, X, idx, dist, k):
     lst = S.laplacian.last_stats()
     out["item_laplacian"] = {"ms": round(ms, 3), "nnz": Lit.nnz, "GB_per_s": round(byt / ms / 1e6, 1),
                              "rows_block_sorted": lst["big_rows"], "hub_rows": lst["hub_rows"]}
+    # the Stage C form of the same assembly (surfface-core/src/laplacian.rs:312-394
+    # build_laplacian_flat: MAX symmetrisation, f32 values, normalised), timed
+    # separately as SURVEY §8(d) asks; bytes as above with f32 values
+    ms, (Lmx, _) = _timed(lambda: S.build_laplacian_from_knn(
+        idx, dist, weight_kernel="rational", symmetrise="max", normalize=True, eps=float("inf"),
+        sigma=1.0, p=2.0))
+    byt = n * k * 8 + Lmx.nnz * 8 + (n + 1) * 8
+    out["item_laplacian_max_sym"] = {"ms": round(ms, 3), "nnz": Lmx.nnz,
+                                     "GB_per_s": round(byt / ms / 1e6, 1)}
+    del Lmx
     ms, (fi, fd, fw, fst) = _timed(lambda: S.knn_cos_columns(X, 4, eps=1.0, sigma=1.0, p=2.0), 1)
     out["feature_knn_cos"] = {"ms": round(ms, 3), "uncertified": fst["n_uncertified"],
                               "gram_tflops": round(2.0 * f * f * n / 2 / (fst["ms_gram"] * 1e9), 2)
@@ -396,6 +406,14 @@ def c3_legs(S, X, idx, dist, k):
     except (OSError, ValueError):
         pass
     out["energy_rows_per_sec"] = n / (ms * 1e-3)
+    # the energymaps.rs pass BASELINE configs[2] names (node_energy_and_dispersion,
+    # src_legacy/energymaps.rs:923-1045: E = x.Lx / x.x, G over the upper
+    # entries, lambda = E) on the same rows and Laplacian, same bytes
+    from surfface_hip import _lib as _L
+    ms_em, _ = _timed(lambda: S.energy_rows(X, Lf, g_mode=_L.MN_G_ENERGYMAPS))
+    out["energymaps_pass"] = {"ms": round(ms_em, 3), "GB_per_s": round(ebytes / ms_em / 1e6, 1),
+                              "rows_per_s": round(n / (ms_em * 1e-3), 1),
+                              "frac_of_hbm": round(ebytes / ms_em / 1e6 / HBM_PEAK_GBS, 4)}
     out["_Lf"] = Lf
     # energymaps diffusion pre-pass (eta 0.1, 4 steps; energymaps.rs:518-546) on
     # the same rows: f32 in, f64 out; bytes = N F (4 + 8)

@@ -157,8 +157,16 @@ struct SymArgs {
 // residual-norm bound is ~8x tighter); SW_SYM only.
 // V (schedule variant, tuning A/B): 0 = each wave issues its LDS-DMA pieces
 // at the start of its read window; 1 = interleaved with its MFMAs (one piece
-// after every 8), so the read window holds only the fragment reads.
-template <int PROBE, int MODE = SW_L2, bool TM = false, bool F16 = false, int V = 0>
+// after every 8), so the read window holds only the fragment reads; 2 = in
+// the read window AFTER the fragment reads (the reads go to the LDS pipe
+// while the DMA issue waits on the CU's shared texture-address unit); 3 = two
+// pieces after the reads, two between the MFMA rows.
+// Default 14 (placement 2, builtin DMA, plain fragment reads): C2 same
+// process 752.6 ms vs 754.4 (asm reads), 763.1 (asm DMA + reads), 766.3 (asm
+// DMA), round 4's build 757.8; placement 0 / 1 / 3 774 / 827 / 777 (with the
+// asm forms; profiles/r05/r05_ab_*.log).  The asm forms keep the compiler
+// from draining the DMA before LDS accesses, but cost more than they save.
+template <int PROBE, int MODE = SW_L2, bool TM = false, bool F16 = false, int V = 14>
 __global__ __launch_bounds__(NT) void k_gram_sweep2(
     const uint16_t *__restrict__ Qk, int64_t nq, const uint16_t *__restrict__ Ck, int64_t nc,
     int nkb, int64_t q_off, int64_t c_off, int excl, const float *__restrict__ tq,
@@ -169,6 +177,10 @@ __global__ __launch_bounds__(NT) void k_gram_sweep2(
     // from panel 0 and its column tiles from panel 1 (L2-resident), with /
     // without the epilogue — the kernel's own ceiling without fabric traffic
     constexpr bool L2RES = PROBE == 5 || PROBE == 6;
+    // V bits: 0..1 the DMA placement; 4: the LDS-DMA through the compiler
+    // builtin instead of inline asm; 8: the fragment reads as plain loads
+    constexpr int VP = V & 3;
+    constexpr bool ASM_DMA = !(V & 4), ASM_READ = !(V & 8);
     constexpr bool EPI = PROBE == 0 || PROBE == 5;
     constexpr bool SYM = MODE == SW_SYM || MODE == SW_COS_SYM;
     constexpr bool COSM = MODE == SW_COS || MODE == SW_COS_SYM;  // product-form acc0, NaN pads
@@ -269,10 +281,18 @@ __global__ __launch_bounds__(NT) void k_gram_sweep2(
         return r;
     };
     auto dma = [&](const u32x4 &rs, int voff, uint16_t *lds) {
-        asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds"
-                     :
-                     : "s"(__builtin_amdgcn_readfirstlane(lds_addr(lds))), "v"(voff), "s"(rs)
-                     : "memory", "m0");
+        if constexpr (ASM_DMA) {
+            asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds"
+                         :
+                         : "s"(__builtin_amdgcn_readfirstlane(lds_addr(lds))), "v"(voff), "s"(rs)
+                         : "memory", "m0");
+        } else {
+            const uint64_t a = ((uint64_t)rs.y << 32) | rs.x;
+            const __amdgpu_buffer_rsrc_t r =
+                __builtin_amdgcn_make_buffer_rsrc((void *)(uintptr_t)a, (short)0, (int)rs.z, (int)rs.w);
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void *)lds,
+                                                     16, voff, 0, 0, 0);
+        }
     };
     // piece i (0, 1: the corpus tile's rows 32w.. / 32w+16..; 2, 3: the
     // query panel's) of the next k-step to stage; advance() moves on
@@ -361,6 +381,16 @@ __global__ __launch_bounds__(NT) void k_gram_sweep2(
     const uint32_t qrd = lds_addr(&rg.Q[0][64 * wq + fr][chs0]);
     const uint32_t crd = lds_addr(&rg.C[0][128 * wc + fr][chs0]);
     auto read_frags = [&](int slot) {
+        if constexpr (!ASM_READ) {
+            const int chs = 8 * swz(fr, fk);
+#pragma unroll
+            for (int f = 0; f < WQF; ++f)
+                fq[f] = *reinterpret_cast<const frag_t *>(&rg.Q[slot][64 * wq + 16 * f + fr][chs]);
+#pragma unroll
+            for (int g = 0; g < WCF; ++g)
+                fc[g] = *reinterpret_cast<const frag_t *>(&rg.C[slot][128 * wc + 16 * g + fr][chs]);
+            return;
+        }
         const uint32_t qa = qrd + (uint32_t)slot * (BQ * KB * 2), ca = crd + (uint32_t)slot * (BC * KB * 2);
         asm volatile("ds_read_b128 %0, %1" : "=v"(fq[0]) : "v"(qa));
         asm volatile("ds_read_b128 %0, %1 offset:1024" : "=v"(fq[1]) : "v"(qa));
@@ -388,14 +418,19 @@ __global__ __launch_bounds__(NT) void k_gram_sweep2(
 #pragma unroll
         for (int f = 0; f < WQF; ++f) mfma_row(f);
     };
-    // V = 1: the next k-step's four pieces between the MFMA rows
+    // V = 1: the next k-step's four pieces between the MFMA rows; V = 3: the
+    // last two (the query panel's) after rows 1 and 3
     auto mfmas_dma = [&]() {
         const bool go = bti < ntile;
 #pragma unroll
         for (int f = 0; f < WQF; ++f) {
             mfma_row(f);
             __builtin_amdgcn_sched_barrier(0);
-            if (go) piece(f);
+            if constexpr (VP == 1) {
+                if (go) piece(f);
+            } else {
+                if (go && (f & 1)) piece(2 + (f >> 1));
+            }
             __builtin_amdgcn_sched_barrier(0);
         }
         if (go) advance();
@@ -435,15 +470,16 @@ __global__ __launch_bounds__(NT) void k_gram_sweep2(
         }
     };
     // candidates of the tile starting at corpus row ct0: positive accumulators.
-    // Per 16 x 16 fragment one max and one ballot (wave-uniform branch); the
-    // staging body runs only for fragments where some lane has a candidate
-    // (a few per wave and tile at the C2 threshold).
-    // one 16 x 16 fragment: per-fragment max + ballot (wave-uniform branch);
-    // the staging body runs only where some lane has a candidate
+    // Per 16 x 16 fragment one prefilter (the max of the four accumulators'
+    // bit patterns as signed integers: positive iff some float is > 0 or a
+    // +NaN, which the exact test below drops) and one ballot (wave-uniform
+    // branch); the staging body runs only for fragments where some lane has
+    // a candidate (a few per wave and tile at the C2 threshold).
     auto check_block = [&](int f, int g, int ct0, int hpar, bool diag) {
         const f32x4 a = acc[f][g];
-        const float m4 = fmaxf(fmaxf(a[0], a[1]), fmaxf(a[2], a[3]));
-        if (__builtin_expect(__ballot(m4 > 0.f) == 0, 1)) return;
+        const int mi = max(max(__float_as_int(a[0]), __float_as_int(a[1])),
+                           max(__float_as_int(a[2]), __float_as_int(a[3])));
+        if (__builtin_expect(__ballot(mi > 0) == 0, 1)) return;
         const int ql = 64 * wq + 16 * f + fr;
         const int qgl = (int)q_off + q0 + ql;  // (global ids fit int32: the outputs are int32)
         const int c = (int)c_off + ct0 + 128 * wc + 16 * g + 4 * fk;  // id of register 0
@@ -470,17 +506,23 @@ __global__ __launch_bounds__(NT) void k_gram_sweep2(
                 return;
             }
             const float t0l = sm.t0[ql];
+            // F16: 2 acc / (s_q s_c) as the two divisions by powers of 2 round
+            // it — two ldexp (correctly rounded) instead of two divisions
+            const int eq = F16 ? 1 - __builtin_amdgcn_frexp_expf(sm.sq[ql]) : 0;
             while (pm) {
                 const int r = __builtin_ctz(pm);
                 pm &= pm - 1;
-                // F16: 2 acc / (s_q s_c), exact (powers of 2)
-                const float a2 = 2.f * (F16 ? a[r] / sm.sq[ql] /
-                                                  sm.sc[hpar][128 * wc + 16 * g + 4 * fk + r]
-                                            : a[r]);
+                const int cl = 128 * wc + 16 * g + 4 * fk + r;
+                float a2 = a[r];
+                if constexpr (F16) {
+                    a2 = __builtin_ldexpf(a2, eq);
+                    a2 = __builtin_ldexpf(a2, 1 - __builtin_amdgcn_frexp_expf(sm.sc[hpar][cl]));
+                }
+                a2 *= 2.f;
                 if (diag) {  // row q's test, as SW_L2
                     emit_sym((uint32_t)qgl, (uint32_t)(c + r), t0l - a2);
                 } else {     // row c's test (acc > 0); row q's only on these hits
-                    const float key = sm.tc[hpar][128 * wc + 16 * g + 4 * fk + r] - a2;
+                    const float key = sm.tc[hpar][cl] - a2;
                     emit_sym((uint32_t)(c + r), (uint32_t)qgl, key);
                     if (key < t0l) emit_sym((uint32_t)qgl, (uint32_t)(c + r), key);
                 }
@@ -568,7 +610,7 @@ __global__ __launch_bounds__(NT) void k_gram_sweep2(
                 asm volatile("global_load_dword %0, %1, off" : "=v"(scn) : "v"(ps) : "memory");
             }
         }
-        if constexpr (V == 0 && (PROBE < 2 || PROBE >= 4)) issue();  // k-step g + 3
+        if constexpr (VP == 0 && (PROBE < 2 || PROBE >= 4)) issue();  // k-step g + 3
         if (kb == 0 && g > 0) {
             // the previous tile's candidates, then this tile's accumulator
             // init (before the fragment reads: the fragments are dead here)
@@ -576,6 +618,16 @@ __global__ __launch_bounds__(NT) void k_gram_sweep2(
             init_acc(par, false);
         }
         if constexpr (PROBE < 3 || PROBE >= 4) read_frags((int)(g & (NSLOT - 1)));
+        if constexpr (PROBE < 2 || PROBE >= 4) {
+            __builtin_amdgcn_sched_barrier(0);
+            if constexpr (VP == 2) issue();  // k-step g + 3, behind the reads
+            if constexpr (VP == 3)
+                if (bti < ntile) {
+                    piece(0);
+                    piece(1);
+                }
+            __builtin_amdgcn_sched_barrier(0);
+        }
         if (kb == nkb - 2 && more && wc == 0) {
             // written 2 k-steps (>= 2 barriers) before init_acc reads it
             const int cb = c0 + cstr + 64 * wq + lane;
@@ -584,17 +636,22 @@ __global__ __launch_bounds__(NT) void k_gram_sweep2(
             if constexpr (F16) sm.sc[par ^ 1][64 * wq + lane] = cb < cend ? scn : 1.f;
         }
         // the fragments are defined here (tied operands), not at the asm reads
-        asm volatile("s_waitcnt lgkmcnt(0)"
-                     : "+v"(fq[0]), "+v"(fq[1]), "+v"(fq[2]), "+v"(fq[3]), "+v"(fc[0]), "+v"(fc[1]),
-                       "+v"(fc[2]), "+v"(fc[3]), "+v"(fc[4]), "+v"(fc[5]), "+v"(fc[6]), "+v"(fc[7])
-                     :
-                     : "memory");
+        if constexpr (ASM_READ)
+            asm volatile("s_waitcnt lgkmcnt(0)"
+                         : "+v"(fq[0]), "+v"(fq[1]), "+v"(fq[2]), "+v"(fq[3]), "+v"(fc[0]),
+                           "+v"(fc[1]), "+v"(fc[2]), "+v"(fc[3]), "+v"(fc[4]), "+v"(fc[5]),
+                           "+v"(fc[6]), "+v"(fc[7])
+                         :
+                         : "memory");
+        else
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         if (PROBE != 4 && wc == 1) {
             // trailing group: k-step g+1 landed for the window after this one
             // (V = 1: k-step g+3 is not issued yet)
             const int rem = gtot - 1 - g;
             if (dirty) MN_VMCNT(0);
-            else if (V == 0 && rem >= 3) MN_VMCNT(8);
+            else if ((VP == 0 || VP == 2) && rem >= 3) MN_VMCNT(8);
+            else if (VP == 3 && rem >= 3) MN_VMCNT(6);  // k-step g+3: 2 of 4 pieces
             else if (rem >= 2) MN_VMCNT(4);
             else MN_VMCNT(0);
             dirty = false;
@@ -604,7 +661,7 @@ __global__ __launch_bounds__(NT) void k_gram_sweep2(
         __builtin_amdgcn_sched_barrier(0);
         // ================= MFMA window of k-step g =================
         __builtin_amdgcn_s_setprio(1);
-        if constexpr (V == 1 && (PROBE < 2 || PROBE >= 4)) mfmas_dma();  // k-step g + 3
+        if constexpr ((VP == 1 || VP == 3) && (PROBE < 2 || PROBE >= 4)) mfmas_dma();  // k-step g + 3
         else mfmas();
         __builtin_amdgcn_s_setprio(0);
         __builtin_amdgcn_sched_barrier(0);

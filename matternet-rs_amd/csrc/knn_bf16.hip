@@ -1086,6 +1086,9 @@ static int knn_cos_bf16_x1(const uint16_t *X, int64_t n, int32_t d, const mn_cos
         const char *probe = knob("MN_BF16_PROBE");  // tuning build: noepi = K loop only
 #ifdef MN_TUNING
         if (probe && !strcmp(probe, "noepi")) kern = ksw2::k_gram_sweep2<1, ksw2::SW_COS_SYM, true>;
+        // MN_SW_V: the DMA-placement variants of gram_sweep2.hpp (default 14)
+        if (knob_int("MN_SW_V", 14) == 0) kern = ksw2::k_gram_sweep2<0, ksw2::SW_COS_SYM, true, false, 0>;
+        if (knob_int("MN_SW_V", 14) == 2) kern = ksw2::k_gram_sweep2<0, ksw2::SW_COS_SYM, true, false, 2>;
 #endif
         hipLaunchKernelGGL(kern, dim3((unsigned)tab.size()), dim3(ksw2::NT), 0, s, XK, n, XK, n, nkb,
                            (int64_t)0, (int64_t)0, 1, tqS, cnS, hcS, (int64_t)0, 1, (int64_t)0,

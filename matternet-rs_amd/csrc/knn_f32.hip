@@ -2549,10 +2549,20 @@ static int knn_x1(const float *Q, int64_t nq, const float *C, int64_t nc, int32_
             // timing probes (results invalid): noepi = K loop only, nodma /
             // noread = also without the DMA issue / fragment reads
             // l2res / l2res_noepi = operands L2-resident (panels 0 / 1)
-            if (knob_int("MN_SW_V", 0) == 1) sk = ksw2::k_gram_sweep2<0, ksw2::SW_SYM, true, true, 1>;
-            if (probe && *probe && knob_int("MN_SW_V", 0) == 1)
-                sk = !strcmp(probe, "l2res_noepi") ? ksw2::k_gram_sweep2<6, ksw2::SW_SYM, true, true, 1>
-                                                   : ksw2::k_gram_sweep2<1, ksw2::SW_SYM, true, true, 1>;
+            // MN_SW_V: the DMA-placement variants of gram_sweep2.hpp (default 2)
+            const int swv = knob_int("MN_SW_V", 14);
+            if (swv == 0) sk = ksw2::k_gram_sweep2<0, ksw2::SW_SYM, true, true, 0>;
+            if (swv == 6) sk = ksw2::k_gram_sweep2<0, ksw2::SW_SYM, true, true, 6>;
+            if (swv == 10) sk = ksw2::k_gram_sweep2<0, ksw2::SW_SYM, true, true, 10>;
+            if (swv == 2) sk = ksw2::k_gram_sweep2<0, ksw2::SW_SYM, true, true, 2>;
+            if (swv == 12) sk = ksw2::k_gram_sweep2<0, ksw2::SW_SYM, true, true, 12>;
+            if (swv == 1) sk = ksw2::k_gram_sweep2<0, ksw2::SW_SYM, true, true, 1>;
+            if (swv == 3) sk = ksw2::k_gram_sweep2<0, ksw2::SW_SYM, true, true, 3>;
+            if (probe && *probe && swv >= 0 && swv <= 3)
+                sk = swv == 0 ? ksw2::k_gram_sweep2<1, ksw2::SW_SYM, true, true, 0>
+                     : swv == 1 ? ksw2::k_gram_sweep2<1, ksw2::SW_SYM, true, true, 1>
+                     : swv == 2 ? ksw2::k_gram_sweep2<1, ksw2::SW_SYM, true, true, 2>
+                                : ksw2::k_gram_sweep2<1, ksw2::SW_SYM, true, true, 3>;
             else if (probe && *probe)
                 sk = !strcmp(probe, "nodma") ? ksw2::k_gram_sweep2<2, ksw2::SW_SYM, true, true>
                      : !strcmp(probe, "noread") ? ksw2::k_gram_sweep2<3, ksw2::SW_SYM, true, true>

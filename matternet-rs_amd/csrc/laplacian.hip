@@ -247,12 +247,16 @@ __device__ __forceinline__ void row_sort_fold(int64_t i, int64_t o, int m, int s
 // first store, so the destination may be the source segment.  Returns false
 // (nothing written) for a run of 3 or more equal columns (duplicate ids in one
 // kNN row): the caller then runs row_sort_fold.
-template <int NR, class KeyF, class WF>
+// FOLD false (the bucket kernel): no degree fold here — the kept weights also
+// go to lw[0 .. u) (LDS, ascending column) and *u_out = u, for the bucket's
+// lane-per-row fold.
+template <int NR, bool FOLD = true, class KeyF, class WF>
 __device__ __forceinline__ bool packed_row(KeyF keyf, WF wf, int m, int64_t i, int64_t od, int sym,
                                            int32_t *__restrict__ col, double *__restrict__ wt,
                                            int32_t *__restrict__ uniq, int32_t *__restrict__ kept,
                                            double *__restrict__ deg64,
-                                           float *__restrict__ deg32) {
+                                           float *__restrict__ deg32, double *lw = nullptr,
+                                           int *u_out = nullptr) {
     const int lane = threadIdx.x & 63;
     uint64_t x[NR];
 #pragma unroll
@@ -334,21 +338,28 @@ __device__ __forceinline__ bool packed_row(KeyF keyf, WF wf, int m, int64_t i, i
             const int pos = base + (int)__popcll(mk & ((1ull << lane) - 1ull));
             col[od + pos] = c;
             wt[od + pos] = w[r];
+            if constexpr (!FOLD) lw[pos] = w[r];
         }
         base += (int)__popcll(mk);
-        if (sym == MN_SYM_UNION) {
-            while (mk) {
-                const int l = __builtin_ctzll(mk);
-                mk &= mk - 1;
-                s64 = s64 + readlane_f64(w[r], l);
-            }
-        } else {
-            while (mk) {
-                const int l = __builtin_ctzll(mk);
-                mk &= mk - 1;
-                s32 = s32 + (float)readlane_f64(w[r], l);
+        if constexpr (FOLD) {
+            if (sym == MN_SYM_UNION) {
+                while (mk) {
+                    const int l = __builtin_ctzll(mk);
+                    mk &= mk - 1;
+                    s64 = s64 + readlane_f64(w[r], l);
+                }
+            } else {
+                while (mk) {
+                    const int l = __builtin_ctzll(mk);
+                    mk &= mk - 1;
+                    s32 = s32 + (float)readlane_f64(w[r], l);
+                }
             }
         }
+    }
+    if constexpr (!FOLD) {
+        *u_out = base;
+        return true;
     }
     if (lane == 0) {
         uniq[i] = base;
@@ -372,6 +383,15 @@ __device__ __forceinline__ int packed_row_any(KeyF keyf, WF wf, int m, A... a) {
         if (m <= 512) return packed_row<8>(keyf, wf, m, a...) ? 1 : 0;
     if constexpr (NRMAX >= 16)
         if (m <= 1024) return packed_row<16>(keyf, wf, m, a...) ? 1 : 0;
+    return -1;
+}
+
+// the bucket kernel's form: no fold (FOLD false), *u_out = kept entries
+template <class KeyF, class WF, typename... A>
+__device__ __forceinline__ int packed_row_nofold(KeyF keyf, WF wf, int m, A... a) {
+    if (m <= 64) return packed_row<1, false>(keyf, wf, m, a...) ? 1 : 0;
+    if (m <= 128) return packed_row<2, false>(keyf, wf, m, a...) ? 1 : 0;
+    if (m <= 256) return packed_row<4, false>(keyf, wf, m, a...) ? 1 : 0;
     return -1;
 }
 
@@ -855,6 +875,7 @@ struct alignas(16) BucketSmem {
     int rfill[BR];
     int nbig;
     int big[BR];
+    int ukept[BR];  // kept entries of a row sorted here (-1: sorted elsewhere)
 };
 
 // one block per bucket of BR rows; offs (the rows' segment starts, int64) is
@@ -940,6 +961,7 @@ __global__ __launch_bounds__(BT) void k_lap_bucket(
         const int o = sm.roff[r], mr = sm.roff[r + 1] - o;
         if (!staged) {  // sorted from global memory by the list kernels
             if (lane == 0) {
+                sm.ukept[r] = -1;
                 if (mr <= 256) wave_list[atomicAdd(wave_count, 1)] = (int32_t)i;
                 else mid_list[atomicAdd(mid_count, 1)] = (int32_t)i;
             }
@@ -947,11 +969,37 @@ __global__ __launch_bounds__(BT) void k_lap_bucket(
         }
         auto keyf = [&](int e) { return sm.key[o + e]; };
         auto wf = [&](uint32_t e) { return sm.w[e]; };
-        const int rc = packed_row_any<4>(keyf, wf, mr, i, gbase + o, P.sym, col, wt, uniq, kept,
-                                         deg64, deg32);
+        // the kept weights go back into the row's own stage region (every
+        // gather of the row is issued before its first store), ascending
+        int u = 0;
+        const int rc = packed_row_nofold(keyf, wf, mr, i, gbase + o, P.sym, col, wt, uniq, kept,
+                                         deg64, deg32, &sm.w[o], &u);
         if (rc != 1) {  // longer rows / duplicate ids: the wave kernel <16> from global
             raw_out(r);
             if (lane == 0) mid_list[atomicAdd(mid_count, 1)] = (int32_t)i;
+        }
+        if (lane == 0) sm.ukept[r] = rc == 1 ? u : -1;
+    }
+    __syncthreads();
+    // the degrees: one lane per row, the row's kept weights in ascending
+    // column order (the reference's sequential sum), all rows of the bucket
+    // at once instead of one lane read at a time per row
+    if (t < nr && staged) {
+        const int u = sm.ukept[t];
+        if (u >= 0) {
+            const int64_t i = row0 + t;
+            const double *wr = &sm.w[sm.roff[t]];
+            uniq[i] = u;
+            if (P.sym == MN_SYM_UNION) {
+                double s64 = -0.0;  // laplacian.rs:367 s.iter().map(w).sum() in ascending j
+                for (int e = 0; e < u; ++e) s64 = s64 + wr[e];
+                deg64[i] = s64;
+                kept[i] = u + 1;
+            } else {
+                float s32 = 0.0f;  // surfface-core/src/laplacian.rs:331-340
+                for (int e = 0; e < u; ++e) s32 = s32 + (float)wr[e];
+                deg32[i] = s32;
+            }
         }
     }
 }

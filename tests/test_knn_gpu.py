@@ -424,8 +424,19 @@ def test_symmetric_fp16_sweep_wide_dynamic_range(case):
     ridx, rdist = O.knn_l2sq(X, k)
     assert_exact(idx, dist, ridx, rdist)
     assert st["ms_total"] < 20_000, st
-    if case == "fp16_edge":
-        assert st["n_uncertified"] <= n // 100, st
+    # the certification cost, per case (profiles/r05: measured values):
+    # log_scales certifies every row; fp16_edge leaves a handful; tiny_mixed
+    # leaves ~all rows — its 1e-30 rows square to 0 in f32, so every tiny row
+    # is at distance exactly |q|^2 from an O(1) row q and those 4000 exact ties
+    # sit at the k-th distance of most rows (a strict certificate cannot
+    # settle a tie at D_k): the refill and the exact scan resolve them
+    if case == "log_scales":
+        assert st["n_uncertified"] <= n // 1000 and st["ms_fallback"] < 50, st
+    elif case == "fp16_edge":
+        assert st["n_uncertified"] <= n // 100 and st["ms_fallback"] < 200, st
+    else:
+        assert st["n_escalated"] <= n and st["ms_escalate"] < 500, st
+        assert st["ms_fallback"] < 2000, st
 
 
 def test_split_scan_small_k_many_parts():
