@@ -386,6 +386,103 @@ __device__ __forceinline__ int packed_row_any(KeyF keyf, WF wf, int m, A... a) {
     return -1;
 }
 
+// 32-bit keys (column << 8 | the entry's index in its row) for rows of <= 256
+// entries when every column < 2^24 - 1: one shuffle and one 32-bit compare
+// per exchange instead of two and a 64-bit one.  The bucket kernel's form
+// (no fold: the kept weights to lw[0 .. u), *u_out = u); keyf(e) the key of
+// entry e (SENT32 for an empty slot), wf(e) its weight.  false: a run of >= 3
+// equal columns (the caller's general path).
+constexpr uint32_t SENT32 = ~0u;
+template <int NR, class KeyF, class WF>
+__device__ __forceinline__ bool packed_row32(KeyF keyf, WF wf, int m, int64_t od,
+                                             int32_t *__restrict__ col, double *__restrict__ wt,
+                                             double *lw, int *u_out) {
+    const int lane = threadIdx.x & 63;
+    uint32_t x[NR];
+#pragma unroll
+    for (int r = 0; r < NR; ++r) {
+        const int e = lane + 64 * r;
+        x[r] = e < m ? keyf(e) : SENT32;
+    }
+#pragma unroll
+    for (int q = 2; q <= 64 * NR; q <<= 1) {
+#pragma unroll
+        for (int j = q >> 1; j > 0; j >>= 1) {
+            if (j >= 64) {
+#pragma unroll
+                for (int r = 0; r < NR; ++r) {
+                    const int pr = r ^ (j >> 6);
+                    if (pr > r) {
+                        const bool asc = ((lane + 64 * r) & q) == 0;
+                        if (asc ? x[pr] < x[r] : x[r] < x[pr]) {
+                            const uint32_t t = x[r]; x[r] = x[pr]; x[pr] = t;
+                        }
+                    }
+                }
+            } else {
+#pragma unroll
+                for (int r = 0; r < NR; ++r) {
+                    const int e = lane + 64 * r;
+                    const uint32_t p = (uint32_t)__shfl_xor((int)x[r], j);
+                    const bool asc = (e & q) == 0, lower = (e & j) == 0;
+                    if ((asc == lower) ? p < x[r] : x[r] < p) x[r] = p;
+                }
+            }
+        }
+    }
+    auto colof = [](uint32_t v) { return v == SENT32 ? EMPTY : (int)(v >> 8); };
+    bool run3 = false;
+    uint32_t xn[NR];
+    int cp[NR];
+#pragma unroll
+    for (int r = 0; r < NR; ++r) {
+        const int c = colof(x[r]);
+        int up = __shfl_up(c, 1);
+        const int prevlast = __shfl(colof(x[r > 0 ? r - 1 : 0]), 63);
+        if (lane == 0) up = r == 0 ? INT_MIN : prevlast;
+        cp[r] = up;
+        uint32_t dn = (uint32_t)__shfl_down((int)x[r], 1);
+        const uint32_t nx0 = (uint32_t)__shfl((int)x[r + 1 < NR ? r + 1 : r], 0);
+        if (lane == 63) dn = r + 1 < NR ? nx0 : SENT32;
+        xn[r] = dn;
+        int dn2 = __shfl_down(c, 2);
+        const int n0 = colof(nx0), n1 = __shfl(colof(x[r + 1 < NR ? r + 1 : r]), 1);
+        if (lane >= 62) dn2 = r + 1 < NR ? (lane == 62 ? n0 : n1) : EMPTY;
+        run3 |= c != EMPTY && c == dn2;
+    }
+    if (__any(run3)) return false;
+    double w[NR];
+#pragma unroll
+    for (int r = 0; r < NR; ++r) {
+        const int c = colof(x[r]);
+        const bool keep = c != EMPTY && c != cp[r];
+        w[r] = 0.0;
+        if (keep) {
+            w[r] = wf((int)(x[r] & 255u));
+            if (colof(xn[r]) == c) {
+                const double wp = wf((int)(xn[r] & 255u));
+                if (wp > w[r]) w[r] = wp;
+            }
+        }
+    }
+    int base = 0;
+#pragma unroll
+    for (int r = 0; r < NR; ++r) {
+        const int c = colof(x[r]);
+        const bool keep = c != EMPTY && c != cp[r];
+        const uint64_t mk = __ballot(keep);
+        if (keep) {
+            const int pos = base + (int)__popcll(mk & ((1ull << lane) - 1ull));
+            col[od + pos] = c;
+            wt[od + pos] = w[r];
+            lw[pos] = w[r];
+        }
+        base += (int)__popcll(mk);
+    }
+    *u_out = base;
+    return true;
+}
+
 // the bucket kernel's form: no fold (FOLD false), *u_out = kept entries
 template <class KeyF, class WF, typename... A>
 __device__ __forceinline__ int packed_row_nofold(KeyF keyf, WF wf, int m, A... a) {
@@ -891,6 +988,7 @@ __global__ __launch_bounds__(BT) void k_lap_bucket(
     int32_t *__restrict__ mid_list, int *__restrict__ mid_count) {
     __shared__ BucketSmem sm;
     const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    const bool k32 = n < (1 << 24) - 1;  // 32-bit row keys (column << 8 | entry)
     const int64_t row0 = (int64_t)blockIdx.x * BR;
     const int nr = (int)min((int64_t)BR, n - row0);
     const int64_t e0 = bstart[blockIdx.x], e1 = bstart[blockIdx.x + 1];
@@ -972,8 +1070,22 @@ __global__ __launch_bounds__(BT) void k_lap_bucket(
         // the kept weights go back into the row's own stage region (every
         // gather of the row is issued before its first store), ascending
         int u = 0;
-        const int rc = packed_row_nofold(keyf, wf, mr, i, gbase + o, P.sym, col, wt, uniq, kept,
-                                         deg64, deg32, &sm.w[o], &u);
+        int rc;
+        if (k32 && mr <= 256) {
+            auto key32 = [&](int e) {
+                const uint64_t kk = sm.key[o + e];
+                return kk == SENT ? SENT32 : (((uint32_t)(kk >> 32) << 8) | (uint32_t)e);
+            };
+            auto w32 = [&](int e) { return sm.w[o + e]; };
+            bool ok;
+            if (mr <= 64) ok = packed_row32<1>(key32, w32, mr, gbase + o, col, wt, &sm.w[o], &u);
+            else if (mr <= 128) ok = packed_row32<2>(key32, w32, mr, gbase + o, col, wt, &sm.w[o], &u);
+            else ok = packed_row32<4>(key32, w32, mr, gbase + o, col, wt, &sm.w[o], &u);
+            rc = ok ? 1 : 0;
+        } else {
+            rc = packed_row_nofold(keyf, wf, mr, i, gbase + o, P.sym, col, wt, uniq, kept, deg64,
+                                   deg32, &sm.w[o], &u);
+        }
         if (rc != 1) {  // longer rows / duplicate ids: the wave kernel <16> from global
             raw_out(r);
             if (lane == 0) mid_list[atomicAdd(mid_count, 1)] = (int32_t)i;
