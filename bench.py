@@ -189,7 +189,8 @@ def main():
         kfull = "k_gram_sweep2<0, 0, true>"
         if sym:  # fp16 operands (x 2^e): the release library's only SW_SYM form
             kname = "k_gram_sweep2<SW_SYM>"
-            kfull = "k_gram_sweep2<0, 2, true, true>"
+            # (V = 14: the round-5 DMA/read placement, gram_sweep2.hpp)
+            kfull = "k_gram_sweep2<0, 2, true, true, 14>"
         flops_launch = 2.0 * nq * nc_sw * d
         # executed: the upper-triangle 256 x 256 tiles of the n_tot rows, a
         # rank's 1/world share of them (the sharded symmetric form)
@@ -424,8 +425,17 @@ def c3_legs(S, X, idx, dist, k):
     # item-graph orientation: the F feature signals against
     # the n x n item Laplacian; bytes = one x_j row gather per stored entry
     ms, _ = _timed(lambda: S.signal_energy_and_dispersion(X, Lit))
-    out["item_graph_signals"] = {"ms": round(ms, 3),
-                                 "GB_per_s": round((Lit.nnz // 2 + n) * f * 4 / ms / 1e6, 1)}
+    # algorithmic bytes: X streamed once plus the Laplacian's CSR (col i32 + f64
+    # value per entry, row pointers); the kernel gathers one x_j row per upper
+    # entry instead (random 3 KB rows: bound by the gather, not the stream),
+    # reported beside it
+    alg = n * f * 4 + Lit.nnz * 12 + (n + 1) * 8
+    gat = (Lit.nnz // 2 + n) * f * 4
+    out["item_graph_signals"] = {"ms": round(ms, 3), "GB_per_s": round(alg / ms / 1e6, 1),
+                                 "bytes_basis": "X once + CSR (algorithmic)",
+                                 "frac_of_hbm": round(alg / ms / 1e6 / HBM_PEAK_GBS, 4),
+                                 "gathered_GB_per_s": round(gat / ms / 1e6, 1),
+                                 "gathered_basis": "one 4F-byte x_j row per upper entry + x_i"}
     # Stage C Bhattacharyya feature kNN (§8(f) rank 3) on 2048 centroid rows of X
     cm = X[:2048].contiguous()
     cv = (X[2048:4096].abs() * 0.3 + 0.05).contiguous()

@@ -679,6 +679,111 @@ __device__ bool wave_select_cnt(const uint32_t (&keys)[NR], int f, int rank, int
     return true;
 }
 
+// Inclusive prefix sum over the wave's 64 lanes through DPP (row_shr 1/2/4/8
+// inside each 16-lane row, then row_bcast15 / row_bcast31 carry the row totals
+// forward); lanes whose DPP source is out of range add 0 (`old`).
+__device__ __forceinline__ int wave_incl_scan(int x) {
+    x += (int)dpp32<0x111, 0xF>(0u, (uint32_t)x);
+    x += (int)dpp32<0x112, 0xF>(0u, (uint32_t)x);
+    x += (int)dpp32<0x114, 0xF>(0u, (uint32_t)x);
+    x += (int)dpp32<0x118, 0xF>(0u, (uint32_t)x);
+    x += (int)dpp32<0x142, 0xA>(0u, (uint32_t)x);
+    x += (int)dpp32<0x143, 0xC>(0u, (uint32_t)x);
+    return x;
+}
+
+// Exact order statistic `rank` (and rank + 1 when need == 2) of a row's f keys
+// (pads 0xFFFFFFFF; vals: the same row as floats) by one value-linear
+// histogram pass (round 5): 256 buckets
+// b(v) = min(255, (v - vmin) * 255.99 / (vmax - vmin)) — monotone in v, so a
+// bucket is a key interval — counted with LDS adds, located by a DPP prefix
+// scan over the lanes' four-bucket sums; the keys of the bucket(s) holding the
+// two ranks are compacted and ranked as in wave_select_cnt.  No probe rounds
+// and no scalar popcount chains.  false: more than 64 keys in those buckets
+// (ties, heavy tails) or non-finite values — the caller tries the next select.
+template <int NR>
+__device__ bool wave_select_hist(const uint32_t (&keys)[NR], const float (&vals)[NR], int f,
+                                 int rank, int need, int *hist, uint32_t &out0, uint32_t &out1) {
+    const int lane = threadIdx.x & 63;
+    uint32_t kmin = 0xFFFFFFFFu, kmax = 0u;
+#pragma unroll
+    for (int r = 0; r < NR; ++r) {
+        kmin = min(kmin, keys[r]);
+        kmax = max(kmax, lane + 64 * r < f ? keys[r] : 0u);
+    }
+    kmin = wave_umin_dpp(kmin);
+    kmax = wave_umax_dpp(kmax);
+    if (kmin == kmax) {
+        out0 = out1 = kmin;
+        return true;
+    }
+    const float vlo = key2f(kmin), vhi = key2f(kmax);
+    if (!__builtin_isfinite(vlo) || !__builtin_isfinite(vhi)) return false;
+    const float sc = 255.99f / (vhi - vlo);  // span overflow: sc = 0, one bucket, > 64
+    reinterpret_cast<int4 *>(hist)[lane] = make_int4(0, 0, 0, 0);
+    __builtin_amdgcn_wave_barrier();
+    uint32_t bk[NR];
+#pragma unroll
+    for (int r = 0; r < NR; ++r) {
+        // fminf first: NaN (0 x inf on a denormal span) -> 255, the cast stays defined
+        const float d = fminf((vals[r] - vlo) * sc, 255.0f);
+        bk[r] = (uint32_t)d;
+        if (lane + 64 * r < f) atomicAdd(&hist[bk[r]], 1);
+    }
+    __builtin_amdgcn_wave_barrier();
+    const int4 h = reinterpret_cast<const int4 *>(hist)[lane];
+    const int c1 = h.x, c2 = c1 + h.y, c3 = c2 + h.z, tot = c3 + h.w;
+    const int incl = wave_incl_scan(tot), excl = incl - tot;
+    // bucket holding order statistic q and the count of keys below it
+    auto locate = [&](int q, uint32_t &b, int &below, int &upto) {
+        const uint64_t hit = __ballot(excl <= q && q < incl);
+        const int L = (int)__builtin_ctzll(hit);
+        const int sb = (q - excl >= c1) + (q - excl >= c2) + (q - excl >= c3);
+        const int lo = excl + (sb == 0 ? 0 : (sb == 1 ? c1 : (sb == 2 ? c2 : c3)));
+        const int hi = excl + (sb == 0 ? c1 : (sb == 1 ? c2 : (sb == 2 ? c3 : tot)));
+        b = (uint32_t)__builtin_amdgcn_readlane(4 * lane + sb, L);
+        below = __builtin_amdgcn_readlane(lo, L);
+        upto = __builtin_amdgcn_readlane(hi, L);
+    };
+    uint32_t b0, b1;
+    int cA, e0, cB0, cB;
+    locate(rank, b0, cA, e0);
+    if (need == 2 && rank + 1 >= e0) locate(rank + 1, b1, cB0, cB);
+    else { b1 = b0; cB = e0; }
+    const int m = cB - cA;
+    if (m > 64) return false;
+    __builtin_amdgcn_wave_barrier();  // every lane has read the histogram
+    uint32_t *cand = (uint32_t *)hist;
+    int base = 0;
+#pragma unroll
+    for (int r = 0; r < NR; ++r) {
+        const bool in = lane + 64 * r < f && bk[r] >= b0 && bk[r] <= b1;
+        const uint64_t mk = __ballot(in);
+        if (in) cand[base + (int)__popcll(mk & ((1ull << lane) - 1ull))] = keys[r];
+        base += (int)__popcll(mk);
+    }
+    if (lane >= m) cand[lane] = 0xFFFFFFFFu;
+    __builtin_amdgcn_wave_barrier();
+    const uint32_t u = cand[lane];
+    int lt = 0, le = 0;
+    for (int q = 0; q < m; q += 4) {
+        const uint4 v = *reinterpret_cast<const uint4 *>(&cand[q]);
+        lt += (v.x < u) + (v.y < u) + (v.z < u) + (v.w < u);
+        le += (v.x <= u) + (v.y <= u) + (v.z <= u) + (v.w <= u);
+    }
+    const int t0 = rank - cA;
+    const uint64_t h0 = __ballot(lane < m && lt <= t0 && t0 < le);
+    out0 = (uint32_t)__builtin_amdgcn_readlane((int)u, (int)__builtin_ctzll(h0));
+    if (need == 2) {
+        const uint64_t h1 = __ballot(lane < m && lt <= t0 + 1 && t0 + 1 < le);
+        out1 = (uint32_t)__builtin_amdgcn_readlane((int)u, (int)__builtin_ctzll(h1));
+    } else {
+        out1 = out0;
+    }
+    __builtin_amdgcn_wave_barrier();  // cand is reused by the next row
+    return true;
+}
+
 // Median / Percentile tau of every row, one wave per row (grid-stride), for
 // k_energy_rows2: a lean kernel (keys in registers, 1 KB LDS per wave) at
 // high occupancy re-reads X instead of holding the select's registers and
@@ -968,7 +1073,7 @@ __global__ __launch_bounds__(64 * E3<S64>::WAVES) void k_energy_rows3(
     int64_t nbP, const uint32_t *__restrict__ geij, const double *__restrict__ gev,
     const double *__restrict__ gdgm, double mA_g, int g_mode, int tau_mode, double tau_param,
     int pct_rank, double *__restrict__ Eo, double *__restrict__ Go, double *__restrict__ Lo,
-    const int32_t *__restrict__ gperm) {
+    const int32_t *__restrict__ gperm, int sel_v) {
     extern __shared__ __attribute__((aligned(16))) unsigned char dsm[];
     constexpr int NW = E3<S64>::WAVES, XB = E3<S64>::XB;
     typedef typename std::conditional<S64, double2, float2>::type stage_t;
@@ -1070,7 +1175,10 @@ __global__ __launch_bounds__(64 * E3<S64>::WAVES) void k_energy_rows3(
                     keys[r] = k | (uint32_t)-(int32_t)(lane + 64 * r >= f);
                 }
                 uint32_t k0, k1;
-                if (wave_select_cnt<NR>(keys, f, rank, need, (uint32_t *)hist, k0, k1)) {
+                // sel_v 1 (default): histogram select, then the counted
+                // selection, then the radix select; 0: the round-4 order
+                if ((sel_v == 1 && wave_select_hist<NR>(keys, cur[t], f, rank, need, hist, k0, k1)) ||
+                    wave_select_cnt<NR>(keys, f, rank, need, (uint32_t *)hist, k0, k1)) {
                     double v = (double)key2f(k0);
                     if (need == 2) v = 0.5 * (v + (double)key2f(k1));
                     tau[t] = fmax(v, 1e-10);
@@ -2154,6 +2262,8 @@ static int energy_impl(const mn_csr *L, const float *X, int64_t n, int32_t f,
         MN_HIP_TRY(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
         const int64_t npass3 = (n + 1) / 2;
         const int64_t blocks3 = std::min<int64_t>((npass3 + nw3 - 1) / nw3, ncu);
+        // tuning build: MN_ENERGY_SEL = 0 skips the histogram select (A/B)
+        const int sel3 = knob_int("MN_ENERGY_SEL", 1);
 #define MN_E3(NRV, S6)                                                                          \
     do {                                                                                        \
         MN_HIP_TRY(hipFuncSetAttribute((const void *)k_energy_rows3<NRV, S6>,                   \
@@ -2161,7 +2271,7 @@ static int energy_impl(const mn_csr *L, const float *X, int64_t n, int32_t f,
         hipLaunchKernelGGL((k_energy_rows3<NRV, S6>), dim3((unsigned)blocks3), dim3(64 * nw3),  \
                            sh3, s, X, n, f, naO, naP3, nbO, nbP3, eij3, ev3, dg, mA_g,          \
                            opts->g_mode, opts->tau_mode, opts->tau_param, pct_rank, E, G, lam,  \
-                           perm3);                                                              \
+                           perm3, sel3);                                                        \
     } while (0)
 #define MN_E3S(NRV) do { if (s64) MN_E3(NRV, true); else MN_E3(NRV, false); } while (0)
         if (nr <= 4) MN_E3S(4);

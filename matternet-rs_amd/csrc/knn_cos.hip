@@ -21,9 +21,11 @@
 //                         split-K over rows, f64 atomics into G.
 //   4. k_cos_select       per node (one wave): approximate distances from G,
 //                         wave bitonic sort, top-L candidates + the (L+1)-th.
-//   5. k_cos_exact_wave   per (node, candidate) wave: the reference's
-//                         sequential f64 dot over the full profile (products
-//                         exact and lane-parallel, the chain of adds ordered).
+//   5. k_cos_exact_q      sixteen (node, candidate) pairs a wave, four lanes a
+//                         pair: the reference's sequential f64 dot over the
+//                         full profile (products exact and lane-parallel, the
+//                         chain of adds ordered; k_cos_exact_wave: the round-4
+//                         four-pairs-a-wave form).
 //                         Only candidates that can reach the top k are
 //                         evaluated: the first topk by approximate distance,
 //                         then those whose lower bound d~ - delta does not
@@ -312,6 +314,9 @@ __global__ __launch_bounds__(256) void k_cos_select(const double *__restrict__ G
         if (j < f && j != i) {
             d[r] = cos_dist(gram_at(G, f, i, j), ni, nrm[j]);
             if (d[r] != d[r]) { d[r] = 2.0; nan = true; }  // non-finite data
+            // n_i n_j at the reference's 1e-12 cut: approximate norms may fall
+            // on the other side of it — the node takes the exact path
+            if (__builtin_fabs(ni * nrm[j] - 1e-12) <= 1e-20) nan = true;
             ix[r] = j;
         } else {
             d[r] = __builtin_inf();
@@ -388,6 +393,133 @@ __global__ __launch_bounds__(256) void k_cos_exact_wave(const T *__restrict__ XT
     const T *pa = XT + (int64_t)(dot ? i : 0) * n, *pb = XT + (int64_t)(dot ? j : 0) * n;
     const double acc = ordered_dot4<T, PFD>(pa, pb, n, buf[w]);
     if ((threadIdx.x & 15) == 0 && act) dist[slot] = dot ? cos_dist(acc, nrm[i], nrm[j]) : 1.0;
+}
+
+// Round 5: sixteen listed pairs per wave (lanes 4g..4g+3 run pair g) in
+// 64-element chunks.  The four-chains-per-wave form above reads every product
+// back as a 16-lane broadcast (1 KB of LDS returned per two elements and
+// chain): with ~3.5 waves a CU the LDS return path, not the add chain, set the
+// pace (~16 cycles an element).  Here a ds_read_b128 serves sixteen chains
+// (the 16 chain buffers sit 528 B apart: bank offsets 4g, conflict-free), the
+// products of a chunk are formed by the chain's four lanes (16 each), and
+// PFD chunks of both profiles are in flight (one wave a CU).
+constexpr int CQ = 64;        // chunk (elements of one profile)
+constexpr int CQP = CQ + 2;   // chain buffer stride in doubles (528 B)
+// RAW (round 5): the chains of the listed pairs write their raw dot into
+// dist[slot] (k_cos_dist turns it into the distance once the norms exist) and
+// fnorm more chains follow the np listed ones: chain np + c folds column c
+// with itself -> nrm[c] = sqrt (the reference's sequential norm).
+template <typename T, int PFD, bool RAW = false>
+__global__ __launch_bounds__(64) void k_cos_exact_q(const T *__restrict__ XT, int64_t n,
+                                                    const int32_t *__restrict__ plist,
+                                                    const int *__restrict__ pcount, int64_t pmax,
+                                                    const int32_t *__restrict__ cand, int L,
+                                                    int fnorm, double *__restrict__ nrm,
+                                                    double *__restrict__ dist) {
+    __shared__ __attribute__((aligned(16))) double buf[2][16][CQP];
+    const int lane = threadIdx.x & 63, g = lane >> 2, gl = lane & 3;
+    const int64_t np = pcount ? (int64_t)*pcount : pmax;
+    const int64_t wq = (int64_t)blockIdx.x * 16;
+    if (wq >= np + (RAW ? fnorm : 0)) return;  // wave-uniform
+    const int64_t q = wq + g;
+    int slot = -1, i = 0, j = 0, ncol = -1;
+    bool act = false;
+    double denom = 0.0;
+    if (q < np) {
+        slot = plist ? plist[q] : (int)q;  // slot = i * L + r
+        i = slot / L;
+        j = cand[slot];
+        if (j != INT_MAX) {
+            if constexpr (!RAW) denom = nrm[i] * nrm[j];
+            act = true;
+        }
+    } else if (RAW && q < np + fnorm) {
+        ncol = (int)(q - np);
+        i = j = ncol;
+    }
+    // else cos = 0 without a dot (RAW: every listed pair and norm chain folds)
+    const bool dot = RAW ? (act || ncol >= 0) : (act && denom > 1e-12);
+    const T *a = XT + (int64_t)(dot ? i : 0) * n, *b = XT + (int64_t)(dot ? j : 0) * n;
+    const int64_t nfull = n / CQ;
+    const bool vec = ((((uintptr_t)a) | ((uintptr_t)b)) & 15) == 0;
+    // Straight-line loop body: the loads are unconditional (past the last
+    // full chunk they re-read it) and the main loop runs whole groups of PFD
+    // chunks, so the wait before a chunk's products counts only the loads
+    // issued after its own (vmcnt(N)); with the loads behind a branch the
+    // compiler waited for all of them (vmcnt(0)) at every group.
+    T ra[PFD][16], rb[PFD][16];
+#define MN_QFETCH(C, H)                                  \
+    do {                                                 \
+        const int64_t o_ = (C) * CQ + 16 * gl;           \
+        load16(a + o_, vec, ra[H]);                      \
+        load16(b + o_, vec, rb[H]);                      \
+    } while (0)
+#define MN_QCHUNK(H)                                                                     \
+    do {                                                                                 \
+        double *bb_ = buf[(H) & 1][g];                                                   \
+        _Pragma("unroll") for (int u = 0; u < 16; u += 2)                               \
+            *reinterpret_cast<double2 *>(bb_ + 16 * gl + u) =                            \
+                make_double2((double)ra[H][u] * (double)rb[H][u],                        \
+                             (double)ra[H][u + 1] * (double)rb[H][u + 1]);               \
+    } while (0)
+    double acc = -0.0;
+    if (nfull > 0) {
+#pragma unroll
+        for (int h = 0; h < PFD; ++h) MN_QFETCH(min((int64_t)h, nfull - 1), h);
+        const int64_t nmain = nfull / PFD * PFD;
+        for (int64_t c0 = 0; c0 < nmain; c0 += PFD) {
+#pragma unroll
+            for (int h = 0; h < PFD; ++h) {
+                MN_QCHUNK(h);
+                MN_QFETCH(min(c0 + h + PFD, nfull - 1), h);
+                __builtin_amdgcn_wave_barrier();
+                acc = lds_chain_f64<CQ>(acc, buf[h & 1][g]);
+                __builtin_amdgcn_wave_barrier();
+            }
+        }
+        const int rem = (int)(nfull - nmain);  // < PFD chunks, already in ra[0..rem)
+#pragma unroll
+        for (int h = 0; h < PFD - 1; ++h) {
+            if (h < rem) {
+                MN_QCHUNK(h);
+                __builtin_amdgcn_wave_barrier();
+                acc = lds_chain_f64<CQ>(acc, buf[h & 1][g]);
+                __builtin_amdgcn_wave_barrier();
+            }
+        }
+    }
+#undef MN_QFETCH
+#undef MN_QCHUNK
+    for (int64_t t = nfull * CQ; t < n; ++t) acc = acc + (double)a[t] * (double)b[t];
+    if (gl == 0) {
+        if constexpr (RAW) {
+            if (act) dist[slot] = acc;
+            else if (ncol >= 0) nrm[ncol] = __builtin_sqrt(acc);
+        } else if (act) {
+            dist[slot] = dot ? cos_dist(acc, nrm[i], nrm[j]) : 1.0;
+        }
+    }
+}
+
+// the listed pairs' distances from their raw dots (k_cos_exact_q RAW) and
+// the exact norms: the reference's cos = dot / (n_i n_j) if n_i n_j > 1e-12
+__global__ void k_cos_dist(const int32_t *__restrict__ plist, const int *__restrict__ pcount,
+                           const int32_t *__restrict__ cand, int L,
+                           const double *__restrict__ nrm, double *__restrict__ dist) {
+    const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= (int64_t)*pcount) return;
+    const int slot = plist[q];
+    const int i = slot / L, j = cand[slot];
+    if (j == INT_MAX) return;
+    const double denom = nrm[i] * nrm[j];
+    dist[slot] = denom > 1e-12 ? cos_dist(dist[slot], nrm[i], nrm[j]) : 1.0;
+}
+
+// sqrt(G_ii): the selection's norms when the exact ones come with the exact
+// pass (|G_ii - n_i^2| <= gamma_n n_i^2, like every G_ij)
+__global__ void k_gram_diag_norms(const double *__restrict__ G, int f, double *__restrict__ out) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < f) out[i] = __builtin_sqrt(gram_at(G, f, i, i));
 }
 
 // slots of the first kq candidates of every node (they are always evaluated)
@@ -618,7 +750,7 @@ static int knn_cos_columns_impl(const T *X, int64_t n, int32_t f, const mn_cos_o
     nchunk = (int)((n + kchunk - 1) / kchunk);
 
     T *XT = (T *)scratch(kSlotGeneric0, sizeof(T) * (size_t)n * f);
-    char *g = (char *)scratch(kSlotGeneric1, sizeof(double) * ((size_t)f * f + f * 2 + 64) +
+    char *g = (char *)scratch(kSlotGeneric1, sizeof(double) * ((size_t)f * f + f * 3 + 64) +
                                                 (size_t)f * L * 24 + (size_t)f * 8 + 64);
     MN_REQUIRE(XT && g, MN_ENOMEM, "mn_knn_cos_columns_f32: scratch allocation failed");
     double *G = (double *)g;
@@ -631,22 +763,31 @@ static int knn_cos_columns_impl(const T *X, int64_t n, int32_t f, const mn_cos_o
     double *cdist = (double *)(((uintptr_t)(pj + (size_t)f * L) + 15) & ~(uintptr_t)15);
     double *capx = cdist + (size_t)f * L;
     int32_t *fb_list = (int32_t *)(capx + (size_t)f * L);
+    double *nrmA = (double *)(((uintptr_t)(fb_list + f) + 15) & ~(uintptr_t)15);
 
     Timer tm;
     tm.start(o->timing != 0, s);
     MN_HIP_TRY(hipMemsetAsync(G, 0, sizeof(double) * (size_t)f * f, s));
     MN_HIP_TRY(hipMemsetAsync(flags, 0, 64, s));
-    // the transpose and the exact norms (768 latency-bound chains) run on the
-    // side stream while the Gram (it reads X itself) occupies the MFMAs
-    // (round 4b: the transpose was ahead of the Gram on the main stream)
+    // the transpose runs on the side stream while the Gram (it reads X itself)
+    // occupies the MFMAs (round 4b).  Round 5: the exact norms (768 latency-
+    // bound chains) join the exact pass as chains of their own (k_cos_exact_q
+    // RAW); the candidate selection takes sqrt(G_ii) instead (error folded into
+    // delta).  On the side stream beside the Gram they took 13.7 ms and held
+    // the Gram phase at 20.5 ms.  The all-exact path (topk > 64) still needs
+    // them first: k_col_norms on the side stream.
     hipStream_t side = side_stream();
     MN_REQUIRE(side, MN_EHIP, "mn_knn_cos_columns_f32: side stream creation failed");
     MN_HIP_TRY(stream_wait(side, s));
     hipLaunchKernelGGL(k_transpose<T>, dim3(grid(n, 64), (unsigned)((f + 63) / 64)), dim3(256), 0, side,
                        X, n, f, XT);
     MN_KCHECK(side, "k_transpose");
-    hipLaunchKernelGGL(k_col_norms<T>, dim3((unsigned)((f + 3) / 4)), dim3(64), 0, side, XT, n, f, nrm);
-    MN_KCHECK(side, "k_col_norms");
+    const bool norms_in_pass = !all_exact && knob_int("MN_COS_NORMS_SIDE", 0) == 0;
+    if (!norms_in_pass) {
+        hipLaunchKernelGGL(k_col_norms<T>, dim3((unsigned)((f + 3) / 4)), dim3(64), 0, side, XT, n,
+                           f, nrm);
+        MN_KCHECK(side, "k_col_norms");
+    }
     const int nr = (f + 63) / 64;
     if (all_exact) {
         MN_HIP_TRY(stream_wait(s, side));
@@ -660,7 +801,12 @@ static int knn_cos_columns_impl(const T *X, int64_t n, int32_t f, const mn_cos_o
         MN_HIP_TRY(hipGetLastError());
         MN_HIP_TRY(stream_wait(s, side));
         tm.mark();
-    #define MN_SEL(NRV) hipLaunchKernelGGL(k_cos_select<NRV>, dim3(grid(f, 4)), dim3(256), 0, s, G, nrm, f, L, cand, capx, gnext)
+        // approximate norms sqrt(G_ii) for the selection when the exact ones
+        // come with the exact pass
+        if (norms_in_pass)
+            hipLaunchKernelGGL(k_gram_diag_norms, dim3(grid(f)), dim3(256), 0, s, G, f, nrmA);
+        const double *nsel = norms_in_pass ? nrmA : nrm;
+    #define MN_SEL(NRV) hipLaunchKernelGGL(k_cos_select<NRV>, dim3(grid(f, 4)), dim3(256), 0, s, G, nsel, f, L, cand, capx, gnext)
         if (nr <= 1) MN_SEL(1); else if (nr <= 2) MN_SEL(2); else if (nr <= 4) MN_SEL(4);
         else if (nr <= 8) MN_SEL(8); else if (nr <= 16) MN_SEL(16); else if (nr <= 32) MN_SEL(32);
         else MN_SEL(64);
@@ -669,7 +815,10 @@ static int knn_cos_columns_impl(const T *X, int64_t n, int32_t f, const mn_cos_o
         // whose lower bound can still reach the top k (the rest stay +inf)
         // |d~ - d| bound: f64 accumulation of n products (f64 inputs: each product
         // rounded once more), norms and the quotient, with a factor-2 margin
-        const double delta = 2.0 * ((double)n + (sizeof(T) == 8 ? 17.0 : 16.0)) * 0x1p-53 + 1e-300;
+        // With the norms from G_ii (error <= the Gram's own, gamma_n each) the
+        // bound doubles: 4 (n + 16) u keeps the factor-2 margin.
+        const double delta = (norms_in_pass ? 4.0 : 2.0) *
+                                 ((double)n + (sizeof(T) == 8 ? 17.0 : 16.0)) * 0x1p-53 + 1e-300;
         const int kq = std::min(o->topk, L);
         const int fkq = f * kq;
         hipLaunchKernelGGL(k_fill_f64, dim3(grid((int64_t)f * L)), dim3(256), 0, s, cdist,
@@ -684,11 +833,31 @@ static int knn_cos_columns_impl(const T *X, int64_t n, int32_t f, const mn_cos_o
         // chunks in flight ahead of the chains: 4 (C3, same process,
         // profiles/r04/r04_c3_pf_ab.log: exact pass 8.33-8.42 ms vs 8.44-8.68 at
         // 2 — the chains are bound by their adds, not by the loads); tuning build: MN_COS_PF
+        // round 5: sixteen chains a wave (k_cos_exact_q);
+        // tuning build: MN_COS_EXACT = 0 runs the four-chain form
         const int pfd = knob_int("MN_COS_PF", 4);
-        auto kx = k_cos_exact_wave<T, 2>;
-        if (pfd == 4) kx = k_cos_exact_wave<T, 4>;
-        hipLaunchKernelGGL(kx, dim3(grid((int64_t)f * L, 16)), dim3(256), 0, s, XT, n, pi,
-                           flags + 1, (int64_t)f * L, cand, L, nrm, cdist);
+        if (norms_in_pass) {
+            // the listed pairs' raw dots (into cdist) and the f norm chains
+            // (into nrm) in one pass, then the distances
+            auto kq = k_cos_exact_q<T, 4, true>;
+            if (pfd == 8) kq = k_cos_exact_q<T, 8, true>;
+            hipLaunchKernelGGL(kq, dim3(grid((int64_t)f * L + f, 16)), dim3(64), 0, s, XT, n, pi,
+                               flags + 1, (int64_t)f * L, cand, L, f, nrm, cdist);
+            hipLaunchKernelGGL(k_cos_dist, dim3(grid((int64_t)f * L)), dim3(256), 0, s, pi, flags + 1,
+                               cand, L, nrm, cdist);
+        } else if (knob_int("MN_COS_EXACT", 1) == 1) {
+            // chunks in flight: 4 (C3: 8.13 ms; 8: 9.0 ms, the four-chain
+            // form 8.36 ms — profiles/r05/r05_c3_exact_ab.log)
+            auto kq8 = k_cos_exact_q<T, 4>;
+            if (pfd == 8) kq8 = k_cos_exact_q<T, 8>;
+            hipLaunchKernelGGL(kq8, dim3(grid((int64_t)f * L, 16)), dim3(64), 0, s, XT, n, pi,
+                               flags + 1, (int64_t)f * L, cand, L, 0, nrm, cdist);
+        } else {
+            auto kx = k_cos_exact_wave<T, 2>;
+            if (pfd == 4) kx = k_cos_exact_wave<T, 4>;
+            hipLaunchKernelGGL(kx, dim3(grid((int64_t)f * L, 16)), dim3(256), 0, s, XT, n, pi,
+                               flags + 1, (int64_t)f * L, cand, L, nrm, cdist);
+        }
         hipLaunchKernelGGL(k_cos_finish, dim3(grid(f, 4)), dim3(256), 0, s, cand, cdist, gnext, f, L,
                            o->topk, o->eps, o->sigma, o->p, delta, out_idx, out_dist, out_w, flags,
                            fb_list);
@@ -710,8 +879,8 @@ static int knn_cos_columns_impl(const T *X, int64_t n, int32_t f, const mn_cos_o
             // node i = slot / f (fb_list is the identity here), cand = j or
             // INT_MAX on the diagonal
             hipLaunchKernelGGL(k_all_cand, dim3(grid(np)), dim3(256), 0, s, f, fpj);
-            hipLaunchKernelGGL(k_cos_exact_wave<T>, dim3(grid(np, 16)), dim3(256), 0, s, XT, n,
-                               (const int32_t *)nullptr, (const int *)nullptr, np, fpj, f, nrm, fd);
+            hipLaunchKernelGGL((k_cos_exact_q<T, 4>), dim3(grid(np, 16)), dim3(64), 0, s, XT, n,
+                               (const int32_t *)nullptr, (const int *)nullptr, np, fpj, f, 0, nrm, fd);
         } else {
             hipLaunchKernelGGL(k_fb_pairs, dim3(grid(np)), dim3(256), 0, s, fb_list, flags, f, fpi, fpj);
             hipLaunchKernelGGL(k_cos_exact<T>, dim3(grid(np)), dim3(256), 0, s, XT, n, fpi, fpj, np, nrm, fd);

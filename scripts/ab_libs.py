@@ -15,7 +15,7 @@ import torch  # noqa: E402
 import surfface_hip as S  # noqa: E402
 from surfface_hip import _lib  # noqa: E402
 
-WORK = os.environ.get("AB_WORK", "c2")  # c2: knn_l2sq f32; c5: knn_cos_bf16
+WORK = os.environ.get("AB_WORK", "c2")  # c2: knn_l2sq f32; c5: knn_cos_bf16; c3: knn_cos_columns
 n = int(sys.argv[1]) if len(sys.argv) > 1 else (1_000_000 if WORK == "c2" else 1 << 20)
 d = int(sys.argv[2]) if len(sys.argv) > 2 else (768 if WORK == "c2" else 3072)
 rounds = int(sys.argv[3]) if len(sys.argv) > 3 else 2
@@ -37,7 +37,7 @@ def load(path):
 
 def main():
     global X
-    if WORK == "c2":
+    if WORK in ("c2", "c3"):
         X = torch.empty((n, d), dtype=torch.float32, device="cuda")
         _lib.check(_lib.lib().mn_fill_uniform_f32(X.data_ptr(), n, d, 42, 0, None))
     else:
@@ -60,6 +60,20 @@ def main():
                 os.environ[k_] = val
             _lib._LIB = load(path)
             t = time.time()
+            if WORK == "c3":
+                fi, fd, fw, st = S.knn_cos_columns(X, 4, eps=1.0, sigma=1.0, p=2.0, timing=True)
+                torch.cuda.synchronize()
+                rec = {"round": r, "v": v, "wall": round(time.time() - t, 4),
+                       **{k_: (round(x, 3) if isinstance(x, float) else x) for k_, x in st.items()}}
+                if ref is None:
+                    ref = (fi.clone(), fd.clone())
+                else:
+                    rec["same_as_first"] = bool(torch.equal(ref[0], fi) and torch.equal(ref[1], fd))
+                best[v] = min(best[v], st["ms_total"])
+                for kv in [x for x in knobs.split(",") if x]:
+                    os.environ.pop(kv.split("=")[0], None)
+                print(json.dumps(rec), flush=True)
+                continue
             if WORK == "c2":
                 out = S.knn_l2sq(X, 32, timing=True, algo="bf16x1")
                 st = out.stats

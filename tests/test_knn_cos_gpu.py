@@ -81,3 +81,33 @@ def test_feature_graph_topk_beyond_64(topk):
     np.testing.assert_array_equal(i, ri)
     np.testing.assert_array_equal(d.view(np.uint64), rd.view(np.uint64))
     np.testing.assert_array_equal(w.view(np.uint64), rw.view(np.uint64))
+
+
+def test_norms_from_the_exact_pass_tiny_columns_and_the_1e12_cut():
+    """Round 5: the exact norms come with the exact pass and the selection
+    uses sqrt(G_ii).  Columns scaled so that n_i n_j straddles the
+    reference's 1e-12 cut (norms ~1e-6), tiny and huge columns side by side,
+    a zero column and a NaN column: bit-exact vs the oracle, and the same
+    graph as the round-4 order (exact norms first, MN_COS_NORMS_SIDE=1)."""
+    import os
+    import surfface_hip as S
+    X = datagen.uniform(3000, 96, seed=21)
+    nrm = np.sqrt((X.astype(np.float64) ** 2).sum(0))
+    for c, target in ((3, 1e-6), (4, 1e-6 * (1 + 1e-12)), (5, 0.999999e-6), (6, 1.0000001e-6),
+                      (7, 1e-9), (8, 1e6)):
+        X[:, c] = (X[:, c] * (target / nrm[c])).astype(np.float32)
+    X[:, 10] = 0.0
+    kw = dict(eps=1.0, sigma=1.0, p=2.0)
+    i, d, w, st = hip_cols(X, 4, **kw)
+    exact((i, d, w), ref_cols(X, 4, **kw))
+    Xn = X.copy()
+    Xn[17, 12] = np.nan  # non-finite data: that column's node and its partners fall back
+    i2, d2, w2, _ = hip_cols(Xn, 4, **kw)
+    exact((i2, d2, w2), ref_cols(Xn, 4, **kw))
+    with S._lib.use_tuning():
+        os.environ["MN_COS_NORMS_SIDE"] = "1"
+        try:
+            i3, d3, w3, _ = hip_cols(X, 4, **kw)
+        finally:
+            os.environ.pop("MN_COS_NORMS_SIDE", None)
+    exact((i, d, w), (i3, d3, w3))
