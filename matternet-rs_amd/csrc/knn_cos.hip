@@ -279,6 +279,176 @@ __global__ __launch_bounds__(256) void k_gram_f64(const T *__restrict__ X, int64
             }
 }
 
+// ---- 3b. Gram on f32 MFMA with an f64 fold (round 5, f32 profiles) ----------
+// G~ = X^T X on v_mfma_f32_16x16x4_f32 (f32 inputs as they are), upper
+// 128 x 128 block tiles (four waves of 64 x 64), split-K over row chunks: the
+// f32 accumulators are folded into f64 every G3F rows, the chunk's f64 tile
+// is added into G.  Error (selection only; the exact chains decide): per fold
+// window the f32 sum of G3F products is within (G3F + 8) 2^-24 sum |x_i x_j|
+// (<= n_i n_j), the f64 folds add (n / G3F + nchunk + 8) 2^-53 — valid while
+// no product or partial leaves the f32 normal range: every column's max |x|
+// (atomicMax into colmax) must lie in [2^-20, 2^40] or be 0, else the driver
+// recomputes G with k_gram_f64.
+constexpr int G3T = 128;  // block tile
+constexpr int G3K = 32;   // rows per LDS stage
+constexpr int G3F = 256;  // rows per f32 window before the f64 fold
+constexpr int G3P = G3T + 16;  // row stride: 4 rows of a fragment read on 4 bank quarters
+typedef float f32x4v __attribute__((ext_vector_type(4)));
+
+__global__ __launch_bounds__(256) void k_gram_f32m(const float *__restrict__ X, int64_t n, int f,
+                                                   int ntile, int64_t kchunk,
+                                                   double *__restrict__ G,
+                                                   unsigned *__restrict__ colmax) {
+    __shared__ __attribute__((aligned(16))) float As[G3K][G3P];
+    __shared__ __attribute__((aligned(16))) float Bs[G3K][G3P];
+    const int ntri = ntile * (ntile + 1) / 2;
+    const int chunk = blockIdx.x / ntri;  // chunk-major: concurrent blocks share rows
+    int t = blockIdx.x % ntri, bi = 0;
+    while (t >= ntile - bi) { t -= ntile - bi; ++bi; }
+    const int bj = bi + t;
+    const bool diag = bi == bj;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int wr = w >> 1, wc = w & 1;
+    const int64_t k0 = (int64_t)chunk * kchunk;
+    const int64_t k1 = min(n, k0 + kchunk);
+    f32x4v acc[4][4];
+    double fold[4][4][4];
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+            acc[a][b] = f32x4v{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int r = 0; r < 4; ++r) fold[a][b][r] = 0.0;
+        }
+    // stage loads: 32 rows x 128 columns of A (and B): thread -> row tid / 8,
+    // 16 consecutive columns (4 x float4 when the row slice is aligned)
+    const int lr = tid >> 3, lc = (tid & 7) * 16;
+    const int ca = bi * G3T + lc, cb = bj * G3T + lc;
+    const bool vec = (f & 3) == 0;
+    float va[16], vb[16];
+    float ma = 0.f, mb = 0.f;  // this thread's max |x| over its columns (fmaxf drops NaN:
+    bool nan_a = false, nan_b = false;  // tracked apart)
+    auto load = [&](int64_t kb) {
+        const int64_t row = kb + lr;
+        const bool rin = row < k1;
+        const float *pr = X + (rin ? row : k0) * (int64_t)f;
+#pragma unroll
+        for (int u = 0; u < 16; u += 4) {
+            if (vec && ca + u + 3 < f) {
+                const float4 x = *reinterpret_cast<const float4 *>(pr + ca + u);
+                va[u] = x.x; va[u + 1] = x.y; va[u + 2] = x.z; va[u + 3] = x.w;
+            } else {
+#pragma unroll
+                for (int e = 0; e < 4; ++e) va[u + e] = ca + u + e < f ? pr[ca + u + e] : 0.f;
+            }
+            if (!diag) {
+                if (vec && cb + u + 3 < f) {
+                    const float4 x = *reinterpret_cast<const float4 *>(pr + cb + u);
+                    vb[u] = x.x; vb[u + 1] = x.y; vb[u + 2] = x.z; vb[u + 3] = x.w;
+                } else {
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) vb[u + e] = cb + u + e < f ? pr[cb + u + e] : 0.f;
+                }
+            }
+        }
+        if (!rin) {
+#pragma unroll
+            for (int u = 0; u < 16; ++u) va[u] = vb[u] = 0.f;
+        }
+    };
+    int since_fold = 0;
+    if (k0 < k1) load(k0);
+    for (int64_t kb = k0; kb < k1; kb += G3K) {
+        __syncthreads();
+#pragma unroll
+        for (int u = 0; u < 16; u += 4) {
+            *reinterpret_cast<float4 *>(&As[lr][lc + u]) = make_float4(va[u], va[u + 1], va[u + 2], va[u + 3]);
+            if (!diag)
+                *reinterpret_cast<float4 *>(&Bs[lr][lc + u]) = make_float4(vb[u], vb[u + 1], vb[u + 2], vb[u + 3]);
+        }
+#pragma unroll
+        for (int u = 0; u < 16; ++u) {
+            ma = fmaxf(ma, __builtin_fabsf(va[u]));
+            nan_a |= va[u] != va[u];
+            if (!diag) {
+                mb = fmaxf(mb, __builtin_fabsf(vb[u]));
+                nan_b |= vb[u] != vb[u];
+            }
+        }
+        __syncthreads();
+        if (kb + G3K < k1) load(kb + G3K);
+        const float (*Bp)[G3P] = diag ? As : Bs;
+#pragma unroll
+        for (int ks = 0; ks < G3K / 4; ++ks) {
+            const int kr = ks * 4 + (lane >> 4);
+            float a[4], b[4];
+#pragma unroll
+            for (int m = 0; m < 4; ++m) a[m] = As[kr][wr * 64 + m * 16 + (lane & 15)];
+#pragma unroll
+            for (int m = 0; m < 4; ++m) b[m] = Bp[kr][wc * 64 + m * 16 + (lane & 15)];
+#pragma unroll
+            for (int ma_ = 0; ma_ < 4; ++ma_)
+#pragma unroll
+                for (int mb_ = 0; mb_ < 4; ++mb_)
+                    acc[ma_][mb_] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[ma_], b[mb_], acc[ma_][mb_],
+                                                                         0, 0, 0);
+        }
+        since_fold += G3K;
+        if (since_fold >= G3F) {
+            since_fold = 0;
+#pragma unroll
+            for (int a = 0; a < 4; ++a)
+#pragma unroll
+                for (int b = 0; b < 4; ++b) {
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) fold[a][b][r] += (double)acc[a][b][r];
+                    acc[a][b] = f32x4v{0.f, 0.f, 0.f, 0.f};
+                }
+        }
+    }
+    // C/D (f32 16x16x4): row = 4 * (lane >> 4) + reg, col = lane & 15
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const double v = fold[a][b][r] + (double)acc[a][b][r];
+                const int gi = bi * G3T + wr * 64 + a * 16 + 4 * (lane >> 4) + r;
+                const int gj = bj * G3T + wc * 64 + b * 16 + (lane & 15);
+                if (gi < f && gj < f) atomicAdd(&G[(int64_t)gi * f + gj], v);
+            }
+    // column maxima (NaN propagates through the unsigned order: NaN bits > inf)
+    const unsigned mra = nan_a ? 0x7FC00000u : __float_as_uint(ma);
+    const unsigned mrb = nan_b ? 0x7FC00000u : __float_as_uint(mb);
+    // fold over the 32 row-threads of each column group (lanes tid & 7 equal)
+    __shared__ unsigned cm[2][G3T];
+    if (tid < 2 * G3T) (&cm[0][0])[tid] = 0u;
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+        atomicMax(&cm[0][lc + u], mra);
+        if (!diag) atomicMax(&cm[1][lc + u], mrb);
+    }
+    __syncthreads();
+    if (tid < G3T) {
+        if (bi * G3T + tid < f) atomicMax(&colmax[bi * G3T + tid], cm[0][tid]);
+        if (!diag && bj * G3T + tid < f) atomicMax(&colmax[bj * G3T + tid], cm[1][tid]);
+    }
+}
+
+// 1 in *bad when a column max leaves [2^-20, 2^40] (zero columns are exact)
+// or is not finite: the f32 Gram's error bound does not hold
+__global__ void k_colmax_check(const unsigned *__restrict__ colmax, int f, int *__restrict__ bad) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= f) return;
+    const unsigned u = colmax[i];
+    const float m = __uint_as_float(u);
+    const bool ok = u == 0u || (u < 0x7F800000u && m >= 0x1p-20f && m <= 0x1p40f);
+    if (!ok) *bad = 1;
+}
+
 __device__ __forceinline__ double gram_at(const double *G, int f, int i, int j) {
     return ((i / GT) <= (j / GT)) ? G[(int64_t)i * f + j] : G[(int64_t)j * f + i];
 }
@@ -300,7 +470,7 @@ __global__ __launch_bounds__(256) void k_cos_select(const double *__restrict__ G
                                                     const double *__restrict__ nrm, int f, int L,
                                                     int32_t *__restrict__ cand,
                                                     double *__restrict__ capx,
-                                                    double *__restrict__ gnext) {
+                                                    double *__restrict__ gnext, double amb) {
     const int lane = threadIdx.x & 63;
     const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (i >= f) return;
@@ -316,7 +486,7 @@ __global__ __launch_bounds__(256) void k_cos_select(const double *__restrict__ G
             if (d[r] != d[r]) { d[r] = 2.0; nan = true; }  // non-finite data
             // n_i n_j at the reference's 1e-12 cut: approximate norms may fall
             // on the other side of it — the node takes the exact path
-            if (__builtin_fabs(ni * nrm[j] - 1e-12) <= 1e-20) nan = true;
+            if (__builtin_fabs(ni * nrm[j] - 1e-12) <= amb) nan = true;
             ix[r] = j;
         } else {
             d[r] = __builtin_inf();
@@ -750,7 +920,7 @@ static int knn_cos_columns_impl(const T *X, int64_t n, int32_t f, const mn_cos_o
     nchunk = (int)((n + kchunk - 1) / kchunk);
 
     T *XT = (T *)scratch(kSlotGeneric0, sizeof(T) * (size_t)n * f);
-    char *g = (char *)scratch(kSlotGeneric1, sizeof(double) * ((size_t)f * f + f * 3 + 64) +
+    char *g = (char *)scratch(kSlotGeneric1, sizeof(double) * ((size_t)f * f + f * 4 + 64) +
                                                 (size_t)f * L * 24 + (size_t)f * 8 + 64);
     MN_REQUIRE(XT && g, MN_ENOMEM, "mn_knn_cos_columns_f32: scratch allocation failed");
     double *G = (double *)g;
@@ -764,6 +934,7 @@ static int knn_cos_columns_impl(const T *X, int64_t n, int32_t f, const mn_cos_o
     double *capx = cdist + (size_t)f * L;
     int32_t *fb_list = (int32_t *)(capx + (size_t)f * L);
     double *nrmA = (double *)(((uintptr_t)(fb_list + f) + 15) & ~(uintptr_t)15);
+    unsigned *colmax = (unsigned *)(nrmA + f);
 
     Timer tm;
     tm.start(o->timing != 0, s);
@@ -796,17 +967,56 @@ static int knn_cos_columns_impl(const T *X, int64_t n, int32_t f, const mn_cos_o
         MN_HIP_TRY(hipMemcpyAsync(flags, &f, 4, hipMemcpyHostToDevice, s));
         MN_HIP_TRY(hipGetLastError());
     } else {
-        hipLaunchKernelGGL(k_gram_f64<T>, dim3((unsigned)(ntri * nchunk)), dim3(256), 0, s, X, n, f, ntile,
-                           kchunk, nchunk, G);
+        // Tuning build, MN_COS_GRAM = 1: the f32-MFMA Gram (k_gram_f32m, f64
+        // fold every G3F rows) when the exact norms come with the exact pass;
+        // its bound needs every column max in [2^-20, 2^40] (or 0) — checked
+        // on the device, else G is recomputed on f64 MFMA.  C3 (same process,
+        // profiles/r05/r05_c3_gram32_ab.log): Gram phase 13.5 vs 14.4 ms, but
+        // the wider delta adds ~1 exact chain per node (exact pass 8.1 -> 9.4
+        // ms): slower overall, not the default.
+        bool f32g = false;
+        double e32 = 0.0;  // |G~_ij - dot_ij| <= e32 n_i n_j (f32 Gram)
+        if (sizeof(T) == 4 && norms_in_pass && knob_int("MN_COS_GRAM", 0) == 1) {
+            const int nt3 = (f + G3T - 1) / G3T;
+            const int ntri3 = nt3 * (nt3 + 1) / 2;
+            int nch3 = (int)std::max<int64_t>(1, std::min<int64_t>((1024 + ntri3 - 1) / ntri3,
+                                                                   (n + G3F - 1) / G3F));
+            int64_t kch3 = (n + nch3 - 1) / nch3;
+            kch3 = (kch3 + G3F - 1) / G3F * G3F;  // fold windows aligned to the chunk
+            nch3 = (int)((n + kch3 - 1) / kch3);
+            MN_HIP_TRY(hipMemsetAsync(colmax, 0, 4 * (size_t)f, s));
+            hipLaunchKernelGGL(k_gram_f32m, dim3((unsigned)(ntri3 * nch3)), dim3(256), 0, s,
+                               (const float *)X, n, f, nt3, kch3, G, colmax);
+            MN_KCHECK(s, "k_gram_f32m");
+            hipLaunchKernelGGL(k_colmax_check, dim3(grid(f)), dim3(256), 0, s, colmax, f, flags + 3);
+            int bad = 0;
+            MN_HIP_TRY(hipMemcpyAsync(&bad, flags + 3, 4, hipMemcpyDeviceToHost, s));
+            MN_HIP_TRY(hipStreamSynchronize(s));
+            if (!bad) {
+                f32g = true;
+                e32 = (double)(G3F + 8) * 0x1p-24 +
+                      ((double)n / G3F + (double)nch3 + 8.0) * 0x1p-53;
+            } else {
+                MN_HIP_TRY(hipMemsetAsync(G, 0, sizeof(double) * (size_t)f * f, s));
+            }
+        }
+        // (measured and dropped: the same f64 arithmetic on 128 x 128 tiles,
+        // 21 instead of 78 upper tiles — 20.7 vs 14.5 ms,
+        // profiles/r05/r05_c3_gram_tiles_ab.log)
+        if (!f32g)
+            hipLaunchKernelGGL(k_gram_f64<T>, dim3((unsigned)(ntri * nchunk)), dim3(256), 0, s, X, n,
+                               f, ntile, kchunk, nchunk, G);
         MN_HIP_TRY(hipGetLastError());
         MN_HIP_TRY(stream_wait(s, side));
         tm.mark();
+        // the selection's band around the reference's 1e-12 cut (relative)
+        const double amb_rel = f32g ? 4.0 * e32 : 1e-8;
         // approximate norms sqrt(G_ii) for the selection when the exact ones
         // come with the exact pass
         if (norms_in_pass)
             hipLaunchKernelGGL(k_gram_diag_norms, dim3(grid(f)), dim3(256), 0, s, G, f, nrmA);
         const double *nsel = norms_in_pass ? nrmA : nrm;
-    #define MN_SEL(NRV) hipLaunchKernelGGL(k_cos_select<NRV>, dim3(grid(f, 4)), dim3(256), 0, s, G, nsel, f, L, cand, capx, gnext)
+    #define MN_SEL(NRV) hipLaunchKernelGGL(k_cos_select<NRV>, dim3(grid(f, 4)), dim3(256), 0, s, G, nsel, f, L, cand, capx, gnext, 1e-12 * amb_rel)
         if (nr <= 1) MN_SEL(1); else if (nr <= 2) MN_SEL(2); else if (nr <= 4) MN_SEL(4);
         else if (nr <= 8) MN_SEL(8); else if (nr <= 16) MN_SEL(16); else if (nr <= 32) MN_SEL(32);
         else MN_SEL(64);
@@ -817,8 +1027,12 @@ static int knn_cos_columns_impl(const T *X, int64_t n, int32_t f, const mn_cos_o
         // rounded once more), norms and the quotient, with a factor-2 margin
         // With the norms from G_ii (error <= the Gram's own, gamma_n each) the
         // bound doubles: 4 (n + 16) u keeps the factor-2 margin.
-        const double delta = (norms_in_pass ? 4.0 : 2.0) *
-                                 ((double)n + (sizeof(T) == 8 ? 17.0 : 16.0)) * 0x1p-53 + 1e-300;
+        // The f32 Gram: |cos~ - cos| <= 2 e32 / (1 - e32) (dot and norms), x 2
+        // margin, plus the f64 rounding of the distance itself.
+        const double delta =
+            f32g ? 4.02 * e32 + 64.0 * 0x1p-53
+                 : (norms_in_pass ? 4.0 : 2.0) * ((double)n + (sizeof(T) == 8 ? 17.0 : 16.0)) * 0x1p-53 +
+                       1e-300;
         const int kq = std::min(o->topk, L);
         const int fkq = f * kq;
         hipLaunchKernelGGL(k_fill_f64, dim3(grid((int64_t)f * L)), dim3(256), 0, s, cdist,

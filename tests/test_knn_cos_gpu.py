@@ -111,3 +111,25 @@ def test_norms_from_the_exact_pass_tiny_columns_and_the_1e12_cut():
         finally:
             os.environ.pop("MN_COS_NORMS_SIDE", None)
     exact((i, d, w), (i3, d3, w3))
+
+
+@pytest.mark.parametrize("case", ["uniform", "tiny_columns"])
+def test_f32_gram_tuning_path_bit_exact(case):
+    """Tuning build, MN_COS_GRAM=1: the f32-MFMA Gram with the f64 fold and
+    its wider certification band (and, for columns whose max |x| leaves
+    [2^-20, 2^40], the device range check sending G back to f64 MFMA): the
+    graph stays bit-exact vs the oracle."""
+    import os
+    import surfface_hip as S
+    X = datagen.uniform(6000, 200, seed=23)
+    if case == "tiny_columns":
+        X[:, 5] *= np.float32(1e-9)  # max |x| below 2^-20: the f64 Gram runs
+        X[:, 6] = 0.0
+    kw = dict(eps=1.0, sigma=1.0, p=2.0)
+    with S._lib.use_tuning():
+        os.environ["MN_COS_GRAM"] = "1"
+        try:
+            i, d, w, st = hip_cols(X, 4, **kw)
+        finally:
+            os.environ.pop("MN_COS_GRAM", None)
+    exact((i, d, w), ref_cols(X, 4, **kw))
