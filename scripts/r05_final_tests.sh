@@ -1,0 +1,4 @@
+set -o pipefail
+mkdir -p gpurun_out
+timeout -k 10 900 python -u -m pytest tests/ -m gpu -x -v --timeout 300 --timeout-method thread > gpurun_out/r05_gpu_tests.log 2>&1 &&
+timeout -k 10 400 python -u bench.py > gpurun_out/r05_bench.log 2>&1
