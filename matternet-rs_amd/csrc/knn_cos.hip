@@ -1054,8 +1054,9 @@ static int knn_cos_columns_impl(const T *X, int64_t n, int32_t f, const mn_cos_o
             // the listed pairs' raw dots (into cdist) and the f norm chains
             // (into nrm) in one pass, then the distances
             // (measured and dropped: a producer / consumer pair of waves per
-            // sixteen chains, one barrier a 64-element chunk — 11.4 vs 8.15 ms,
-            // profiles/r05/r05_c3_pc_ab.log)
+            // sixteen chains, one barrier a 64-element chunk — 11.4 vs 8.15 ms
+            // with __syncthreads and with a raw s_barrier alike,
+            // profiles/r05/r05_c3_pc_ab.log, r05_c3_pc2_ab.log)
             auto kq = k_cos_exact_q<T, 4, true>;
             if (pfd == 8) kq = k_cos_exact_q<T, 8, true>;
             hipLaunchKernelGGL(kq, dim3(grid((int64_t)f * L + f, 16)), dim3(64), 0, s, XT, n, pi,

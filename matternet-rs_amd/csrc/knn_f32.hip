@@ -2518,7 +2518,9 @@ static int knn_x1(const float *Q, int64_t nq, const float *C, int64_t nc, int32_
             const int TPB = (tpe2 && *tpe2) ? std::max(1, atoi(tpe2)) : 256;
             const char *ore = knob("MN_SYM_ORDER");
             const int order = (ore && *ore) ? atoi(ore) : 2;
-            const std::vector<int4> tab = ksw2::sym_block_table(nbk, TPB, order, 2);  // 2 x 16 groups
+            // 2 x 16 groups (tuning build: MN_SYM_GSHAPE = rows of a 32-block group)
+            const std::vector<int4> tab =
+                ksw2::sym_block_table(nbk, TPB, order, knob_int("MN_SYM_GSHAPE", 2));
             int4 *dtab = (int4 *)scratch(kSlotSymTab, tab.size() * sizeof(int4) + 64);
             MN_REQUIRE(dtab, MN_ENOMEM, "mn_knn: block table allocation failed");
             MN_HIP_TRY(hipMemcpyAsync(dtab, tab.data(), tab.size() * sizeof(int4),
