@@ -579,17 +579,41 @@ constexpr int CQP = CQ + 2;   // chain buffer stride in doubles (528 B)
 // dist[slot] (k_cos_dist turns it into the distance once the norms exist) and
 // fnorm more chains follow the np listed ones: chain np + c folds column c
 // with itself -> nrm[c] = sqrt (the reference's sequential norm).
-template <typename T, int PFD, bool RAW = false>
+// LPC lanes a chain (4: sixteen chains a wave; 8: eight chains, half the
+// product work a lane and twice the waves), EPL = 64 / LPC elements a lane
+// per chunk.
+template <int N>
+__device__ __forceinline__ void loadn(const float *p, bool vec, float (&o)[N]) {
+#pragma unroll
+    for (int u = 0; u < N; u += 4) {
+        float4 x;
+        if (vec) x = *reinterpret_cast<const float4 *>(p + u);
+        else x = make_float4(p[u], p[u + 1], p[u + 2], p[u + 3]);
+        o[u] = x.x; o[u + 1] = x.y; o[u + 2] = x.z; o[u + 3] = x.w;
+    }
+}
+template <int N>
+__device__ __forceinline__ void loadn(const double *p, bool vec, double (&o)[N]) {
+#pragma unroll
+    for (int u = 0; u < N; u += 2) {
+        double2 x;
+        if (vec) x = *reinterpret_cast<const double2 *>(p + u);
+        else x = make_double2(p[u], p[u + 1]);
+        o[u] = x.x; o[u + 1] = x.y;
+    }
+}
+template <typename T, int PFD, bool RAW = false, int LPC = 4>
 __global__ __launch_bounds__(64) void k_cos_exact_q(const T *__restrict__ XT, int64_t n,
                                                     const int32_t *__restrict__ plist,
                                                     const int *__restrict__ pcount, int64_t pmax,
                                                     const int32_t *__restrict__ cand, int L,
                                                     int fnorm, double *__restrict__ nrm,
                                                     double *__restrict__ dist) {
-    __shared__ __attribute__((aligned(16))) double buf[2][16][CQP];
-    const int lane = threadIdx.x & 63, g = lane >> 2, gl = lane & 3;
+    constexpr int CPW = 64 / LPC, EPL = CQ / LPC;
+    __shared__ __attribute__((aligned(16))) double buf[2][CPW][CQP];
+    const int lane = threadIdx.x & 63, g = lane / LPC, gl = lane % LPC;
     const int64_t np = pcount ? (int64_t)*pcount : pmax;
-    const int64_t wq = (int64_t)blockIdx.x * 16;
+    const int64_t wq = (int64_t)blockIdx.x * CPW;
     if (wq >= np + (RAW ? fnorm : 0)) return;  // wave-uniform
     const int64_t q = wq + g;
     int slot = -1, i = 0, j = 0, ncol = -1;
@@ -617,18 +641,18 @@ __global__ __launch_bounds__(64) void k_cos_exact_q(const T *__restrict__ XT, in
     // chunks, so the wait before a chunk's products counts only the loads
     // issued after its own (vmcnt(N)); with the loads behind a branch the
     // compiler waited for all of them (vmcnt(0)) at every group.
-    T ra[PFD][16], rb[PFD][16];
+    T ra[PFD][EPL], rb[PFD][EPL];
 #define MN_QFETCH(C, H)                                  \
     do {                                                 \
-        const int64_t o_ = (C) * CQ + 16 * gl;           \
-        load16(a + o_, vec, ra[H]);                      \
-        load16(b + o_, vec, rb[H]);                      \
+        const int64_t o_ = (C) * CQ + EPL * gl;          \
+        loadn<EPL>(a + o_, vec, ra[H]);                  \
+        loadn<EPL>(b + o_, vec, rb[H]);                  \
     } while (0)
 #define MN_QCHUNK(H)                                                                     \
     do {                                                                                 \
         double *bb_ = buf[(H) & 1][g];                                                   \
-        _Pragma("unroll") for (int u = 0; u < 16; u += 2)                               \
-            *reinterpret_cast<double2 *>(bb_ + 16 * gl + u) =                            \
+        _Pragma("unroll") for (int u = 0; u < EPL; u += 2)                              \
+            *reinterpret_cast<double2 *>(bb_ + EPL * gl + u) =                           \
                 make_double2((double)ra[H][u] * (double)rb[H][u],                        \
                              (double)ra[H][u + 1] * (double)rb[H][u + 1]);               \
     } while (0)
@@ -1057,9 +1081,15 @@ static int knn_cos_columns_impl(const T *X, int64_t n, int32_t f, const mn_cos_o
             // sixteen chains, one barrier a 64-element chunk — 11.4 vs 8.15 ms
             // with __syncthreads and with a raw s_barrier alike,
             // profiles/r05/r05_c3_pc_ab.log, r05_c3_pc2_ab.log)
-            auto kq = k_cos_exact_q<T, 4, true>;
-            if (pfd == 8) kq = k_cos_exact_q<T, 8, true>;
-            hipLaunchKernelGGL(kq, dim3(grid((int64_t)f * L + f, 16)), dim3(64), 0, s, XT, n, pi,
+            // lanes a chain: 8 — eight chains a wave, twice the waves of the
+            // sixteen-chain form (C3 exact pass 8.17 -> 7.6 ms, same process,
+            // profiles/r05/r05_c3_lpc_ab.log); tuning build: MN_COS_LPC = 4 / 16
+            const int lpc = knob_int("MN_COS_LPC", 8);
+            auto kq = k_cos_exact_q<T, 4, true, 8>;
+            if (lpc == 4) kq = pfd == 8 ? k_cos_exact_q<T, 8, true, 4> : k_cos_exact_q<T, 4, true, 4>;
+            if (lpc == 16) kq = k_cos_exact_q<T, 4, true, 16>;
+            const int cpw = 64 / (lpc == 4 ? 4 : (lpc == 16 ? 16 : 8));
+            hipLaunchKernelGGL(kq, dim3(grid((int64_t)f * L + f, cpw)), dim3(64), 0, s, XT, n, pi,
                                flags + 1, (int64_t)f * L, cand, L, f, nrm, cdist);
             hipLaunchKernelGGL(k_cos_dist, dim3(grid((int64_t)f * L)), dim3(256), 0, s, pi, flags + 1,
                                cand, L, nrm, cdist);
