@@ -938,7 +938,12 @@ static int knn_cos_columns_impl(const T *X, int64_t n, int32_t f, const mn_cos_o
     hipStream_t s = (hipStream_t)o->stream;
     const int ntile = (f + GT - 1) / GT;
     const int ntri = ntile * (ntile + 1) / 2;
-    int nchunk = (int)std::max<int64_t>(1, std::min<int64_t>((2048 + ntri - 1) / ntri, (n + 255) / 256));
+    // ~2048 Gram blocks.  Tuning build: MN_COS_GBLK = the target block count
+    // (C3, same process, bit-identical: 8192 -> Gram phase 13.35 ms vs 14.6,
+    // 4096 13.8, 1024 16.1 — profiles/r05/r05_c3_gblk_ab.log; not the default
+    // until the parity suite has run on it)
+    const int64_t gblk = knob_int("MN_COS_GBLK", 2048);
+    int nchunk = (int)std::max<int64_t>(1, std::min<int64_t>((gblk + ntri - 1) / ntri, (n + 255) / 256));
     int64_t kchunk = (n + nchunk - 1) / nchunk;
     kchunk = ((kchunk + GK - 1) / GK) * GK;
     nchunk = (int)((n + kchunk - 1) / kchunk);
