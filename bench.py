@@ -259,8 +259,10 @@ def main():
 
     # C3 legs (configs[2]): Laplacian assembly + energymaps/taumode pass + index,
     # on this rank's rows (timed individually after the headline step)
+    # (N > 1: the rank's rows carry global neighbour ids of the N x 1M graph,
+    # which the single-graph C3 legs do not take — they run at N = 1 only)
     c3 = None
-    if a.c3:
+    if a.c3 and world == 1:
         c3 = c3_legs(S, X, out[0], out[1], k)
 
     c5 = None

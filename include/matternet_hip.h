@@ -191,8 +191,10 @@ int mn_knn_l2_f64(const void *Q, int64_t nq, const void *C, int64_t nc, int32_t 
  * code, the others MN_EHIP "another rank failed"), and every collective is
  * waited for by polling the stream and ncclCommGetAsyncError against the
  * mn_rccl_set_timeout deadline: an RCCL error or a peer that never arrives
- * ends the call with MN_ECOMM after ncclCommAbort (destroying that
- * communicator afterwards is a no-op; later calls on it return MN_EINVAL). */
+ * ends the call with MN_ECOMM at that deadline: the communicator is aborted
+ * (destroying it afterwards is a no-op; later calls on it return MN_EINVAL)
+ * and the call's buffers are freed off the calling thread once the stream
+ * has drained (mn_shard_quiesce). */
 int mn_knn_sharded_f32(const float *X_shard, int64_t n_local, int32_t d, void *rccl_comm,
                        const mn_knn_opts *opts, int64_t query_chunk, int32_t *out_idx,
                        float *out_dist);
@@ -211,6 +213,27 @@ int mn_knn_sharded_f32(const float *X_shard, int64_t n_local, int32_t d, void *r
 int mn_knn_sharded_sim_f32(const float *X_all, int64_t n_tot, int32_t d, int32_t world,
                            const mn_knn_opts *opts, int32_t *out_idx, float *out_dist,
                            float *rank_ms);
+/* The same sharded build with `world` ranks on ONE device, ONE HOST THREAD
+ * PER RANK (replaces nothing in the reference: SURVEY.md §8(e) — the
+ * reference has no distribution; this is the concurrency rehearsal of
+ * mn_knn_sharded_f32): each thread drives its rank exactly as one RCCL process
+ * does (nlocal 1, its own stream and scratch), the ranks' stages and
+ * collectives run concurrently, and every collective is a rendezvous that
+ * checks that all ranks issued the same collective (kind, sequence number,
+ * name, byte size).  A divergent collective order, or a rank that left the
+ * driver while others wait in a collective, ends every rank with MN_ECOMM
+ * (message: which ranks, which collectives) where RCCL would hang; a rank
+ * that never arrives, at the mn_rccl_set_timeout deadline.  Arguments,
+ * outputs and rank_ms as mn_knn_sharded_sim_f32 (mn_knn_last_stats: maxima
+ * of the ranks' times, sums of their counts). */
+int mn_knn_sharded_threads_f32(const float *X_all, int64_t n_tot, int32_t d, int32_t world,
+                               const mn_knn_opts *opts, int32_t *out_idx, float *out_dist,
+                               float *rank_ms);
+/* After a sharded call ended with MN_ECOMM its communicator is aborted and its
+ * buffers are released by a background thread once the device work queued on
+ * them has drained (the call itself returns at its deadline).  Waits up to
+ * timeout_s for those releases; MN_ECOMM if some are still pending. */
+int mn_shard_quiesce(double timeout_s);
 /* Host only (no device work): rank `rank`'s share of the symmetric form's
  * node-wide tile table over nbk 256-row blocks — entries (I, Jfirst, tiles,
  * stride) = row block I against column blocks Jfirst + t stride, t < tiles

@@ -38,9 +38,12 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <condition_variable>
 #include <cstring>
+#include <memory>
 #include <mutex>
 #include <set>
+#include <string>
 #include <thread>
 #include <vector>
 
@@ -127,8 +130,29 @@ int mn_rccl_set_timeout(double seconds) {
 
 namespace {
 
+// Release of a failed call's resources off the caller's thread.  Once a
+// collective has failed, the caller's stream may still hold queued work that
+// targets the call's buffers: a stalled kernel, or RCCL kernels that exit
+// only when they see the abort.  hipFree / hipHostFree wait for the device
+// to drain, so a failed call hands its buffers to a detached reaper thread
+// that aborts the communicator and then frees them; the call returns
+// MN_ECOMM at its deadline, not when the stream drains
+// (mn_shard_quiesce waits for the reapers).
+struct Graveyard {
+    std::mutex mu;
+    std::condition_variable cv;
+    bool active = false;  // the call failed: buffers go to the reaper
+    bool sealed = false;  // every buffer of the call has been handed over
+    std::vector<void *> dev, host;
+};
+
+std::mutex g_reap_mu;
+std::condition_variable g_reap_cv;
+int g_reapers = 0;
+
 struct DevBufs {
     std::vector<void *> v;
+    std::shared_ptr<Graveyard> gy;  // may be null (the loopback transports)
     void *get(size_t bytes) {
         void *p = nullptr;
         if (hipMalloc(&p, bytes ? bytes : 16) != hipSuccess) return nullptr;
@@ -136,6 +160,13 @@ struct DevBufs {
         return p;
     }
     ~DevBufs() {
+        if (gy) {
+            std::lock_guard<std::mutex> g(gy->mu);
+            if (gy->active) {
+                gy->dev.insert(gy->dev.end(), v.begin(), v.end());
+                return;
+            }
+        }
         for (void *p : v) (void)hipFree(p);
     }
 };
@@ -169,6 +200,10 @@ class Transport {
                            size_t bytes, const char *what) = 0;
     // *out = max over every rank of mine[l] (0 ok, 1 per-shard form, 2 error)
     virtual int agree(const int *mine, int *out) = 0;
+    // where the driver's buffers go if a collective fails (null: freed in place)
+    virtual std::shared_ptr<Graveyard> graveyard() { return nullptr; }
+    // the tuning build's collective-order fault injection (MN_SHARD_REORDER=<rank>)
+    virtual bool reorder_gathers() const { return false; }
 };
 
 #ifdef MN_TUNING
@@ -180,27 +215,39 @@ __global__ void k_stall(uint64_t ticks) {  // fault injection (tuning build only
 
 class RcclTransport final : public Transport {
   public:
-    RcclTransport(ncclComm_t c, hipStream_t s) : c_(c), s_(s), timeout_(g_timeout_s.load()) {}
+    RcclTransport(ncclComm_t c, hipStream_t s)
+        : c_(c), s_(s), timeout_(g_timeout_s.load()), gy_(std::make_shared<Graveyard>()) {}
     ~RcclTransport() override {
+        {
+            std::lock_guard<std::mutex> g(gy_->mu);
+            if (gy_->active) {  // the reaper frees them once the stream drained
+                if (pin_) gy_->host.push_back(pin_);
+                if (dflag_) gy_->dev.push_back(dflag_);
+                gy_->sealed = true;
+                gy_->cv.notify_all();
+                return;
+            }
+        }
+        if (dflag_) (void)hipFree(dflag_);
         if (pin_) (void)hipHostFree(pin_);
     }
     int init() {
         MN_NCCL_TRY(ncclCommCount(c_, &world_));
         MN_NCCL_TRY(ncclCommUserRank(c_, &rank_));
+        MN_HIP_TRY(hipGetDevice(&dev_));
         MN_HIP_TRY(hipHostMalloc((void **)&pin_, 64, hipHostMallocDefault));
         if (hipMalloc((void **)&dflag_, 64) != hipSuccess) {
+            dflag_ = nullptr;
             set_error("mn_knn_sharded_f32: device allocation failed");
             return MN_ENOMEM;
         }
-        bufs_.v.push_back(dflag_);
         // tuning build: stall the stream before the first collective (tests of
         // the deadline: the call must end with MN_ECOMM, not hang)
 #ifdef MN_TUNING
         const int stall_ms = mn::knob_int("MN_SHARD_STALL_MS", 0);
         if (stall_ms > 0) {
-            int dev = 0, khz = 0;
-            MN_HIP_TRY(hipGetDevice(&dev));
-            MN_HIP_TRY(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev));
+            int khz = 0;
+            MN_HIP_TRY(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev_));
             hipLaunchKernelGGL(k_stall, dim3(1), dim3(64), 0, s_, (uint64_t)stall_ms * (uint64_t)khz);
             MN_HIP_TRY(hipGetLastError());
         }
@@ -212,6 +259,11 @@ class RcclTransport final : public Transport {
     int rank(int) const override { return rank_; }
     hipStream_t stream(int) const override { return s_; }
     int stage_done(int) override { return MN_OK; }
+    std::shared_ptr<Graveyard> graveyard() override { return gy_; }
+    bool reorder_gathers() const override {
+        const char *e = mn::knob("MN_SHARD_REORDER");
+        return e && *e && atoi(e) == rank_;
+    }
 
     int all_gather(const void *const *send, void *const *recv, size_t bytes,
                    const char *what) override {
@@ -236,20 +288,24 @@ class RcclTransport final : public Transport {
     // pinned host flag: every copy is asynchronous, so the only blocking
     // point is the polled wait
     int agree(const int *mine, int *out) override {
+        static const char *what = "the shard status all-reduce";
         pin_[0] = mine[0];
-        MN_HIP_TRY(hipMemcpyAsync(dflag_, pin_, 4, hipMemcpyHostToDevice, s_));
+        hipError_t e = hipMemcpyAsync(dflag_, pin_, 4, hipMemcpyHostToDevice, s_);
+        if (e != hipSuccess) return fail(what, hipGetErrorString(e));
         const ncclResult_t r = ncclAllReduce(dflag_, dflag_, 1, ncclInt32, ncclMax, c_, s_);
-        if (r != ncclSuccess) return fail("ncclAllReduce of the shard status", ncclGetErrorString(r));
-        MN_HIP_TRY(hipMemcpyAsync(pin_ + 1, dflag_, 4, hipMemcpyDeviceToHost, s_));
-        const int rc = wait("the shard status all-reduce");
+        if (r != ncclSuccess) return fail(what, ncclGetErrorString(r));
+        e = hipMemcpyAsync(pin_ + 1, dflag_, 4, hipMemcpyDeviceToHost, s_);
+        if (e != hipSuccess) return fail(what, hipGetErrorString(e));
+        const int rc = wait(what);
         if (rc != MN_OK) return rc;
         *out = pin_[1];
         return MN_OK;
     }
 
   private:
-    // the stream drained, or the communicator aborted: an RCCL async error,
-    // or no completion before the deadline (a peer died or stalled)
+    // the stream drained, or the communicator aborted: a stream error, an
+    // RCCL async error, or no completion before the deadline (a peer died or
+    // stalled)
     int wait(const char *what) {
         using clk = std::chrono::steady_clock;
         const auto t0 = clk::now();
@@ -258,8 +314,9 @@ class RcclTransport final : public Transport {
             const hipError_t e = hipStreamQuery(s_);
             if (e == hipSuccess) return MN_OK;
             if (e != hipErrorNotReady) {
-                set_error("%s: stream error %s", what, hipGetErrorString(e));
-                return MN_EHIP;
+                char why[160];
+                snprintf(why, sizeof(why), "stream error %s", hipGetErrorString(e));
+                return fail(what, why);
             }
             ncclResult_t ae = ncclSuccess;
             const ncclResult_t q = ncclCommGetAsyncError(c_, &ae);
@@ -276,11 +333,56 @@ class RcclTransport final : public Transport {
             nap_us = std::min(nap_us * 2, 1000);
         }
     }
+    // Abort the communicator and hand the call's buffers to a reaper thread:
+    // ncclCommAbort sets the abort flag the RCCL kernels poll, then releases
+    // the communicator's memory, which (like our hipFree) waits for the
+    // device; neither may hold up the return.
     int fail(const char *what, const char *why) {
-        (void)ncclCommAbort(c_);
+        bool first = false;
         {
-            std::lock_guard<std::mutex> g(g_abort_mu);
-            g_aborted.insert((void *)c_);
+            std::lock_guard<std::mutex> g(gy_->mu);
+            first = !gy_->active;
+            gy_->active = true;
+        }
+        if (first) {
+            {
+                std::lock_guard<std::mutex> g(g_abort_mu);
+                g_aborted.insert((void *)c_);
+            }
+            std::shared_ptr<Graveyard> gy = gy_;
+            const ncclComm_t c = c_;
+            const int dev = dev_;
+            {
+                std::lock_guard<std::mutex> g(g_reap_mu);
+                ++g_reapers;
+            }
+            auto reap = [c, gy, dev]() {
+                (void)hipSetDevice(dev);
+                (void)ncclCommAbort(c);
+                std::unique_lock<std::mutex> lk(gy->mu);
+                gy->cv.wait(lk, [&] { return gy->sealed; });
+                for (void *p : gy->dev) (void)hipFree(p);
+                for (void *p : gy->host) (void)hipHostFree(p);
+                gy->dev.clear();
+                gy->host.clear();
+                lk.unlock();
+                {
+                    std::lock_guard<std::mutex> g(g_reap_mu);
+                    --g_reapers;
+                }
+                g_reap_cv.notify_all();
+            };
+            try {
+                std::thread(reap).detach();
+            } catch (...) {
+                // no thread: abort here (the buffers are released when the
+                // transport is destroyed, i.e. once the stream drained)
+                (void)ncclCommAbort(c);
+                std::lock_guard<std::mutex> g(gy_->mu);
+                gy_->active = false;
+                std::lock_guard<std::mutex> g2(g_reap_mu);
+                --g_reapers;
+            }
         }
         set_error("mn_knn_sharded_f32: %s: %s; the RCCL communicator was aborted "
                   "(mn_rccl_comm_destroy on it is a no-op)", what, why);
@@ -290,9 +392,9 @@ class RcclTransport final : public Transport {
     ncclComm_t c_;
     hipStream_t s_;
     double timeout_;
-    int world_ = 1, rank_ = 0;
+    std::shared_ptr<Graveyard> gy_;
+    int world_ = 1, rank_ = 0, dev_ = 0;
     int *pin_ = nullptr, *dflag_ = nullptr;
-    DevBufs bufs_;
 };
 
 // R ranks on one device: rank l on stream l (rank 0 on the caller's stream),
@@ -300,16 +402,14 @@ class RcclTransport final : public Transport {
 // collectives as device copies between full drains.
 class LoopbackTransport final : public Transport {
   public:
-    LoopbackTransport(int world, hipStream_t s0) : s_((size_t)world, s0) {}
+    LoopbackTransport(int world, hipStream_t s0) : s_((size_t)world, nullptr) { s_[0] = s0; }
     ~LoopbackTransport() override {
-        for (size_t l = 1; l < s_.size(); ++l)
+        for (size_t l = 1; l < s_.size(); ++l)  // only the streams this object created
             if (s_[l]) (void)hipStreamDestroy(s_[l]);
     }
     int init() {
-        for (size_t l = 1; l < s_.size(); ++l) {
-            s_[l] = nullptr;
+        for (size_t l = 1; l < s_.size(); ++l)
             MN_HIP_TRY(hipStreamCreateWithFlags(&s_[l], hipStreamNonBlocking));
-        }
         return MN_OK;
     }
     int world() const override { return (int)s_.size(); }
@@ -362,6 +462,216 @@ class LoopbackTransport final : public Transport {
         return hipSuccess;
     }
     std::vector<hipStream_t> s_;
+};
+
+// R ranks on one device, ONE HOST THREAD EACH (mn_knn_sharded_threads_f32):
+// the ranks run concurrently, as the processes of a node do, each through
+// the driver with nlocal() == 1 exactly as over RCCL.  Every collective is a
+// rendezvous that first checks that all ranks issued the same collective —
+// kind, sequence number, name and byte size.  A divergence in the collective
+// order (one rank in the status agreement while another is in an
+// all-gather), or a rank that left the driver while others wait in a
+// collective, is reported on every rank as MN_ECOMM where RCCL would hang.
+class Rendezvous {
+  public:
+    enum Kind { kAllGather = 1, kAllToAll, kAgree };
+    struct Post {
+        int kind = 0;
+        int64_t seq = -1;
+        size_t bytes = 0;
+        const char *what = "";
+        int na = 0;
+        const void *send[2] = {nullptr, nullptr};
+        void *recv[2] = {nullptr, nullptr};
+        int val = 0;
+    };
+    Rendezvous(int R, double timeout_s) : R_(R), timeout_(timeout_s), post_((size_t)R), left_((size_t)R, 0) {}
+
+    // post, wait for every rank, check that they all posted the same collective
+    int enter(int r, const Post &p, std::vector<Post> *all) {
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            post_[(size_t)r] = p;
+        }
+        const int rc = barrier(r, p);
+        if (rc != MN_OK) return rc;
+        std::lock_guard<std::mutex> g(mu_);
+        for (int q = 0; q < R_; ++q) {
+            const Post &o = post_[(size_t)q];
+            if (o.kind != p.kind || o.seq != p.seq || o.bytes != p.bytes || strcmp(o.what, p.what) != 0) {
+                if (!broken_) {
+                    char b[512];
+                    snprintf(b, sizeof(b),
+                             "collective order diverged at collective #%lld: rank %d issued %s "
+                             "(kind %d, %zu bytes) while rank %d issued %s (kind %d, %zu bytes)",
+                             (long long)p.seq, r, p.what, p.kind, p.bytes, q, o.what, o.kind, o.bytes);
+                    why_ = b;
+                    broken_ = true;
+                    cv_.notify_all();
+                }
+                set_error("mn_knn_sharded_threads_f32: %s", why_.c_str());
+                return MN_ECOMM;
+            }
+        }
+        *all = post_;
+        return MN_OK;
+    }
+    // every rank done with the others' buffers of this collective
+    int leave_collective(int r, const Post &p) { return barrier(r, p); }
+    // rank r left the driver (after its last collective, or early on an error)
+    void depart(int r) {
+        std::lock_guard<std::mutex> g(mu_);
+        left_[(size_t)r] = 1;
+        cv_.notify_all();
+    }
+    void abort(const char *why) {
+        std::lock_guard<std::mutex> g(mu_);
+        if (!broken_) why_ = why;
+        broken_ = true;
+        cv_.notify_all();
+    }
+
+  private:
+    int barrier(int r, const Post &p) {
+        using clk = std::chrono::steady_clock;
+        std::unique_lock<std::mutex> lk(mu_);
+        if (broken_) {
+            set_error("mn_knn_sharded_threads_f32: %s", why_.c_str());
+            return MN_ECOMM;
+        }
+        const uint64_t g = gen_;
+        if (++arrived_ == R_) {
+            arrived_ = 0;
+            ++gen_;
+            cv_.notify_all();
+            return MN_OK;
+        }
+        const auto dl = clk::now() + std::chrono::duration_cast<clk::duration>(
+                                         std::chrono::duration<double>(timeout_));
+        while (gen_ == g && !broken_) {
+            for (int q = 0; q < R_; ++q)
+                if (left_[(size_t)q] && !broken_) {
+                    char b[384];
+                    snprintf(b, sizeof(b),
+                             "rank %d left the driver while rank %d waits in %s (collective #%lld)", q,
+                             r, p.what, (long long)p.seq);
+                    why_ = b;
+                    broken_ = true;
+                }
+            if (broken_) break;
+            if (cv_.wait_until(lk, dl) == std::cv_status::timeout && gen_ == g && !broken_) {
+                char b[384];
+                snprintf(b, sizeof(b), "no completion of %s (collective #%lld) within %.3g s: a rank "
+                         "never arrived", p.what, (long long)p.seq, timeout_);
+                why_ = b;
+                broken_ = true;
+            }
+        }
+        if (gen_ != g) return MN_OK;
+        cv_.notify_all();
+        set_error("mn_knn_sharded_threads_f32: %s", why_.c_str());
+        return MN_ECOMM;
+    }
+
+    const int R_;
+    const double timeout_;
+    std::mutex mu_;
+    std::condition_variable cv_;
+    uint64_t gen_ = 0;
+    int arrived_ = 0;
+    bool broken_ = false;
+    std::string why_;
+    std::vector<Post> post_;
+    std::vector<char> left_;
+};
+
+class ThreadedTransport final : public Transport {
+  public:
+    ThreadedTransport(Rendezvous &h, int world, int rank, hipStream_t s)
+        : h_(h), world_(world), rank_(rank), s_(s) {}
+    int world() const override { return world_; }
+    int nlocal() const override { return 1; }
+    int rank(int) const override { return rank_; }
+    hipStream_t stream(int) const override { return s_; }
+    int stage_done(int) override { return MN_OK; }
+    bool reorder_gathers() const override {
+        const char *e = mn::knob("MN_SHARD_REORDER");
+        return e && *e && atoi(e) == rank_;
+    }
+    int all_gather(const void *const *send, void *const *recv, size_t bytes,
+                   const char *what) override {
+        Rendezvous::Post p = post(Rendezvous::kAllGather, what, bytes);
+        p.na = 1;
+        p.send[0] = send[0];
+        p.recv[0] = recv[0];
+        std::vector<Rendezvous::Post> all;
+        int rc = h_.enter(rank_, p, &all);
+        if (rc != MN_OK) return rc;
+        for (int q = 0; q < world_; ++q) {
+            char *dst = (char *)recv[0] + (size_t)q * bytes;
+            if (dst == (const char *)all[(size_t)q].send[0]) continue;  // in place (a shared X_all)
+            rc = copy(dst, all[(size_t)q].send[0], bytes);
+            if (rc != MN_OK) break;
+        }
+        if (rc == MN_OK) rc = sync();
+        const int lrc = h_.leave_collective(rank_, p);
+        return rc != MN_OK ? rc : lrc;
+    }
+    int all_to_all(int na, const void *const *const *send, void *const *const *recv, size_t bytes,
+                   const char *what) override {
+        Rendezvous::Post p = post(Rendezvous::kAllToAll, what, bytes);
+        p.na = na;
+        for (int a = 0; a < na && a < 2; ++a) {
+            p.send[a] = send[a][0];
+            p.recv[a] = recv[a][0];
+        }
+        std::vector<Rendezvous::Post> all;
+        int rc = h_.enter(rank_, p, &all);
+        if (rc != MN_OK) return rc;
+        for (int a = 0; a < na && a < 2 && rc == MN_OK; ++a)
+            for (int q = 0; q < world_ && rc == MN_OK; ++q)
+                rc = copy((char *)recv[a][0] + (size_t)q * bytes,
+                          (const char *)all[(size_t)q].send[a] + (size_t)rank_ * bytes, bytes);
+        if (rc == MN_OK) rc = sync();
+        const int lrc = h_.leave_collective(rank_, p);
+        return rc != MN_OK ? rc : lrc;
+    }
+    int agree(const int *mine, int *out) override {
+        Rendezvous::Post p = post(Rendezvous::kAgree, "the shard status agreement", 4);
+        p.val = mine[0];
+        std::vector<Rendezvous::Post> all;
+        const int rc = h_.enter(rank_, p, &all);
+        if (rc != MN_OK) return rc;
+        int m = 0;
+        for (const auto &o : all) m = std::max(m, o.val);
+        *out = m;
+        return h_.leave_collective(rank_, p);
+    }
+
+  private:
+    // the rank's stage work is complete before its buffers are shared
+    Rendezvous::Post post(int kind, const char *what, size_t bytes) {
+        Rendezvous::Post p;
+        p.kind = kind;
+        p.seq = seq_++;
+        p.bytes = bytes;
+        p.what = what;
+        const hipError_t e = hipStreamSynchronize(s_);
+        if (e != hipSuccess) h_.abort("a rank's stream failed before a collective");
+        return p;
+    }
+    int copy(void *dst, const void *src, size_t bytes) {
+        MN_HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, s_));
+        return MN_OK;
+    }
+    int sync() {
+        MN_HIP_TRY(hipStreamSynchronize(s_));
+        return MN_OK;
+    }
+    Rendezvous &h_;
+    int world_, rank_;
+    hipStream_t s_;
+    int64_t seq_ = 0;
 };
 
 // ---- the driver ---------------------------------------------------------------
@@ -436,6 +746,7 @@ int sharded_drive(Transport &T, const RankIO *io, int64_t nl, int d, const mn_kn
     // per local rank: X_all, part lists of all rows li/ld [N][k], received
     // parts pi/pd [R][n_local][k], per-row tau0 / norms / Tc [3][N]
     DevBufs B;
+    B.gy = T.graveyard();  // a failed collective leaves the frees to the reaper
     std::vector<float *> xall(NL);
     std::vector<int32_t *> li(NL), pi(NL);
     std::vector<float *> ld(NL), pd(NL), rowv(NL);
@@ -506,20 +817,26 @@ int sharded_drive(Transport &T, const RankIO *io, int64_t nl, int d, const mn_kn
         sym = agreed == 0;
     }
     if (sym) {
-        std::vector<const void *> snd(NL);
-        std::vector<void *> rcv(NL);
         const size_t rb = sizeof(float) * (size_t)nl;
-        for (int l = 0; l < NL; ++l) {
-            snd[l] = tau0(l) + (int64_t)T.rank(l) * nl;
-            rcv[l] = tau0(l);
-        }
-        int grc = T.all_gather(snd.data(), rcv.data(), rb, "the all-gather of the thresholds");
+        // in-place all-gather of one per-row array (0 tau0, 1 the norms)
+        auto gather_rows = [&](int which) -> int {
+            std::vector<const void *> snd(NL);
+            std::vector<void *> rcv(NL);
+            for (int l = 0; l < NL; ++l) {
+                float *base = which == 0 ? tau0(l) : qn(l);
+                snd[l] = base + (int64_t)T.rank(l) * nl;
+                rcv[l] = base;
+            }
+            return T.all_gather(snd.data(), rcv.data(), rb,
+                                which == 0 ? "the all-gather of the thresholds"
+                                           : "the all-gather of the row norms");
+        };
+        // (tuning build: one rank issues the two in the other order — the
+        // threaded loopback must report it, RCCL would hang or mix the data)
+        const int first = T.reorder_gathers() ? 1 : 0;
+        int grc = gather_rows(first);
         if (grc != MN_OK) return grc;
-        for (int l = 0; l < NL; ++l) {
-            snd[l] = qn(l) + (int64_t)T.rank(l) * nl;
-            rcv[l] = qn(l);
-        }
-        grc = T.all_gather(snd.data(), rcv.data(), rb, "the all-gather of the row norms");
+        grc = gather_rows(1 - first);
         if (grc != MN_OK) return grc;
         // 3. stage B: this rank's share, part lists of all rows
         for (int l = 0; l < NL; ++l) {
@@ -707,6 +1024,118 @@ int mn_knn_sharded_sim_f32(const float *X_all, int64_t n_tot, int32_t d, int32_t
     if (rc != MN_OK) return rc;
     knn_stats_ref() = res.st;
     if (rank_ms) std::memcpy(rank_ms, res.rank_ms.data(), sizeof(float) * res.rank_ms.size());
+    return MN_OK;
+}
+
+// The sharded build of `world` ranks on ONE device with one host thread per
+// rank (ThreadedTransport): the ranks' stages and collectives run
+// concurrently, each rank through the driver exactly as one RCCL process
+// does, and every collective checks that all ranks issued the same one.
+// Arguments as mn_knn_sharded_sim_f32; the collective deadline is
+// mn_rccl_set_timeout's.
+int mn_knn_sharded_threads_f32(const float *X_all, int64_t n_tot, int32_t d, int32_t world,
+                               const mn_knn_opts *opts, int32_t *out_idx, float *out_dist,
+                               float *rank_ms) {
+    using namespace mn;
+    clear_error();
+    MN_REQUIRE(X_all && opts && out_idx && out_dist, MN_EINVAL,
+               "mn_knn_sharded_threads_f32: NULL argument");
+    MN_REQUIRE(world >= 1 && world <= kMaxShardRanks && n_tot >= world && n_tot % world == 0 &&
+                   d >= 1 && opts->k >= 1 && n_tot <= INT32_MAX,
+               MN_EINVAL, "mn_knn_sharded_threads_f32: bad shape (n_tot a multiple of world <= 16)");
+    const int64_t nl = n_tot / world;
+    int dev = 0;
+    MN_HIP_TRY(hipGetDevice(&dev));
+    MN_HIP_TRY(hipStreamSynchronize((hipStream_t)opts->stream));  // X_all is complete
+    const bool timing = opts->timing != 0 || rank_ms != nullptr;
+    Rendezvous hub(world, g_timeout_s.load());
+    std::vector<int> rc((size_t)world, MN_OK);
+    std::vector<std::string> err((size_t)world);
+    std::vector<DriveOut> res((size_t)world);
+    auto run_rank = [&](int r) {
+        int code = MN_OK;
+        hipStream_t s = nullptr;
+        if (hipSetDevice(dev) != hipSuccess ||
+            hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) {
+            set_error("mn_knn_sharded_threads_f32: rank %d could not get a stream", r);
+            code = MN_EHIP;
+        } else {
+            mn_knn_opts o = *opts;
+            o.stream = s;
+            ThreadedTransport T(hub, world, r, s);
+            const RankIO io{X_all + (size_t)r * nl * d, out_idx + (size_t)r * nl * opts->k,
+                            out_dist + (size_t)r * nl * opts->k};
+            code = sharded_drive(T, &io, nl, d, &o, 0, X_all, false, timing, &res[(size_t)r]);
+        }
+        hub.depart(r);
+        if (code != MN_OK) err[(size_t)r] = mn_last_error();
+        if (s) {
+            (void)hipStreamSynchronize(s);
+            (void)hipStreamDestroy(s);
+        }
+        rc[(size_t)r] = code;
+    };
+    std::vector<std::thread> th;
+    th.reserve((size_t)world);
+    for (int r = 0; r < world; ++r) {
+        try {
+            th.emplace_back(run_rank, r);
+        } catch (...) {
+            hub.abort("a rank's host thread could not be started");
+            for (int q = r; q < world; ++q) {
+                rc[(size_t)q] = MN_EHIP;
+                err[(size_t)q] = "mn_knn_sharded_threads_f32: could not start a host thread";
+            }
+            break;
+        }
+    }
+    for (auto &t : th) t.join();
+    // the error to report: the first rank whose own stage or collective
+    // failed (the others only say that another rank failed)
+    int bad = -1;
+    for (int r = 0; r < world; ++r)
+        if (rc[(size_t)r] != MN_OK &&
+            (bad < 0 || (err[(size_t)bad].find("another rank failed") != std::string::npos &&
+                         err[(size_t)r].find("another rank failed") == std::string::npos)))
+            bad = r;
+    if (bad >= 0) {
+        set_error("rank %d: %s", bad, err[(size_t)bad].c_str());
+        return rc[(size_t)bad];
+    }
+    mn_knn_stats st = res[0].st;
+    for (int r = 1; r < world; ++r) {
+        const mn_knn_stats &o = res[(size_t)r].st;
+        st.n_queries += o.n_queries;
+        st.n_uncertified += o.n_uncertified;
+        st.n_candidates += o.n_candidates;
+        st.ms_norms = std::max(st.ms_norms, o.ms_norms);
+        st.ms_sample = std::max(st.ms_sample, o.ms_sample);
+        st.ms_sweep = std::max(st.ms_sweep, o.ms_sweep);
+        st.ms_rerank = std::max(st.ms_rerank, o.ms_rerank);
+        st.ms_fallback = std::max(st.ms_fallback, o.ms_fallback);
+        st.ms_total = std::max(st.ms_total, o.ms_total);
+        st.ms_gram = std::max(st.ms_gram, o.ms_gram);
+    }
+    knn_stats_ref() = st;
+    if (rank_ms)
+        for (int r = 0; r < world; ++r)
+            for (int c = 0; c < 3; ++c)
+                rank_ms[3 * r + c] = res[(size_t)r].rank_ms.size() == 3 ? res[(size_t)r].rank_ms[(size_t)c] : 0.f;
+    return MN_OK;
+}
+
+// Wait (up to timeout_s) for the reaper threads of failed sharded calls to
+// abort their communicators and free those calls' buffers.
+int mn_shard_quiesce(double timeout_s) {
+    mn::clear_error();
+    std::unique_lock<std::mutex> lk(g_reap_mu);
+    const bool done = g_reap_cv.wait_for(lk, std::chrono::duration<double>(timeout_s > 0 ? timeout_s : 0),
+                                         [] { return g_reapers == 0; });
+    if (!done) {
+        mn::set_error("mn_shard_quiesce: %d failed call(s) still releasing after %.3g s", g_reapers,
+                      timeout_s);
+        return MN_ECOMM;
+    }
     return MN_OK;
 }
 

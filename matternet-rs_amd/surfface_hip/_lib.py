@@ -125,6 +125,8 @@ SIGNATURES = {
     "mn_libm_pow_f64": (C.c_int, [P, P, I64, P, P]),
     "mn_knn_sharded_f32": (C.c_int, [P, I64, I32, P, C.POINTER(KnnOpts), I64, P, P]),
     "mn_knn_sharded_sim_f32": (C.c_int, [P, I64, I32, I32, C.POINTER(KnnOpts), P, P, P]),
+    "mn_knn_sharded_threads_f32": (C.c_int, [P, I64, I32, I32, C.POINTER(KnnOpts), P, P, P]),
+    "mn_shard_quiesce": (C.c_int, [C.c_double]),
     "mn_sym_share_table": (C.c_int, [I32, I32, I32, P, I64, P]),
     "mn_rccl_unique_id": (C.c_int, [P]),
     "mn_rccl_comm_init": (C.c_int, [P, I32, I32, C.POINTER(C.c_void_p)]),

@@ -87,13 +87,34 @@ def sharded_knn_sym(X_shard: torch.Tensor, k: int, share_fn, finish_fn, group=No
 
 # ---- the same build behind the library's C entry (caller-owned RCCL comm) ----
 
+_QUIESCE_AT_EXIT = []
+
+
+def quiesce(timeout_s: float = 60.0) -> None:
+    """mn_shard_quiesce: wait for the background release of failed sharded
+    calls (their communicators aborted, their buffers freed once the device
+    work queued on them drained)."""
+    from . import _lib
+    _lib.check(_lib.lib().mn_shard_quiesce(float(timeout_s)))
+
+
+def _quiesce_at_exit():
+    from . import _lib
+    for L in list(_lib._LOADED.values()):
+        L.mn_shard_quiesce(60.0)
+
+
 class RcclComm:
     """An RCCL communicator created through the library (mn_rccl_comm_init):
     rank 0 makes the 128-byte id (`unique_id()`), every rank passes it here."""
 
     def __init__(self, uid: bytes, world: int, rank: int):
+        import atexit
         import ctypes as C
         from . import _lib
+        if not _QUIESCE_AT_EXIT:  # no release thread may outlive the process's GPU state
+            atexit.register(_quiesce_at_exit)
+            _QUIESCE_AT_EXIT.append(True)
         self._lib = _lib
         buf = C.create_string_buffer(bytes(uid), 128)
         h = C.c_void_p()
@@ -142,13 +163,16 @@ def knn_sharded_capi(X_shard: torch.Tensor, k: int, comm: RcclComm, query_chunk:
 
 
 def knn_sharded_sim(X_all: torch.Tensor, k: int, world: int, timing: bool = False, stream=None,
-                    algo: int | None = None):
+                    algo: int | None = None, threads: bool = False):
     """mn_knn_sharded_sim_f32: the sharded build of `world` ranks on this
     device — mn_knn_sharded_f32's driver over the loopback transport (X_all =
     the shards, rank r's at r * n / world).  `algo` (default AUTO) picks the
     form as the RCCL entry would: AUTO / BF16X1 the symmetric form, F32 /
     BF16X3 the per-shard form.  Returns (idx [n, k] int32, dist [n, k] f32,
-    rank_ms [world][3] = per rank the stage A / B / C milliseconds, stats)."""
+    rank_ms [world][3] = per rank the stage A / B / C milliseconds, stats).
+    threads=True: mn_knn_sharded_threads_f32 — one host thread per rank, the
+    ranks concurrent, every collective checked for the same order on every
+    rank (a divergence raises MN_ECOMM instead of hanging)."""
     import ctypes as C
     import numpy as np
     from . import _lib
@@ -163,6 +187,7 @@ def knn_sharded_sim(X_all: torch.Tensor, k: int, world: int, timing: bool = Fals
                      timing=1 if timing else 0,
                      algo=_lib.MN_KNN_AUTO if algo is None else algo,
                      stream=stream_handle(stream))
-    _lib.check(_lib.lib().mn_knn_sharded_sim_f32(ptr(X_all), n, d, world, C.byref(o), ptr(idx),
-                                                 ptr(dd), ms.ctypes.data_as(C.c_void_p)))
+    fn = _lib.lib().mn_knn_sharded_threads_f32 if threads else _lib.lib().mn_knn_sharded_sim_f32
+    _lib.check(fn(ptr(X_all), n, d, world, C.byref(o), ptr(idx), ptr(dd),
+                  ms.ctypes.data_as(C.c_void_p)))
     return idx, dd, ms, last_stats()
