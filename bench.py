@@ -188,9 +188,9 @@ def main():
         # the exact instantiation (rocprofv3 name) the PMC reference must match
         kfull = "k_gram_sweep2<0, 0, true>"
         if sym:  # fp16 operands (x 2^e): the release library's only SW_SYM form
-            kname = "k_gram_sweep2<SW_SYM>"
-            # (V = 14: the round-5 DMA/read placement, gram_sweep2.hpp)
-            kfull = "k_gram_sweep2<0, 2, true, true, 14>"
+            kname = "k_gram_sweep3<SW_SYM>"
+            # (round 6: gram_sweep3.hpp, DMA two k-steps ahead)
+            kfull = "k_gram_sweep3<0, 2, 2>"
         flops_launch = 2.0 * nq * nc_sw * d
         # executed: the upper-triangle 256 x 256 tiles of the n_tot rows, a
         # rank's 1/world share of them (the sharded symmetric form)
@@ -556,7 +556,7 @@ def c5_leg(S, _lib, L, a, dev, stream):
     if m0 > 0 and st.get("sweep_slices") == -1:
         # SW_COS_SYM: the sweep decides all n^2 pairs, executing the upper-
         # triangle 256 x 256 tiles (each unordered pair once)
-        kname, kms = "k_gram_sweep2<SW_COS_SYM, tile-major>", st["ms_sweep"]
+        kname, kms = "k_gram_sweep3<SW_COS_SYM, tile-major>", st["ms_sweep"]
         flops = 2.0 * n * n * d
         nbk = (n + 255) // 256
         exec_fl = 2.0 * 256 * 256 * ((d + 31) // 32 * 32) * nbk * (nbk + 1) / 2

@@ -46,6 +46,7 @@
 #include "glibc_f64.hpp"
 #include "gram_bf16.hpp"
 #include "gram_sweep2.hpp"
+#include "gram_sweep3.hpp"
 
 namespace mn {
 namespace kb16 {
@@ -1082,18 +1083,27 @@ static int knn_cos_bf16_x1(const uint16_t *X, int64_t n, int32_t d, const mn_cos
                                   hipMemcpyHostToDevice, s));
         MN_HIP_TRY(hipMemsetAsync(cnt2, 0, (size_t)n * 4, s));
         MN_REQUIRE(tab.size() < INT_MAX, MN_ENOTSUP, "mn_knn_cos_bf16: sweep grid too large");
-        auto kern = ksw2::k_gram_sweep2<0, ksw2::SW_COS_SYM, true>;
+        // the default: gram_sweep3.hpp's schedule, DMA two k-steps ahead
+        auto kern = ksw2::k_gram_sweep3<0, ksw2::SW_COS_SYM, 2>;
         const char *probe = knob("MN_BF16_PROBE");  // tuning build: noepi = K loop only
 #ifdef MN_TUNING
-        if (probe && !strcmp(probe, "noepi")) kern = ksw2::k_gram_sweep2<1, ksw2::SW_COS_SYM, true>;
-        // MN_SW_V: the DMA-placement variants of gram_sweep2.hpp (default 14)
-        if (knob_int("MN_SW_V", 14) == 0) kern = ksw2::k_gram_sweep2<0, ksw2::SW_COS_SYM, true, false, 0>;
-        if (knob_int("MN_SW_V", 14) == 2) kern = ksw2::k_gram_sweep2<0, ksw2::SW_COS_SYM, true, false, 2>;
+        const int sweep_gen = knob_int("MN_SWEEP", 4);  // 2: round 5's k_gram_sweep2
+        const bool noepi = probe && !strcmp(probe, "noepi");
+        if (sweep_gen == 4 && noepi) kern = ksw2::k_gram_sweep3<1, ksw2::SW_COS_SYM, 2>;
+        if (sweep_gen == 3)
+            kern = noepi ? ksw2::k_gram_sweep3<1, ksw2::SW_COS_SYM> : ksw2::k_gram_sweep3<0, ksw2::SW_COS_SYM>;
+        if (sweep_gen == 2) {
+            kern = noepi ? ksw2::k_gram_sweep2<1, ksw2::SW_COS_SYM, true>
+                         : ksw2::k_gram_sweep2<0, ksw2::SW_COS_SYM, true>;
+            // MN_SW_V: the DMA-placement variants of gram_sweep2.hpp (default 14)
+            if (knob_int("MN_SW_V", 14) == 0) kern = ksw2::k_gram_sweep2<0, ksw2::SW_COS_SYM, true, false, 0>;
+            if (knob_int("MN_SW_V", 14) == 2) kern = ksw2::k_gram_sweep2<0, ksw2::SW_COS_SYM, true, false, 2>;
+        }
 #endif
         hipLaunchKernelGGL(kern, dim3((unsigned)tab.size()), dim3(ksw2::NT), 0, s, XK, n, XK, n, nkb,
                            (int64_t)0, (int64_t)0, 1, tqS, cnS, hcS, (int64_t)0, 1, (int64_t)0,
                            cap2, buf2, cnt2, pst, ksw2::SymArgs{dtab, taS, hoS, 0});
-        MN_KCHECK(s, "k_gram_sweep2<COS_SYM>");
+        MN_KCHECK(s, "k_gram_sweep3<COS_SYM>");
         if (probe && *probe) {  // timing probe: no outputs are produced
             tm.mark();
             MN_HIP_TRY(hipStreamSynchronize(s));

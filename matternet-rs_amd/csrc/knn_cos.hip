@@ -938,19 +938,23 @@ static int knn_cos_columns_impl(const T *X, int64_t n, int32_t f, const mn_cos_o
     hipStream_t s = (hipStream_t)o->stream;
     const int ntile = (f + GT - 1) / GT;
     const int ntri = ntile * (ntile + 1) / 2;
-    // ~2048 Gram blocks.  Tuning build: MN_COS_GBLK = the target block count
-    // (C3, same process, bit-identical: 8192 -> Gram phase 13.35 ms vs 14.6,
-    // 4096 13.8, 1024 16.1 — profiles/r05/r05_c3_gblk_ab.log; not the default
-    // until the parity suite has run on it)
-    const int64_t gblk = knob_int("MN_COS_GBLK", 2048);
+    // ~8192 Gram blocks (round 6; was 2048).  Tuning build: MN_COS_GBLK = the
+    // target block count (C3, same process, bit-identical: 8192 -> Gram phase
+    // 13.35 ms vs 14.6 at 2048, 4096 13.8, 1024 16.1 —
+    // profiles/r05/r05_c3_gblk_ab.log)
+    const int64_t gblk = knob_int("MN_COS_GBLK", 8192);
     int nchunk = (int)std::max<int64_t>(1, std::min<int64_t>((gblk + ntri - 1) / ntri, (n + 255) / 256));
     int64_t kchunk = (n + nchunk - 1) / nchunk;
     kchunk = ((kchunk + GK - 1) / GK) * GK;
     nchunk = (int)((n + kchunk - 1) / kchunk);
 
     T *XT = (T *)scratch(kSlotGeneric0, sizeof(T) * (size_t)n * f);
-    char *g = (char *)scratch(kSlotGeneric1, sizeof(double) * ((size_t)f * f + f * 4 + 64) +
-                                                (size_t)f * L * 24 + (size_t)f * 8 + 64);
+    // layout (bytes): G f^2 x 8, nrm / gnext f x 8 each, flags 64, cand / pi /
+    // pj f L x 4 each, (16-aligned) cdist / capx f L x 8 each, fb_list f x 4,
+    // (16-aligned) nrmA f x 8, colmax f x 4
+    const size_t gbytes = 8 * ((size_t)f * f + 2 * (size_t)f) + 64 + 28 * (size_t)f * L + 16 +
+                          4 * (size_t)f + 16 + 12 * (size_t)f + 64;
+    char *g = (char *)scratch(kSlotGeneric1, gbytes);
     MN_REQUIRE(XT && g, MN_ENOMEM, "mn_knn_cos_columns_f32: scratch allocation failed");
     double *G = (double *)g;
     double *nrm = G + (size_t)f * f;
@@ -1039,7 +1043,9 @@ static int knn_cos_columns_impl(const T *X, int64_t n, int32_t f, const mn_cos_o
         MN_HIP_TRY(stream_wait(s, side));
         tm.mark();
         // the selection's band around the reference's 1e-12 cut (relative)
-        const double amb_rel = f32g ? 4.0 * e32 : 1e-8;
+        // (f64 Gram: |G_ii - n_i^2| <= gamma_n n_i^2 grows like n u, so the
+        // band scales with n once 4 (n + 16) 2^-53 passes 1e-8, n ~ 9e7)
+        const double amb_rel = f32g ? 4.0 * e32 : std::max(1e-8, 4.0 * ((double)n + 16.0) * 0x1p-53);
         // approximate norms sqrt(G_ii) for the selection when the exact ones
         // come with the exact pass
         if (norms_in_pass)

@@ -39,6 +39,7 @@
 #include "common.hpp"
 #include "gram_bf16.hpp"
 #include "gram_sweep2.hpp"
+#include "gram_sweep3.hpp"
 #include "shard_sym.hpp"
 
 namespace mn {
@@ -2546,13 +2547,17 @@ static int knn_x1(const float *Q, int64_t nq, const float *C, int64_t nc, int32_
             // diagonal tile: acc0 = U_q s_c + V_c s_q (tq = U, hc = V);
             // off-diagonal: V_q s_c + U_c s_q (aoff = V, hoff = U); keys from Teff
             ksw2::SymArgs sa{dtab, Vp, Up, scP};
-            auto sk = ksw2::k_gram_sweep2<0, ksw2::SW_SYM, true, true>;
+            // the default: gram_sweep3.hpp's schedule, DMA two k-steps ahead
+            auto sk = ksw2::k_gram_sweep3<0, ksw2::SW_SYM, 2>;
 #ifdef MN_TUNING
+            // MN_SWEEP=2: round 5's k_gram_sweep2 (and its MN_SW_V variants)
+            const int sweep_gen = knob_int("MN_SWEEP", 4);
+            if (sweep_gen == 2) sk = ksw2::k_gram_sweep2<0, ksw2::SW_SYM, true, true>;
             // timing probes (results invalid): noepi = K loop only, nodma /
             // noread = also without the DMA issue / fragment reads
             // l2res / l2res_noepi = operands L2-resident (panels 0 / 1)
             // MN_SW_V: the DMA-placement variants of gram_sweep2.hpp (default 2)
-            const int swv = knob_int("MN_SW_V", 14);
+            const int swv = sweep_gen == 2 ? knob_int("MN_SW_V", 14) : -1;
             if (swv == 0) sk = ksw2::k_gram_sweep2<0, ksw2::SW_SYM, true, true, 0>;
             if (swv == 6) sk = ksw2::k_gram_sweep2<0, ksw2::SW_SYM, true, true, 6>;
             if (swv == 10) sk = ksw2::k_gram_sweep2<0, ksw2::SW_SYM, true, true, 10>;
@@ -2560,7 +2565,8 @@ static int knn_x1(const float *Q, int64_t nq, const float *C, int64_t nc, int32_
             if (swv == 12) sk = ksw2::k_gram_sweep2<0, ksw2::SW_SYM, true, true, 12>;
             if (swv == 1) sk = ksw2::k_gram_sweep2<0, ksw2::SW_SYM, true, true, 1>;
             if (swv == 3) sk = ksw2::k_gram_sweep2<0, ksw2::SW_SYM, true, true, 3>;
-            if (probe && *probe && swv >= 0 && swv <= 3)
+            if (sweep_gen != 2) {
+            } else if (probe && *probe && swv >= 0 && swv <= 3)
                 sk = swv == 0 ? ksw2::k_gram_sweep2<1, ksw2::SW_SYM, true, true, 0>
                      : swv == 1 ? ksw2::k_gram_sweep2<1, ksw2::SW_SYM, true, true, 1>
                      : swv == 2 ? ksw2::k_gram_sweep2<1, ksw2::SW_SYM, true, true, 2>
@@ -2571,11 +2577,18 @@ static int knn_x1(const float *Q, int64_t nq, const float *C, int64_t nc, int32_
                      : !strcmp(probe, "l2res") ? ksw2::k_gram_sweep2<5, ksw2::SW_SYM, true, true>
                      : !strcmp(probe, "l2res_noepi") ? ksw2::k_gram_sweep2<6, ksw2::SW_SYM, true, true>
                                                 : ksw2::k_gram_sweep2<1, ksw2::SW_SYM, true, true>;
+            // MN_SWEEP=3: gram_sweep3.hpp's schedule (PROBE noepi: K loop only)
+            if (sweep_gen == 4 && probe && *probe) sk = ksw2::k_gram_sweep3<1, ksw2::SW_SYM, 2>;
+            if (sweep_gen == 3)  // DMA three k-steps ahead
+                sk = !(probe && *probe)          ? ksw2::k_gram_sweep3<0, ksw2::SW_SYM>
+                     : !strcmp(probe, "initonly") ? ksw2::k_gram_sweep3<2, ksw2::SW_SYM>
+                     : !strcmp(probe, "prefilter") ? ksw2::k_gram_sweep3<3, ksw2::SW_SYM>
+                                                   : ksw2::k_gram_sweep3<1, ksw2::SW_SYM>;
 #endif
             hipLaunchKernelGGL(sk, dim3((unsigned)tab.size()), dim3(ksw2::NT), 0, s, XK, nc, XK,
                                nc, nkb, (int64_t)0, (int64_t)0, 1, Up, teffP, Vp, (int64_t)0, 1,
                                (int64_t)0, cap2, cbuf2, cnt2, pst1, sa);
-            MN_KCHECK(s, "k_gram_sweep2<SYM>");
+            MN_KCHECK(s, "k_gram_sweep<SYM>");
             S1r = 0;
             tau_r = tauP;   // the certificate: T > D_k (the bound is in the folds)
             dlt_r = zdlt;
@@ -3041,10 +3054,12 @@ int shard_share(const float *X_all, const ShardPlan &pl, const float *tau0_all,
     MN_HIP_TRY(hipMemsetAsync(cnt2, 0, nn * 4, s));
     if (!tab.empty()) {
         ksw2::SymArgs sa{dtab, Vp, Up, scP};
-        hipLaunchKernelGGL((ksw2::k_gram_sweep2<0, ksw2::SW_SYM, true, true>), dim3((unsigned)tab.size()),
-                           dim3(ksw2::NT), 0, s, XK, N, XK, N, nkb, (int64_t)0, (int64_t)0, 1, Up,
-                           teffP, Vp, (int64_t)0, 1, (int64_t)0, cap2, cbuf2, cnt2, pst1, sa);
-        MN_KCHECK(s, "k_gram_sweep2<SYM, shard>");
+        auto sk = ksw2::k_gram_sweep3<0, ksw2::SW_SYM, 2>;
+        if (knob_int("MN_SWEEP", 4) == 2) sk = ksw2::k_gram_sweep2<0, ksw2::SW_SYM, true, true>;
+        hipLaunchKernelGGL(sk, dim3((unsigned)tab.size()), dim3(ksw2::NT), 0, s, XK, N, XK, N, nkb,
+                           (int64_t)0, (int64_t)0, 1, Up, teffP, Vp, (int64_t)0, 1, (int64_t)0, cap2,
+                           cbuf2, cnt2, pst1, sa);
+        MN_KCHECK(s, "k_gram_sweep3<SYM, shard>");
     }
     // partial re-rank of every row: 128 candidates a wave first, the rows with
     // more (up to 1024) in a second launch

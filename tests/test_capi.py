@@ -71,6 +71,7 @@ def test_release_library_has_no_probes_or_tuning_knobs():
     # k_gram_sweep2<PROBE, ...> / k_gram_bf16<MODE, PROBE>: only PROBE = 0
     assert re.search(rb"k_gram_sweep2ILi0E", blob)
     assert not re.search(rb"k_gram_sweep2ILi[1-9]E", blob)
+    assert re.search(rb"k_gram_sweep3ILi0E", blob) and not re.search(rb"k_gram_sweep3ILi[1-9]E", blob)
     assert not re.search(rb"k_gram_bf16ILi\d+ELi[1-9]E", blob)
     # the legacy sweep of gram_sweep.hpp is gone
     assert not re.search(rb"k_gram_sweepILi", blob)

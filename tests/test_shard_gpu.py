@@ -38,6 +38,7 @@ def test_simulated_shards_at_c2_size_bit_exact(R):
     n, d, k = 1_000_000 - 1_000_000 % R, 768, 32
     X = _uniform(n, d)
     full = S.knn_l2sq(X, k)
+    knn_sharded_sim(X, k, R)  # warm: the shares' scratch is allocated by the first rank's stages
     idx, dist, ms, st = knn_sharded_sim(X, k, R, timing=True)
     print(f"C2 as {R} simulated ranks", json.dumps({"rank_ms": ms.round(2).tolist(),
                                                    "n_uncertified": st["n_uncertified"],

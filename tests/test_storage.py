@@ -159,3 +159,11 @@ def test_config_value_accessors_and_nonfinite_json(tmp_path):
     raw = json.loads(text)
     assert raw["builder_config"]["lambda_eps"] == {"F64": None}
     assert raw["builder_config"]["eps2"] == {"OptionF64": None}
+    # the round trip: a plain F64 written as null does not load back (serde_json
+    # refuses null for f64; parity unpinned: no reference fixture holds it),
+    # while OptionF64 null is None
+    with pytest.raises(ST.StorageError):
+        ST.ArrowSpaceMetadata.from_json(text)
+    md.builder_config["lambda_eps"] = ST.config_value("F64", 0.25)
+    back = ST.ArrowSpaceMetadata.from_json(md.to_json())
+    assert back.lambda_eps() == 0.25 and back.builder_config["eps2"] == {"OptionF64": None}
