@@ -52,6 +52,7 @@ constexpr int NSLOT = 4;     // LDS ring of k-steps
 constexpr int WQF = 4;       // 16-query fragments per wave
 constexpr int WCF = 8;       // 16-row corpus fragments per wave
 constexpr int SCAP = 224;    // staged candidates per wave
+constexpr uint32_t kSkip = 0xffffffffu;  // a reserved staging slot left empty
 
 // the LDS-DMA ring is its own LDS object: the compiler's wait insertion then
 // knows the DMA never writes the per-tile arrays below (one shared object made
@@ -448,7 +449,7 @@ __global__ __launch_bounds__(NT) void k_gram_sweep2(
             if constexpr (SYM) {  // pq = the row; its slot from the row's counter
                 const int pos = atomicAdd(&cnt[pq], 1);
                 if (pos < cap) buf[(int64_t)pq * cap + pos] = sm.stk[w][e];
-            } else {
+            } else if (pq != kSkip) {
                 const int ql = (int)(pq & 255u), pos = (int)(pq >> 8);
                 buf[((int64_t)(q0 + ql) * S + sl) * cap + pos] = sm.stk[w][e];
             }
@@ -551,6 +552,11 @@ __global__ __launch_bounds__(NT) void k_gram_sweep2(
                         buf[((int64_t)(q0 + ql) * S + sl) * cap + pos] = kv;
                         dirty = true;
                     }
+                } else if (e < SCAP) {
+                    // past the row's cap (an overflow): the slot was reserved
+                    // with the others; mark it empty, or the flush would write
+                    // whatever an earlier entry (or another block) left there
+                    sm.stp[w][e] = kSkip;
                 }
                 ++e;
                 ++pos;

@@ -54,7 +54,14 @@ struct alignas(16) Smem3 {
 };
 static_assert(sizeof(Smem3) + sizeof(Ring) <= 163840, "LDS budget");
 
-template <int PROBE, int MODE, int AHEAD = 3>
+// PH (tuning A/B): windows per k-step and group.  1: one read window (12
+// fragment reads, 4 DMA pieces) and one MFMA window (32 MFMAs); 2: two of
+// each (8 reads + the corpus tile's 2 pieces | 16 MFMAs, then 4 reads + the
+// query panel's 2 pieces | 16 MFMAs) — half the burst per window.
+// EMI (tuning A/B): 0 = the fragments' hit mask, then a switch picks each
+// hit fragment into one staging body; 1 = the (small) staging body inline
+// per fragment behind its ballot.
+template <int PROBE, int MODE, int AHEAD = 3, int PH = 1, int EMI = 0>
 __global__ __launch_bounds__(NT) void k_gram_sweep3(
     const uint16_t *__restrict__ Qk, int64_t nq, const uint16_t *__restrict__ Ck, int64_t nc,
     int nkb, int64_t q_off, int64_t c_off, int excl, const float *__restrict__ tq,
@@ -128,9 +135,11 @@ __global__ __launch_bounds__(NT) void k_gram_sweep3(
     const int kend = nkb * (KB * BC * 2);
     // stage the next k-step (four pieces, always: past the block's last
     // k-step the last one again, into the slot nobody reads any more)
-    auto issue = [&]() __attribute__((always_inline)) {
+    auto issue_c = [&]() __attribute__((always_inline)) {
         dma(rc, dsoff, vo0, ldsC + dsl);
         dma(rc, dsoff, vo1, ldsC + dsl + 1024);
+    };
+    auto issue_q = [&]() __attribute__((always_inline)) {  // then the next step
         dma(rq, dsoff, vo0, ldsQ + dsl);
         dma(rq, dsoff, vo1, ldsQ + dsl + 1024);
         dsl = (dsl + (uint32_t)(BC * KB * 2)) & (uint32_t)(NSLOT * BC * KB * 2 - 1);
@@ -144,6 +153,10 @@ __global__ __launch_bounds__(NT) void k_gram_sweep3(
                 dsoff -= KB * BC * 2;
             }
         }
+    };
+    auto issue = [&]() __attribute__((always_inline)) {
+        issue_c();
+        issue_q();
     };
 
     typedef typename std::conditional<F16, f16x8, bf16x8>::type frag_t;
@@ -184,6 +197,24 @@ __global__ __launch_bounds__(NT) void k_gram_sweep3(
     const int chs0 = 8 * swz(fr, fk);
     const uint32_t qrd = lds_addr(&rg.Q[0][64 * wq + fr][chs0]);
     const uint32_t crd = lds_addr(&rg.C[0][128 * wc + fr][chs0]);
+    auto read_frags_h0 = [&](uint32_t so) __attribute__((always_inline)) {
+        const uint32_t qa = qrd + so, ca = crd + so;
+        asm volatile("ds_read_b128 %0, %1" : "=v"(fq[0]) : "v"(qa));
+        asm volatile("ds_read_b128 %0, %1 offset:1024" : "=v"(fq[1]) : "v"(qa));
+        asm volatile("ds_read_b128 %0, %1 offset:2048" : "=v"(fq[2]) : "v"(qa));
+        asm volatile("ds_read_b128 %0, %1 offset:3072" : "=v"(fq[3]) : "v"(qa));
+        asm volatile("ds_read_b128 %0, %1" : "=v"(fc[0]) : "v"(ca));
+        asm volatile("ds_read_b128 %0, %1 offset:1024" : "=v"(fc[1]) : "v"(ca));
+        asm volatile("ds_read_b128 %0, %1 offset:2048" : "=v"(fc[2]) : "v"(ca));
+        asm volatile("ds_read_b128 %0, %1 offset:3072" : "=v"(fc[3]) : "v"(ca));
+    };
+    auto read_frags_h1 = [&](uint32_t so) __attribute__((always_inline)) {
+        const uint32_t ca = crd + so;
+        asm volatile("ds_read_b128 %0, %1 offset:4096" : "=v"(fc[4]) : "v"(ca));
+        asm volatile("ds_read_b128 %0, %1 offset:5120" : "=v"(fc[5]) : "v"(ca));
+        asm volatile("ds_read_b128 %0, %1 offset:6144" : "=v"(fc[6]) : "v"(ca));
+        asm volatile("ds_read_b128 %0, %1 offset:7168" : "=v"(fc[7]) : "v"(ca));
+    };
     auto read_frags = [&](uint32_t so) __attribute__((always_inline)) {
         const uint32_t qa = qrd + so, ca = crd + so;
         asm volatile("ds_read_b128 %0, %1" : "=v"(fq[0]) : "v"(qa));
@@ -199,11 +230,11 @@ __global__ __launch_bounds__(NT) void k_gram_sweep3(
         asm volatile("ds_read_b128 %0, %1 offset:6144" : "=v"(fc[6]) : "v"(ca));
         asm volatile("ds_read_b128 %0, %1 offset:7168" : "=v"(fc[7]) : "v"(ca));
     };
-    auto mfmas = [&]() __attribute__((always_inline)) {
+    auto mfmas = [&](int g0, int g1) __attribute__((always_inline)) {
 #pragma unroll
         for (int f = 0; f < WQF; ++f)
 #pragma unroll
-            for (int g = 0; g < WCF; ++g)
+            for (int g = g0; g < g1; ++g)
                 if constexpr (F16)
                     acc[f][g] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fc[g], fq[f], acc[f][g], 0, 0, 0);
                 else
@@ -215,15 +246,13 @@ __global__ __launch_bounds__(NT) void k_gram_sweep3(
     // its candidates (row, key, id) appended to the per-row buffers through
     // the per-row counters: every slot atomic first, then the entries (one
     // round trip).  Keys exactly as sweep2 forms them.
-    auto expand = [&](bool valid, uint32_t qw, uint32_t cw, const f32x4 a4) __attribute__((always_inline)) {
+    // build(): the up to 8 candidates of one raw hit into rw / kv / go
+    auto build = [&](bool valid, uint32_t qw, uint32_t cw, const f32x4 a4, uint32_t (&rw)[8],
+                     uint2 (&kv)[8], bool (&go)[8]) __attribute__((always_inline)) {
         const int q = (int)(qw & 0x7fffffffu), c = (int)(cw & 0x0fffffffu);
         const bool dg = (qw >> 31) != 0u;
         const unsigned pm = valid ? (cw >> 28) : 0u;
         const int ql = q - (int)q_off - q0;
-        uint32_t rw[8];
-        int pos[8];
-        uint2 kv[8];
-        bool go[8];
         float colv[4], cols[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) {  // the columns' values (global: the tile may be gone)
@@ -274,6 +303,13 @@ __global__ __launch_bounds__(NT) void k_gram_sweep3(
             rw[2 * r + 1] = go[2 * r + 1] ? rw[2 * r + 1] : 0u;
             rw[2 * r] = go[2 * r] ? rw[2 * r] : 0u;
         }
+    };
+    auto expand = [&](bool valid, uint32_t qw, uint32_t cw, const f32x4 a4) __attribute__((always_inline)) {
+        uint32_t rw[8];
+        uint2 kv[8];
+        bool go[8];
+        int pos[8];
+        build(valid, qw, cw, a4, rw, kv, go);
 #pragma unroll
         for (int j = 0; j < 8; ++j) pos[j] = go[j] ? atomicAdd(&cnt[rw[j]], 1) : cap;
 #pragma unroll
@@ -281,15 +317,31 @@ __global__ __launch_bounds__(NT) void k_gram_sweep3(
             if (pos[j] < cap) buf[(int64_t)rw[j] * cap + pos[j]] = kv[j];
     };
     int ns = 0;  // raw entries staged by this wave (wave-uniform)
+    static_assert(RCAP <= 128, "flush: two raw entries per lane");
     auto flush = [&]() __attribute__((always_inline)) {
         const int n = min(ns, RCAP);
+        // both entries of the lane built first, then all 16 slot atomics, then
+        // the entries: one round trip per flush
+        uint32_t rw[2][8];
+        uint2 kv[2][8];
+        bool go[2][8];
+        int pos[2][8];
 #pragma unroll
-        for (int j = 0; j < (RCAP + 63) / 64; ++j) {
+        for (int j = 0; j < 2; ++j) {
             const int e = lane + 64 * j;
             const bool ok = e < n;
             const int ee = ok ? e : 0;
-            expand(ok, sm.rid[w][ee].x, sm.rid[w][ee].y, sm.racc[w][ee]);
+            build(ok, sm.rid[w][ee].x, sm.rid[w][ee].y, sm.racc[w][ee], rw[j], kv[j], go[j]);
         }
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int i = 0; i < 8; ++i) pos[j][i] = go[j][i] ? atomicAdd(&cnt[rw[j][i]], 1) : cap;
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int i = 0; i < 8; ++i)
+                if (pos[j][i] < cap) buf[(int64_t)rw[j][i] * cap + pos[j][i]] = kv[j][i];
         ns = 0;
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no store left for the counted waits
     };
@@ -315,8 +367,20 @@ __global__ __launch_bounds__(NT) void k_gram_sweep3(
             sm.rid[w][e] = make_uint2(qw, cw);
             sm.racc[w][e] = a;
         }
-        if (ns > RCAP) {  // area full: those lanes' entries straight out (rare)
-            expand(h && e >= RCAP, qw, cw, a);
+        if (ns > RCAP) {  // area full (rare)
+            if constexpr (EMI == 1) {
+                // (the body is inlined per fragment: no expansion here) the
+                // rows those entries would feed are marked overflowed, so
+                // they take the exact path
+                if (h && e >= RCAP) {
+                    atomicMax(&cnt[qgl - (int)q_off], cap + 1);
+#pragma unroll
+                    for (int r = 0; r < 4; ++r)
+                        if ((pm >> r) & 1u) atomicMax(&cnt[c + r - (int)c_off], cap + 1);
+                }
+            } else {  // those lanes' entries straight out
+                expand(h && e >= RCAP, qw, cw, a);
+            }
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
     };
@@ -334,7 +398,11 @@ __global__ __launch_bounds__(NT) void k_gram_sweep3(
                     const f32x4 a = acc[f][g];
                     const int mi = max(max(__float_as_int(a[0]), __float_as_int(a[1])),
                                        max(__float_as_int(a[2]), __float_as_int(a[3])));
-                    fm |= __ballot(mi > 0) != 0 ? (1u << (8 * f + g)) : 0u;
+                    if constexpr (EMI == 1) {
+                        if (__builtin_expect(__ballot(mi > 0) != 0, 0)) emit_frag(a, f, g, ct0, diag);
+                    } else {
+                        fm |= __ballot(mi > 0) != 0 ? (1u << (8 * f + g)) : 0u;
+                    }
                 }
             if constexpr (PROBE == 3) {  // keep the mask live; never a staged entry
                 if (fm == 0x12345u) sm.ta[0] = 0.f;
@@ -375,6 +443,16 @@ __global__ __launch_bounds__(NT) void k_gram_sweep3(
         if constexpr (AHEAD == 3) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
         else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
     };
+    auto lgkm_wait_h0 = [&]() __attribute__((always_inline)) {
+        asm volatile("s_waitcnt lgkmcnt(0)"
+                     : "+v"(fq[0]), "+v"(fq[1]), "+v"(fq[2]), "+v"(fq[3]), "+v"(fc[0]),
+                       "+v"(fc[1]), "+v"(fc[2]), "+v"(fc[3])
+                     :
+                     : "memory");
+    };
+    auto lgkm_wait_h1 = [&]() __attribute__((always_inline)) {
+        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(fc[4]), "+v"(fc[5]), "+v"(fc[6]), "+v"(fc[7]) : : "memory");
+    };
     auto lgkm_wait = [&]() __attribute__((always_inline)) {
         asm volatile("s_waitcnt lgkmcnt(0)"
                      : "+v"(fq[0]), "+v"(fq[1]), "+v"(fq[2]), "+v"(fq[3]), "+v"(fc[0]),
@@ -414,6 +492,48 @@ __global__ __launch_bounds__(NT) void k_gram_sweep3(
                 check(c0 - cstr, par ^ 1, diag0 && ti == 1);
                 if constexpr (INIT) init_acc(par, false);
             }
+            if constexpr (PH == 2) {
+                static_assert(PH != 2 || AHEAD == 2, "PH 2 takes AHEAD 2");
+                read_frags_h0(so);
+                __builtin_amdgcn_sched_barrier(0);
+                issue_c();  // k-step + 2: the corpus tile's pieces
+                __builtin_amdgcn_sched_barrier(0);
+                __builtin_amdgcn_s_barrier();
+                __builtin_amdgcn_sched_barrier(0);
+                lgkm_wait_h0();
+                __builtin_amdgcn_sched_barrier(0);
+                __builtin_amdgcn_s_setprio(1);
+                mfmas(0, WCF / 2);
+                __builtin_amdgcn_s_setprio(0);
+                __builtin_amdgcn_sched_barrier(0);
+                __builtin_amdgcn_s_barrier();
+                __builtin_amdgcn_sched_barrier(0);
+                read_frags_h1(so);
+                __builtin_amdgcn_sched_barrier(0);
+                issue_q();  // k-step + 2: the query panel's pieces
+                __builtin_amdgcn_sched_barrier(0);
+                if (kb == nkb - 2 && more && wc == 0) {
+                    const int cb = c0 + cstr + 64 * wq + lane;
+                    sm.hc[par ^ 1][64 * wq + lane] = cb < cend ? hcn : pad;
+                    sm.tc[par ^ 1][64 * wq + lane] = cb < cend ? tcn : pad;
+                    if constexpr (F16) sm.sc[par ^ 1][64 * wq + lane] = cb < cend ? scn : 1.f;
+                }
+                if (wc == 1) vm_wait();
+                __builtin_amdgcn_sched_barrier(0);
+                __builtin_amdgcn_s_barrier();
+                __builtin_amdgcn_sched_barrier(0);
+                lgkm_wait_h1();
+                __builtin_amdgcn_sched_barrier(0);
+                __builtin_amdgcn_s_setprio(1);
+                mfmas(WCF / 2, WCF);
+                __builtin_amdgcn_s_setprio(0);
+                __builtin_amdgcn_sched_barrier(0);
+                if (wc == 0) vm_wait();
+                __builtin_amdgcn_s_barrier();
+                __builtin_amdgcn_sched_barrier(0);
+                so = (so + (uint32_t)(BC * KB * 2)) & (uint32_t)(NSLOT * BC * KB * 2 - 1);
+                continue;
+            }
             read_frags(so);
             __builtin_amdgcn_sched_barrier(0);
             issue();  // k-step + AHEAD, behind the reads
@@ -436,7 +556,7 @@ __global__ __launch_bounds__(NT) void k_gram_sweep3(
                 __builtin_amdgcn_sched_barrier(0);
             }
             __builtin_amdgcn_s_setprio(1);
-            mfmas();
+            mfmas(0, WCF);
             __builtin_amdgcn_s_setprio(0);
             __builtin_amdgcn_sched_barrier(0);
             if (wc == 0) vm_wait();

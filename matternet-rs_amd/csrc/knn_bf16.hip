@@ -1090,6 +1090,9 @@ static int knn_cos_bf16_x1(const uint16_t *X, int64_t n, int32_t d, const mn_cos
         const int sweep_gen = knob_int("MN_SWEEP", 4);  // 2: round 5's k_gram_sweep2
         const bool noepi = probe && !strcmp(probe, "noepi");
         if (sweep_gen == 4 && noepi) kern = ksw2::k_gram_sweep3<1, ksw2::SW_COS_SYM, 2>;
+        if (sweep_gen == 5)
+            kern = noepi ? ksw2::k_gram_sweep3<1, ksw2::SW_COS_SYM, 2, 2>
+                         : ksw2::k_gram_sweep3<0, ksw2::SW_COS_SYM, 2, 2>;
         if (sweep_gen == 3)
             kern = noepi ? ksw2::k_gram_sweep3<1, ksw2::SW_COS_SYM> : ksw2::k_gram_sweep3<0, ksw2::SW_COS_SYM>;
         if (sweep_gen == 2) {

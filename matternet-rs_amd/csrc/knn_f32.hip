@@ -1248,6 +1248,12 @@ __global__ __launch_bounds__(64 * WPB) void k_rerank_x1(
     const int64_t q = qlist ? qlist[wq] : wq;
     // qo: the row of Q / the output (refill: the buffers are per refilled row)
     const int64_t qo = qmap ? (int64_t)qmap[q] : q;
+#ifdef MN_TUNING
+    if (qo < 0 || qo > nvalid_max + 1) {  // (diagnostics)
+        if (lane == 0) printf("k_rerank_x1: row %lld maps to %lld\n", (long long)q, (long long)qo);
+        return;
+    }
+#endif
     const float T = tau0[q];
     bool forced = T == -__builtin_inff();
     // rel > 0 (SW_SYM): buffered keys are per-pair LOWER bounds (k_sym_pos),
@@ -1262,7 +1268,16 @@ __global__ __launch_bounds__(64 * WPB) void k_rerank_x1(
     auto gather = [&](const uint2 *bp, int cnt, bool) {
         for (int e0 = 0; e0 < cnt; e0 += 64) {
             const int e = e0 + lane;
-            const uint2 v = e < cnt ? bp[e] : make_uint2(0x7f800000u, 0u);
+            uint2 v = e < cnt ? bp[e] : make_uint2(0x7f800000u, 0u);
+#ifdef MN_TUNING
+            // (diagnostics: an id past the corpus is reported and dropped)
+            if (e < cnt && (int64_t)v.y > nvalid_max + 1) {
+                printf("k_rerank_x1: row %lld (out %lld) entry %d of %d: id %u > %lld, key %g\n",
+                       (long long)q, (long long)qo, e, cnt, v.y, (long long)nvalid_max + 1,
+                       (double)__uint_as_float(v.x));
+                v = make_uint2(0x7f800000u, 0u);
+            }
+#endif
             int64_t gid = (int64_t)v.y;
             if (e < cnt) gid = c_off + perm[gid];
             const bool pass = e < cnt && __uint_as_float(v.x) < Tg && !(excl && gid == q_off + qo);
@@ -2579,6 +2594,9 @@ static int knn_x1(const float *Q, int64_t nq, const float *C, int64_t nc, int32_
                                                 : ksw2::k_gram_sweep2<1, ksw2::SW_SYM, true, true>;
             // MN_SWEEP=3: gram_sweep3.hpp's schedule (PROBE noepi: K loop only)
             if (sweep_gen == 4 && probe && *probe) sk = ksw2::k_gram_sweep3<1, ksw2::SW_SYM, 2>;
+            if (sweep_gen == 5)  // two windows per k-step and group
+                sk = (probe && *probe) ? ksw2::k_gram_sweep3<1, ksw2::SW_SYM, 2, 2>
+                                       : ksw2::k_gram_sweep3<0, ksw2::SW_SYM, 2, 2>;
             if (sweep_gen == 3)  // DMA three k-steps ahead
                 sk = !(probe && *probe)          ? ksw2::k_gram_sweep3<0, ksw2::SW_SYM>
                      : !strcmp(probe, "initonly") ? ksw2::k_gram_sweep3<2, ksw2::SW_SYM>
@@ -2704,7 +2722,9 @@ static int knn_x1(const float *Q, int64_t nq, const float *C, int64_t nc, int32_
     // instead of the exact scan, whose cost is O(nc d) per row.  No x1 buffer
     // (phase-1 / sweep lists, sample) is read after this point; perm, chc and
     // ubv stay live.
-    if (nfb > 256) {
+    // tuning build: MN_X1_NOREFILL=1 sends every uncertified row to the exact
+    // scan (diagnostics of the refill)
+    if (nfb > 256 && !knob_int("MN_X1_NOREFILL", 0)) {
         Timer te;
         te.start(true, s);
         const int nkb3 = 3 * nkb;
