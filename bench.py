@@ -190,7 +190,7 @@ def main():
         if sym:  # fp16 operands (x 2^e): the release library's only SW_SYM form
             kname = "k_gram_sweep3<SW_SYM>"
             # (round 6: gram_sweep3.hpp, DMA two k-steps ahead)
-            kfull = "k_gram_sweep3<0, 2, 2>"
+            kfull = "k_gram_sweep3<0, 2, 2, 1, 0>"
         flops_launch = 2.0 * nq * nc_sw * d
         # executed: the upper-triangle 256 x 256 tiles of the n_tot rows, a
         # rank's 1/world share of them (the sharded symmetric form)

@@ -473,12 +473,18 @@ __global__ __launch_bounds__(NT) void k_gram_sweep3(
     uint32_t so = 0;  // ring slot of the current k-step (bytes)
     int par = 0;
     float hcn = 0.f, tcn = 0.f, scn = 1.f;  // next tile's folds (waves 0-3)
+    // the k-steps of a tile that carry extra work, as one compare each (the
+    // conditions folded per tile: ~45 -> ~30 SALU a k-step and wave)
+    const bool lead = wc == 0, trail = wc == 1;
     for (int ti = 0; ti < ntile; ++ti) {
         const int c0 = cbeg + ti * cstr;
         const bool more = ti + 1 < ntile;
+        const int k_chk = ti > 0 ? 0 : -1;                    // the previous tile's epilogue
+        const int k_ld = (more && lead) ? nkb - 4 : -1;        // the next tile's fold loads
+        const int k_st = (more && lead) ? nkb - 2 : -1;        //   and their stores
         for (int kb = 0; kb < nkb; ++kb) {
             // ================= READ window =================
-            if (wc == 0 && kb == nkb - 4 && more) {
+            if (kb == k_ld) {
                 // the next tile's off-diagonal folds: one value per lane, asm
                 // loads older than the DMA issued below (the counted waits
                 // retire them 2 k-steps before the store)
@@ -488,7 +494,7 @@ __global__ __launch_bounds__(NT) void k_gram_sweep3(
                 if constexpr (F16)
                     asm volatile("global_load_dword %0, %1, off" : "=v"(scn) : "v"(sym.scale + cn) : "memory");
             }
-            if (kb == 0 && ti > 0) {
+            if (kb == k_chk) {
                 check(c0 - cstr, par ^ 1, diag0 && ti == 1);
                 if constexpr (INIT) init_acc(par, false);
             }
@@ -538,7 +544,7 @@ __global__ __launch_bounds__(NT) void k_gram_sweep3(
             __builtin_amdgcn_sched_barrier(0);
             issue();  // k-step + AHEAD, behind the reads
             __builtin_amdgcn_sched_barrier(0);
-            if (kb == nkb - 2 && more && wc == 0) {
+            if (kb == k_st) {
                 const int cb = c0 + cstr + 64 * wq + lane;
                 sm.hc[par ^ 1][64 * wq + lane] = cb < cend ? hcn : pad;
                 sm.tc[par ^ 1][64 * wq + lane] = cb < cend ? tcn : pad;
@@ -546,7 +552,7 @@ __global__ __launch_bounds__(NT) void k_gram_sweep3(
             }
             if constexpr (AHEAD == 3) lgkm_wait();
             // trailing group: its k-step + 1 landed before the barrier
-            if (wc == 1) vm_wait();
+            if (trail) vm_wait();
             __builtin_amdgcn_sched_barrier(0);
             __builtin_amdgcn_s_barrier();
             __builtin_amdgcn_sched_barrier(0);
@@ -559,7 +565,7 @@ __global__ __launch_bounds__(NT) void k_gram_sweep3(
             mfmas(0, WCF);
             __builtin_amdgcn_s_setprio(0);
             __builtin_amdgcn_sched_barrier(0);
-            if (wc == 0) vm_wait();
+            if (lead) vm_wait();
             __builtin_amdgcn_s_barrier();
             __builtin_amdgcn_sched_barrier(0);
             so = (so + (uint32_t)(BC * KB * 2)) & (uint32_t)(NSLOT * BC * KB * 2 - 1);

@@ -206,8 +206,12 @@ template <typename T>
 __global__ __launch_bounds__(256) void k_gram_f64(const T *__restrict__ X, int64_t n, int f,
                                                   int ntile, int64_t kchunk, int nchunk,
                                                   double *__restrict__ G) {
-    __shared__ T As[GK][GT + 4];
-    __shared__ T Bs[GK][GT + 4];
+    // rows GT + 16 apart (round 6; was GT + 4): the fragment reads take 16
+    // consecutive columns of four rows, and a row stride of 16 (mod 32)
+    // words for f32 / 32 (mod 64) for f64 puts a lane group's rows on
+    // disjoint banks (GT + 4: 3.2 bank-conflict cycles per LDS instruction)
+    __shared__ T As[GK][GT + 16];
+    __shared__ T Bs[GK][GT + 16];
     // blockIdx.x = chunk-major over upper-triangle tiles (concurrent blocks share rows)
     const int ntri = ntile * (ntile + 1) / 2;
     const int chunk = blockIdx.x / ntri;
@@ -575,6 +579,39 @@ __global__ __launch_bounds__(256) void k_cos_exact_wave(const T *__restrict__ XT
 // PFD chunks of both profiles are in flight (one wave a CU).
 constexpr int CQ = 64;        // chunk (elements of one profile)
 constexpr int CQP = CQ + 2;   // chain buffer stride in doubles (528 B)
+// Round 6 (LPC 8): a lane's EPL = 8 products were written as four 16-B
+// pieces 64 B apart per lane — in a ds_write_b128 lane group (8 lanes, banks
+// (a / 4) mod 32) lanes gl and gl + 2 hit the same banks: 4-way conflicts
+// (SQ_LDS_BANK_CONFLICT 4.8 cycles per LDS instruction, profiles/r05_legs).
+// Segments of 8 products are now 10 doubles apart (80 B: the 8 lanes' pieces
+// of one store cover all 32 banks) and chain buffers 84 doubles apart (672 B:
+// the four chains of a ds_read_b128 lane group read distinct 16-B slots).
+constexpr int CQS = 10;               // segment stride (8 products + 2 pad)
+constexpr int CQP8 = 8 * CQS + 4;     // chain buffer stride, LPC 8 (672 B)
+
+// The ordered fold over one chunk in the segmented layout (element e at
+// b[(e / 8) CQS + e % 8]): lds_chain_f64<64> with the segment gaps skipped.
+__device__ __forceinline__ double lds_chain_f64_seg(double acc, const double *b) {
+    const double2 *b2 = reinterpret_cast<const double2 *>(b);
+    double2 v[2][16];
+    // batch bt = elements 32 bt .. 32 bt + 31 = segments 4 bt .. 4 bt + 3
+#pragma unroll
+    for (int q = 0; q < 16; ++q) v[0][q] = b2[(q >> 2) * (CQS / 2) + (q & 3)];
+    __builtin_amdgcn_sched_group_barrier(0x100, 16, 0);
+#pragma unroll
+    for (int q = 0; q < 16; ++q) v[1][q] = b2[(4 + (q >> 2)) * (CQS / 2) + (q & 3)];
+    __builtin_amdgcn_sched_group_barrier(0x100, 16, 0);
+#pragma unroll
+    for (int bt = 0; bt < 2; ++bt) {
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+            acc = acc + v[bt][q].x;
+            acc = acc + v[bt][q].y;
+        }
+        __builtin_amdgcn_sched_group_barrier(0x002, 32, 0);
+    }
+    return acc;
+}
 // RAW (round 5): the chains of the listed pairs write their raw dot into
 // dist[slot] (k_cos_dist turns it into the distance once the norms exist) and
 // fnorm more chains follow the np listed ones: chain np + c folds column c
@@ -610,7 +647,8 @@ __global__ __launch_bounds__(64) void k_cos_exact_q(const T *__restrict__ XT, in
                                                     int fnorm, double *__restrict__ nrm,
                                                     double *__restrict__ dist) {
     constexpr int CPW = 64 / LPC, EPL = CQ / LPC;
-    __shared__ __attribute__((aligned(16))) double buf[2][CPW][CQP];
+    constexpr bool SEG = LPC == 8;  // the segmented, conflict-free layout
+    __shared__ __attribute__((aligned(16))) double buf[2][CPW][SEG ? CQP8 : CQP];
     const int lane = threadIdx.x & 63, g = lane / LPC, gl = lane % LPC;
     const int64_t np = pcount ? (int64_t)*pcount : pmax;
     const int64_t wq = (int64_t)blockIdx.x * CPW;
@@ -652,7 +690,7 @@ __global__ __launch_bounds__(64) void k_cos_exact_q(const T *__restrict__ XT, in
     do {                                                                                 \
         double *bb_ = buf[(H) & 1][g];                                                   \
         _Pragma("unroll") for (int u = 0; u < EPL; u += 2)                              \
-            *reinterpret_cast<double2 *>(bb_ + EPL * gl + u) =                           \
+            *reinterpret_cast<double2 *>(bb_ + (SEG ? CQS : EPL) * gl + u) =             \
                 make_double2((double)ra[H][u] * (double)rb[H][u],                        \
                              (double)ra[H][u + 1] * (double)rb[H][u + 1]);               \
     } while (0)
@@ -667,7 +705,8 @@ __global__ __launch_bounds__(64) void k_cos_exact_q(const T *__restrict__ XT, in
                 MN_QCHUNK(h);
                 MN_QFETCH(min(c0 + h + PFD, nfull - 1), h);
                 __builtin_amdgcn_wave_barrier();
-                acc = lds_chain_f64<CQ>(acc, buf[h & 1][g]);
+                if constexpr (SEG) acc = lds_chain_f64_seg(acc, buf[h & 1][g]);
+                else acc = lds_chain_f64<CQ>(acc, buf[h & 1][g]);
                 __builtin_amdgcn_wave_barrier();
             }
         }
@@ -677,7 +716,8 @@ __global__ __launch_bounds__(64) void k_cos_exact_q(const T *__restrict__ XT, in
             if (h < rem) {
                 MN_QCHUNK(h);
                 __builtin_amdgcn_wave_barrier();
-                acc = lds_chain_f64<CQ>(acc, buf[h & 1][g]);
+                if constexpr (SEG) acc = lds_chain_f64_seg(acc, buf[h & 1][g]);
+                else acc = lds_chain_f64<CQ>(acc, buf[h & 1][g]);
                 __builtin_amdgcn_wave_barrier();
             }
         }

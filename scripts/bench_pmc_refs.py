@@ -26,7 +26,7 @@ def pick(prefix):
 
 # the energy pass is one kernel since round 4 (k_energy_rows3: the tau select
 # inline, X streamed once); a list of prefixes is summed per call
-for fname, prefixes, extra in (("bench_pmc_gram.json", ("k_gram_sweep2<0, 2, true",), {"rows_per_gpu": n}),
+for fname, prefixes, extra in (("bench_pmc_gram.json", ("k_gram_sweep3<0, 2, 2, 1, 0>",), {"rows_per_gpu": n}),
                                ("bench_pmc_energy.json", ("k_energy_rows3",), {"rows": n})):
     kk = [pick(p) for p in prefixes]
     if not all(kk) or any("fetch_bytes" not in ks[k] or "write_bytes" not in ks[k] for k in kk):

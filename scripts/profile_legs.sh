@@ -11,7 +11,7 @@ OUT=$ROOT/gpurun_out/legs_$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 cd /tmp || exit 1
-ARGS=(--cpu-seconds 0 --warmup 0 --steps 1 "$@")
+ARGS=(--cpu-seconds 0 --warmup 0 --steps 1 --no-c4-sim "$@")
 run() {  # name, rocprofv3 options...
     local name=$1; shift
     timeout -k 10 300 rocprofv3 "$@" --output-format csv -d "$OUT/$name" -o run -- \
