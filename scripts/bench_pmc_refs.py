@@ -38,5 +38,10 @@ for fname, prefixes, extra in (("bench_pmc_gram.json", ("k_gram_sweep3<0, 2, 2, 
            "kernel_full": " + ".join(kk), "avg_ms": sum(ks[k]["avg_ms"] for k in kk),
            "fetch_bytes_per_launch": fb, "write_bytes_per_launch": wb,
            "hbm_bytes_per_launch": fb + wb, "source": src, **extra}
+    k0 = ks[kk[0]]
+    if k0.get("mfma_busy") is not None and len(kk) == 1:
+        out["mfma_busy"] = k0["mfma_busy"]
+        if k0.get("SQ_INSTS_MFMA"):
+            out["salu_per_mfma"] = round(k0["SQ_INSTS_SALU"] / k0["SQ_INSTS_MFMA"], 3)
     json.dump(out, open(os.path.join(ROOT, fname), "w"), indent=1)
     print(fname, json.dumps({kk: out[kk] for kk in ("kernel", "avg_ms", "hbm_bytes_per_launch")}))
