@@ -2,7 +2,9 @@
 // x 2^e operands; SW_COS_SYM: C5's bf16 cosine item graph) re-scheduled for
 // instruction issue.  Same contract, block table, LDS layout, ring protocol
 // and ping-pong as gram_sweep2.hpp's k_gram_sweep2<0, SW_SYM / SW_COS_SYM,
-// TM>; the outputs are identical bit for bit.  What changed (round 6):
+// TM>; the outputs are identical bit for bit.  The query-major modes SW_L2 /
+// SW_COS run the phase-1 sample sweeps of C2 and C5 (per-(row, slice)
+// buffers through global counters).  What changed (round 6):
 //
 //  * The read window's SALU.  sweep2 rebuilt two buffer descriptors per
 //    k-step, walked a branch tree per window to pick vmcnt(8 / 4 / 0) and a
@@ -65,11 +67,18 @@ template <int PROBE, int MODE, int AHEAD = 3, int PH = 1, int EMI = 0>
 __global__ __launch_bounds__(NT) void k_gram_sweep3(
     const uint16_t *__restrict__ Qk, int64_t nq, const uint16_t *__restrict__ Ck, int64_t nc,
     int nkb, int64_t q_off, int64_t c_off, int excl, const float *__restrict__ tq,
-    const float *__restrict__ tau0, const float *__restrict__ hc, int64_t, int, int64_t, int cap,
-    uint2 *__restrict__ buf, int *__restrict__ cnt, int pst, SymArgs sym) {
-    static_assert(MODE == SW_SYM || MODE == SW_COS_SYM, "k_gram_sweep3: symmetric modes only");
+    const float *__restrict__ tau0, const float *__restrict__ hc, int64_t c_begin, int S,
+    int64_t chunk, int cap, uint2 *__restrict__ buf, int *__restrict__ cnt, int pst, SymArgs sym) {
+    // QM (round 6): the query-major sweeps SW_L2 / SW_COS (the phase-1 sample
+    // sweeps of C2 and C5): block v takes query panel v / S against slice
+    // v % S ([c_begin + sl chunk, + chunk)), bf16 operands, the row's own
+    // test only; candidates go to buf[(q S + sl) cap + pos] through global
+    // counters cnt[q S + sl] (a count past cap = overflow; the callers'
+    // selects read it as a full buffer)
+    constexpr bool QM = MODE == SW_L2 || MODE == SW_COS;
     constexpr bool F16 = MODE == SW_SYM;     // fp16 x 2^e operands, per-row scales
-    constexpr bool COSM = MODE == SW_COS_SYM;
+    constexpr bool COSM = MODE == SW_COS_SYM || MODE == SW_COS;
+    static_assert(!(QM && EMI == 1), "k_gram_sweep3: EMI 1 marks symmetric rows only");
     // PROBE (tuning build, results invalid): 1 = K loop only (no check, no
     // init), 2 = init only, 3 = init + prefilter (no emission)
     constexpr bool EPI = PROBE == 0 || PROBE == 3;
@@ -81,22 +90,38 @@ __global__ __launch_bounds__(NT) void k_gram_sweep3(
     const int wq = w & 3, wc = w >> 2;
     const int fr = lane & 15, fk = lane >> 4;
     const int v = xcd_remap((int)blockIdx.x, (int)gridDim.x);
-    const int4 te = sym.tab[v];
-    const int q0 = te.x * BQ, cbeg = te.y * BC, cend = (int)nc, ntile = te.z, cstr = te.w * BC;
-    const float pad = COSM ? __builtin_nanf("") : -__builtin_inff();
-    const bool diag0 = cbeg == q0;
+    int q0, sl = 0, cbeg, cend, ntile, cstr;
+    if constexpr (QM) {
+        q0 = (v / S) * BQ;
+        sl = v % S;
+        cbeg = (int)(c_begin + (int64_t)sl * chunk);
+        cend = (int)min(nc, (int64_t)cbeg + chunk);
+        ntile = cend > cbeg ? (cend - cbeg + BC - 1) / BC : 0;
+        cstr = BC;
+    } else {
+        const int4 te = sym.tab[v];
+        q0 = te.x * BQ;
+        cbeg = te.y * BC;
+        cend = (int)nc;
+        ntile = te.z;
+        cstr = te.w * BC;
+    }
+    // padding columns never qualify: COS NaN, SW_L2 +inf (acc0 = tq - inf),
+    // SW_SYM -inf (the fold is added)
+    const float pad = COSM ? __builtin_nanf("") : (QM ? __builtin_inff() : -__builtin_inff());
+    const bool diag0 = !QM && cbeg == q0;
     if (ntile == 0) return;  // the per-XCD padding entries of the table (block-uniform)
 
     if (tid < BQ) {
         sm.tq[tid] = q0 + tid < nq ? tq[q0 + tid] : (COSM ? pad : -__builtin_inff());
         sm.t0[tid] = q0 + tid < nq ? tau0[q0 + tid] : 0.f;
-        sm.ta[tid] = q0 + tid < nq ? sym.aoff[q0 + tid] : (COSM ? pad : -__builtin_inff());
+        if constexpr (!QM) sm.ta[tid] = q0 + tid < nq ? sym.aoff[q0 + tid] : (COSM ? pad : -__builtin_inff());
         if constexpr (F16) sm.sq[tid] = q0 + tid < nq ? sym.scale[q0 + tid] : 1.f;
     }
     if (ntile > 0 && tid < BC) {
         const int c = cbeg + tid;
-        sm.hc[0][tid] = (c < cend) ? (diag0 ? hc[c] : sym.hoff[c]) : pad;
-        sm.tc[0][tid] = (c < cend) ? tau0[c] : pad;
+        sm.hc[0][tid] = (c < cend) ? ((QM || diag0) ? hc[c] : sym.hoff[c]) : pad;
+        if constexpr (!QM) sm.tc[0][tid] = (c < cend) ? tau0[c] : pad;
         if constexpr (F16) sm.sc[0][tid] = (c < cend) ? sym.scale[c] : 1.f;
     }
 
@@ -164,7 +189,7 @@ __global__ __launch_bounds__(NT) void k_gram_sweep3(
     frag_t fq[WQF], fc[WCF];
     auto init_acc = [&](int par, bool diag) __attribute__((always_inline)) {
         float tql[WQF];
-        const float *qa = diag ? sm.tq : sm.ta;
+        const float *qa = (QM || diag) ? sm.tq : sm.ta;
 #pragma unroll
         for (int f = 0; f < WQF; ++f) tql[f] = qa[64 * wq + 16 * f + fr];
         float sql[WQF];
@@ -185,11 +210,16 @@ __global__ __launch_bounds__(NT) void k_gram_sweep3(
                     acc[f][g][1] = __builtin_fmaf(tql[f], sc4.y, x.y * sql[f]);
                     acc[f][g][2] = __builtin_fmaf(tql[f], sc4.z, x.z * sql[f]);
                     acc[f][g][3] = __builtin_fmaf(tql[f], sc4.w, x.w * sql[f]);
-                } else {
+                } else if constexpr (COSM) {
                     acc[f][g][0] = tql[f] * x.x;
                     acc[f][g][1] = tql[f] * x.y;
                     acc[f][g][2] = tql[f] * x.z;
                     acc[f][g][3] = tql[f] * x.w;
+                } else {  // SW_L2: acc0 = tq(q) - hc(c)
+                    acc[f][g][0] = tql[f] - x.x;
+                    acc[f][g][1] = tql[f] - x.y;
+                    acc[f][g][2] = tql[f] - x.z;
+                    acc[f][g][3] = tql[f] - x.w;
                 }
             }
         }
@@ -254,6 +284,26 @@ __global__ __launch_bounds__(NT) void k_gram_sweep3(
         const unsigned pm = valid ? (cw >> 28) : 0u;
         const int ql = q - (int)q_off - q0;
         float colv[4], cols[4];
+        if constexpr (QM) {  // the row's own test: one candidate per register
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const bool h = (pm >> r) & 1u;
+                float key;
+                if constexpr (COSM) {  // hc = -|c|: key = -acc / |c|
+                    const int cc = min(c + r - (int)c_off, (int)nc - 1);
+                    key = a4[r] / (h ? hc[cc] : 1.f);
+                } else {
+                    key = sm.t0[ql] - 2.f * a4[r];
+                }
+                go[2 * r] = h;
+                rw[2 * r] = h ? (uint32_t)(ql + q0) * (uint32_t)S + (uint32_t)sl : 0u;
+                kv[2 * r] = make_uint2(__float_as_uint(key), (uint32_t)(c + r));
+                go[2 * r + 1] = false;
+                rw[2 * r + 1] = 0u;
+                kv[2 * r + 1] = make_uint2(0u, 0u);
+            }
+            return;
+        }
 #pragma unroll
         for (int r = 0; r < 4; ++r) {  // the columns' values (global: the tile may be gone)
             const int cc = min(c + r - (int)c_off, (int)nc - 1);
@@ -489,8 +539,9 @@ __global__ __launch_bounds__(NT) void k_gram_sweep3(
                 // loads older than the DMA issued below (the counted waits
                 // retire them 2 k-steps before the store)
                 const int cn = min(c0 + cstr + 64 * wq + lane, (int)nc - 1);
-                asm volatile("global_load_dword %0, %1, off" : "=v"(hcn) : "v"(sym.hoff + cn) : "memory");
-                asm volatile("global_load_dword %0, %1, off" : "=v"(tcn) : "v"(tau0 + cn) : "memory");
+                asm volatile("global_load_dword %0, %1, off" : "=v"(hcn) : "v"((QM ? hc : sym.hoff) + cn) : "memory");
+                if constexpr (!QM)
+                    asm volatile("global_load_dword %0, %1, off" : "=v"(tcn) : "v"(tau0 + cn) : "memory");
                 if constexpr (F16)
                     asm volatile("global_load_dword %0, %1, off" : "=v"(scn) : "v"(sym.scale + cn) : "memory");
             }

@@ -882,10 +882,16 @@ static int cos_sweep_phase1(const uint16_t *X, int64_t n, int32_t d, int dp, int
     MN_REQUIRE(cbuf && cnt, MN_ENOMEM, "mn_knn_cos_bf16: phase-1 sweep buffer allocation failed");
     MN_HIP_TRY(hipMemsetAsync(cnt, 0, (size_t)n * 4, s));
     const int64_t nqb = (n + ksw2::BQ - 1) / ksw2::BQ;
-    hipLaunchKernelGGL((ksw2::k_gram_sweep2<0, ksw2::SW_COS, true>), dim3((unsigned)nqb), dim3(ksw2::NT),
-                       0, s, XK, n, XK, m0, nkb, (int64_t)0, (int64_t)0, 0, tq_pos, tq_pos, negn,
-                       (int64_t)0, 1, m0, cap, cbuf, cnt, pst, ksw2::SymArgs{});
-    MN_KCHECK(s, "k_gram_sweep2<COS> (phase 1)");
+    // round 6: gram_sweep3.hpp's query-major mode (tuning build
+    // MN_P1_SWEEP3=0: round 5's sweep2)
+    auto p1k = ksw2::k_gram_sweep3<0, ksw2::SW_COS, 2>;
+#ifdef MN_TUNING
+    if (!knob_int("MN_P1_SWEEP3", 1)) p1k = ksw2::k_gram_sweep2<0, ksw2::SW_COS, true>;
+#endif
+    hipLaunchKernelGGL(p1k, dim3((unsigned)nqb), dim3(ksw2::NT), 0, s, XK, n, XK, m0, nkb, (int64_t)0,
+                       (int64_t)0, 0, tq_pos, tq_pos, negn, (int64_t)0, 1, m0, cap, cbuf, cnt, pst,
+                       ksw2::SymArgs{});
+    MN_KCHECK(s, "k_gram_sweep3<COS> (phase 1)");
     // (c) the L1-th smallest key per position
     MN_HIP_TRY(hipMemsetAsync(cntr, 0, 4, s));
     const unsigned g4 = (unsigned)((n + 3) / 4);

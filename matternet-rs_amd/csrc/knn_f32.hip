@@ -2251,10 +2251,16 @@ static int sweep_phase1(const uint16_t *QR, const uint16_t *QK, int64_t nq, cons
     MN_HIP_TRY(hipMemsetAsync(cnt, 0, (size_t)nq * 4, s));
     const int64_t nqb = (nq + ksw2::BQ - 1) / ksw2::BQ;
     MN_REQUIRE(nqb < INT_MAX && nq * 32 < INT_MAX, MN_ENOTSUP, "mn_knn: phase-1 sweep grid too large");
-    hipLaunchKernelGGL((ksw2::k_gram_sweep2<0, ksw2::SW_L2, true>), dim3((unsigned)nqb),
-                       dim3(ksw2::NT), 0, s, QK, nq, CKs, m0, nkb, q_off, (int64_t)0, 0, tq, tau0, chc,
-                       (int64_t)0, 1, m0, cap, cbuf, cnt, pst1, ksw2::SymArgs{});
-    MN_KCHECK(s, "k_gram_sweep2<SW_L2, phase 1>");
+    // round 6: gram_sweep3.hpp's schedule in its query-major mode (global
+    // per-row counters; tuning build MN_P1_SWEEP3=0: round 5's sweep2)
+    auto p1k = ksw2::k_gram_sweep3<0, ksw2::SW_L2, 2>;
+#ifdef MN_TUNING
+    if (!knob_int("MN_P1_SWEEP3", 1)) p1k = ksw2::k_gram_sweep2<0, ksw2::SW_L2, true>;
+#endif
+    hipLaunchKernelGGL(p1k, dim3((unsigned)nqb), dim3(ksw2::NT), 0, s, QK, nq, CKs, m0, nkb, q_off,
+                       (int64_t)0, 0, tq, tau0, chc, (int64_t)0, 1, m0, cap, cbuf, cnt, pst1,
+                       ksw2::SymArgs{});
+    MN_KCHECK(s, "k_gram_sweep3<SW_L2, phase 1>");
     tdb.mark();
     // (c) the L1-th smallest buffered key per row
     MN_HIP_TRY(hipMemsetAsync(cntr, 0, 4, s));
