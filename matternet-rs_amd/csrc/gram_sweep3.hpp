@@ -81,8 +81,11 @@ __global__ __launch_bounds__(NT) void k_gram_sweep3(
     static_assert(!(QM && EMI == 1), "k_gram_sweep3: EMI 1 marks symmetric rows only");
     // PROBE (tuning build, results invalid): 1 = K loop only (no check, no
     // init), 2 = init only, 3 = init + prefilter (no emission)
+    // 4 / 5 / 6 = K loop only and also without the in-loop LDS-DMA issue /
+    // the in-loop barriers / the fragment reads (timing only)
     constexpr bool EPI = PROBE == 0 || PROBE == 3;
-    constexpr bool INIT = PROBE != 1;
+    constexpr bool INIT = PROBE == 0 || PROBE == 2 || PROBE == 3;
+    constexpr bool NODMA = PROBE == 4, NOBAR = PROBE == 5, NOREAD = PROBE == 6;
     __shared__ Ring rg;
     __shared__ Smem3 sm;
     const int tid = threadIdx.x, lane = tid & 63;
@@ -518,7 +521,7 @@ __global__ __launch_bounds__(NT) void k_gram_sweep3(
     vm_wait();
     __syncthreads();  // also publishes sm.hc[0], t0, tq
     init_acc(0, diag0);
-    if (wc == 1) __builtin_amdgcn_s_barrier();  // the trailing group starts one window late
+    if (wc == 1 && !NOBAR) __builtin_amdgcn_s_barrier();  // the trailing group starts one window late
 
     uint32_t so = 0;  // ring slot of the current k-step (bytes)
     int par = 0;
@@ -591,9 +594,9 @@ __global__ __launch_bounds__(NT) void k_gram_sweep3(
                 so = (so + (uint32_t)(BC * KB * 2)) & (uint32_t)(NSLOT * BC * KB * 2 - 1);
                 continue;
             }
-            read_frags(so);
+            if constexpr (!NOREAD) read_frags(so);
             __builtin_amdgcn_sched_barrier(0);
-            issue();  // k-step + AHEAD, behind the reads
+            if constexpr (!NODMA) issue();  // k-step + AHEAD, behind the reads
             __builtin_amdgcn_sched_barrier(0);
             if (kb == k_st) {
                 const int cb = c0 + cstr + 64 * wq + lane;
@@ -601,14 +604,14 @@ __global__ __launch_bounds__(NT) void k_gram_sweep3(
                 sm.tc[par ^ 1][64 * wq + lane] = cb < cend ? tcn : pad;
                 if constexpr (F16) sm.sc[par ^ 1][64 * wq + lane] = cb < cend ? scn : 1.f;
             }
-            if constexpr (AHEAD == 3) lgkm_wait();
+            if constexpr (AHEAD == 3 && !NOREAD) lgkm_wait();
             // trailing group: its k-step + 1 landed before the barrier
-            if (trail) vm_wait();
+            if (trail && !NODMA) vm_wait();
             __builtin_amdgcn_sched_barrier(0);
-            __builtin_amdgcn_s_barrier();
+            if constexpr (!NOBAR) __builtin_amdgcn_s_barrier();
             __builtin_amdgcn_sched_barrier(0);
             // ================= MFMA window =================
-            if constexpr (AHEAD == 2) {
+            if constexpr (AHEAD == 2 && !NOREAD) {
                 lgkm_wait();
                 __builtin_amdgcn_sched_barrier(0);
             }
@@ -616,14 +619,14 @@ __global__ __launch_bounds__(NT) void k_gram_sweep3(
             mfmas(0, WCF);
             __builtin_amdgcn_s_setprio(0);
             __builtin_amdgcn_sched_barrier(0);
-            if (lead) vm_wait();
-            __builtin_amdgcn_s_barrier();
+            if (lead && !NODMA) vm_wait();
+            if constexpr (!NOBAR) __builtin_amdgcn_s_barrier();
             __builtin_amdgcn_sched_barrier(0);
             so = (so + (uint32_t)(BC * KB * 2)) & (uint32_t)(NSLOT * BC * KB * 2 - 1);
         }
         par ^= 1;
     }
-    if (wc == 0) __builtin_amdgcn_s_barrier();  // match the trailing group's extra window
+    if (wc == 0 && !NOBAR) __builtin_amdgcn_s_barrier();  // match the trailing group's extra window
     if (ntile > 0) check(cbeg + (ntile - 1) * cstr, par ^ 1, diag0 && ntile == 1);
     if (ns > 0) flush();
     // the re-staged pieces past the last k-step land before the LDS is released

@@ -2599,7 +2599,11 @@ static int knn_x1(const float *Q, int64_t nq, const float *C, int64_t nc, int32_
                      : !strcmp(probe, "l2res_noepi") ? ksw2::k_gram_sweep2<6, ksw2::SW_SYM, true, true>
                                                 : ksw2::k_gram_sweep2<1, ksw2::SW_SYM, true, true>;
             // MN_SWEEP=3: gram_sweep3.hpp's schedule (PROBE noepi: K loop only)
-            if (sweep_gen == 4 && probe && *probe) sk = ksw2::k_gram_sweep3<1, ksw2::SW_SYM, 2>;
+            if (sweep_gen == 4 && probe && *probe)
+                sk = !strcmp(probe, "nodma")    ? ksw2::k_gram_sweep3<4, ksw2::SW_SYM, 2>
+                     : !strcmp(probe, "nobar")  ? ksw2::k_gram_sweep3<5, ksw2::SW_SYM, 2>
+                     : !strcmp(probe, "noread") ? ksw2::k_gram_sweep3<6, ksw2::SW_SYM, 2>
+                                                : ksw2::k_gram_sweep3<1, ksw2::SW_SYM, 2>;
             if (sweep_gen == 5)  // two windows per k-step and group
                 sk = (probe && *probe) ? ksw2::k_gram_sweep3<1, ksw2::SW_SYM, 2, 2>
                                        : ksw2::k_gram_sweep3<0, ksw2::SW_SYM, 2, 2>;
