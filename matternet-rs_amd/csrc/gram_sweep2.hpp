@@ -30,6 +30,7 @@
 //    wave's READ window, beside its partner's MFMAs.
 #pragma once
 #include <algorithm>
+#include <array>
 #include <climits>
 #include <type_traits>
 #include <vector>
@@ -860,6 +861,52 @@ inline std::vector<int4> sym_block_table(int nbk, int TPB, int order, int gr = 4
             tab.push_back(make_int4(I, J0, std::min(J0 + TPB, nbk) - J0, 1));
     std::stable_sort(tab.begin(), tab.end(), [](const int4 &a, const int4 &b) { return a.z > b.z; });
     return tab;
+}
+
+// The block table is a pure function of (nbk, TPB, order, group shape,
+// rank, world): built once per thread and shape (the build is ~17 ms of host
+// time at C2, during which the device idles) and uploaded into kSlotSymTab
+// only when that slot does not already hold it.  Returns the table; *dtab the
+// device copy (nullptr on an allocation failure).
+inline const std::vector<int4> &sym_table_device(int nbk, int TPB, int order, int gr, int rank,
+                                                 int world, hipStream_t s, int4 **dtab) {
+    struct Entry {
+        std::array<int, 6> key;
+        std::vector<int4> tab;
+    };
+    thread_local std::vector<Entry> cache;
+    struct Up {
+        int dev = -1;
+        void *p = nullptr;
+        std::array<int, 6> key{};
+        bool valid = false;
+    };
+    thread_local Up last;
+    const std::array<int, 6> key{nbk, TPB, order, gr, rank, world};
+    const std::vector<int4> *tp = nullptr;
+    for (const Entry &e : cache)
+        if (e.key == key) tp = &e.tab;
+    if (!tp) {
+        if (cache.size() >= 8) cache.erase(cache.begin());
+        std::vector<int4> t = (order == 2 || world > 1) ? sym_block_table_share(nbk, TPB, rank, world, gr)
+                                                        : sym_block_table(nbk, TPB, order, gr);
+        cache.push_back(Entry{key, std::move(t)});
+        tp = &cache.back().tab;
+    }
+    *dtab = (int4 *)scratch(kSlotSymTab, tp->size() * sizeof(int4) + 64);
+    int dev = -1;
+    (void)hipGetDevice(&dev);
+    if (!*dtab) return *tp;
+    if (!(last.valid && last.p == (void *)*dtab && last.key == key && last.dev == dev)) {
+        if (hipMemcpyAsync(*dtab, tp->data(), tp->size() * sizeof(int4), hipMemcpyHostToDevice, s) !=
+            hipSuccess) {
+            last.valid = false;
+            *dtab = nullptr;
+            return *tp;
+        }
+        last = Up{dev, (void *)*dtab, key, true};
+    }
+    return *tp;
 }
 
 }  // namespace ksw2

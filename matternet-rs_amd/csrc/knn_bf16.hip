@@ -1082,11 +1082,10 @@ static int knn_cos_bf16_x1(const uint16_t *X, int64_t n, int32_t d, const mn_cos
     MN_REQUIRE(buf2 && cnt2, MN_ENOMEM, "mn_knn_cos_bf16: sweep buffer allocation failed");
     if (sym) {
         const int nbk = (int)((n + ksw2::BC - 1) / ksw2::BC);
-        const std::vector<int4> tab = ksw2::sym_block_table(nbk, 256, knob_int("MN_BF16_SYM_ORDER", 2));
-        int4 *dtab = (int4 *)scratch(kSlotSymTab, tab.size() * sizeof(int4) + 64);
-        MN_REQUIRE(dtab, MN_ENOMEM, "mn_knn_cos_bf16: block table allocation failed");
-        MN_HIP_TRY(hipMemcpyAsync(dtab, tab.data(), tab.size() * sizeof(int4),
-                                  hipMemcpyHostToDevice, s));
+        int4 *dtab = nullptr;
+        const std::vector<int4> &tab =
+            ksw2::sym_table_device(nbk, 256, knob_int("MN_BF16_SYM_ORDER", 2), 4, 0, 1, s, &dtab);
+        MN_REQUIRE(dtab, MN_ENOMEM, "mn_knn_cos_bf16: block table allocation / upload failed");
         MN_HIP_TRY(hipMemsetAsync(cnt2, 0, (size_t)n * 4, s));
         MN_REQUIRE(tab.size() < INT_MAX, MN_ENOTSUP, "mn_knn_cos_bf16: sweep grid too large");
         // the default: gram_sweep3.hpp's schedule, DMA two k-steps ahead

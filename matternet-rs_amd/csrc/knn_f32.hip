@@ -2541,12 +2541,10 @@ static int knn_x1(const float *Q, int64_t nq, const float *C, int64_t nc, int32_
             const char *ore = knob("MN_SYM_ORDER");
             const int order = (ore && *ore) ? atoi(ore) : 2;
             // 2 x 16 groups (tuning build: MN_SYM_GSHAPE = rows of a 32-block group)
-            const std::vector<int4> tab =
-                ksw2::sym_block_table(nbk, TPB, order, knob_int("MN_SYM_GSHAPE", 2));
-            int4 *dtab = (int4 *)scratch(kSlotSymTab, tab.size() * sizeof(int4) + 64);
-            MN_REQUIRE(dtab, MN_ENOMEM, "mn_knn: block table allocation failed");
-            MN_HIP_TRY(hipMemcpyAsync(dtab, tab.data(), tab.size() * sizeof(int4),
-                                      hipMemcpyHostToDevice, s));
+            int4 *dtab = nullptr;
+            const std::vector<int4> &tab =
+                ksw2::sym_table_device(nbk, TPB, order, knob_int("MN_SYM_GSHAPE", 2), 0, 1, s, &dtab);
+            MN_REQUIRE(dtab, MN_ENOMEM, "mn_knn: block table allocation / upload failed");
             // per-row buffers: expect ~ L1 nc / m0 candidates a row
             const double expect = (double)L1 * (double)nc / (double)m0;
             const char *cpe = knob("MN_SYM_CAP");
@@ -3064,11 +3062,10 @@ int shard_share(const float *X_all, const ShardPlan &pl, const float *tau0_all,
     MN_HIP_TRY(hipMemsetAsync(zdlt, 0, nn * 4, s));
     MN_KCHECK(s, "k_sym_pos<shard>");
     const int nbk = (int)((N + ksw2::BC - 1) / ksw2::BC);
-    const std::vector<int4> tab = ksw2::sym_block_table_share(nbk, 256, rank, world);
-    int4 *dtab = (int4 *)scratch(kSlotSymTab, tab.size() * sizeof(int4) + 64);
-    MN_REQUIRE(dtab, MN_ENOMEM, "shard_share: block table allocation failed");
+    int4 *dtab = nullptr;
+    const std::vector<int4> &tab = ksw2::sym_table_device(nbk, 256, 2, 4, rank, world, s, &dtab);
+    MN_REQUIRE(dtab, MN_ENOMEM, "shard_share: block table allocation / upload failed");
     MN_REQUIRE(tab.size() < INT_MAX, MN_ENOTSUP, "shard_share: sweep grid too large");
-    MN_HIP_TRY(hipMemcpyAsync(dtab, tab.data(), tab.size() * sizeof(int4), hipMemcpyHostToDevice, s));
     // per-row buffers: a share holds ~1/world of the ~L1 N / m0 candidates of
     // a row on average, but unevenly (a row's candidates in one column range
     // go to one rank): a 256-entry cap overflowed 0.9% of the rows at C2 with
