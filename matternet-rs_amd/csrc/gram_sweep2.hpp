@@ -882,7 +882,9 @@ inline const std::vector<int4> &sym_table_device(int nbk, int TPB, int order, in
         bool valid = false;
     };
     thread_local Up last;
-    const std::array<int, 6> key{nbk, TPB, order, gr, rank, world};
+    // (the tuning knob MN_SYM_GR overrides the group shape inside the
+    // builder: part of the key, so same-process A/Bs rebuild)
+    const std::array<int, 6> key{nbk, TPB, order, knob_int("MN_SYM_GR", gr) * 64 + gr, rank, world};
     const std::vector<int4> *tp = nullptr;
     for (const Entry &e : cache)
         if (e.key == key) tp = &e.tab;
