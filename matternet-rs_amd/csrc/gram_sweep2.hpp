@@ -753,8 +753,9 @@ inline SweepPlan plan_sweep(int64_t nq, int64_t nc2, double expect) {
 //     world = 1 is order 2.
 //   group shape gr x 32/gr (row blocks x column phases): 4 x 8 by default;
 //   C2's knn_x1 uses 2 x 16 (d = 768: 754 vs 759-760 ms same process, 8 x 4
-//   767-769, 16 x 2 785, 1 x 32 755-782; C5's d = 3072 prefers 4 x 8: 2711 vs
-//   2803-2817 ms — profiles/r04/r04_gr_ab*.log); tuning build: MN_SYM_GR
+//   767-769, 16 x 2 785, 1 x 32 755-782 — profiles/r04/r04_gr_ab*.log); C5's
+//   d = 3072 takes 8 x 4 since round 6 (sweep3: 2510-2524 vs 2630-2652 ms for
+//   4 x 8 — profiles/r06/r06_c5_gr_scan*.log); tuning build: MN_SYM_GR
 inline std::vector<int4> sym_block_table_share(int nbk, int TPB, int rank, int world, int gr = 4) {
     const int gre = knob_int("MN_SYM_GR", gr);
     const int GR = (gre == 1 || gre == 2 || gre == 8 || gre == 16) ? gre : 4, GC = 32 / GR;

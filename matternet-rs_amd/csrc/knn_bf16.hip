@@ -1082,9 +1082,12 @@ static int knn_cos_bf16_x1(const uint16_t *X, int64_t n, int32_t d, const mn_cos
     MN_REQUIRE(buf2 && cnt2, MN_ENOMEM, "mn_knn_cos_bf16: sweep buffer allocation failed");
     if (sym) {
         const int nbk = (int)((n + ksw2::BC - 1) / ksw2::BC);
+        // group shape 8 row blocks x 4 column phases (round 6, sweep3: 2510-2524
+        // vs 2630-2652 ms for 4 x 8 same process, 2 x 16 2830, 16 x 2 2608;
+        // profiles/r06/r06_c5_gr_scan*.log)
         int4 *dtab = nullptr;
         const std::vector<int4> &tab =
-            ksw2::sym_table_device(nbk, 256, knob_int("MN_BF16_SYM_ORDER", 2), 4, 0, 1, s, &dtab);
+            ksw2::sym_table_device(nbk, 256, knob_int("MN_BF16_SYM_ORDER", 2), 8, 0, 1, s, &dtab);
         MN_REQUIRE(dtab, MN_ENOMEM, "mn_knn_cos_bf16: block table allocation / upload failed");
         MN_HIP_TRY(hipMemsetAsync(cnt2, 0, (size_t)n * 4, s));
         MN_REQUIRE(tab.size() < INT_MAX, MN_ENOTSUP, "mn_knn_cos_bf16: sweep grid too large");

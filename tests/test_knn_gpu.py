@@ -439,6 +439,24 @@ def test_symmetric_fp16_sweep_wide_dynamic_range(case):
         assert st["ms_fallback"] < 2000, st
 
 
+def test_symmetric_sweep_block_table_cache_across_shapes():
+    """Round 6: the SW_SYM block table is built once per shape and thread and
+    uploaded only when the device slot lacks it.  Interleaved shapes (n = 36k,
+    40k, 36k again) and a repeated call must each use their own table: every
+    row bit-exact vs the oracle, and the repeat identical to the first call."""
+    d, k = 32, 8
+    XA = datagen.uniform(36_000, d, seed=61)
+    XB = datagen.uniform(40_000, d, seed=62)
+    ia, da, sa = hip_knn(XA, k, algo="bf16x1", timing=True)
+    ib, db, sb = hip_knn(XB, k, algo="bf16x1", timing=True)
+    ia2, da2, _ = hip_knn(XA, k, algo="bf16x1", timing=True)
+    assert sa["sweep_slices"] == -1 and sb["sweep_slices"] == -1  # SW_SYM ran
+    for X, i, dd in ((XA, ia, da), (XB, ib, db)):
+        ri, rd = O.knn_l2sq(X, k)
+        assert_exact(i, dd, ri, rd)
+    assert np.array_equal(ia, ia2) and np.array_equal(da.view(np.int32), da2.view(np.int32))
+
+
 def test_split_scan_small_k_many_parts():
     """the split exact scan's final merge with k < 8 over
     more than 512 corpus parts (nc > 600K: 684 parts of 1024 rows) — the
