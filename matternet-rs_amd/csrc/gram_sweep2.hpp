@@ -756,6 +756,7 @@ inline SweepPlan plan_sweep(int64_t nq, int64_t nc2, double expect) {
 //   767-769, 16 x 2 785, 1 x 32 755-782 — profiles/r04/r04_gr_ab*.log); C5's
 //   d = 3072 takes 8 x 4 since round 6 (sweep3: 2510-2524 vs 2630-2652 ms for
 //   4 x 8 — profiles/r06/r06_c5_gr_scan*.log); tuning build: MN_SYM_GR
+constexpr int kShareGR = 8;  // the sharded (C4) table's group rows (knn_f32.hip shard_share)
 inline std::vector<int4> sym_block_table_share(int nbk, int TPB, int rank, int world, int gr = 4) {
     const int gre = knob_int("MN_SYM_GR", gr);
     const int GR = (gre == 1 || gre == 2 || gre == 8 || gre == 16) ? gre : 4, GC = 32 / GR;

@@ -3063,7 +3063,10 @@ int shard_share(const float *X_all, const ShardPlan &pl, const float *tau0_all,
     MN_KCHECK(s, "k_sym_pos<shard>");
     const int nbk = (int)((N + ksw2::BC - 1) / ksw2::BC);
     int4 *dtab = nullptr;
-    const std::vector<int4> &tab = ksw2::sym_table_device(nbk, 256, 2, 4, rank, world, s, &dtab);
+    // groups of 8 row blocks x 4 column phases (round 6: largest share 6.23-6.25
+    // vs 6.39-6.52 s for 4 x 8 over the 8M C4 in one process, 2 x 16 slower;
+    // profiles/r06/r06_c4_gr*_ab.log)
+    const std::vector<int4> &tab = ksw2::sym_table_device(nbk, 256, 2, ksw2::kShareGR, rank, world, s, &dtab);
     MN_REQUIRE(dtab, MN_ENOMEM, "shard_share: block table allocation / upload failed");
     MN_REQUIRE(tab.size() < INT_MAX, MN_ENOTSUP, "shard_share: sweep grid too large");
     // per-row buffers: a share holds ~1/world of the ~L1 N / m0 candidates of

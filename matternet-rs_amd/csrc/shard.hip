@@ -980,7 +980,7 @@ int mn_sym_share_table(int32_t nbk, int32_t rank, int32_t world, int32_t *out4, 
     clear_error();
     MN_REQUIRE(nbk >= 1 && world >= 1 && rank >= 0 && rank < world && n_out, MN_EINVAL,
                "mn_sym_share_table: bad arguments");
-    const std::vector<int4> tab = ksw2::sym_block_table_share(nbk, 256, rank, world);
+    const std::vector<int4> tab = ksw2::sym_block_table_share(nbk, 256, rank, world, ksw2::kShareGR);
     *n_out = (int64_t)tab.size();
     if (!out4) return MN_OK;
     MN_REQUIRE((int64_t)tab.size() <= cap, MN_ECAP, "mn_sym_share_table: cap < %zu", tab.size());
