@@ -877,9 +877,10 @@ inline const std::vector<int4> &sym_table_device(int nbk, int TPB, int order, in
         std::vector<int4> tab;
     };
     thread_local std::vector<Entry> cache;
-    struct Up {
-        int dev = -1;
+    struct Up {  // the last upload: its slot, key and stream (another stream re-uploads,
+        int dev = -1;          // so no kernel can read the table ahead of its copy)
         void *p = nullptr;
+        hipStream_t s = nullptr;
         std::array<int, 6> key{};
         bool valid = false;
     };
@@ -901,14 +902,14 @@ inline const std::vector<int4> &sym_table_device(int nbk, int TPB, int order, in
     int dev = -1;
     (void)hipGetDevice(&dev);
     if (!*dtab) return *tp;
-    if (!(last.valid && last.p == (void *)*dtab && last.key == key && last.dev == dev)) {
+    if (!(last.valid && last.p == (void *)*dtab && last.key == key && last.dev == dev && last.s == s)) {
         if (hipMemcpyAsync(*dtab, tp->data(), tp->size() * sizeof(int4), hipMemcpyHostToDevice, s) !=
             hipSuccess) {
             last.valid = false;
             *dtab = nullptr;
             return *tp;
         }
-        last = Up{dev, (void *)*dtab, key, true};
+        last = Up{dev, (void *)*dtab, s, key, true};
     }
     return *tp;
 }
