@@ -1239,7 +1239,7 @@ __global__ __launch_bounds__(64 * WPB) void k_rerank_x1(
     int *__restrict__ big_list, const int *__restrict__ perm, int64_t q_off, int excl,
     const int *__restrict__ qmap, float *__restrict__ ub, int32_t *__restrict__ out_idx,
     float *__restrict__ out_dist, int *__restrict__ fb_count, int *__restrict__ fb_list,
-    float rel, int *__restrict__ why = nullptr) {
+    float rel, int *__restrict__ why, int m1) {
     __shared__ int cand[WPB][64 * NR];
     __shared__ float candk[WPB][64 * NR];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -1318,23 +1318,34 @@ __global__ __launch_bounds__(64 * WPB) void k_rerank_x1(
     const float dlt = delta[q];
     const float *qrow = Q + qo * (int64_t)d;
     const int kq = min(k, M);
+    // first pass: the kq1 best keys (round 6: k + m1 of them, k + m1 <= 64 —
+    // the lanes the k-best pass left idle — so Dp, the k-th exact distance
+    // among them, is tighter and the second pass rarely runs; m1 = 0: k)
+    const int kq1 = (m1 > 0 && k + m1 <= 64) ? min(M, k + m1) : kq;
     float dd[NR];
 #pragma unroll
     for (int r = 0; r < NR; ++r) {
         const int e = lane + 64 * r;
         dd[r] = __builtin_inff();
-        if (e < kq) dd[r] = exact_l2sq<VEC4>(qrow, C + ((int64_t)ix[r] - c_off) * d, d);
+        if (e < kq1) dd[r] = exact_l2sq<VEC4>(qrow, C + ((int64_t)ix[r] - c_off) * d, d);
     }
     float Dp = -__builtin_inff();
+    if (kq1 == kq) {
 #pragma unroll
-    for (int r = 0; r < NR; ++r) Dp = fmaxf(Dp, (lane + 64 * r) < kq ? dd[r] : -__builtin_inff());
+        for (int r = 0; r < NR; ++r) Dp = fmaxf(Dp, (lane + 64 * r) < kq ? dd[r] : -__builtin_inff());
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) Dp = fmaxf(Dp, __shfl_xor(Dp, o));
+        for (int o = 32; o > 0; o >>= 1) Dp = fmaxf(Dp, __shfl_xor(Dp, o));
+    } else {  // the kq-th smallest of the kq1 (<= 64: register 0) exact distances
+        float t[1] = {lane < kq1 ? dd[0] : __builtin_inff()};
+        int ti[1] = {lane};
+        wave_bitonic_sort<1>(t, ti);
+        Dp = __shfl(t[0], kq - 1);
+    }
 #pragma unroll
     for (int r = 0; r < NR; ++r) {
         const int e = lane + 64 * r;
         const float lb = kk[r] - dlt - rel * (__builtin_fabsf(kk[r]) + __builtin_fabsf(T));
-        if (e >= kq && e < M && !(lb > Dp))
+        if (e >= kq1 && e < M && !(lb > Dp))
             dd[r] = exact_l2sq<VEC4>(qrow, C + ((int64_t)ix[r] - c_off) * d, d);
     }
 #pragma unroll
@@ -2690,11 +2701,13 @@ static int knn_x1(const float *Q, int64_t nq, const float *C, int64_t nc, int32_
                 pass, h[0], h[1], h[2], h[3], h[4], h[5]);
         (void)hipMemsetAsync(why, 0, 24, s);
     };
+    // the re-rank's first-pass margin (k_rerank_x1 m1; tuning build MN_RR_M1, 0 = round 5)
+    const int rr_m1 = knob_int("MN_RR_M1", 16);
 #define MN_RRX(NRV, WPB, V, NB, QL, QN, BC, BL)                                                 \
     hipLaunchKernelGGL((k_rerank_x1<NRV, WPB, V>), dim3((unsigned)(NB)), dim3(64 * WPB), 0, s, \
                        Q, nq, C, d, c_off, S1r, pl.cap, cbuf1, bcnt1, tau_r, S2, cap2,          \
                        cbuf2, cnt2, dlt_r, k, nvalid, QL, QN, BC, BL, perm_r, q_off, excl,      \
-                       qmap_r, ubv, out_idx, out_dist, fb_count, fb_list, rel_r, why)
+                       qmap_r, ubv, out_idx, out_dist, fb_count, fb_list, rel_r, why, rr_m1)
     const int64_t nb1 = (nq + 3) / 4;
     if (vec4) MN_RRX(8, 4, true, nb1, (const int *)nullptr, (const int *)nullptr, big_count, big_list);
     else MN_RRX(8, 4, false, nb1, (const int *)nullptr, (const int *)nullptr, big_count, big_list);
@@ -2793,7 +2806,7 @@ static int knn_x1(const float *Q, int64_t nq, const float *C, int64_t nc, int32_
                        Q, (int64_t)nfb, C, d, c_off, 0, 0, (const uint2 *)nullptr,            \
                        (const int *)nullptr, tau3, (int)p3.S, p3.cap, cbuf3, cnt3, dlt3, k,    \
                        nvalid, QL, QN, BC, BL, perm_r, q_off, excl, erows, (float *)nullptr,     \
-                       out_idx, out_dist, fb_count, fb_list, 0.f, why)
+                       out_idx, out_dist, fb_count, fb_list, 0.f, why, rr_m1)
         const int64_t nb3 = (nfb + 3) / 4;
         if (vec4) MN_RR3(8, 4, true, nb3, (const int *)nullptr, (const int *)nullptr, big_count3, big_list3);
         else MN_RR3(8, 4, false, nb3, (const int *)nullptr, (const int *)nullptr, big_count3, big_list3);
@@ -3096,12 +3109,13 @@ int shard_share(const float *X_all, const ShardPlan &pl, const float *tau0_all,
     int *big_count = flags + 6;
     const float rel = (d + 8.0f) * 0x1p-24f;
     const int64_t nvalid = N - 1;
+    const int rr_m1 = knob_int("MN_RR_M1", 16);  // the re-rank's first-pass margin
 #define MN_RRS(NRV, WPB, V, NB, QL, QN, BCN, BL)                                                  \
     hipLaunchKernelGGL((k_rerank_x1<NRV, WPB, V>), dim3((unsigned)(NB)), dim3(64 * WPB), 0, s,   \
                        X_all, N, X_all, d, (int64_t)0, 0, 0, (const uint2 *)nullptr,              \
                        (const int *)nullptr, tauP, 1, cap2, cbuf2, cnt2, zdlt, k, nvalid, QL, QN, \
                        BCN, BL, pi, (int64_t)0, 1, pi, (float *)nullptr, pidx, pdist,             \
-                       (int *)nullptr, (int *)nullptr, rel, (int *)nullptr)
+                       (int *)nullptr, (int *)nullptr, rel, (int *)nullptr, rr_m1)
     const int64_t nb1 = (N + 3) / 4;
     if (vec4) MN_RRS(2, 4, true, nb1, (const int *)nullptr, (const int *)nullptr, big_count, big_list);
     else MN_RRS(2, 4, false, nb1, (const int *)nullptr, (const int *)nullptr, big_count, big_list);
