@@ -2701,8 +2701,9 @@ static int knn_x1(const float *Q, int64_t nq, const float *C, int64_t nc, int32_
                 pass, h[0], h[1], h[2], h[3], h[4], h[5]);
         (void)hipMemsetAsync(why, 0, 24, s);
     };
-    // the re-rank's first-pass margin (k_rerank_x1 m1; tuning build MN_RR_M1, 0 = round 5)
-    const int rr_m1 = knob_int("MN_RR_M1", 16);
+    // the re-rank's first-pass margin (k_rerank_x1 m1; tuning build MN_RR_M1, 0 = round 5;
+    // 8 measured best, profiles/r06/r06_c2_rerank_m1_scan*.log)
+    const int rr_m1 = knob_int("MN_RR_M1", 8);
 #define MN_RRX(NRV, WPB, V, NB, QL, QN, BC, BL)                                                 \
     hipLaunchKernelGGL((k_rerank_x1<NRV, WPB, V>), dim3((unsigned)(NB)), dim3(64 * WPB), 0, s, \
                        Q, nq, C, d, c_off, S1r, pl.cap, cbuf1, bcnt1, tau_r, S2, cap2,          \
@@ -3109,7 +3110,7 @@ int shard_share(const float *X_all, const ShardPlan &pl, const float *tau0_all,
     int *big_count = flags + 6;
     const float rel = (d + 8.0f) * 0x1p-24f;
     const int64_t nvalid = N - 1;
-    const int rr_m1 = knob_int("MN_RR_M1", 16);  // the re-rank's first-pass margin
+    const int rr_m1 = knob_int("MN_RR_M1", 8);  // the re-rank's first-pass margin
 #define MN_RRS(NRV, WPB, V, NB, QL, QN, BCN, BL)                                                  \
     hipLaunchKernelGGL((k_rerank_x1<NRV, WPB, V>), dim3((unsigned)(NB)), dim3(64 * WPB), 0, s,   \
                        X_all, N, X_all, d, (int64_t)0, 0, 0, (const uint2 *)nullptr,              \
