@@ -520,7 +520,7 @@ __global__ __launch_bounds__(256) void k_cos_rerank_x1(
     int topk, double delta, double eps, double sigma, double p, const int *__restrict__ qlist,
     const int *__restrict__ qlist_n, int *__restrict__ big_count, int *__restrict__ big_list,
     int32_t *__restrict__ out_idx, double *__restrict__ out_dist, double *__restrict__ out_w,
-    int *__restrict__ fb_count, int *__restrict__ fb_list) {
+    int *__restrict__ fb_count, int *__restrict__ fb_list, int m1) {
     __shared__ int cand[4][64 * NR];
     __shared__ float candk[4][64 * NR];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -588,25 +588,36 @@ __global__ __launch_bounds__(256) void k_cos_rerank_x1(
     wave_bitonic_sort<NR>(kk, ix);
     const uint16_t *qrow = X + q * (int64_t)d;
     const int kq = min(topk, M);
+    // first pass over the kq1 = topk + m1 best keys (<= 64: register 0), the
+    // pruning bound the topk-th exact distance among them (as k_rerank_x1,
+    // round 6); m1 = 0: the topk best, bound their maximum
+    const int kq1 = (m1 > 0 && topk + m1 <= 64) ? min(M, topk + m1) : kq;
     double dd[NR];
 #pragma unroll
     for (int r = 0; r < NR; ++r) {
         const int e = lane + 64 * r;
         dd[r] = __builtin_inf();
-        if (e < kq) dd[r] = cos_dist(exact_dot(qrow, X + (int64_t)ix[r] * d, d), xn[q], xn[ix[r]]);
+        if (e < kq1) dd[r] = cos_dist(exact_dot(qrow, X + (int64_t)ix[r] * d, d), xn[q], xn[ix[r]]);
     }
     double Dp = -__builtin_inf();
+    if (kq1 == kq) {
 #pragma unroll
-    for (int r = 0; r < NR; ++r) Dp = fmax(Dp, (lane + 64 * r) < kq ? dd[r] : -__builtin_inf());
+        for (int r = 0; r < NR; ++r) Dp = fmax(Dp, (lane + 64 * r) < kq ? dd[r] : -__builtin_inf());
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) Dp = fmax(Dp, __shfl_xor(Dp, o));
+        for (int o = 32; o > 0; o >>= 1) Dp = fmax(Dp, __shfl_xor(Dp, o));
+    } else {
+        double t[1] = {lane < kq1 ? dd[0] : __builtin_inf()};
+        int ti[1] = {lane};
+        wave_bitonic_sort<1>(t, ti);
+        Dp = __shfl(t[0], kq - 1);
+    }
     // pruning bound: the sweep keys carry two extra f32 roundings (2 delta
     // covers them with a wide margin)
     const double dprune = 2.0 * delta + 1e-6;
 #pragma unroll
     for (int r = 0; r < NR; ++r) {
         const int e = lane + 64 * r;
-        if (e >= kq && e < M) {
+        if (e >= kq1 && e < M) {
             const double cub = -(double)kk[r] + dprune;
             const double lb = 1.0 - (cub > 0.0 ? cub : 0.0);
             if (lb <= Dp) dd[r] = cos_dist(exact_dot(qrow, X + (int64_t)ix[r] * d, d), xn[q], xn[ix[r]]);
@@ -1172,11 +1183,14 @@ static int knn_cos_bf16_x1(const uint16_t *X, int64_t n, int32_t d, const mn_cos
     int *big_list = fb_list + n;
     const int *pix = sym ? (const int *)pi : (const int *)nullptr;
     const int S1r = sym ? 0 : (int)pl.S;  // SW_COS_SYM decided the sample pairs too
+    // the re-rank's first-pass margin: 0 (C5: 106.8 ms; 4 / 8 / 16: 113 / 158 / 215 ms —
+    // profiles/r06/r06_c5_rerank_m1_ab.log: its 6-KB rows make every extra one cost)
+    const int crr_m1 = knob_int("MN_CRR_M1", 0);
 #define MN_RRC(NRV, NB, QL, QN, BC, BL)                                                          \
     hipLaunchKernelGGL(k_cos_rerank_x1<NRV>, dim3((unsigned)(NB)), dim3(256), 0, s, X, n, d, pm, \
                        pix, xn, xinv, S1r, pl.cap, buf1, cnt1, btau1, S2, cap2, buf2, cnt2,     \
                        tcos, topk, delta, o->eps, o->sigma, o->p, QL, QN, BC, BL, out_idx,      \
-                       out_dist, out_w, fb_count, fb_list)
+                       out_dist, out_w, fb_count, fb_list, crr_m1)
     MN_RRC(8, (n + 3) / 4, (const int *)nullptr, (const int *)nullptr, big_count, big_list);
     MN_KCHECK(s, "k_cos_rerank_x1<8>");
     int hb[4] = {0, 0, 0, 0};
