@@ -48,7 +48,11 @@ def test_simulated_shards_at_c2_size_bit_exact(R):
     assert torch.equal(idx, full.idx)
     assert torch.equal(dist.view(torch.int32), full.dist.view(torch.int32))
     # the shares are balanced: the largest stage-B time within 15% of the mean
-    assert ms[:, 1].max() <= 1.15 * ms[:, 1].mean()
+    # (per rank the faster of two timed calls: one host hiccup during a rank's
+    # stage B — 147 vs 112 ms on one box — is not an imbalance of the table)
+    _, _, ms2, _ = knn_sharded_sim(X, k, R, timing=True)
+    b = np.minimum(ms[:, 1], ms2[:, 1])
+    assert b.max() <= 1.15 * b.mean(), (ms[:, 1], ms2[:, 1])
 
 
 def test_per_shard_form_through_the_loopback():
